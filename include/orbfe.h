@@ -1,0 +1,237 @@
+/*
+ * orbfe.h — C ABI of the MI355X-native ORB front-end (extractor + matchers).
+ *
+ * This is the drop-in seam for ORB-SLAM2's hot path as shipped in skaegy/ORBSLAM_MapSave.
+ * Every entry point below replaces one reference interface; the replaced interface is cited
+ * (file:line under the reference tree).  Plain C: no C++ types, no torch types, no exceptions.
+ *
+ * Conventions
+ *   - Every function returns an int status (ORBFE_OK == 0, negative on error) unless it is a
+ *     pure getter.  No function throws or aborts across the ABI.
+ *   - "host" pointers are ordinary CPU memory; "_device" entry points take HIP device pointers
+ *     and run asynchronously on the handle's stream (orbfe_set_stream); every other entry point
+ *     is synchronous on return, matching the blocking semantics of the reference.
+ *   - One handle is NOT reentrant (the reference ORBextractor keeps mvImagePyramid as instance
+ *     state, ORBextractor.h:90).  Distinct handles are fully independent (own stream, own
+ *     device buffers) and may be used from different threads concurrently.
+ *   - The library never falls back to a CPU path: if no gfx950 device is usable, orbfe_create /
+ *     orbfe_matcher_create fail with ORBFE_ERR_HIP.
+ */
+#ifndef ORBFE_H
+#define ORBFE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------------------------- */
+#define ORBFE_OK               0
+#define ORBFE_ERR_ARG         -1   /* bad argument (NULL, negative size, ...)                   */
+#define ORBFE_ERR_CAPACITY    -2   /* caller buffer too small; *n_out holds the required count  */
+#define ORBFE_ERR_HIP         -3   /* HIP runtime error / no usable device                      */
+#define ORBFE_ERR_UNSUPPORTED -4   /* input the reference handles only through UB (see DESIGN) */
+#define ORBFE_ERR_NOMEM       -5   /* device allocation failed                                  */
+
+/* ---- plain data types ----------------------------------------------------------------------- */
+
+/* Extractor parameters: the five ctor arguments of ORBextractor (ORBextractor.h:56-57),
+ * read from ORBextractor.{nFeatures,scaleFactor,nLevels,iniThFAST,minThFAST} (Tracking.cc:200-204). */
+typedef struct orbfe_params {
+    int32_t nfeatures;
+    float   scale_factor;
+    int32_t nlevels;
+    int32_t ini_th_fast;
+    int32_t min_th_fast;
+} orbfe_params;
+
+/* Layout-compatible with cv::KeyPoint (28 bytes): pt.x, pt.y, size, angle, response, octave,
+ * class_id.  Extractor output sets class_id = -1 exactly as cv::FAST does. */
+typedef struct orbfe_keypoint {
+    float   x, y;
+    float   size;
+    float   angle;
+    float   response;
+    int32_t octave;
+    int32_t class_id;
+} orbfe_keypoint;
+
+typedef struct orbfe_extractor orbfe_extractor;
+typedef struct orbfe_matcher   orbfe_matcher;
+
+/* ---- extractor ---------------------------------------------------------------------------- */
+
+/* Replaces ORBextractor::ORBextractor (ORBextractor.cc:409-469).  `device` is the HIP ordinal;
+ * `max_width`/`max_height`/`max_batch` size the device workspace (0 => 1920 x 1080 x 1, grown
+ * on demand outside any captured region). */
+orbfe_extractor* orbfe_create(const orbfe_params* params, int device, int max_width,
+                              int max_height, int max_batch, int* status);
+void orbfe_destroy(orbfe_extractor* h);
+
+/* Getters — ORBextractor::GetLevels / GetScaleFactor / GetScaleFactors /
+ * GetInverseScaleFactors / GetScaleSigmaSquares / GetInverseScaleSigmaSquares
+ * (ORBextractor.h:68-88).  Table outputs hold nlevels floats each; any may be NULL. */
+int   orbfe_get_levels(const orbfe_extractor* h);
+float orbfe_get_scale_factor(const orbfe_extractor* h);
+int   orbfe_get_scale_tables(const orbfe_extractor* h, float* scale, float* inv_scale,
+                             float* sigma2, float* inv_sigma2);
+/* mnFeaturesPerLevel (ORBextractor.cc:434-445). */
+int   orbfe_get_features_per_level(const orbfe_extractor* h, int32_t* out);
+/* Per-frame keypoint capacity that can never overflow for this handle's params
+ * (sum over levels of the oct-tree bound, see DESIGN.md "capacity"). */
+int   orbfe_keypoint_capacity(const orbfe_extractor* h);
+
+/* Replaces ORBextractor::operator()(image, mask, keypoints, descriptors)
+ * (ORBextractor.h:64-66, ORBextractor.cc:1042-1108), called from Frame::ExtractORB
+ * (Frame.cc:358-364, mask empty) and Frame::ExtractORBMask (Frame.cc:366-371).
+ *   img   : w x h u8 gray, row stride `stride` bytes (CV_8UC1, asserted at ORBextractor.cc:1051)
+ *   mask  : NULL for none, else w x h u8 with row stride `mask_stride`; pixels where mask==0
+ *           are zeroed before the pyramid (Mat::copyTo(dst, mask), ORBextractor.cc:1053)
+ *   kps   : kps_cap keypoints out, level-major order (ORBextractor.cc:1079-1107)
+ *   desc  : kps_cap x 32 bytes out, row i <-> kps[i]
+ *   n_out : number of keypoints written.
+ * Empty image (img==NULL or w==0 or h==0): returns ORBFE_OK and touches nothing
+ * (ORBextractor.cc:1045-1046).  kps_cap too small: ORBFE_ERR_CAPACITY, *n_out = required. */
+int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int w, int hgt, size_t stride,
+                  const uint8_t* mask, size_t mask_stride, orbfe_keypoint* kps, int kps_cap,
+                  uint8_t* desc, int* n_out);
+
+/* Throughput form of orbfe_extract over n same-size frames (host buffers).  Frame f's
+ * keypoints go to kps[f*kps_cap ...], descriptors to desc[f*kps_cap*32 ...], count n_out[f].
+ * masks may be NULL (no masks) or an array of n pointers (entries may be NULL). */
+int orbfe_extract_batch(orbfe_extractor* h, const uint8_t* const* imgs, int n, int w, int hgt,
+                        size_t stride, const uint8_t* const* masks, size_t mask_stride,
+                        orbfe_keypoint* kps, int kps_cap, uint8_t* desc, int32_t* n_out);
+
+/* Device-resident throughput form: d_imgs holds n frames, frame f at d_imgs + f*frame_pitch,
+ * rows `stride` bytes apart.  d_masks NULL or laid out like d_imgs.  Outputs are device
+ * slabs laid out as in orbfe_extract_batch.  Asynchronous on the handle's stream. */
+int orbfe_extract_batch_device(orbfe_extractor* h, const uint8_t* d_imgs, int n, int w, int hgt,
+                               size_t stride, size_t frame_pitch, const uint8_t* d_masks,
+                               orbfe_keypoint* d_kps, int kps_cap, uint8_t* d_desc,
+                               int32_t* d_n_out);
+
+/* Stream control: `hip_stream` is a hipStream_t (NULL => the handle's own stream). */
+int orbfe_set_stream(orbfe_extractor* h, void* hip_stream);
+int orbfe_synchronize(orbfe_extractor* h);
+
+/* Pyramid access — replaces the public member mvImagePyramid (ORBextractor.h:90) read by
+ * stereo matching (Frame.cc:589, 679, 696).  Copies level `level` of frame `frame` of the
+ * most recent extraction (interior pixels only, rows w bytes apart) into `out`
+ * (out may be NULL to query w/h). */
+int orbfe_get_level(orbfe_extractor* h, int frame, int level, uint8_t* out, int* w, int* hgt);
+
+/* Stage probes of the most recent extraction, for parity tests against the oracle:
+ * blurred level (GaussianBlur 7x7 sigma 2 REFLECT_101, ORBextractor.cc:1088-1089) and the
+ * per-level FAST output before distribution (vToDistributeKeys, ORBextractor.cc:777-828;
+ * coordinates relative to (16,16), response = FAST score). */
+int orbfe_get_blurred_level(orbfe_extractor* h, int frame, int level, uint8_t* out, int* w,
+                            int* hgt);
+int orbfe_get_fast_keys(orbfe_extractor* h, int frame, int level, orbfe_keypoint* out, int cap,
+                        int* n_out);
+
+/* ---- matchers ------------------------------------------------------------------------------- */
+
+/* Frame data the matchers read.  Mirrors the Frame members the reference matchers touch:
+ * mvKeysUn (x, y, octave, angle), mDescriptors, mvuRight, image bounds mnMin/MaxX/Y and
+ * mfGridElementWidthInv/HeightInv (Frame.cc:212-213), mvScaleFactors.  The 64 x 48 grid of
+ * Frame::AssignFeaturesToGrid (Frame.cc:341-356) is rebuilt from keys_un inside the call. */
+typedef struct orbfe_frame_view {
+    int32_t               n;
+    const orbfe_keypoint* keys_un;        /* n                                                 */
+    const uint8_t*        desc;           /* n x 32                                            */
+    const float*          u_right;        /* n, or NULL for monocular (all -1)                 */
+    float                 min_x, max_x, min_y, max_y;
+    float                 grid_w_inv, grid_h_inv;
+    const float*          scale_factors;  /* nlevels                                           */
+    int32_t               nlevels;
+} orbfe_frame_view;
+
+/* Per-MapPoint tracking scratch (MapPoint.h:106-111) + the getters SearchByProjection reads. */
+typedef struct orbfe_mappoint_view {
+    int32_t        m;
+    const uint8_t* track_in_view;  /* mbTrackInView                                         */
+    const uint8_t* is_bad;         /* isBad()                                               */
+    const float*   proj_x;         /* mTrackProjX                                           */
+    const float*   proj_y;         /* mTrackProjY                                           */
+    const float*   proj_xr;        /* mTrackProjXR                                          */
+    const int32_t* pred_level;     /* mnTrackScaleLevel                                     */
+    const float*   view_cos;       /* mTrackViewCos                                         */
+    const uint8_t* desc;           /* GetDescriptor(), m x 32                               */
+    const int32_t* n_obs;          /* Observations()                                        */
+} orbfe_mappoint_view;
+
+/* Camera + pose for the last-frame projection matcher (ORBmatcher.cc:1341-1379). Row-major
+ * 3x4 [R|t] world->camera. */
+typedef struct orbfe_camera {
+    float fx, fy, cx, cy, bf, b;   /* mbf and mb (= mbf/fx, Frame.cc:225)                    */
+} orbfe_camera;
+
+orbfe_matcher* orbfe_matcher_create(int device, int* status);
+void orbfe_matcher_destroy(orbfe_matcher* m);
+int  orbfe_matcher_set_stream(orbfe_matcher* m, void* hip_stream);
+
+/* ORBmatcher::DescriptorDistance (ORBmatcher.cc:1650-1666): dist[i] = Hamming(a_i, b_i). */
+int orbfe_hamming(orbfe_matcher* m, const uint8_t* a, const uint8_t* b, int n, int32_t* dist);
+
+/* Brute-force Hamming (config 3, no single reference function): for each query the best and
+ * second-best distance over all references with the first-wins update rule of
+ * ORBmatcher.cc:102-114 (best/second start at 256).  Host buffers. */
+int orbfe_bf_match(orbfe_matcher* m, const uint8_t* q, int nq, const uint8_t* r, int nr,
+                   int32_t* best_idx, int32_t* best_dist, int32_t* second_dist);
+/* Device-resident batched form: `nb` independent (query-set, reference-set) problems;
+ * problem b reads d_q + b*q_pitch (nq_b = d_nq[b] rows) against d_r + b*r_pitch
+ * (nr_b = d_nr[b] rows) and writes d_out + b*nq_cap*3 as (best_idx, best, second) triples. */
+int orbfe_bf_match_batch_device(orbfe_matcher* m, const uint8_t* d_q, size_t q_pitch,
+                                const int32_t* d_nq, int nq_cap, const uint8_t* d_r,
+                                size_t r_pitch, const int32_t* d_nr, int nb, int32_t* d_out);
+
+/* ORBmatcher::SearchForInitialization (ORBmatcher.cc:408-523), matcher built as
+ * ORBmatcher(nnratio, check_ori) (Tracking.cc:843).  prev_matched: inout F1.n (x,y) pairs
+ * (vbPrevMatched); matches12: out F1.n (vnMatches12). */
+int orbfe_search_for_initialization(orbfe_matcher* m, float nnratio, int check_ori,
+                                    const orbfe_frame_view* f1, const orbfe_frame_view* f2,
+                                    float* prev_matched, int window, int32_t* matches12,
+                                    int32_t* nmatches);
+
+/* ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th) (ORBmatcher.cc:45-129).
+ * frame_mp: inout F.n, id of the MapPoint held by each keypoint or -1 (F.mvpMapPoints);
+ * frame_mp_obs: inout F.n, Observations() of that MapPoint.  A match writes
+ * mp_ids[i] (or i when mp_ids is NULL) and mps->n_obs[i]. */
+int orbfe_search_by_projection_local(orbfe_matcher* m, float nnratio,
+                                     const orbfe_frame_view* f, int32_t* frame_mp,
+                                     int32_t* frame_mp_obs, const orbfe_mappoint_view* mps,
+                                     const int32_t* mp_ids, float th, int32_t* nmatches);
+
+/* ORBmatcher::SearchByProjection(Frame& Cur, const Frame& Last, th, bMono)
+ * (ORBmatcher.cc:1331-1473).  The last frame is given as its N_last keypoints (octave, angle
+ * from last_keys), the world position/descriptor/Observations() of the MapPoint it holds
+ * (last_mp_valid[i] == 0 <=> NULL), and mvbOutlier. Poses are row-major 3x4 world->camera. */
+int orbfe_search_by_projection_last(orbfe_matcher* m, int check_ori,
+                                    const orbfe_frame_view* cur, const float* tcw_cur,
+                                    const orbfe_camera* cam, int32_t* frame_mp,
+                                    int32_t* frame_mp_obs, int n_last,
+                                    const orbfe_keypoint* last_keys,
+                                    const uint8_t* last_mp_valid, const uint8_t* last_outlier,
+                                    const float* last_mp_xyz, const uint8_t* last_mp_desc,
+                                    const int32_t* last_mp_nobs, const int32_t* last_mp_ids,
+                                    const float* tcw_last, float th, int mono,
+                                    int32_t* nmatches);
+
+/* Frame::isInFrustum (Frame.cc:387-443) + MapPoint::PredictScale (MapPoint.cc:633-642) over
+ * m MapPoints: world pos (m x 3), normal (m x 3), mfMinDistance/mfMaxDistance.  Writes the
+ * tracking scratch fields (mbTrackInView, mTrackProjX/Y/XR, mnTrackScaleLevel,
+ * mTrackViewCos). log_scale_factor = mfLogScaleFactor (Frame.cc:185). */
+int orbfe_is_in_frustum(orbfe_matcher* m, int n, const float* xyz, const float* normal,
+                        const float* min_dist, const float* max_dist, const float* tcw,
+                        const orbfe_camera* cam, float min_x, float max_x, float min_y,
+                        float max_y, float log_scale_factor, float viewing_cos_limit,
+                        uint8_t* in_view, float* proj_x, float* proj_y, float* proj_xr,
+                        int32_t* pred_level, float* view_cos);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORBFE_H */

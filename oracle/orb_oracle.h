@@ -1,0 +1,90 @@
+/*
+ * orb_oracle.h — TEST INFRASTRUCTURE ONLY (parity checker + CPU baseline), never shipped.
+ *
+ * CPU restatement of the reference hot path (skaegy/ORBSLAM_MapSave src/ORBextractor.cc,
+ * src/ORBmatcher.cc, src/Frame.cc, src/MapPoint.cc) and of the OpenCV 3.3.1 primitives it
+ * calls.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it.  The product library (liborbfe.so) never links or calls it.
+ *
+ * PARITY UNPINNED: the reference cannot be built here (OpenCV/Boost/Eigen/Pangolin absent)
+ * and holds no tests, fixtures or golden vectors for this path.  See
+ * DESIGN.md "Oracle" for every semantic choice (H1-H8) this restatement fixes.
+ *
+ * Signatures mirror include/orbfe.h with an `oracle_` prefix and host pointers only.
+ */
+#ifndef ORB_ORACLE_H
+#define ORB_ORACLE_H
+#include "../include/orbfe.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* A1 tables: scale, inv_scale, sigma2, inv_sigma2, features per level, umax[16]. */
+int oracle_tables(const orbfe_params* p, float* scale, float* inv_scale, float* sigma2,
+                  float* inv_sigma2, int32_t* nfeat, int32_t* umax);
+/* Level sizes of the pyramid for a w x h input (ORBextractor.cc:1114-1115). */
+int oracle_level_sizes(const orbfe_params* p, int w, int h, int32_t* lw, int32_t* lh);
+
+/* Full operator() (ORBextractor.cc:1042-1108). */
+int oracle_extract(const orbfe_params* p, const uint8_t* img, int w, int h, size_t stride,
+                   const uint8_t* mask, size_t mask_stride, orbfe_keypoint* kps, int kps_cap,
+                   uint8_t* desc, int* n_out);
+/* n frames on `nthreads` CPU threads, one extractor state per thread (Frame.cc:78-81). */
+int oracle_extract_batch(const orbfe_params* p, const uint8_t* imgs, int n, int w, int h,
+                         size_t frame_pitch, orbfe_keypoint* kps, int kps_cap, uint8_t* desc,
+                         int32_t* n_out, int nthreads);
+
+/* Stage probes. */
+int oracle_pyramid(const orbfe_params* p, const uint8_t* img, int w, int h, size_t stride,
+                   const uint8_t* mask, size_t mask_stride, uint8_t* out /* levels packed,
+                   rows dense */);
+int oracle_resize_linear(const uint8_t* src, int sw, int sh, size_t sstride, uint8_t* dst,
+                         int dw, int dh, size_t dstride);
+int oracle_gaussian_blur(const uint8_t* src, int w, int h, size_t stride, uint8_t* dst);
+int oracle_fast(const uint8_t* roi, int rows, int cols, size_t stride, int threshold,
+                orbfe_keypoint* out, int cap, int* n_out);
+int oracle_fast_keys(const orbfe_params* p, const uint8_t* level, int lw, int lh,
+                     size_t stride, orbfe_keypoint* out, int cap, int* n_out);
+int oracle_distribute(const orbfe_params* p, int level, int lw, int lh,
+                      const orbfe_keypoint* keys, int n, orbfe_keypoint* out, int cap,
+                      int* n_out);
+int oracle_fast_atan2(const float* y, const float* x, int n, float* out);
+int oracle_ic_angle(const uint8_t* level, int lw, int lh, size_t stride,
+                    const orbfe_keypoint* kps, int n, float* angle);
+int oracle_describe(const uint8_t* blurred, int lw, int lh, size_t stride,
+                    const orbfe_keypoint* kps, int n, uint8_t* desc);
+
+/* Matchers. */
+int oracle_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* dist);
+int oracle_bf_match(const uint8_t* q, int nq, const uint8_t* r, int nr, int32_t* best_idx,
+                    int32_t* best_dist, int32_t* second_dist);
+int oracle_features_in_area(const orbfe_frame_view* f, float x, float y, float r,
+                            int min_level, int max_level, int32_t* out, int cap, int* n_out);
+int oracle_search_for_initialization(float nnratio, int check_ori, const orbfe_frame_view* f1,
+                                     const orbfe_frame_view* f2, float* prev_matched,
+                                     int window, int32_t* matches12, int32_t* nmatches);
+int oracle_search_by_projection_local(float nnratio, const orbfe_frame_view* f,
+                                      int32_t* frame_mp, int32_t* frame_mp_obs,
+                                      const orbfe_mappoint_view* mps, const int32_t* mp_ids,
+                                      float th, int32_t* nmatches);
+int oracle_search_by_projection_last(int check_ori, const orbfe_frame_view* cur,
+                                     const float* tcw_cur, const orbfe_camera* cam,
+                                     int32_t* frame_mp, int32_t* frame_mp_obs, int n_last,
+                                     const orbfe_keypoint* last_keys,
+                                     const uint8_t* last_mp_valid, const uint8_t* last_outlier,
+                                     const float* last_mp_xyz, const uint8_t* last_mp_desc,
+                                     const int32_t* last_mp_nobs, const int32_t* last_mp_ids,
+                                     const float* tcw_last, float th, int mono,
+                                     int32_t* nmatches);
+int oracle_is_in_frustum(int n, const float* xyz, const float* normal, const float* min_dist,
+                         const float* max_dist, const float* tcw, const orbfe_camera* cam,
+                         float min_x, float max_x, float min_y, float max_y,
+                         float log_scale_factor, float viewing_cos_limit, uint8_t* in_view,
+                         float* proj_x, float* proj_y, float* proj_xr, int32_t* pred_level,
+                         float* view_cos);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,100 @@
+// orbfe_device.hpp — gfx950 device helpers shared by the extractor and matcher kernels.
+// Built with -ffp-contract=off: every float expression below is evaluated operation by
+// operation exactly as the reference writes it (H3/H4 in DESIGN.md).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define ORBFE_WAVE 64
+
+namespace orbfe {
+
+// cvRound(float): round half to even (v_rndne_f32), App. A.5.
+__device__ __forceinline__ int rne(float v) { return (int)__builtin_rintf(v); }
+
+// cv::fastAtan2 (App. A.4; reference call ORBextractor.cc:102), degrees in [0, 360).
+__device__ __forceinline__ float fast_atan2(float y, float x) {
+    const float k180pi = (float)(180.0 / 3.14159265358979323846);
+    const float p1 = 0.9997878412794807f * k180pi;
+    const float p3 = -0.3258083974640975f * k180pi;
+    const float p5 = 0.1555786518463281f * k180pi;
+    const float p7 = -0.04432655554792128f * k180pi;
+    const float eps = (float)2.220446049250313e-16;  // (float)DBL_EPSILON
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + eps);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + eps);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+// ORBmatcher::DescriptorDistance (ORBmatcher.cc:1650-1666): popcount of XOR over 8 words.
+// v_bcnt_u32_b32 accumulates, so a 256-bit distance is 8 XORs + 8 bit-counts.
+__device__ __forceinline__ int hamming256(const uint4 a0, const uint4 a1, const uint4 b0,
+                                          const uint4 b1) {
+    int d = __builtin_popcount(a0.x ^ b0.x);
+    d += __builtin_popcount(a0.y ^ b0.y);
+    d += __builtin_popcount(a0.z ^ b0.z);
+    d += __builtin_popcount(a0.w ^ b0.w);
+    d += __builtin_popcount(a1.x ^ b1.x);
+    d += __builtin_popcount(a1.y ^ b1.y);
+    d += __builtin_popcount(a1.z ^ b1.z);
+    d += __builtin_popcount(a1.w ^ b1.w);
+    return d;
+}
+
+// Inclusive sum over a 64-lane wave.
+__device__ __forceinline__ int wave_inclusive_sum(int x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    return x;
+}
+
+__device__ __forceinline__ int wave_sum(int x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+
+// Block-wide exclusive scan of one int per thread.  `tmp` holds >= BLOCK/64 ints of LDS.
+// Returns the exclusive prefix; `total` receives the block sum.  Contains barriers: every
+// thread of the block must call it.
+template <int BLOCK>
+__device__ __forceinline__ int block_exclusive_scan(int v, int* tmp, int& total) {
+    constexpr int NW = BLOCK / 64;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int inc = wave_inclusive_sum(v);
+    if (lane == 63) tmp[wid] = inc;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        int w = threadIdx.x < NW ? tmp[threadIdx.x] : 0;
+        w = wave_inclusive_sum(w);
+        if (threadIdx.x < NW) tmp[threadIdx.x] = w;
+    }
+    __syncthreads();
+    const int before = wid ? tmp[wid - 1] : 0;
+    total = tmp[NW - 1];
+    __syncthreads();
+    return before + inc - v;
+}
+
+template <int BLOCK>
+__device__ __forceinline__ int block_sum(int v, int* tmp) {
+    int total;
+    block_exclusive_scan<BLOCK>(v, tmp, total);
+    return total;
+}
+
+}  // namespace orbfe

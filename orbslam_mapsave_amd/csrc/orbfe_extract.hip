@@ -1,0 +1,941 @@
+// orbfe_extract.hip — MI355X (gfx950) ORB extractor: the HIP replacement for ORB-SLAM2's
+// ORBextractor::operator() (skaegy/ORBSLAM_MapSave src/ORBextractor.cc:1042-1108).
+//
+// Pipeline for a batch of B same-size frames (one launch per stage, every launch covers the
+// whole batch; DESIGN.md "Kernels" has the roofline and bytes of each):
+//   K0 mask_kernel      Mat::copyTo(dst, mask) (1053)                       [only with a mask]
+//   K1 resize_kernel    cascaded cv::resize INTER_LINEAR 8U, levels 1..L-1 (1123)
+//   K2 fast_kernel      per-cell FAST-9 score + cell-local 3x3 NMS + iniTh->minTh fallback
+//                       (764-831); one workgroup per (frame, cell)
+//   K3 octree_kernel    DistributeOctTree (538-762) as a data-parallel list emulation; one
+//                       workgroup per (frame, level)
+//   K4 blur_kernel      GaussianBlur 7x7 sigma 2 REFLECT_101 (1088-1089), integer path
+//   K5 describe_kernel  IC_Angle (76-103) + rBRIEF (107-146) + level scaling (1098-1104);
+//                       one wave per keypoint, 256 tests packed with 4 ballots
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/orbfe.h"
+#include "orbfe_device.hpp"
+#include "orbfe_internal.hpp"
+
+namespace orbfe {
+
+// ---------------------------------------------------------------------------------------------
+// constant tables
+__constant__ int8_t c_pattern[1024] = {
+#include "../../include/orbfe_pattern.inc"
+};
+__constant__ int c_umax[16];
+
+constexpr int kEdge = 19;       // EDGE_THRESHOLD (ORBextractor.cc:73)
+constexpr int kMinBorder = 16;  // EDGE_THRESHOLD - 3 (772)
+constexpr int kCellW = 30;      // W (768)
+
+// ---------------------------------------------------------------------------------------------
+// K0 — masked copy into pyramid level 0 (Mat::copyTo with a mask, App. A.7).
+__global__ void mask_kernel(const uint8_t* src, long long src_fpitch, int src_pitch,
+                            const uint8_t* mask, long long mask_fpitch,
+                            int mask_pitch, uint8_t* dst, long long dst_fpitch,
+                            int dst_pitch, int w, int h) {
+    const int f = blockIdx.z;
+    const int y = blockIdx.y;
+    const uint8_t* s = src + f * src_fpitch + (long long)y * src_pitch;
+    const uint8_t* m = mask + f * mask_fpitch + (long long)y * mask_pitch;
+    uint8_t* d = dst + f * dst_fpitch + (long long)y * dst_pitch;
+    for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < w; x += gridDim.x * blockDim.x)
+        d[x] = m[x] ? s[x] : 0;
+    (void)h;
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1 — one pyramid level from the previous one (App. A.1, scalar FixedPtCast<int,uchar,22>).
+// Host-built tables: xt[3*dx] = {sx, min(sx+1,sw-1), a0 | a1<<16}; yt[3*dy] likewise with the
+// source rows clipped to [0, sh-1].  Each thread writes 4 consecutive pixels.
+__global__ __launch_bounds__(256) void resize_kernel(
+    const uint8_t* __restrict__ src, long long src_fpitch, int src_pitch,
+    uint8_t* __restrict__ dst, long long dst_fpitch, int dst_pitch, int dw, int dh,
+    const int* __restrict__ xt, const int* __restrict__ yt) {
+    const int f = blockIdx.z;
+    const int y = blockIdx.y * 4 + threadIdx.y;
+    const int x = (blockIdx.x * 64 + threadIdx.x) * 4;
+    if (y >= dh || x >= dw) return;
+    const int r0 = yt[3 * y], r1 = yt[3 * y + 1], bb = yt[3 * y + 2];
+    const int b0 = bb & 0xffff, b1 = (int)((unsigned)bb >> 16);
+    const uint8_t* s0 = src + f * src_fpitch + (long long)r0 * src_pitch;
+    const uint8_t* s1 = src + f * src_fpitch + (long long)r1 * src_pitch;
+    uint8_t* d = dst + f * dst_fpitch + (long long)y * dst_pitch;
+    uint32_t packed = 0;
+    const int n = min(4, dw - x);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (k >= n) break;
+        const int dx = x + k;
+        const int x0 = xt[3 * dx], x1 = xt[3 * dx + 1], aa = xt[3 * dx + 2];
+        const int a0 = aa & 0xffff, a1 = (int)((unsigned)aa >> 16);
+        const int t0 = s0[x0] * a0 + s0[x1] * a1;
+        const int t1 = s1[x0] * a0 + s1[x1] * a1;
+        const int v = min(max((t0 * b0 + t1 * b1 + (1 << 21)) >> 22, 0), 255);
+        packed |= (uint32_t)v << (8 * k);
+    }
+    if (n == 4) {
+        *reinterpret_cast<uint32_t*>(d + x) = packed;  // dst pitch and x are multiples of 4
+    } else {
+        for (int k = 0; k < n; ++k) d[x + k] = (uint8_t)(packed >> (8 * k));
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K2 — FAST per cell.  S(p) = max(q0, -q1) - 1 where q0 (q1) is the max (min) over the 16
+// nine-pixel arcs of the min (max) of d = v - circle: p is a cv::FAST corner at threshold t iff
+// S(p) >= t, and cornerScore<16> returns exactly S(p) for such p (DESIGN.md "FAST").  So S is
+// computed once per pixel and both thresholds of the fallback reuse it.
+constexpr int kFastBlock = 256;
+constexpr int kRoiMax = 72;  // cell ROI <= (59+6) x (59+6): wCell < 2*W for every level size
+
+__device__ __forceinline__ int fast_S(const uint8_t* p, int st) {
+    const int v = p[0];
+    int d[16];
+    d[0] = v - p[3 * st];
+    d[1] = v - p[3 * st + 1];
+    d[2] = v - p[2 * st + 2];
+    d[3] = v - p[st + 3];
+    d[4] = v - p[3];
+    d[5] = v - p[-st + 3];
+    d[6] = v - p[-2 * st + 2];
+    d[7] = v - p[-3 * st + 1];
+    d[8] = v - p[-3 * st];
+    d[9] = v - p[-3 * st - 1];
+    d[10] = v - p[-2 * st - 2];
+    d[11] = v - p[-st - 3];
+    d[12] = v - p[-3];
+    d[13] = v - p[st - 3];
+    d[14] = v - p[2 * st - 2];
+    d[15] = v - p[3 * st - 1];
+    int a2[16], b2[16], a4[16], b4[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        a2[k] = min(d[k], d[(k + 1) & 15]);
+        b2[k] = max(d[k], d[(k + 1) & 15]);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        a4[k] = min(a2[k], a2[(k + 2) & 15]);
+        b4[k] = max(b2[k], b2[(k + 2) & 15]);
+    }
+    int q0 = -1000, q1 = 1000;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int a9 = min(min(a4[k], a4[(k + 4) & 15]), d[(k + 8) & 15]);
+        const int b9 = max(max(b4[k], b4[(k + 4) & 15]), d[(k + 8) & 15]);
+        q0 = max(q0, a9);
+        q1 = min(q1, b9);
+    }
+    return max(q0, -q1) - 1;
+}
+
+// Strict 3x3 NMS inside the cell's detection area at threshold t (cv::FAST nonmax, H1).
+__device__ __forceinline__ bool fast_is_max(const uint8_t* S, int nr, int nc, int r, int c, int t) {
+    const int s = (int)S[r * nc + c] - 1;
+    if (s < t) return false;
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+            if (!dy && !dx) continue;
+            const int rr = r + dy, cc = c + dx;
+            int nv = 0;
+            if (rr >= 0 && rr < nr && cc >= 0 && cc < nc) {
+                const int ns = (int)S[rr * nc + cc] - 1;
+                nv = ns >= t ? ns : 0;
+            }
+            if (!(s > nv)) return false;
+        }
+    return true;
+}
+
+__global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
+    __shared__ uint8_t roi[kRoiMax * kRoiMax];
+    __shared__ uint8_t S[(kRoiMax - 6) * (kRoiMax - 6)];
+    __shared__ int tmp[kFastBlock / 64 + 1];
+    const int c = blockIdx.x, f = blockIdx.y;
+    const CellDesc cell = a.cells[c];
+    const LevelPtr lp = a.pyr[cell.level];
+    const int rows = cell.y1 - cell.y0, cols = cell.x1 - cell.x0;
+    const uint8_t* img = lp.base + f * lp.fpitch + (long long)cell.y0 * lp.pitch + cell.x0;
+    for (int i = threadIdx.x; i < rows * cols; i += kFastBlock) {
+        const int r = i / cols, cc = i - r * cols;
+        roi[r * kRoiMax + cc] = img[(long long)r * lp.pitch + cc];
+    }
+    __syncthreads();
+    const int nr = rows - 6, nc = cols - 6;  // candidates: ROI rows/cols 3 .. n-4
+    const int ncand = (nr > 0 && nc > 0) ? nr * nc : 0;
+    for (int i = threadIdx.x; i < ncand; i += kFastBlock) {
+        const int r = i / nc, cc = i - r * nc;
+        S[i] = (uint8_t)(fast_S(roi + (r + 3) * kRoiMax + cc + 3, kRoiMax) + 1);
+    }
+    __syncthreads();
+    // ordered compaction: thread t owns candidates [t*chunk, (t+1)*chunk) in row-major order
+    const int chunk = (ncand + kFastBlock - 1) / kFastBlock;
+    const int p0 = min(threadIdx.x * chunk, ncand), p1 = min(p0 + chunk, ncand);
+    int t = a.ini_th;
+    int mine = 0;
+    for (int p = p0; p < p1; ++p) {
+        const int r = p / nc;
+        mine += fast_is_max(S, nr, nc, r, p - r * nc, t);
+    }
+    int total;
+    int before = block_exclusive_scan<kFastBlock>(mine, tmp, total);
+    if (total == 0) {  // no corner survived at iniThFAST: rerun at minThFAST (811-815)
+        t = a.min_th;
+        mine = 0;
+        for (int p = p0; p < p1; ++p) {
+            const int r = p / nc;
+            mine += fast_is_max(S, nr, nc, r, p - r * nc, t);
+        }
+        before = block_exclusive_scan<kFastBlock>(mine, tmp, total);
+    }
+    uint32_t* out = a.cell_keys + f * a.cell_cap_total + cell.slot;
+    const int cap = cell.cap;
+    if (mine) {
+        int o = before;
+        for (int p = p0; p < p1 && o < cap; ++p) {
+            const int r = p / nc, cc = p - r * nc;
+            if (!fast_is_max(S, nr, nc, r, cc, t)) continue;
+            const int s = (int)S[p] - 1;
+            // key relative to (minBorderX, minBorderY): pt + (j*wCell, i*hCell) (819-824)
+            const int xr = cell.x0 + 3 + cc - kMinBorder, yr = cell.y0 + 3 + r - kMinBorder;
+            out[o++] = pack_key(xr, yr, s);
+        }
+    }
+    if (threadIdx.x == 0) a.cell_cnt[f * a.ncells + c] = min(total, cap);
+}
+
+// ---------------------------------------------------------------------------------------------
+// K3 — DistributeOctTree as a data-parallel emulation of the reference's std::list.
+//
+// The list is an array in list order, rebuilt every pass into the other buffer:
+//   phase-1 pass: new list = reverse(children of the divided nodes, in list order, each
+//                 n1..n4) ++ (single-key nodes, in order)              (push_front, 605-663)
+//   phase-2 round: the expandable nodes sorted by (size desc, creation seq desc) [H2] are
+//                 divided in that order until size >= N: new list = reverse(children in
+//                 processing order) ++ (untouched nodes, in order)     (675-736)
+// Keys stay in original order (cell-row-major, FAST emission order); each live key carries the
+// list position of its node.  Single-key nodes remember their key and drop out of the key set.
+// Final: per node the max response, first (lowest original index) on ties (741-759).
+constexpr int kOctBlock = 512;
+
+struct OctLds {  // carve of the dynamic LDS region (sizes in elements)
+    int* box[2];    // x0 | x1 << 16
+    int* boy[2];    // y0 | y1 << 16
+    int* cnt[2];
+    int* seq[2];
+    int* key[2];
+    int* qc;        // 4 per node: keys per quadrant
+    int* qk;        // 4 per node: a key of the quadrant, then the child's new list position
+    int* aux;       // per node: scan offsets / kept position / processed flag
+    int* aux2;
+    unsigned long long* s64;  // sort keys (phase 2) / best response (final)
+    int* tmp;
+    int* scal;      // scalars
+};
+
+__device__ __forceinline__ int quadrant(int box, int boy, int x, int y) {
+    const int x0 = box & 0xffff, x1 = box >> 16, y0 = boy & 0xffff, y1 = boy >> 16;
+    const int hx = (x1 - x0 + 1) >> 1, hy = (y1 - y0 + 1) >> 1;  // ceil((UR.x-UL.x)/2.f)
+    const bool left = x < x0 + hx, top = y < y0 + hy;
+    return left ? (top ? 0 : 2) : (top ? 1 : 3);
+}
+
+__device__ __forceinline__ void child_box(int box, int boy, int q, int& cbx, int& cby) {
+    const int x0 = box & 0xffff, x1 = box >> 16, y0 = boy & 0xffff, y1 = boy >> 16;
+    const int xm = x0 + ((x1 - x0 + 1) >> 1), ym = y0 + ((y1 - y0 + 1) >> 1);
+    const int cx0 = (q & 1) ? xm : x0, cx1 = (q & 1) ? x1 : xm;
+    const int cy0 = (q & 2) ? ym : y0, cy1 = (q & 2) ? y1 : ym;
+    cbx = cx0 | (cx1 << 16);
+    cby = cy0 | (cy1 << 16);
+}
+
+__global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    const int level = blockIdx.x, f = blockIdx.y;
+    const LevelGeo& L = a.geo.lv[level];
+    const int NC = a.ncap_max;
+    const int tid = threadIdx.x;
+    OctLds s;
+    {
+        int* p = reinterpret_cast<int*>(lds_raw);
+        s.s64 = reinterpret_cast<unsigned long long*>(p);
+        p += 2 * a.sort_cap;
+        for (int b = 0; b < 2; ++b) {
+            s.box[b] = p; p += NC;
+            s.boy[b] = p; p += NC;
+            s.cnt[b] = p; p += NC;
+            s.seq[b] = p; p += NC;
+            s.key[b] = p; p += NC;
+        }
+        s.qc = p; p += 4 * NC;
+        s.qk = p; p += 4 * NC;
+        s.aux = p; p += NC;
+        s.aux2 = p; p += NC;
+        s.tmp = p; p += 64;
+        s.scal = p;
+    }
+    uint32_t* out = a.oct_out + f * a.geo.out_total + L.out_off;
+    int* out_cnt = a.oct_cnt + f * a.geo.nlevels + level;
+    const int ncap = L.ncap;
+    const int N = L.nfeat;
+
+    // ---- 1. compact this level's cell outputs into original key order
+    uint32_t* K = a.keys + f * a.geo.key_total + L.key_off;
+    int nkeys = 0;
+    for (int base = L.cell_begin; base < L.cell_end; base += kOctBlock) {
+        const int c = base + tid;
+        const int n = c < L.cell_end ? a.cell_cnt[f * a.ncells + c] : 0;
+        int chunk_total;
+        const int off = block_exclusive_scan<kOctBlock>(n, s.tmp, chunk_total);
+        if (n) {
+            const uint32_t* src = a.cell_keys + f * a.cell_cap_total + a.cells[c].slot;
+            for (int i = 0; i < n; ++i) K[nkeys + off + i] = src[i];
+        }
+        nkeys += chunk_total;
+    }
+    __syncthreads();
+    if (nkeys == 0 || L.nini < 1) {
+        if (tid == 0) *out_cnt = 0;
+        return;
+    }
+
+    int2* act[2] = {a.act + f * a.geo.key_total * 2 + L.key_off * 2,
+                    a.act + f * a.geo.key_total * 2 + L.key_off * 2 + L.key_cap};
+    int* nact_sh = s.scal;        // scal[0..1]: active counters
+    int* flag_sh = s.scal + 2;    // scal[2]: overflow / misc
+    int* rmin_sh = s.scal + 3;    // scal[3]: phase-2 cut index
+
+    // ---- 2. initial nodes (542-584)
+    const int nini = L.nini;
+    const float hX = L.hx;
+    const int H = L.bh;
+    for (int i = tid; i < nini; i += kOctBlock) {
+        s.qc[i] = 0;
+        s.qk[i] = -1;
+    }
+    if (tid == 0) { nact_sh[0] = 0; nact_sh[1] = 0; flag_sh[0] = 0; }
+    __syncthreads();
+    for (int k = tid; k < nkeys; k += kOctBlock) {
+        const uint32_t kk = K[k];
+        const int x = key_x(kk);
+        const int node = min((int)((float)x / hX), nini - 1);  // vpIniNodes[kp.pt.x/hX] (568)
+        atomicAdd(&s.qc[node], 1);
+        s.qk[node] = k;
+    }
+    __syncthreads();
+    int size;
+    {   // list = non-empty initial nodes in index order; single-key nodes are closed
+        int total = 0;
+        for (int base = 0; base < nini; base += kOctBlock) {
+            const int i = base + tid;
+            const int ne = i < nini && s.qc[i] > 0;
+            int chunk_total;
+            const int off = block_exclusive_scan<kOctBlock>(ne, s.tmp, chunk_total);
+            if (ne) {
+                const int pos = total + off;
+                const int x0 = (int)(hX * (float)i), x1 = (int)(hX * (float)(i + 1));
+                s.box[0][pos] = x0 | (x1 << 16);
+                s.boy[0][pos] = 0 | (H << 16);
+                s.cnt[0][pos] = s.qc[i];
+                s.seq[0][pos] = i;
+                s.key[0][pos] = s.qc[i] == 1 ? s.qk[i] : -1;
+                s.aux[i] = pos;
+            }
+            total += chunk_total;
+        }
+        size = total;
+    }
+    __syncthreads();
+    for (int k = tid; k < nkeys; k += kOctBlock) {
+        const int x = key_x(K[k]);
+        const int node = s.aux[min((int)((float)x / hX), nini - 1)];
+        if (s.cnt[0][node] >= 2) act[0][atomicAdd(&nact_sh[0], 1)] = make_int2(k, node);
+    }
+    __syncthreads();
+    int cur = 0;
+    int nact = nact_sh[0];
+    int seq_base = nini;
+    bool finished = false;
+    bool phase2 = false;
+    __syncthreads();
+
+    // ---- 3. phase 1: split every open node per pass (593-671)
+    for (int pass = 0; pass < 64 && !finished && !phase2; ++pass) {
+        const int prev = size;
+        const int nxt = cur ^ 1;
+        for (int i = tid; i < 4 * size; i += kOctBlock) s.qc[i] = 0;
+        if (tid == 0) nact_sh[nxt] = 0;
+        __syncthreads();
+        for (int e = tid; e < nact; e += kOctBlock) {
+            const int2 en = act[cur][e];
+            const uint32_t kk = K[en.x];
+            const int q = quadrant(s.box[cur][en.y], s.boy[cur][en.y], key_x(kk), key_y(kk));
+            atomicAdd(&s.qc[en.y * 4 + q], 1);
+            s.qk[en.y * 4 + q] = en.x;
+        }
+        __syncthreads();
+        // per node: children (divided) or kept (single); aux = child offset, aux2 = kept offset
+        int csize = 0, ksize = 0, nexp = 0;
+        for (int base = 0; base < size; base += kOctBlock) {
+            const int i = base + tid;
+            int nch = 0, keep = 0, ne = 0;
+            if (i < size) {
+                if (s.cnt[cur][i] >= 2) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int qn = s.qc[i * 4 + q];
+                        nch += qn > 0;
+                        ne += qn > 1;
+                    }
+                } else {
+                    keep = 1;
+                }
+            }
+            int t1, t2;
+            const int o1 = block_exclusive_scan<kOctBlock>(nch, s.tmp, t1);
+            const int o2 = block_exclusive_scan<kOctBlock>(keep, s.tmp, t2);
+            const int te = block_sum<kOctBlock>(ne, s.tmp);
+            if (i < size) {
+                s.aux[i] = csize + o1;
+                s.aux2[i] = ksize + o2;
+            }
+            csize += t1;
+            ksize += t2;
+            nexp += te;
+        }
+        const int nsize = csize + ksize;
+        if (nsize > ncap) {  // cannot happen for ncap >= max(N + 3, 4 * nIni)
+            if (tid == 0) *out_cnt = -1;
+            return;
+        }
+        __syncthreads();
+        for (int i = tid; i < size; i += kOctBlock) {
+            if (s.cnt[cur][i] >= 2) {
+                int cp = s.aux[i];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int qn = s.qc[i * 4 + q];
+                    if (!qn) continue;
+                    const int np = csize - 1 - cp;
+                    int cbx, cby;
+                    child_box(s.box[cur][i], s.boy[cur][i], q, cbx, cby);
+                    s.box[nxt][np] = cbx;
+                    s.boy[nxt][np] = cby;
+                    s.cnt[nxt][np] = qn;
+                    s.seq[nxt][np] = seq_base + cp;
+                    s.key[nxt][np] = qn == 1 ? s.qk[i * 4 + q] : -1;
+                    s.qk[i * 4 + q] = np;
+                    ++cp;
+                }
+            } else {
+                const int np = csize + s.aux2[i];
+                s.box[nxt][np] = s.box[cur][i];
+                s.boy[nxt][np] = s.boy[cur][i];
+                s.cnt[nxt][np] = s.cnt[cur][i];
+                s.seq[nxt][np] = s.seq[cur][i];
+                s.key[nxt][np] = s.key[cur][i];
+            }
+        }
+        __syncthreads();
+        for (int e = tid; e < nact; e += kOctBlock) {
+            const int2 en = act[cur][e];
+            const uint32_t kk = K[en.x];
+            const int q = quadrant(s.box[cur][en.y], s.boy[cur][en.y], key_x(kk), key_y(kk));
+            const int np = s.qk[en.y * 4 + q];
+            if (s.cnt[nxt][np] >= 2) act[nxt][atomicAdd(&nact_sh[nxt], 1)] = make_int2(en.x, np);
+        }
+        __syncthreads();
+        nact = nact_sh[nxt];
+        cur = nxt;
+        size = nsize;
+        seq_base += csize;
+        if (size >= N || size == prev) finished = true;
+        else if (size + nexp * 3 > N) phase2 = true;
+        __syncthreads();
+    }
+
+    // ---- 4. phase 2: divide the biggest nodes first until the budget is reached (675-736)
+    for (int round = 0; round < 64 && !finished; ++round) {
+        const int prev = size;
+        const int nxt = cur ^ 1;
+        // expandable nodes -> sort keys (size desc, seq desc); carries the list position
+        if (tid == 0) { flag_sh[0] = 0; nact_sh[nxt] = 0; *rmin_sh = 0x7fffffff; }
+        for (int i = tid; i < 4 * size; i += kOctBlock) s.qc[i] = 0;
+        __syncthreads();
+        for (int i = tid; i < size; i += kOctBlock)
+            if (s.cnt[cur][i] >= 2) {
+                const int slot = atomicAdd(&flag_sh[0], 1);
+                s.s64[slot] = ((unsigned long long)s.cnt[cur][i] << 40) |
+                              ((unsigned long long)(unsigned)s.seq[cur][i] << 14) | (unsigned)i;
+            }
+        __syncthreads();
+        const int m = flag_sh[0];
+        int P = 1;
+        while (P < m) P <<= 1;
+        for (int i = m + tid; i < P; i += kOctBlock) s.s64[i] = 0ull;
+        __syncthreads();
+        for (int k = 2; k <= P; k <<= 1)  // bitonic sort, descending
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = tid; i < P; i += kOctBlock) {
+                    const int ij = i ^ j;
+                    if (ij > i) {
+                        const unsigned long long x = s.s64[i], y = s.s64[ij];
+                        const bool desc = (i & k) == 0;
+                        if (desc ? (x < y) : (x > y)) { s.s64[i] = y; s.s64[ij] = x; }
+                    }
+                }
+                __syncthreads();
+            }
+        for (int e = tid; e < nact; e += kOctBlock) {
+            const int2 en = act[cur][e];
+            const uint32_t kk = K[en.x];
+            const int q = quadrant(s.box[cur][en.y], s.boy[cur][en.y], key_x(kk), key_y(kk));
+            atomicAdd(&s.qc[en.y * 4 + q], 1);
+            s.qk[en.y * 4 + q] = en.x;
+        }
+        __syncthreads();
+        // cut: first j in sorted order with size + sum_{<=j}(nch-1) >= N (else all m)
+        {
+            int run = 0;
+            for (int base = 0; base < m; base += kOctBlock) {
+                const int j = base + tid;
+                int delta = 0;
+                if (j < m) {
+                    const int i = (int)(s.s64[j] & 0x3fff);
+                    for (int q = 0; q < 4; ++q) delta += s.qc[i * 4 + q] > 0;
+                    delta -= 1;
+                }
+                int t;
+                const int ex = block_exclusive_scan<kOctBlock>(delta, s.tmp, t);
+                if (j < m && size + run + ex + delta >= N) atomicMin(rmin_sh, j);
+                run += t;
+            }
+            __syncthreads();
+        }
+        const int r = min(*rmin_sh, m - 1);
+        // processed flags + children offsets (processing order), kept offsets (list order)
+        for (int i = tid; i < size; i += kOctBlock) s.aux2[i] = 0;
+        __syncthreads();
+        int csize = 0;
+        for (int base = 0; base <= r; base += kOctBlock) {
+            const int j = base + tid;
+            int nch = 0, i = -1;
+            if (j <= r) {
+                i = (int)(s.s64[j] & 0x3fff);
+                for (int q = 0; q < 4; ++q) nch += s.qc[i * 4 + q] > 0;
+            }
+            int t;
+            const int o = block_exclusive_scan<kOctBlock>(nch, s.tmp, t);
+            if (j <= r) {
+                s.aux[i] = csize + o;
+                s.aux2[i] = 1;
+            }
+            csize += t;
+        }
+        __syncthreads();
+        int ksize = 0;
+        for (int base = 0; base < size; base += kOctBlock) {
+            const int i = base + tid;
+            const int keep = i < size && !s.aux2[i];
+            int t;
+            const int o = block_exclusive_scan<kOctBlock>(keep, s.tmp, t);
+            if (keep) s.aux2[i] = -(1 + ksize + o);  // kept: encoded new offset
+            ksize += t;
+        }
+        const int nsize = csize + ksize;
+        if (nsize > ncap) {
+            if (tid == 0) *out_cnt = -1;
+            return;
+        }
+        __syncthreads();
+        for (int i = tid; i < size; i += kOctBlock) {
+            if (s.aux2[i] > 0) {  // processed: children
+                int cp = s.aux[i];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int qn = s.qc[i * 4 + q];
+                    if (!qn) continue;
+                    const int np = csize - 1 - cp;
+                    int cbx, cby;
+                    child_box(s.box[cur][i], s.boy[cur][i], q, cbx, cby);
+                    s.box[nxt][np] = cbx;
+                    s.boy[nxt][np] = cby;
+                    s.cnt[nxt][np] = qn;
+                    s.seq[nxt][np] = seq_base + cp;
+                    s.key[nxt][np] = qn == 1 ? s.qk[i * 4 + q] : -1;
+                    s.qk[i * 4 + q] = np;
+                    ++cp;
+                }
+            } else {
+                const int np = csize + (-s.aux2[i] - 1);
+                s.box[nxt][np] = s.box[cur][i];
+                s.boy[nxt][np] = s.boy[cur][i];
+                s.cnt[nxt][np] = s.cnt[cur][i];
+                s.seq[nxt][np] = s.seq[cur][i];
+                s.key[nxt][np] = s.key[cur][i];
+                s.aux[i] = np;
+            }
+        }
+        __syncthreads();
+        for (int e = tid; e < nact; e += kOctBlock) {
+            const int2 en = act[cur][e];
+            int np;
+            if (s.aux2[en.y] > 0) {
+                const uint32_t kk = K[en.x];
+                const int q = quadrant(s.box[cur][en.y], s.boy[cur][en.y], key_x(kk), key_y(kk));
+                np = s.qk[en.y * 4 + q];
+            } else {
+                np = s.aux[en.y];
+            }
+            if (s.cnt[nxt][np] >= 2) act[nxt][atomicAdd(&nact_sh[nxt], 1)] = make_int2(en.x, np);
+        }
+        __syncthreads();
+        nact = nact_sh[nxt];
+        cur = nxt;
+        size = nsize;
+        seq_base += csize;
+        if (size >= N || size == prev) finished = true;
+        __syncthreads();
+    }
+
+    // ---- 5. retain the best key per node (740-759), emit in list order
+    for (int i = tid; i < size; i += kOctBlock) s.s64[i] = 0ull;
+    __syncthreads();
+    for (int e = tid; e < nact; e += kOctBlock) {
+        const int2 en = act[cur][e];
+        const uint32_t kk = K[en.x];
+        const unsigned long long v =
+            ((unsigned long long)key_score(kk) << 32) | (0xffffffffu - (unsigned)en.x);
+        atomicMax(&s.s64[en.y], v);
+    }
+    __syncthreads();
+    for (int i = tid; i < size; i += kOctBlock) {
+        const int k = s.cnt[cur][i] == 1 ? s.key[cur][i]
+                                          : (int)(0xffffffffu - (unsigned)(s.s64[i] & 0xffffffffu));
+        const uint32_t kk = K[k];
+        out[i] = pack_key(key_x(kk) + kMinBorder, key_y(kk) + kMinBorder, key_score(kk));
+    }
+    if (tid == 0) *out_cnt = size;
+}
+
+// ---------------------------------------------------------------------------------------------
+// K4 — GaussianBlur(7x7, sigma 2, REFLECT_101) integer path: row pass R = sum k_i I, column
+// pass (sum k_j R + 2^15) >> 16 saturated (App. A.2).  64 x 16 output tile per workgroup.
+constexpr int kBlurTW = 64, kBlurTH = 16;
+__global__ __launch_bounds__(256) void blur_kernel(BlurArgs a) {
+    __shared__ uint8_t in[(kBlurTH + 6) * (kBlurTW + 8)];
+    __shared__ int rowp[(kBlurTH + 6) * kBlurTW];
+    const int f = blockIdx.y;
+    int t = blockIdx.x, l = 0;
+    while (l + 1 < a.nlevels && t >= a.tile_begin[l + 1]) ++l;
+    t -= a.tile_begin[l];
+    const int w = a.w[l], h = a.h[l];
+    const int tx = (w + kBlurTW - 1) / kBlurTW;
+    const int ox = (t % tx) * kBlurTW, oy = (t / tx) * kBlurTH;
+    const LevelPtr sp = a.src[l];
+    const uint8_t* src = sp.base + f * sp.fpitch;
+    constexpr int IW = kBlurTW + 6, IH = kBlurTH + 6;
+    for (int i = threadIdx.x; i < IW * IH; i += 256) {
+        const int r = i / IW, c = i - r * IW;
+        int yy = oy + r - 3, xx = ox + c - 3;
+        yy = yy < 0 ? -yy : (yy >= h ? 2 * h - yy - 2 : yy);  // reflect-101 (h, w >= 4)
+        xx = xx < 0 ? -xx : (xx >= w ? 2 * w - xx - 2 : xx);
+        yy = min(max(yy, 0), h - 1);
+        xx = min(max(xx, 0), w - 1);
+        in[r * (kBlurTW + 8) + c] = src[(long long)yy * sp.pitch + xx];
+    }
+    __syncthreads();
+    const int k0 = a.taps[0], k1 = a.taps[1], k2 = a.taps[2], k3 = a.taps[3];
+    for (int i = threadIdx.x; i < IH * kBlurTW; i += 256) {
+        const int r = i / kBlurTW, c = i - r * kBlurTW;
+        const uint8_t* p = in + r * (kBlurTW + 8) + c;
+        rowp[i] = k0 * (p[0] + p[6]) + k1 * (p[1] + p[5]) + k2 * (p[2] + p[4]) + k3 * p[3];
+    }
+    __syncthreads();
+    const LevelPtr dp = a.dst[l];
+    uint8_t* dst = const_cast<uint8_t*>(dp.base) + f * dp.fpitch;
+    for (int i = threadIdx.x; i < kBlurTH * kBlurTW; i += 256) {
+        const int r = i / kBlurTW, c = i - r * kBlurTW;
+        const int y = oy + r, x = ox + c;
+        if (y >= h || x >= w) continue;
+        const int* p = rowp + r * kBlurTW + c;
+        const int acc = k0 * (p[0] + p[6 * kBlurTW]) + k1 * (p[kBlurTW] + p[5 * kBlurTW]) +
+                        k2 * (p[2 * kBlurTW] + p[4 * kBlurTW]) + k3 * p[3 * kBlurTW];
+        dst[(long long)y * dp.pitch + x] = (uint8_t)min(max((acc + (1 << 15)) >> 16, 0), 255);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K5 — one wave per keypoint: IC angle on the unblurred level, rBRIEF on the blurred level,
+// output keypoint scaled to level 0 (1098-1104).
+constexpr int kDescBlock = 256;
+__global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
+    const int f = blockIdx.y;
+    const int lane = threadIdx.x & 63;
+    const int slot = blockIdx.x * (kDescBlock / 64) + (threadIdx.x >> 6);
+    const int* cnt = a.oct_cnt + f * a.nlevels;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        int n = 0;
+        for (int l = 0; l < a.nlevels; ++l) n += max(cnt[l], 0);
+        a.n_out[f] = min(n, a.kps_cap);
+    }
+    if (slot >= a.out_total) return;
+    int l = 0;
+    while (l + 1 < a.nlevels && slot >= a.out_off[l + 1]) ++l;
+    const int idx = slot - a.out_off[l];
+    if (idx >= cnt[l]) return;
+    int o = idx;
+    for (int q = 0; q < l; ++q) o += max(cnt[q], 0);
+    if (o >= a.kps_cap) return;
+    const uint32_t kk = a.oct_out[f * a.out_total + slot];
+    const int x = key_x(kk), y = key_y(kk), score = key_score(kk);
+
+    // IC angle: lane handles column u = (lane & 31) - 15, rows v <= 0 (half 0) or v > 0.
+    const LevelPtr pp = a.pyr[l];
+    const uint8_t* img = pp.base + f * pp.fpitch + (long long)y * pp.pitch + x;
+    const int u = (lane & 31) - 15;
+    const int half = lane >> 5;
+    int m10 = 0, m01 = 0;
+    if ((lane & 31) < 31) {
+        for (int vv = 0; vv < 16; ++vv) {
+            const int v = half ? vv + 1 : -vv;
+            if (half && vv == 15) break;
+            const int av = v < 0 ? -v : v;
+            if (u < -c_umax[av] || u > c_umax[av]) continue;
+            const int val = img[(long long)v * pp.pitch + u];
+            m10 += u * val;
+            m01 += v * val;
+        }
+    }
+    m10 = wave_sum(m10);
+    m01 = wave_sum(m01);
+    const float angle = fast_atan2((float)m01, (float)m10);
+
+    // rBRIEF: lane handles pairs lane + 64 r; bit k of byte i = pair 8 i + k (122-143)
+    const float ang = angle * (float)(3.14159265358979323846 / 180.f);
+    const float ca = (float)cos((double)ang), sb = (float)sin((double)ang);
+    const LevelPtr bp = a.blur[l];
+    const uint8_t* c = bp.base + f * bp.fpitch + (long long)y * bp.pitch + x;
+    const long long st = bp.pitch;
+    unsigned long long words[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int pair = lane + 64 * r;
+        const float px0 = (float)c_pattern[4 * pair], py0 = (float)c_pattern[4 * pair + 1];
+        const float px1 = (float)c_pattern[4 * pair + 2], py1 = (float)c_pattern[4 * pair + 3];
+        const int i0 = c[rne(px0 * sb + py0 * ca) * st + rne(px0 * ca - py0 * sb)];
+        const int i1 = c[rne(px1 * sb + py1 * ca) * st + rne(px1 * ca - py1 * sb)];
+        words[r] = __ballot(i0 < i1);
+    }
+    const long long outi = (long long)f * a.kps_cap + o;
+    if (lane < 4) {
+        unsigned long long wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
+        reinterpret_cast<unsigned long long*>(a.desc + outi * 32)[lane] = wv;
+    }
+    if (lane == 0) {
+        orbfe_keypoint kp;
+        const float sc = a.scale[l];
+        kp.x = l ? (float)x * sc : (float)x;
+        kp.y = l ? (float)y * sc : (float)y;
+        kp.size = a.size[l];
+        kp.angle = angle;
+        kp.response = (float)score;
+        kp.octave = l;
+        kp.class_id = -1;
+        a.kps[outi] = kp;
+    }
+}
+
+// =============================================================================================
+// host side
+
+namespace {
+inline int cv_round_f(float v) { return (int)std::lrintf(v); }
+inline short sat_short(float v) {
+    int iv = cv_round_f(v);
+    return (short)std::min(std::max(iv, -32768), 32767);
+}
+}  // namespace
+
+int make_tables(const orbfe_params& p, HostTables& t) {
+    if (p.nlevels < 1 || p.nlevels > kMaxLevels || p.nfeatures < 0 || !(p.scale_factor > 1.0f))
+        return ORBFE_ERR_ARG;
+    t.p = p;
+    const double sd = (double)p.scale_factor;
+    t.scale[0] = 1.0f;
+    t.sigma2[0] = 1.0f;
+    for (int i = 1; i < p.nlevels; ++i) {  // ORBextractor.cc:414-430
+        t.scale[i] = (float)((double)t.scale[i - 1] * sd);
+        t.sigma2[i] = t.scale[i] * t.scale[i];
+    }
+    for (int i = 0; i < p.nlevels; ++i) {
+        t.inv[i] = 1.0f / t.scale[i];
+        t.inv_sigma2[i] = 1.0f / t.sigma2[i];
+    }
+    const float factor = (float)(1.0 / sd);  // 434-445
+    float per = (float)p.nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)p.nlevels));
+    int sum = 0;
+    for (int l = 0; l < p.nlevels - 1; ++l) {
+        t.nfeat[l] = cv_round_f(per);
+        sum += t.nfeat[l];
+        per *= factor;
+    }
+    t.nfeat[p.nlevels - 1] = std::max(p.nfeatures - sum, 0);
+    const int vmax = (int)std::floor(15 * std::sqrt(2.f) / 2 + 1);  // 453-468
+    const int vmin = (int)std::ceil(15 * std::sqrt(2.f) / 2);
+    for (int v = 0; v <= vmax; ++v) t.umax[v] = (int)std::lrint(std::sqrt(225.0 - v * v));
+    for (int v = 15, v0 = 0; v >= vmin; --v) {
+        while (t.umax[v0] == t.umax[v0 + 1]) ++v0;
+        t.umax[v] = v0;
+        ++v0;
+    }
+    // getGaussianKernel(7, 2, CV_32F) * 256 rounded (App. A.2)
+    float g[7];
+    double gs = 0;
+    for (int i = 0; i < 7; ++i) {
+        const double x = i - 3.0;
+        g[i] = (float)std::exp(-0.125 * x * x);
+        gs += g[i];
+    }
+    gs = 1. / gs;
+    for (int i = 0; i < 7; ++i) g[i] = (float)(g[i] * gs);
+    for (int i = 0; i < 7; ++i) t.taps[i] = cv_round_f(g[i] * 256.f + 0.f);
+    return ORBFE_OK;
+}
+
+// Plans every size-dependent table for a w x h input (cached per extractor).
+int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
+    const int L = t.p.nlevels;
+    g.w = w;
+    g.h = h;
+    g.geo.nlevels = L;
+    long long slab = 0, keys = 0;
+    int out = 0, ncap_max = 0, tiles = 0;
+    g.cells.clear();
+    g.xtab.clear();
+    g.ytab.clear();
+    for (int l = 0; l < L; ++l) {
+        LevelGeo& lv = g.geo.lv[l];
+        lv.w = cv_round_f((float)w * t.inv[l]);
+        lv.h = cv_round_f((float)h * t.inv[l]);
+        if (lv.w < 4 || lv.h < 4) return ORBFE_ERR_UNSUPPORTED;
+        lv.pitch = (lv.w + 63) & ~63;
+        lv.off = slab;
+        slab += (long long)lv.pitch * lv.h;
+        slab = (slab + 255) & ~255ll;
+        lv.scale = t.scale[l];
+        lv.size = (float)(int)(31 * t.scale[l]);  // scaledPatchSize (836)
+        lv.nfeat = t.nfeat[l];
+        // FAST cells (772-806)
+        const int maxbx = lv.w - kEdge + 3, maxby = lv.h - kEdge + 3;
+        const float width = (float)(maxbx - kMinBorder), height = (float)(maxby - kMinBorder);
+        const int ncols = (int)(width / kCellW), nrows = (int)(height / kCellW);
+        lv.cell_begin = (int)g.cells.size();
+        lv.key_off = keys;
+        long long kcap = 0;
+        if (ncols > 0 && nrows > 0) {
+            const int wc = (int)std::ceil(width / ncols), hc = (int)std::ceil(height / nrows);
+            for (int i = 0; i < nrows; ++i) {
+                const int y0 = kMinBorder + i * hc;
+                int y1 = y0 + hc + 6;
+                if (y0 >= maxby - 3) continue;
+                if (y1 > maxby) y1 = maxby;
+                for (int j = 0; j < ncols; ++j) {
+                    const int x0 = kMinBorder + j * wc;
+                    int x1 = x0 + wc + 6;
+                    if (x0 >= maxbx - 6) continue;
+                    if (x1 > maxbx) x1 = maxbx;
+                    CellDesc c;
+                    c.level = l;
+                    c.y0 = y0; c.y1 = y1; c.x0 = x0; c.x1 = x1;
+                    if (y1 - y0 > kRoiMax || x1 - x0 > kRoiMax) return ORBFE_ERR_UNSUPPORTED;
+                    const int dh = std::max(y1 - y0 - 6, 0), dw = std::max(x1 - x0 - 6, 0);
+                    c.cap = ((dh + 1) / 2) * ((dw + 1) / 2);  // strict NMS: <= 1 per 2x2
+                    c.slot = g.cell_cap_total;
+                    g.cell_cap_total += c.cap;
+                    kcap += c.cap;
+                    g.cells.push_back(c);
+                }
+            }
+        }
+        lv.cell_end = (int)g.cells.size();
+        lv.key_cap = (int)kcap;
+        keys += kcap;
+        // oct-tree (538-584)
+        lv.bw = maxbx - kMinBorder;
+        lv.bh = maxby - kMinBorder;
+        if (kcap > 0) {
+            lv.nini = (int)std::round((float)lv.bw / lv.bh);
+            if (lv.nini < 1) return ORBFE_ERR_UNSUPPORTED;  // reference UB
+            lv.hx = (float)lv.bw / lv.nini;
+        } else {
+            lv.nini = 0;
+            lv.hx = 1.f;
+        }
+        // list bound: phase 1 <= max(N, 4 nIni), phase 2 <= N + 2 (DESIGN.md "oct-tree")
+        if (lv.nini > 4) return ORBFE_ERR_UNSUPPORTED;
+        lv.ncap = std::max(lv.nfeat + 4, 20);
+        lv.out_off = out;
+        out += lv.ncap;
+        ncap_max = std::max(ncap_max, lv.ncap);
+        // blur tiles
+        g.tile_begin[l] = tiles;
+        tiles += ((lv.w + kBlurTW - 1) / kBlurTW) * ((lv.h + kBlurTH - 1) / kBlurTH);
+        // resize tables for level l from level l-1 (App. A.1)
+        if (l > 0) {
+            const LevelGeo& sv = g.geo.lv[l - 1];
+            const int sw = sv.w, sh = sv.h, dw = lv.w, dh = lv.h;
+            const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
+            g.xoff[l] = (int)g.xtab.size();
+            for (int dx = 0; dx < dw; ++dx) {
+                float fx = (float)((dx + 0.5) * scale_x - 0.5);
+                int sx = (int)std::floor(fx);
+                fx -= sx;
+                if (sx < 0) { fx = 0; sx = 0; }
+                if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+                const int a0 = sat_short((1.f - fx) * 2048), a1 = sat_short(fx * 2048);
+                g.xtab.push_back(sx);
+                g.xtab.push_back(std::min(sx + 1, sw - 1));
+                g.xtab.push_back((a0 & 0xffff) | (a1 << 16));
+            }
+            g.yoff[l] = (int)g.ytab.size();
+            for (int dy = 0; dy < dh; ++dy) {
+                float fy = (float)((dy + 0.5) * scale_y - 0.5);
+                int sy = (int)std::floor(fy);
+                fy -= sy;
+                const int b0 = sat_short((1.f - fy) * 2048), b1 = sat_short(fy * 2048);
+                g.ytab.push_back(std::min(std::max(sy, 0), sh - 1));
+                g.ytab.push_back(std::min(std::max(sy + 1, 0), sh - 1));
+                g.ytab.push_back((b0 & 0xffff) | (b1 << 16));
+            }
+        }
+    }
+    if (w > 4096 || h > 4096) return ORBFE_ERR_UNSUPPORTED;
+    g.geo.key_total = keys;
+    g.geo.out_total = out;
+    g.slab = slab;
+    g.ncap_max = ncap_max;
+    g.tiles_total = tiles;
+    int sort_cap = 1;
+    while (sort_cap < ncap_max) sort_cap <<= 1;
+    g.sort_cap = sort_cap;
+    g.oct_lds = (size_t)2 * sort_cap * 4 + (size_t)ncap_max * 4 * (10 + 8 + 2) + 64 * 4 + 64;
+    return ORBFE_OK;
+}
+
+}  // namespace orbfe

@@ -1,0 +1,146 @@
+// orbfe_internal.hpp — structs shared by the extractor kernels and their host orchestration.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "../../include/orbfe.h"
+
+namespace orbfe {
+
+constexpr int kMaxLevels = 16;
+
+// FAST candidate / oct-tree key: x, y (12 bits each; level coords or coords relative to
+// (16,16)) and the FAST score (8 bits).  Images are limited to 4096 x 4096.
+__host__ __device__ __forceinline__ uint32_t pack_key(int x, int y, int s) {
+    return ((uint32_t)y << 20) | ((uint32_t)x << 8) | (uint32_t)s;
+}
+__host__ __device__ __forceinline__ int key_x(uint32_t k) { return (int)((k >> 8) & 0xfff); }
+__host__ __device__ __forceinline__ int key_y(uint32_t k) { return (int)(k >> 20); }
+__host__ __device__ __forceinline__ int key_score(uint32_t k) { return (int)(k & 0xff); }
+
+struct LevelGeo {
+    int w, h, pitch;       // level size; row pitch inside the pyramid / blur slabs
+    long long off;         // byte offset of the level inside a frame's slab
+    int cell_begin, cell_end;
+    int key_cap;           // sum of the level's cell capacities
+    long long key_off;     // offset (keys) of the level inside a frame's key region
+    int nfeat;             // mnFeaturesPerLevel[level]
+    int nini;              // initial oct-tree nodes round(bw / bh) (542)
+    float hx;              // (maxX - minX) / nIni (544)
+    int bw, bh;            // maxBorderX - minBorderX, maxBorderY - minBorderY
+    int ncap;              // oct-tree list capacity max(N + 4, 4 nIni + 4)
+    int out_off;           // offset of the level inside a frame's oct-tree output
+    float scale, size;     // mvScaleFactor[level], (int)(31 * scale)
+};
+
+struct Geo {
+    int nlevels;
+    long long key_total;   // keys per frame (all levels)
+    int out_total;         // oct-tree output slots per frame (all levels)
+    LevelGeo lv[kMaxLevels];
+};
+
+struct CellDesc {
+    int level;
+    int y0, y1, x0, x1;    // FAST ROI rows [y0,y1) cols [x0,x1) in level coords
+    int cap;               // max keys the cell can emit
+    long long slot;        // offset of the cell's keys inside a frame's cell-key region
+};
+
+struct LevelPtr {
+    const uint8_t* base;   // frame 0, level origin
+    long long fpitch;      // bytes between frames
+    int pitch;             // bytes between rows
+};
+
+struct FastArgs {
+    const CellDesc* cells;
+    int ncells;
+    long long cell_cap_total;
+    int ini_th, min_th;
+    int* cell_cnt;         // [frame][cell]
+    uint32_t* cell_keys;   // [frame][cell_cap_total]
+    LevelPtr pyr[kMaxLevels];
+};
+
+struct OctArgs {
+    Geo geo;
+    const CellDesc* cells;
+    int ncells;
+    long long cell_cap_total;
+    const int* cell_cnt;
+    const uint32_t* cell_keys;
+    uint32_t* keys;        // [frame][key_total] compacted per level
+    int2* act;             // [frame][2 * key_total] live keys (key index, node)
+    uint32_t* oct_out;     // [frame][out_total]
+    int* oct_cnt;          // [frame][nlevels]
+    int ncap_max, sort_cap;
+};
+
+struct BlurArgs {
+    int nlevels;
+    int tile_begin[kMaxLevels];
+    int w[kMaxLevels], h[kMaxLevels];
+    int taps[4];
+    LevelPtr src[kMaxLevels];
+    LevelPtr dst[kMaxLevels];
+};
+
+struct DescArgs {
+    int nlevels, out_total, kps_cap;
+    int out_off[kMaxLevels];
+    float scale[kMaxLevels], size[kMaxLevels];
+    LevelPtr pyr[kMaxLevels];
+    LevelPtr blur[kMaxLevels];
+    const uint32_t* oct_out;
+    const int* oct_cnt;
+    orbfe_keypoint* kps;
+    uint8_t* desc;
+    int32_t* n_out;
+};
+
+// Host-side ctor tables (ORBextractor.cc:409-469) + blur taps.
+struct HostTables {
+    orbfe_params p;
+    float scale[kMaxLevels], inv[kMaxLevels], sigma2[kMaxLevels], inv_sigma2[kMaxLevels];
+    int nfeat[kMaxLevels];
+    int umax[16];
+    int taps[7];
+};
+
+// Everything that depends on the input size.
+struct Plan {
+    int w = 0, h = 0;
+    Geo geo{};
+    std::vector<CellDesc> cells;
+    long long cell_cap_total = 0;
+    std::vector<int> xtab, ytab;
+    int xoff[kMaxLevels] = {}, yoff[kMaxLevels] = {};
+    long long slab = 0;
+    int ncap_max = 0, sort_cap = 0, tiles_total = 0;
+    int tile_begin[kMaxLevels] = {};
+    size_t oct_lds = 0;
+};
+
+int make_tables(const orbfe_params& p, HostTables& t);
+int plan_geometry(const HostTables& t, int w, int h, Plan& g);
+
+// kernels (orbfe_extract.hip)
+__global__ void mask_kernel(const uint8_t*, long long, int, const uint8_t*, long long, int,
+                            uint8_t*, long long, int, int, int);
+__global__ void resize_kernel(const uint8_t*, long long, int, uint8_t*, long long, int, int, int,
+                              const int*, const int*);
+__global__ void fast_kernel(FastArgs);
+__global__ void octree_kernel(OctArgs);
+__global__ void blur_kernel(BlurArgs);
+__global__ void describe_kernel(DescArgs);
+extern __constant__ int c_umax[16];
+
+constexpr int kFastBlockSize = 256;
+constexpr int kOctBlockSize = 512;
+constexpr int kDescBlockSize = 256;
+constexpr int kBlurTileW = 64, kBlurTileH = 16;
+
+}  // namespace orbfe

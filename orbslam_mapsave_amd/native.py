@@ -1,0 +1,331 @@
+"""ctypes binding of liborbfe.so (the HIP product library) and the host-side mirror of the
+reference interface for the hot path:
+
+* :class:`ORBextractor` mirrors ``ORB_SLAM2::ORBextractor`` (include/ORBextractor.h:50-119):
+  same ctor arguments, ``__call__(image, mask)`` for ``operator()`` and the six getters;
+* :class:`ORBmatcher` mirrors the hot subset of ``ORB_SLAM2::ORBmatcher``
+  (include/ORBmatcher.h:38-110): ``DescriptorDistance``, ``SearchForInitialization`` and the two
+  tracking ``SearchByProjection`` overloads, plus the brute-force match of config 3.
+
+There is no CPU fallback: importing works anywhere, but constructing an extractor or matcher
+needs the built library and a gfx950 device, and raises otherwise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from .abi import (KEYPOINT_DTYPE, ORBFE_ERR_CAPACITY, ORBFE_OK, Camera, Frame, MapPoints,
+                  OrbfeError, Params, ptr)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "liborbfe.so")
+_lib: C.CDLL | None = None
+
+# every symbol include/orbfe.h declares (checked by tests/test_abi.py)
+EXPORTED = [
+    "orbfe_create", "orbfe_destroy", "orbfe_get_levels", "orbfe_get_scale_factor",
+    "orbfe_get_scale_tables", "orbfe_get_features_per_level", "orbfe_keypoint_capacity",
+    "orbfe_extract", "orbfe_extract_batch", "orbfe_extract_batch_device", "orbfe_set_stream",
+    "orbfe_synchronize", "orbfe_get_level", "orbfe_get_blurred_level", "orbfe_get_fast_keys",
+    "orbfe_matcher_create", "orbfe_matcher_destroy", "orbfe_matcher_set_stream", "orbfe_hamming",
+    "orbfe_bf_match", "orbfe_bf_match_batch_device", "orbfe_search_for_initialization",
+    "orbfe_search_by_projection_local", "orbfe_search_by_projection_last", "orbfe_is_in_frustum",
+]
+
+
+def lib() -> C.CDLL:
+    """Load liborbfe.so; raise loudly if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with "
+                               "`python -c 'import __graft_entry__ as g; g.build()'`")
+        L = C.CDLL(LIB_PATH)
+        L.orbfe_create.restype = C.c_void_p
+        L.orbfe_create.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        L.orbfe_destroy.argtypes = [C.c_void_p]
+        L.orbfe_get_scale_factor.restype = C.c_float
+        for fn in ("orbfe_get_levels", "orbfe_get_scale_factor", "orbfe_keypoint_capacity",
+                   "orbfe_synchronize"):
+            getattr(L, fn).argtypes = [C.c_void_p]
+        L.orbfe_matcher_create.restype = C.c_void_p
+        L.orbfe_matcher_create.argtypes = [C.c_int, C.c_void_p]
+        L.orbfe_matcher_destroy.argtypes = [C.c_void_p]
+        _lib = L
+    return _lib
+
+
+def _check(fn: str, st: int) -> None:
+    if st != ORBFE_OK:
+        raise OrbfeError(fn, st)
+
+
+class ORBextractor:
+    """``ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)`` on a gfx950 GPU
+    (ORBextractor.cc:409-469).  One instance is not reentrant; use one per thread."""
+
+    def __init__(self, nfeatures: int, scaleFactor: float, nlevels: int, iniThFAST: int,
+                 minThFAST: int, device: int = 0, max_width: int = 0, max_height: int = 0,
+                 max_batch: int = 1):
+        self._p = Params(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
+        st = C.c_int(0)
+        h = lib().orbfe_create(C.byref(self._p), device, max_width, max_height, max_batch,
+                               C.byref(st))
+        if not h:
+            raise OrbfeError("orbfe_create", st.value)
+        self._h = C.c_void_p(h)
+        self.nlevels = nlevels
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().orbfe_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- getters (ORBextractor.h:68-88)
+    def GetLevels(self) -> int:
+        return lib().orbfe_get_levels(self._h)
+
+    def GetScaleFactor(self) -> float:
+        return lib().orbfe_get_scale_factor(self._h)
+
+    def _tables(self):
+        t = [np.zeros(self.nlevels, np.float32) for _ in range(4)]
+        _check("orbfe_get_scale_tables", lib().orbfe_get_scale_tables(self._h, *map(ptr, t)))
+        return t
+
+    def GetScaleFactors(self) -> np.ndarray:
+        return self._tables()[0]
+
+    def GetInverseScaleFactors(self) -> np.ndarray:
+        return self._tables()[1]
+
+    def GetScaleSigmaSquares(self) -> np.ndarray:
+        return self._tables()[2]
+
+    def GetInverseScaleSigmaSquares(self) -> np.ndarray:
+        return self._tables()[3]
+
+    def features_per_level(self) -> np.ndarray:
+        out = np.zeros(self.nlevels, np.int32)
+        _check("orbfe_get_features_per_level", lib().orbfe_get_features_per_level(self._h, ptr(out)))
+        return out
+
+    def capacity(self) -> int:
+        return lib().orbfe_keypoint_capacity(self._h)
+
+    # ---- operator() (ORBextractor.cc:1042-1108)
+    def __call__(self, image: np.ndarray, mask: np.ndarray | None = None):
+        """Returns (keypoints[KEYPOINT_DTYPE], descriptors uint8 (n, 32)); an empty image
+        returns (None, None) like the reference, which leaves its outputs untouched."""
+        image = np.ascontiguousarray(image, np.uint8)
+        if image.size == 0:
+            return None, None
+        h, w = image.shape
+        m = None if mask is None or np.size(mask) == 0 else np.ascontiguousarray(mask, np.uint8)
+        cap = self.capacity()
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = C.c_int(0)
+        _check("orbfe_extract", lib().orbfe_extract(
+            self._h, ptr(image), w, h, C.c_size_t(w), ptr(m), C.c_size_t(w), ptr(kps), cap,
+            ptr(desc), C.byref(n)))
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def extract_batch(self, images: np.ndarray, masks: np.ndarray | None = None):
+        """Host batch: (n, h, w) uint8 -> (kps (n, cap), desc (n, cap, 32), counts (n,))."""
+        images = np.ascontiguousarray(images, np.uint8)
+        n, h, w = images.shape
+        cap = self.capacity()
+        kps = np.zeros((n, cap), KEYPOINT_DTYPE)
+        desc = np.zeros((n, cap, 32), np.uint8)
+        cnt = np.zeros(n, np.int32)
+        arr = (C.c_void_p * n)(*[images[i].ctypes.data for i in range(n)])
+        marr = None
+        if masks is not None:
+            masks = np.ascontiguousarray(masks, np.uint8)
+            marr = (C.c_void_p * n)(*[masks[i].ctypes.data for i in range(n)])
+        _check("orbfe_extract_batch", lib().orbfe_extract_batch(
+            self._h, arr, n, w, h, C.c_size_t(w), marr, C.c_size_t(w), ptr(kps), cap, ptr(desc),
+            ptr(cnt)))
+        return kps, desc, cnt
+
+    def extract_batch_device(self, d_imgs: int, n: int, w: int, h: int, stride: int,
+                             frame_pitch: int, d_kps: int, kps_cap: int, d_desc: int,
+                             d_n_out: int, d_masks: int | None = None) -> None:
+        """Device-resident batch (raw device pointers, e.g. torch ``data_ptr()``); async."""
+        _check("orbfe_extract_batch_device", lib().orbfe_extract_batch_device(
+            self._h, C.c_void_p(d_imgs), n, w, h, C.c_size_t(stride), C.c_size_t(frame_pitch),
+            C.c_void_p(d_masks) if d_masks else None, C.c_void_p(d_kps), kps_cap,
+            C.c_void_p(d_desc), C.c_void_p(d_n_out)))
+
+    def set_stream(self, stream_handle: int | None) -> None:
+        _check("orbfe_set_stream", lib().orbfe_set_stream(
+            self._h, C.c_void_p(stream_handle) if stream_handle else None))
+
+    def synchronize(self) -> None:
+        _check("orbfe_synchronize", lib().orbfe_synchronize(self._h))
+
+    # ---- probes of the last extraction
+    def _level(self, fn, frame: int, level: int) -> np.ndarray:
+        w, h = C.c_int(0), C.c_int(0)
+        _check(fn.__name__, fn(self._h, frame, level, None, C.byref(w), C.byref(h)))
+        out = np.zeros((h.value, w.value), np.uint8)
+        _check(fn.__name__, fn(self._h, frame, level, ptr(out), C.byref(w), C.byref(h)))
+        return out
+
+    def get_level(self, level: int, frame: int = 0) -> np.ndarray:
+        """mvImagePyramid[level] of the last extraction (ORBextractor.h:90)."""
+        return self._level(lib().orbfe_get_level, frame, level)
+
+    @property
+    def mvImagePyramid(self) -> list[np.ndarray]:
+        return [self.get_level(l) for l in range(self.nlevels)]
+
+    def get_blurred_level(self, level: int, frame: int = 0) -> np.ndarray:
+        return self._level(lib().orbfe_get_blurred_level, frame, level)
+
+    def get_fast_keys(self, level: int, frame: int = 0) -> np.ndarray:
+        cap = 65536
+        while True:
+            out = np.zeros(cap, KEYPOINT_DTYPE)
+            n = C.c_int(0)
+            st = lib().orbfe_get_fast_keys(self._h, frame, level, ptr(out), cap, C.byref(n))
+            if st == ORBFE_ERR_CAPACITY:
+                cap = n.value
+                continue
+            _check("orbfe_get_fast_keys", st)
+            return out[:n.value].copy()
+
+
+class ORBmatcher:
+    """``ORBmatcher(nnratio=0.6, checkOri=true)`` (ORBmatcher.cc:41-43), GPU-backed."""
+
+    TH_HIGH, TH_LOW, HISTO_LENGTH = 100, 50, 30  # ORBmatcher.cc:37-39
+
+    def __init__(self, nnratio: float = 0.6, checkOri: bool = True, device: int = 0):
+        self.mfNNratio = float(nnratio)
+        self.mbCheckOrientation = bool(checkOri)
+        st = C.c_int(0)
+        h = lib().orbfe_matcher_create(device, C.byref(st))
+        if not h:
+            raise OrbfeError("orbfe_matcher_create", st.value)
+        self._h = C.c_void_p(h)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().orbfe_matcher_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def DescriptorDistance(self, a: np.ndarray, b: np.ndarray) -> np.ndarray | int:
+        """Row-wise Hamming distance (ORBmatcher.cc:1650-1666)."""
+        a2 = np.ascontiguousarray(a, np.uint8).reshape(-1, 32)
+        b2 = np.ascontiguousarray(b, np.uint8).reshape(-1, 32)
+        out = np.zeros(len(a2), np.int32)
+        _check("orbfe_hamming", lib().orbfe_hamming(self._h, ptr(a2), ptr(b2), len(a2), ptr(out)))
+        return int(out[0]) if np.ndim(a) == 1 else out
+
+    def bf_match(self, q: np.ndarray, r: np.ndarray):
+        q = np.ascontiguousarray(q, np.uint8).reshape(-1, 32)
+        r = np.ascontiguousarray(r, np.uint8).reshape(-1, 32)
+        bi, bd, sd = (np.zeros(len(q), np.int32) for _ in range(3))
+        _check("orbfe_bf_match", lib().orbfe_bf_match(self._h, ptr(q), len(q), ptr(r), len(r),
+                                                      ptr(bi), ptr(bd), ptr(sd)))
+        return bi, bd, sd
+
+    def bf_match_batch_device(self, d_q: int, q_pitch: int, d_nq: int, nq_cap: int, d_r: int,
+                              r_pitch: int, d_nr: int, nb: int, d_out: int) -> None:
+        _check("orbfe_bf_match_batch_device", lib().orbfe_bf_match_batch_device(
+            self._h, C.c_void_p(d_q), C.c_size_t(q_pitch), C.c_void_p(d_nq), nq_cap,
+            C.c_void_p(d_r), C.c_size_t(r_pitch), C.c_void_p(d_nr), nb, C.c_void_p(d_out)))
+
+    def set_stream(self, stream_handle: int | None) -> None:
+        _check("orbfe_matcher_set_stream", lib().orbfe_matcher_set_stream(
+            self._h, C.c_void_p(stream_handle) if stream_handle else None))
+
+    def SearchForInitialization(self, F1: Frame, F2: Frame, vbPrevMatched: np.ndarray,
+                                windowSize: int = 10):
+        """Returns (vnMatches12, nmatches, updated vbPrevMatched) (ORBmatcher.cc:408-523)."""
+        prev = np.ascontiguousarray(vbPrevMatched, np.float32).reshape(-1, 2).copy()
+        m12 = np.zeros(F1.n, np.int32)
+        nm = C.c_int32(0)
+        v1, v2 = F1.view(), F2.view()
+        _check("orbfe_search_for_initialization", lib().orbfe_search_for_initialization(
+            self._h, C.c_float(self.mfNNratio), int(self.mbCheckOrientation), C.byref(v1),
+            C.byref(v2), ptr(prev), windowSize, ptr(m12), C.byref(nm)))
+        return m12, nm.value, prev
+
+    def SearchByProjection(self, F: Frame, mps: MapPoints, th: float = 3.0, frame_mp=None,
+                           frame_mp_obs=None, mp_ids=None):
+        """Local-map overload (ORBmatcher.cc:45-129).  Returns (frame_mp, frame_mp_obs,
+        nmatches): the MapPoint id held by each keypoint (-1 = none)."""
+        fmp = (np.full(F.n, -1, np.int32) if frame_mp is None
+               else np.ascontiguousarray(frame_mp, np.int32).copy())
+        fobs = (np.zeros(F.n, np.int32) if frame_mp_obs is None
+                else np.ascontiguousarray(frame_mp_obs, np.int32).copy())
+        ids = None if mp_ids is None else np.ascontiguousarray(mp_ids, np.int32)
+        nm = C.c_int32(0)
+        fv, mv = F.view(), mps.view()
+        _check("orbfe_search_by_projection_local", lib().orbfe_search_by_projection_local(
+            self._h, C.c_float(self.mfNNratio), C.byref(fv), ptr(fmp), ptr(fobs), C.byref(mv),
+            ptr(ids), C.c_float(th), C.byref(nm)))
+        return fmp, fobs, nm.value
+
+    def SearchByProjectionLast(self, cur: Frame, tcw_cur, cam: Camera, last_keys, last_valid,
+                               last_outlier, last_xyz, last_desc, last_nobs, tcw_last,
+                               th: float, bMono: bool, frame_mp=None, frame_mp_obs=None,
+                               last_ids=None):
+        """Last-frame overload (ORBmatcher.cc:1331-1473)."""
+        fmp = (np.full(cur.n, -1, np.int32) if frame_mp is None
+               else np.ascontiguousarray(frame_mp, np.int32).copy())
+        fobs = (np.zeros(cur.n, np.int32) if frame_mp_obs is None
+                else np.ascontiguousarray(frame_mp_obs, np.int32).copy())
+        a = [np.ascontiguousarray(tcw_cur, np.float32).reshape(12),
+             np.ascontiguousarray(last_keys, KEYPOINT_DTYPE),
+             np.ascontiguousarray(last_valid, np.uint8),
+             np.ascontiguousarray(last_outlier, np.uint8),
+             np.ascontiguousarray(last_xyz, np.float32).reshape(-1, 3),
+             np.ascontiguousarray(last_desc, np.uint8).reshape(-1, 32),
+             np.ascontiguousarray(last_nobs, np.int32),
+             np.ascontiguousarray(tcw_last, np.float32).reshape(12)]
+        ids = None if last_ids is None else np.ascontiguousarray(last_ids, np.int32)
+        nm = C.c_int32(0)
+        cv = cur.view()
+        _check("orbfe_search_by_projection_last", lib().orbfe_search_by_projection_last(
+            self._h, int(self.mbCheckOrientation), C.byref(cv), ptr(a[0]), C.byref(cam),
+            ptr(fmp), ptr(fobs), len(a[1]), ptr(a[1]), ptr(a[2]), ptr(a[3]), ptr(a[4]),
+            ptr(a[5]), ptr(a[6]), ptr(ids), ptr(a[7]), C.c_float(th), int(bMono),
+            C.byref(nm)))
+        return fmp, fobs, nm.value
+
+    def is_in_frustum(self, xyz, normal, min_dist, max_dist, tcw, cam: Camera, bounds,
+                      log_scale: float, cos_limit: float = 0.5):
+        """Frame::isInFrustum + MapPoint::PredictScale over all map points (Frame.cc:387)."""
+        xyz = np.ascontiguousarray(xyz, np.float32).reshape(-1, 3)
+        n = len(xyz)
+        normal = np.ascontiguousarray(normal, np.float32).reshape(-1, 3)
+        mn = np.ascontiguousarray(min_dist, np.float32)
+        mx = np.ascontiguousarray(max_dist, np.float32)
+        t = np.ascontiguousarray(tcw, np.float32).reshape(12)
+        inv = np.zeros(n, np.uint8)
+        px, py, pxr, vc = (np.zeros(n, np.float32) for _ in range(4))
+        pl = np.zeros(n, np.int32)
+        _check("orbfe_is_in_frustum", lib().orbfe_is_in_frustum(
+            self._h, n, ptr(xyz), ptr(normal), ptr(mn), ptr(mx), ptr(t), C.byref(cam),
+            *(C.c_float(b) for b in bounds), C.c_float(log_scale), C.c_float(cos_limit),
+            ptr(inv), ptr(px), ptr(py), ptr(pxr), ptr(pl), ptr(vc)))
+        return inv, px, py, pxr, pl, vc

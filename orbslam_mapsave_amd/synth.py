@@ -1,0 +1,107 @@
+"""Seeded synthetic frames for parity tests and the bench (SURVEY.md §8d "Synthetic images").
+
+Textured, not white noise (noise would saturate every FAST cell): multi-octave value noise
+smoothed with a sigma=1.5 Gaussian, 200 filled rectangles/ellipses of random gray and 50
+anti-aliased lines, clipped to u8.  Variants exercise the reference's edge paths:
+``low_contrast`` (x0.15 around mid-gray: the minThFAST fallback, ORBextractor.cc:811-815),
+``constant`` (no corners: the zero-keypoint path, ORBextractor.cc:1067-1068) and a mask with a
+zero rectangle (Mat::copyTo(dst, mask), ORBextractor.cc:1053).
+
+Pure numpy (PCG64), identical here and on the GPU box.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def _gauss1d(sigma: float) -> np.ndarray:
+    r = int(np.ceil(3 * sigma))
+    x = np.arange(-r, r + 1, dtype=np.float64)
+    k = np.exp(-0.5 * (x / sigma) ** 2)
+    return (k / k.sum()).astype(np.float32)
+
+
+def _smooth(img: np.ndarray, sigma: float) -> np.ndarray:
+    k = _gauss1d(sigma)
+    r = len(k) // 2
+    p = np.pad(img, ((0, 0), (r, r)), mode="reflect")
+    out = sum(k[i] * p[:, i:i + img.shape[1]] for i in range(len(k)))
+    p = np.pad(out, ((r, r), (0, 0)), mode="reflect")
+    return sum(k[i] * p[i:i + img.shape[0], :] for i in range(len(k)))
+
+
+def _value_noise(rng: np.random.Generator, h: int, w: int) -> np.ndarray:
+    img = np.zeros((h, w), np.float32)
+    for cell, amp in ((96, 55.0), (24, 35.0), (6, 22.0)):
+        gh, gw = h // cell + 2, w // cell + 2
+        g = rng.uniform(-1.0, 1.0, (gh, gw)).astype(np.float32)
+        ys = np.arange(h, dtype=np.float32) / cell
+        xs = np.arange(w, dtype=np.float32) / cell
+        y0 = ys.astype(np.int64)
+        x0 = xs.astype(np.int64)
+        fy = (ys - y0)[:, None]
+        fx = (xs - x0)[None, :]
+        v = (g[y0][:, x0] * (1 - fy) * (1 - fx) + g[y0 + 1][:, x0] * fy * (1 - fx)
+             + g[y0][:, x0 + 1] * (1 - fy) * fx + g[y0 + 1][:, x0 + 1] * fy * fx)
+        img += amp * v
+    return img + 128.0
+
+
+def synthetic_frame(seed: int, w: int = 640, h: int = 480, kind: str = "textured") -> np.ndarray:
+    """Return an (h, w) uint8 frame for `seed`; kind in textured|low_contrast|constant."""
+    if kind == "constant":
+        return np.full((h, w), 97, np.uint8)
+    rng = np.random.Generator(np.random.PCG64(seed))
+    img = _smooth(_value_noise(rng, h, w), 1.5)
+    scale = max(w, h) / 640.0
+    for _ in range(200):  # filled rectangles / ellipses
+        cx, cy = rng.uniform(0, w), rng.uniform(0, h)
+        rx, ry = rng.uniform(4, 40) * scale, rng.uniform(4, 40) * scale
+        gray = rng.uniform(0, 255)
+        x0, x1 = int(max(cx - rx, 0)), int(min(cx + rx + 1, w))
+        y0, y1 = int(max(cy - ry, 0)), int(min(cy + ry + 1, h))
+        if x1 <= x0 or y1 <= y0:
+            continue
+        if rng.uniform() < 0.5:
+            img[y0:y1, x0:x1] = gray
+        else:
+            yy, xx = np.mgrid[y0:y1, x0:x1]
+            inside = ((xx - cx) / rx) ** 2 + ((yy - cy) / ry) ** 2 <= 1.0
+            img[y0:y1, x0:x1][inside] = gray
+    for _ in range(50):  # anti-aliased lines: coverage from distance to the segment
+        ax, ay, bx, by = rng.uniform(0, w), rng.uniform(0, h), rng.uniform(0, w), rng.uniform(0, h)
+        width = rng.uniform(0.8, 3.0) * scale
+        gray = rng.uniform(0, 255)
+        x0, x1 = int(max(min(ax, bx) - width - 1, 0)), int(min(max(ax, bx) + width + 2, w))
+        y0, y1 = int(max(min(ay, by) - width - 1, 0)), int(min(max(ay, by) + width + 2, h))
+        if x1 <= x0 or y1 <= y0:
+            continue
+        yy, xx = np.mgrid[y0:y1, x0:x1].astype(np.float32)
+        dx, dy = bx - ax, by - ay
+        t = np.clip(((xx - ax) * dx + (yy - ay) * dy) / max(dx * dx + dy * dy, 1e-6), 0, 1)
+        dist = np.hypot(xx - (ax + t * dx), yy - (ay + t * dy))
+        cov = np.clip(width / 2 + 0.5 - dist, 0, 1)
+        sub = img[y0:y1, x0:x1]
+        img[y0:y1, x0:x1] = sub * (1 - cov) + gray * cov
+    if kind == "low_contrast":
+        img = 128.0 + (img - 128.0) * 0.15
+    elif kind != "textured":
+        raise ValueError(f"unknown kind {kind!r}")
+    return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+
+
+def synthetic_mask(w: int = 640, h: int = 480, seed: int = 0) -> np.ndarray:
+    """A human-mask-like u8 mask: ones with one zero rectangle (DetectHumanPose.cpp:453-489)."""
+    rng = np.random.Generator(np.random.PCG64(seed + 1000))
+    m = np.ones((h, w), np.uint8)
+    x0, y0 = int(rng.uniform(0.2, 0.5) * w), int(rng.uniform(0.1, 0.4) * h)
+    m[y0:y0 + h // 3, x0:x0 + w // 4] = 0
+    return m
+
+
+def synthetic_batch(n: int, w: int = 640, h: int = 480, first_seed: int = 0,
+                    distinct: int | None = None) -> np.ndarray:
+    """(n, h, w) uint8 frames; with `distinct` set, that many seeds are generated and cycled."""
+    d = n if distinct is None else max(1, min(distinct, n))
+    frames = [synthetic_frame(first_seed + i, w, h) for i in range(d)]
+    return np.stack([frames[i % d] for i in range(n)])
