@@ -97,7 +97,8 @@ __global__ __launch_bounds__(256) void resize_kernel(
 // K2 — FAST per cell.  S(p) = max(q0, -q1) - 1 where q0 (q1) is the max (min) over the 16
 // nine-pixel arcs of the min (max) of d = v - circle: p is a cv::FAST corner at threshold t iff
 // S(p) >= t, and cornerScore<16> returns exactly S(p) for such p (DESIGN.md "FAST").  So S is
-// computed once per pixel and both thresholds of the fallback reuse it.
+// computed once per pixel and both thresholds of the fallback reuse it.  S ranges over
+// [-256, 254]; only S >= 0 can be a corner, so LDS keeps max(S, -1) + 1 as a byte.
 constexpr int kFastBlock = 256;
 constexpr int kRoiMax = 72;  // cell ROI <= (59+6) x (59+6): wCell < 2*W for every level size
 
@@ -180,7 +181,8 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
     const int ncand = (nr > 0 && nc > 0) ? nr * nc : 0;
     for (int i = threadIdx.x; i < ncand; i += kFastBlock) {
         const int r = i / nc, cc = i - r * nc;
-        S[i] = (uint8_t)(fast_S(roi + (r + 3) * kRoiMax + cc + 3, kRoiMax) + 1);
+        // S < 0 is never a corner for t >= 0: clamp to -1 so S + 1 fits a byte
+        S[i] = (uint8_t)(max(fast_S(roi + (r + 3) * kRoiMax + cc + 3, kRoiMax), -1) + 1);
     }
     __syncthreads();
     // ordered compaction: thread t owns candidates [t*chunk, (t+1)*chunk) in row-major order

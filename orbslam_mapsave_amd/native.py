@@ -51,9 +51,10 @@ def lib() -> C.CDLL:
         for fn in ("orbfe_get_levels", "orbfe_get_scale_factor", "orbfe_keypoint_capacity",
                    "orbfe_synchronize"):
             getattr(L, fn).argtypes = [C.c_void_p]
-        L.orbfe_matcher_create.restype = C.c_void_p
-        L.orbfe_matcher_create.argtypes = [C.c_int, C.c_void_p]
-        L.orbfe_matcher_destroy.argtypes = [C.c_void_p]
+        if hasattr(L, "orbfe_matcher_create"):
+            L.orbfe_matcher_create.restype = C.c_void_p
+            L.orbfe_matcher_create.argtypes = [C.c_int, C.c_void_p]
+            L.orbfe_matcher_destroy.argtypes = [C.c_void_p]
         _lib = L
     return _lib
 
