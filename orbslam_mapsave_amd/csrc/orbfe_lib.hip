@@ -2,3 +2,5 @@
 // __constant__ tables they read must share one code object).
 #include "orbfe_extract.hip"
 #include "orbfe_api.hip"
+#include "orbfe_match.hip"
+#include "orbfe_match_api.hip"

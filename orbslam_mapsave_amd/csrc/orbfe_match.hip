@@ -1,0 +1,660 @@
+// orbfe_match.hip — MI355X (gfx950) replacement for the hot subset of ORB-SLAM2's ORBmatcher
+// (skaegy/ORBSLAM_MapSave src/ORBmatcher.cc) and the Frame grid it queries (src/Frame.cc).
+//
+//   hamming_kernel       DescriptorDistance (1650-1666), one row pair per lane
+//   bf_match_kernel      brute-force best/second (config 3): queries in lanes, references
+//                        streamed through LDS and read as wave-wide broadcasts
+//   grid_kernel          Frame::AssignFeaturesToGrid (Frame.cc:341-356) as a CSR
+//   *_cand_kernel        GetFeaturesInArea (Frame.cc:445-498) + distances for every query in
+//                        parallel (counts, scan, fill)
+//   *_resolve_kernel     the reference's sequential greedy semantics (H7): one wave decides 64
+//                        consecutive queries against the committed state, commits the prefix
+//                        that no earlier lane of the chunk can have influenced, and resumes at
+//                        the first conflicting lane.  Bit-identical to the in-order loop.
+//   frustum_kernel       Frame::isInFrustum (387-443) + MapPoint::PredictScale (MapPoint.cc:633)
+#include <hip/hip_runtime.h>
+
+#include <climits>
+
+#include "../../include/orbfe.h"
+#include "orbfe_device.hpp"
+
+namespace orbfe {
+
+constexpr int kGridCols = 64, kGridRows = 48;  // FRAME_GRID_COLS/ROWS (Frame.h:37-38)
+constexpr int kGridCells = kGridCols * kGridRows;
+constexpr int kThHigh = 100, kThLow = 50, kHistLen = 30;  // ORBmatcher.cc:37-39
+
+struct DevFrame {
+    const orbfe_keypoint* k;
+    const uint4* desc;  // 2 x uint4 per keypoint
+    const float* ur;    // NULL: monocular
+    int n;
+    float minx, maxx, miny, maxy, gwi, ghi;
+    const int* cstart;  // kGridCells + 1
+    const int* citems;
+};
+
+__device__ __forceinline__ int hamming_rows(const uint4* a, const uint4* b) {
+    return hamming256(a[0], a[1], b[0], b[1]);
+}
+
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void hamming_kernel(const uint4* a, const uint4* b, int n,
+                                                      int* dist) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) dist[i] = hamming_rows(a + 2 * i, b + 2 * i);
+}
+
+// Brute force: problem b = blockIdx.y; each lane owns one query; 256 references per LDS tile.
+constexpr int kBfBlock = 256;
+__global__ __launch_bounds__(kBfBlock) void bf_match_kernel(const uint8_t* q, long long q_pitch,
+                                                            const int* nq_arr, int nq_cap,
+                                                            const uint8_t* r, long long r_pitch,
+                                                            const int* nr_arr, int* out) {
+    __shared__ uint4 tile[kBfBlock * 2];
+    const int b = blockIdx.y;
+    const int nq = nq_arr[b], nr = nr_arr[b];
+    const int qi = blockIdx.x * kBfBlock + threadIdx.x;
+    if (blockIdx.x * kBfBlock >= nq) return;
+    const uint4* Q = reinterpret_cast<const uint4*>(q + b * q_pitch);
+    const uint4* R = reinterpret_cast<const uint4*>(r + b * r_pitch);
+    uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
+    if (qi < nq) {
+        a0 = Q[2 * qi];
+        a1 = Q[2 * qi + 1];
+    }
+    int best = 256, second = 256, bi = -1;
+    for (int base = 0; base < nr; base += kBfBlock) {
+        const int cnt = min(kBfBlock, nr - base);
+        __syncthreads();
+        if (threadIdx.x < cnt) {
+            tile[2 * threadIdx.x] = R[2 * (base + threadIdx.x)];
+            tile[2 * threadIdx.x + 1] = R[2 * (base + threadIdx.x) + 1];
+        }
+        __syncthreads();
+        for (int j = 0; j < cnt; ++j) {  // in reference order: first-wins ties (ORBmatcher.cc:102-114)
+            const int d = hamming256(a0, a1, tile[2 * j], tile[2 * j + 1]);
+            if (d < best) {
+                second = best;
+                best = d;
+                bi = base + j;
+            } else if (d < second) {
+                second = d;
+            }
+        }
+    }
+    if (qi < nq) {
+        int* o = out + ((long long)b * nq_cap + qi) * 3;
+        o[0] = bi;
+        o[1] = best;
+        o[2] = second;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Grid as CSR.  cellof[i] = -1 for keypoints outside the 64 x 48 grid (PosInGrid, 500-510).
+constexpr int kGridBlock = 1024;
+__global__ __launch_bounds__(kGridBlock) void grid_kernel(const orbfe_keypoint* k, int n,
+                                                          float minx, float miny, float gwi,
+                                                          float ghi, int* cellof, int* cstart,
+                                                          int* citems) {
+    __shared__ int cnt[kGridCells];
+    __shared__ int tmp[kGridBlock / 64 + 1];
+    for (int c = threadIdx.x; c < kGridCells; c += kGridBlock) cnt[c] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += kGridBlock) {
+        const int gx = (int)roundf((k[i].x - minx) * gwi);
+        const int gy = (int)roundf((k[i].y - miny) * ghi);
+        int c = -1;
+        if (gx >= 0 && gx < kGridCols && gy >= 0 && gy < kGridRows) {
+            c = gx * kGridRows + gy;  // mGrid[ix][iy]
+            atomicAdd(&cnt[c], 1);
+        }
+        cellof[i] = c;
+    }
+    __syncthreads();
+    constexpr int PER = (kGridCells + kGridBlock - 1) / kGridBlock;
+    int local[PER], sum = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int c = threadIdx.x * PER + j;
+        local[j] = c < kGridCells ? cnt[c] : 0;
+        sum += local[j];
+    }
+    int total;
+    int off = block_exclusive_scan<kGridBlock>(sum, tmp, total);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int c = threadIdx.x * PER + j;
+        if (c < kGridCells) {
+            cstart[c] = off;
+            cnt[c] = off;  // cursor
+        }
+        off += local[j];
+    }
+    if (threadIdx.x == 0) cstart[kGridCells] = total;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += kGridBlock) {
+        const int c = cellof[i];
+        if (c >= 0) citems[atomicAdd(&cnt[c], 1)] = i;
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < kGridCells; c += kGridBlock) {  // insertion order = index order
+        const int s = cstart[c], e = cstart[c + 1];
+        for (int a = s + 1; a < e; ++a) {
+            const int v = citems[a];
+            int b = a - 1;
+            while (b >= s && citems[b] > v) {
+                citems[b + 1] = citems[b];
+                --b;
+            }
+            citems[b + 1] = v;
+        }
+    }
+}
+
+// Frame::GetFeaturesInArea (Frame.cc:445-498): visits candidates in ix-major, iy, insertion
+// order and calls fn(idx) for each.
+template <class Fn>
+__device__ __forceinline__ void features_in_area(const DevFrame& F, float x, float y, float r,
+                                                 int min_level, int max_level, Fn fn) {
+    const int cx0 = max(0, (int)floorf((x - F.minx - r) * F.gwi));
+    if (cx0 >= kGridCols) return;
+    const int cx1 = min(kGridCols - 1, (int)ceilf((x - F.minx + r) * F.gwi));
+    if (cx1 < 0) return;
+    const int cy0 = max(0, (int)floorf((y - F.miny - r) * F.ghi));
+    if (cy0 >= kGridRows) return;
+    const int cy1 = min(kGridRows - 1, (int)ceilf((y - F.miny + r) * F.ghi));
+    if (cy1 < 0) return;
+    const bool check = min_level > 0 || max_level >= 0;
+    for (int ix = cx0; ix <= cx1; ++ix)
+        for (int iy = cy0; iy <= cy1; ++iy) {
+            const int c = ix * kGridRows + iy;
+            for (int e = F.cstart[c]; e < F.cstart[c + 1]; ++e) {
+                const int idx = F.citems[e];
+                const orbfe_keypoint kp = F.k[idx];
+                if (check) {
+                    if (kp.octave < min_level) continue;
+                    if (max_level >= 0 && kp.octave > max_level) continue;
+                }
+                if (fabsf(kp.x - x) < r && fabsf(kp.y - y) < r) fn(idx);
+            }
+        }
+}
+
+// Exclusive scan of counts[0..n) into off[0..n], single workgroup.
+__global__ __launch_bounds__(1024) void scan_kernel(const int* counts, int n, int* off) {
+    __shared__ int tmp[1024 / 64 + 1];
+    int run = 0;
+    for (int base = 0; base < n; base += 1024) {
+        const int i = base + threadIdx.x;
+        const int v = i < n ? counts[i] : 0;
+        int t;
+        const int ex = block_exclusive_scan<1024>(v, tmp, t);
+        if (i < n) off[i] = run + ex;
+        run += t;
+    }
+    if (threadIdx.x == 0) off[n] = run;
+}
+
+// ---------------------------------------------------------------------------------------------
+// SearchForInitialization (ORBmatcher.cc:408-523)
+struct SfiArgs {
+    DevFrame f1, f2;
+    const float* prev;  // 2 per F1 keypoint
+    float window;
+    int* cnt;           // per F1 keypoint
+    const int* off;     // n1 + 1
+    int2* cand;         // (i2, dist)
+};
+
+template <bool FILL>
+__global__ __launch_bounds__(256) void sfi_cand_kernel(SfiArgs a) {
+    const int i1 = blockIdx.x * 256 + threadIdx.x;
+    if (i1 >= a.f1.n) return;
+    const orbfe_keypoint k1 = a.f1.k[i1];
+    if (k1.octave > 0) {
+        if (!FILL) a.cnt[i1] = 0;
+        return;
+    }
+    const uint4* d1 = a.f1.desc + 2 * i1;
+    const uint4 q0 = d1[0], q1 = d1[1];
+    int n = 0;
+    int2* out = FILL ? a.cand + a.off[i1] : nullptr;
+    features_in_area(a.f2, a.prev[2 * i1], a.prev[2 * i1 + 1], a.window, k1.octave, k1.octave,
+                     [&](int i2) {
+                         if (FILL) {
+                             const uint4* d2 = a.f2.desc + 2 * i2;
+                             out[n] = make_int2(i2, hamming256(q0, q1, d2[0], d2[1]));
+                         }
+                         ++n;
+                     });
+    if (!FILL) a.cnt[i1] = n;
+}
+
+__device__ __forceinline__ int rot_bin(float a1, float a2) {  // ORBmatcher.cc:478-483
+    float rot = a1 - a2;
+    if (rot < 0.0) rot += 360.0f;
+    int bin = (int)roundf(rot * (1.0f / kHistLen));
+    if (bin == kHistLen) bin = 0;
+    return bin;
+}
+
+// ComputeThreeMaxima (ORBmatcher.cc:1604-1645) over 30 bin counts.
+__device__ __forceinline__ void three_maxima(const int* h, int& i1, int& i2, int& i3) {
+    int m1 = 0, m2 = 0, m3 = 0;
+    i1 = i2 = i3 = -1;
+    for (int i = 0; i < kHistLen; ++i) {
+        const int s = h[i];
+        if (s > m1) { m3 = m2; m2 = m1; m1 = s; i3 = i2; i2 = i1; i1 = i; }
+        else if (s > m2) { m3 = m2; m2 = s; i3 = i2; i2 = i; }
+        else if (s > m3) { m3 = s; i3 = i; }
+    }
+    if (m2 < 0.1f * (float)m1) { i2 = -1; i3 = -1; }
+    else if (m3 < 0.1f * (float)m1) { i3 = -1; }
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// Lowest lane of the wave with `pred` set, 64 if none.
+__device__ __forceinline__ int first_lane(bool pred) {
+    const unsigned long long b = __ballot(pred);
+    return b ? __builtin_ctzll(b) : 64;
+}
+
+struct SfiResolveArgs {
+    int n1, n2;
+    const orbfe_keypoint* k1;
+    const orbfe_keypoint* k2;
+    const int* off;
+    const int2* cand;
+    float nnratio;
+    int check_ori;
+    int* md;        // n2 scratch: vMatchedDistance
+    int* m21;       // n2 scratch: vnMatches21
+    int* claim;     // n2 scratch: lowest claiming lane, 64 = none
+    int* m12;       // n1 out: vnMatches12
+    int* rotbin;    // n1 scratch
+    float* prev;    // 2 n1 inout
+    int* nmatches;
+};
+
+__global__ __launch_bounds__(64) void sfi_resolve_kernel(SfiResolveArgs a) {
+    __shared__ int hist[kHistLen];
+    const int lane = lane_id();
+    for (int i = lane; i < a.n2; i += 64) {
+        a.md[i] = INT_MAX;
+        a.m21[i] = -1;
+        a.claim[i] = 64;
+    }
+    for (int i = lane; i < a.n1; i += 64) {
+        a.m12[i] = -1;
+        a.rotbin[i] = -1;
+    }
+    if (lane < kHistLen) hist[lane] = 0;
+    __syncthreads();
+    for (int base = 0; base < a.n1;) {
+        const int i1 = base + lane;
+        const bool valid = i1 < a.n1;
+        int best = INT_MAX, second = INT_MAX, bi = -1;
+        const int e0 = valid ? a.off[i1] : 0, e1 = valid ? a.off[i1 + 1] : 0;
+        for (int e = e0; e < e1; ++e) {
+            const int2 c = a.cand[e];
+            if (a.md[c.x] <= c.y) continue;  // ORBmatcher.cc:447-448
+            if (c.y < best) { second = best; best = c.y; bi = c.x; }
+            else if (c.y < second) { second = c.y; }
+        }
+        const bool acc = valid && best <= kThLow && best < (float)second * a.nnratio;
+        if (acc) atomicMin(&a.claim[bi], lane);
+        __syncthreads();
+        bool conf = false;
+        for (int e = e0; e < e1 && !conf; ++e) conf = a.claim[a.cand[e].x] < lane;
+        const int stop = first_lane(conf);  // lanes below `stop` saw the committed state
+        if (acc && lane < stop) {
+            const int old = a.m21[bi];
+            if (old >= 0) a.m12[old] = -1;  // steal (466-470)
+            a.m12[i1] = bi;
+            a.m21[bi] = i1;
+            a.md[bi] = best;
+            if (a.check_ori) a.rotbin[i1] = rot_bin(a.k1[i1].angle, a.k2[bi].angle);
+        }
+        __syncthreads();
+        if (acc) a.claim[bi] = 64;
+        __syncthreads();
+        base += stop;
+    }
+    // rotation consistency (492-515) and vbPrevMatched update (518-520)
+    if (a.check_ori) {
+        for (int i = lane; i < a.n1; i += 64)
+            if (a.rotbin[i] >= 0) atomicAdd(&hist[a.rotbin[i]], 1);
+        __syncthreads();
+        int t1, t2, t3;
+        three_maxima(hist, t1, t2, t3);
+        for (int i = lane; i < a.n1; i += 64) {
+            const int b = a.rotbin[i];
+            if (b >= 0 && b != t1 && b != t2 && b != t3) a.m12[i] = -1;
+        }
+        __syncthreads();
+    }
+    int nm = 0;
+    for (int i = lane; i < a.n1; i += 64) {
+        const int j = a.m12[i];
+        if (j >= 0) {
+            ++nm;
+            a.prev[2 * i] = a.k2[j].x;
+            a.prev[2 * i + 1] = a.k2[j].y;
+        }
+    }
+    nm = wave_sum(nm);
+    if (lane == 0) *a.nmatches = nm;
+}
+
+// ---------------------------------------------------------------------------------------------
+// SearchByProjection(Frame&, const vector<MapPoint*>&, th) (ORBmatcher.cc:45-129)
+struct SbpMps {
+    int m;
+    const uint8_t* in_view;
+    const uint8_t* bad;
+    const float* px;
+    const float* py;
+    const float* pxr;
+    const int* lvl;
+    const float* vcos;
+    const uint4* desc;
+    const int* nobs;
+};
+
+struct SbpLocalArgs {
+    DevFrame f;
+    SbpMps mp;
+    const float* scale;  // per level
+    float th;
+    int* cnt;
+    const int* off;
+    int2* cand;          // (idx, dist | octave << 16)
+};
+
+template <bool FILL>
+__global__ __launch_bounds__(256) void sbp_local_cand_kernel(SbpLocalArgs a) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.mp.m) return;
+    if (!a.mp.in_view[i] || a.mp.bad[i]) {
+        if (!FILL) a.cnt[i] = 0;
+        return;
+    }
+    const int pl = a.mp.lvl[i];
+    float r = a.mp.vcos[i] > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos (131-137)
+    if (a.th != 1.0) r *= a.th;
+    const float rs = r * a.scale[pl];
+    const float pxr = a.mp.pxr[i];
+    const uint4 q0 = a.mp.desc[2 * i], q1 = a.mp.desc[2 * i + 1];
+    int n = 0;
+    int2* out = FILL ? a.cand + a.off[i] : nullptr;
+    features_in_area(a.f, a.mp.px[i], a.mp.py[i], rs, pl - 1, pl, [&](int idx) {
+        if (a.f.ur && a.f.ur[idx] > 0) {  // stereo consistency (91-96)
+            const float er = fabsf(pxr - a.f.ur[idx]);
+            if (er > r * a.scale[pl]) return;
+        }
+        if (FILL) {
+            const uint4* d = a.f.desc + 2 * idx;
+            out[n] = make_int2(idx, hamming256(q0, q1, d[0], d[1]) | (a.f.k[idx].octave << 16));
+        }
+        ++n;
+    });
+    if (!FILL) a.cnt[i] = n;
+}
+
+struct SbpLocalResolveArgs {
+    int m, nkp;
+    const int* off;
+    const int2* cand;
+    const int* nobs;
+    const int* ids;      // NULL: index
+    float nnratio;
+    int* fmp;            // nkp inout
+    int* fobs;           // nkp inout
+    int* claim;          // nkp scratch
+    int* nmatches;
+};
+
+__global__ __launch_bounds__(64) void sbp_local_resolve_kernel(SbpLocalResolveArgs a) {
+    const int lane = lane_id();
+    for (int i = lane; i < a.nkp; i += 64) a.claim[i] = 64;
+    __syncthreads();
+    int nm = 0;
+    for (int base = 0; base < a.m;) {
+        const int i = base + lane;
+        const bool valid = i < a.m;
+        const int e0 = valid ? a.off[i] : 0, e1 = valid ? a.off[i + 1] : 0;
+        int best = 256, bl = -1, second = 256, sl = -1, bi = -1;
+        for (int e = e0; e < e1; ++e) {
+            const int2 c = a.cand[e];
+            if (a.fmp[c.x] >= 0 && a.fobs[c.x] > 0) continue;  // already observed (87-89)
+            const int d = c.y & 0xffff, lv = c.y >> 16;
+            if (d < best) { second = best; best = d; sl = bl; bl = lv; bi = c.x; }
+            else if (d < second) { sl = lv; second = d; }
+        }
+        bool acc = valid && best <= kThHigh;
+        if (acc && bl == sl && best > a.nnratio * second) acc = false;  // ratio, same level only
+        const int nobs = acc ? a.nobs[i] : 0;
+        if (acc && nobs > 0) atomicMin(&a.claim[bi], lane);
+        __syncthreads();
+        bool conf = false;
+        for (int e = e0; e < e1 && !conf; ++e) {
+            const int idx = a.cand[e].x;
+            conf = a.claim[idx] < lane && !(a.fmp[idx] >= 0 && a.fobs[idx] > 0);
+        }
+        const int stop = first_lane(conf);
+        const bool commit = acc && lane < stop;
+        __syncthreads();
+        if (commit) atomicMax(&a.claim[bi], 1000 + lane);  // last committed writer wins
+        __syncthreads();
+        if (commit && a.claim[bi] == 1000 + lane) {
+            a.fmp[bi] = a.ids ? a.ids[i] : i;
+            a.fobs[bi] = nobs;
+        }
+        nm += commit;
+        __syncthreads();
+        if (acc) a.claim[bi] = 64;
+        __syncthreads();
+        base += stop;
+    }
+    nm = wave_sum(nm);
+    if (lane == 0) *a.nmatches = nm;
+}
+
+// ---------------------------------------------------------------------------------------------
+// SearchByProjection(Frame& Cur, const Frame& Last, th, bMono) (ORBmatcher.cc:1331-1473)
+struct SbpLastArgs {
+    DevFrame cur;
+    int n_last;
+    const orbfe_keypoint* lk;
+    const uint8_t* valid;
+    const uint8_t* outlier;
+    const float* xyz;
+    const uint4* desc;
+    float T[12];           // current pose [R|t]
+    float fx, fy, cx, cy, bf;
+    float minx, maxx, miny, maxy;
+    const float* scale;
+    float th;
+    int mode;              // 0: [o-1, o+1], 1: forward [o, -], 2: backward [0, o]
+    int* cnt;
+    const int* off;
+    int2* cand;
+};
+
+template <bool FILL>
+__global__ __launch_bounds__(256) void sbp_last_cand_kernel(SbpLastArgs a) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n_last) return;
+    int n = 0;
+    if (a.valid[i] && !a.outlier[i]) {
+        const float* P = a.xyz + 3 * i;
+        float pc[3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+            pc[r] = ((a.T[4 * r] * P[0] + a.T[4 * r + 1] * P[1]) + a.T[4 * r + 2] * P[2]) + a.T[4 * r + 3];
+        const float invz = (float)(1.0 / (double)pc[2]);
+        const float u = a.fx * pc[0] * invz + a.cx;
+        const float v = a.fy * pc[1] * invz + a.cy;
+        if (!(invz < 0) && !(u < a.minx || u > a.maxx) && !(v < a.miny || v > a.maxy)) {
+            const int o = a.lk[i].octave;
+            const float radius = a.th * a.scale[o];
+            const int lo = a.mode == 0 ? o - 1 : a.mode == 1 ? o : 0;
+            const int hi = a.mode == 0 ? o + 1 : a.mode == 1 ? -1 : o;
+            const uint4 q0 = a.desc[2 * i], q1 = a.desc[2 * i + 1];
+            int2* out = FILL ? a.cand + a.off[i] : nullptr;
+            features_in_area(a.cur, u, v, radius, lo, hi, [&](int i2) {
+                if (a.cur.ur && a.cur.ur[i2] > 0) {
+                    const float ur = u - a.bf * invz;
+                    if (fabsf(ur - a.cur.ur[i2]) > radius) return;
+                }
+                if (FILL) {
+                    const uint4* d = a.cur.desc + 2 * i2;
+                    out[n] = make_int2(i2, hamming256(q0, q1, d[0], d[1]));
+                }
+                ++n;
+            });
+        }
+    }
+    if (!FILL) a.cnt[i] = n;
+}
+
+struct SbpLastResolveArgs {
+    int n_last, nkp;
+    const int* off;
+    const int2* cand;
+    const int* nobs;
+    const int* ids;
+    const orbfe_keypoint* lk;
+    const orbfe_keypoint* ck;
+    int check_ori;
+    int* fmp;
+    int* fobs;
+    int* claim;
+    int2* events;   // (i2, bin) in acceptance order, capacity n_last
+    int* nmatches;
+};
+
+__global__ __launch_bounds__(64) void sbp_last_resolve_kernel(SbpLastResolveArgs a) {
+    __shared__ int hist[kHistLen];
+    const int lane = lane_id();
+    for (int i = lane; i < a.nkp; i += 64) a.claim[i] = 64;
+    if (lane < kHistLen) hist[lane] = 0;
+    __syncthreads();
+    int nev = 0;
+    for (int base = 0; base < a.n_last;) {
+        const int i = base + lane;
+        const bool valid = i < a.n_last;
+        const int e0 = valid ? a.off[i] : 0, e1 = valid ? a.off[i + 1] : 0;
+        int best = 256, bi = -1;
+        for (int e = e0; e < e1; ++e) {
+            const int2 c = a.cand[e];
+            if (a.fmp[c.x] >= 0 && a.fobs[c.x] > 0) continue;  // 1406-1408
+            if (c.y < best) { best = c.y; bi = c.x; }
+        }
+        const bool acc = valid && best <= kThHigh;
+        const int nobs = acc ? a.nobs[i] : 0;
+        if (acc && nobs > 0) atomicMin(&a.claim[bi], lane);
+        __syncthreads();
+        bool conf = false;
+        for (int e = e0; e < e1 && !conf; ++e) {
+            const int idx = a.cand[e].x;
+            conf = a.claim[idx] < lane && !(a.fmp[idx] >= 0 && a.fobs[idx] > 0);
+        }
+        const int stop = first_lane(conf);
+        const bool commit = acc && lane < stop;
+        __syncthreads();
+        if (commit) atomicMax(&a.claim[bi], 1000 + lane);
+        __syncthreads();
+        if (commit && a.claim[bi] == 1000 + lane) {
+            a.fmp[bi] = a.ids ? a.ids[i] : i;
+            a.fobs[bi] = nobs;
+        }
+        const unsigned long long cm = __ballot(commit);
+        if (commit) {
+            const int slot = nev + __popcll(cm & ((1ull << lane) - 1));
+            const int bin = a.check_ori ? rot_bin(a.lk[i].angle, a.ck[bi].angle) : 0;
+            a.events[slot] = make_int2(bi, bin);
+            if (a.check_ori) atomicAdd(&hist[bin], 1);
+        }
+        nev += __popcll(cm);
+        __syncthreads();
+        if (acc) a.claim[bi] = 64;
+        __syncthreads();
+        base += stop;
+    }
+    int nm = nev;
+    if (a.check_ori) {  // 1451-1470: every event in a non-top bin clears its keypoint
+        int t1, t2, t3;
+        three_maxima(hist, t1, t2, t3);
+        int removed = 0;
+        for (int e = lane; e < nev; e += 64) {
+            const int2 ev = a.events[e];
+            if (ev.y != t1 && ev.y != t2 && ev.y != t3) {
+                a.fmp[ev.x] = -1;
+                a.fobs[ev.x] = 0;
+                ++removed;
+            }
+        }
+        nm -= wave_sum(removed);
+    }
+    if (lane == 0) *a.nmatches = nm;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Frame::isInFrustum (Frame.cc:387-443) with MapPoint::PredictScale (MapPoint.cc:633-642).
+struct FrustumArgs {
+    int n;
+    const float* xyz;
+    const float* normal;
+    const float* mind;
+    const float* maxd;
+    float T[12];
+    float ow[3];   // camera centre -R^T t (computed on the host, double accumulation)
+    float fx, fy, cx, cy, bf;
+    float minx, maxx, miny, maxy, log_scale, cos_limit;
+    uint8_t* in_view;
+    float* px;
+    float* py;
+    float* pxr;
+    int* lvl;
+    float* vcos;
+};
+
+__global__ __launch_bounds__(256) void frustum_kernel(FrustumArgs a) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n) return;
+    a.in_view[i] = 0;
+    const float* P = a.xyz + 3 * i;
+    float pc[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+        pc[r] = ((a.T[4 * r] * P[0] + a.T[4 * r + 1] * P[1]) + a.T[4 * r + 2] * P[2]) + a.T[4 * r + 3];
+    if (pc[2] < 0.0f) return;
+    const float invz = 1.0f / pc[2];
+    const float u = a.fx * pc[0] * invz + a.cx;
+    const float v = a.fy * pc[1] * invz + a.cy;
+    if (u < a.minx || u > a.maxx) return;
+    if (v < a.miny || v > a.maxy) return;
+    const float dmax = 1.2f * a.maxd[i], dmin = 0.8f * a.mind[i];
+    const float po0 = P[0] - a.ow[0], po1 = P[1] - a.ow[1], po2 = P[2] - a.ow[2];
+    const float dist = (float)sqrt((double)po0 * po0 + (double)po1 * po1 + (double)po2 * po2);
+    if (dist < dmin || dist > dmax) return;
+    const float* nv = a.normal + 3 * i;
+    const double dot = (double)po0 * nv[0] + (double)po1 * nv[1] + (double)po2 * nv[2];
+    const float vc = (float)(dot / dist);
+    if (vc < a.cos_limit) return;
+    const float ratio = a.maxd[i] / dist;
+    const int lvl = (int)ceilf((float)log((double)ratio) / a.log_scale);
+    a.in_view[i] = 1;
+    a.px[i] = u;
+    a.pxr[i] = u - a.bf * invz;
+    a.py[i] = v;
+    a.lvl[i] = lvl;
+    a.vcos[i] = vc;
+}
+
+}  // namespace orbfe

@@ -1,0 +1,490 @@
+// orbfe_match_api.hip — host orchestration and C ABI of the matchers (include/orbfe.h).
+// Every call uploads the flat SoA views, runs the kernels of orbfe_match.hip on the matcher's
+// stream and downloads the results (synchronous, like the reference's member functions).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "../../include/orbfe.h"
+
+using namespace orbfe;
+
+struct orbfe_matcher {
+    int device = 0;
+    hipStream_t own = nullptr, stream = nullptr;
+    DevBuf fa_k, fa_d, fa_ur, fa_cs, fa_ci, fa_co;  // frame A (+ grid)
+    DevBuf fb_k, fb_d, fb_ur, fb_cs, fb_ci, fb_co;  // frame B (+ grid)
+    DevBuf q, r, nq, nr, out;                       // brute force / hamming
+    DevBuf cnt, off, cand;                          // candidate CSR
+    DevBuf s1, s2, s3, s4, s5;                      // resolve scratch / outputs
+    DevBuf m_f0, m_f1, m_f2, m_f3, m_f4, m_u0, m_u1, m_i0, m_i1, m_d;  // per-map-point inputs
+    DevBuf o_u, o_f0, o_f1, o_f2, o_f3, o_i;        // frustum outputs
+    DevBuf scal;
+
+    ~orbfe_matcher() {
+        for (DevBuf* b : {&fa_k, &fa_d, &fa_ur, &fa_cs, &fa_ci, &fa_co, &fb_k, &fb_d, &fb_ur,
+                          &fb_cs, &fb_ci, &fb_co, &q, &r, &nq, &nr, &out, &cnt, &off, &cand, &s1,
+                          &s2, &s3, &s4, &s5, &m_f0, &m_f1, &m_f2, &m_f3, &m_f4, &m_u0, &m_u1,
+                          &m_i0, &m_i1, &m_d, &o_u, &o_f0, &o_f1, &o_f2, &o_f3, &o_i, &scal})
+            b->release();
+        if (own) hipStreamDestroy(own);
+    }
+
+    int up(DevBuf& b, const void* src, size_t bytes) {
+        int st = b.ensure(std::max<size_t>(bytes, 16));
+        if (st) return st;
+        if (bytes) ORBFE_HIP(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, stream));
+        return ORBFE_OK;
+    }
+    int down(void* dst, const DevBuf& b, size_t bytes) {
+        if (bytes) ORBFE_HIP(hipMemcpyAsync(dst, b.p, bytes, hipMemcpyDeviceToHost, stream));
+        return ORBFE_OK;
+    }
+
+    // Uploads a frame view and builds its 64 x 48 grid (Frame::AssignFeaturesToGrid).
+    int frame(const orbfe_frame_view* v, bool second, DevFrame& F) {
+        DevBuf& k = second ? fb_k : fa_k;
+        DevBuf& d = second ? fb_d : fa_d;
+        DevBuf& u = second ? fb_ur : fa_ur;
+        DevBuf& cs = second ? fb_cs : fa_cs;
+        DevBuf& ci = second ? fb_ci : fa_ci;
+        DevBuf& co = second ? fb_co : fa_co;
+        const int n = v->n;
+        int st;
+        if ((st = up(k, v->keys_un, (size_t)n * sizeof(orbfe_keypoint)))) return st;
+        if ((st = up(d, v->desc, (size_t)n * 32))) return st;
+        if (v->u_right && (st = up(u, v->u_right, (size_t)n * sizeof(float)))) return st;
+        if ((st = cs.ensure((kGridCells + 1) * sizeof(int)))) return st;
+        if ((st = ci.ensure(std::max(n, 1) * sizeof(int)))) return st;
+        if ((st = co.ensure(std::max(n, 1) * sizeof(int)))) return st;
+        hipLaunchKernelGGL(grid_kernel, dim3(1), dim3(kGridBlock), 0, stream, k.as<orbfe_keypoint>(),
+                           n, v->min_x, v->min_y, v->grid_w_inv, v->grid_h_inv, co.as<int>(),
+                           cs.as<int>(), ci.as<int>());
+        F.k = k.as<orbfe_keypoint>();
+        F.desc = d.as<uint4>();
+        F.ur = v->u_right ? u.as<float>() : nullptr;
+        F.n = n;
+        F.minx = v->min_x;
+        F.maxx = v->max_x;
+        F.miny = v->min_y;
+        F.maxy = v->max_y;
+        F.gwi = v->grid_w_inv;
+        F.ghi = v->grid_h_inv;
+        F.cstart = cs.as<int>();
+        F.citems = ci.as<int>();
+        return ORBFE_OK;
+    }
+
+    // count -> scan -> fill for a candidate kernel family; returns the candidate total.
+    template <class Args, class CountK, class FillK>
+    int csr(Args& a, int nq, CountK ck, FillK fk, int& total) {
+        int st;
+        if ((st = cnt.ensure(std::max(nq, 1) * sizeof(int)))) return st;
+        if ((st = off.ensure((nq + 1) * sizeof(int)))) return st;
+        a.cnt = cnt.as<int>();
+        a.off = off.as<int>();
+        const int blocks = std::max(1, (nq + 255) / 256);
+        hipLaunchKernelGGL(ck, dim3(blocks), dim3(256), 0, stream, a);
+        hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, stream, cnt.as<int>(), nq, off.as<int>());
+        ORBFE_HIP(hipMemcpyAsync(&total, off.as<int>() + nq, sizeof(int), hipMemcpyDeviceToHost, stream));
+        ORBFE_HIP(hipStreamSynchronize(stream));
+        if ((st = cand.ensure(std::max(total, 1) * sizeof(int2)))) return st;
+        a.cand = cand.as<int2>();
+        hipLaunchKernelGGL(fk, dim3(blocks), dim3(256), 0, stream, a);
+        ORBFE_HIP(hipGetLastError());
+        return ORBFE_OK;
+    }
+};
+
+namespace {
+int frame_ok(const orbfe_frame_view* f) {
+    if (!f || f->n < 0 || (f->n && (!f->keys_un || !f->desc)) || !f->scale_factors ||
+        f->nlevels < 1)
+        return 0;
+    return 1;
+}
+// 3x4 [R|t]: camera centre -R^T t, accumulated in double like cv::gemm's GEMM_1_T path.
+void camera_center(const float* T, float* c) {
+    for (int i = 0; i < 3; ++i)
+        c[i] = (float)-((double)T[i] * T[3] + (double)T[4 + i] * T[7] + (double)T[8 + i] * T[11]);
+}
+void rigid(const float* T, const float* p, float* out) {
+    for (int r = 0; r < 3; ++r)
+        out[r] = ((T[4 * r] * p[0] + T[4 * r + 1] * p[1]) + T[4 * r + 2] * p[2]) + T[4 * r + 3];
+}
+template <class F>
+int guarded(orbfe_matcher* m, F&& f) {
+    if (!m) return ORBFE_ERR_ARG;
+    try {
+        DeviceGuard dg(m->device);
+        return f();
+    } catch (const std::bad_alloc&) {
+        return ORBFE_ERR_NOMEM;
+    } catch (...) {
+        return ORBFE_ERR_HIP;
+    }
+}
+}  // namespace
+
+extern "C" {
+
+orbfe_matcher* orbfe_matcher_create(int device, int* status) {
+    int st = check_device(device);
+    orbfe_matcher* m = nullptr;
+    if (st == ORBFE_OK) {
+        try {
+            DeviceGuard dg(device);
+            m = new orbfe_matcher();
+            m->device = device;
+            if (hipStreamCreateWithFlags(&m->own, hipStreamNonBlocking) != hipSuccess) st = ORBFE_ERR_HIP;
+            m->stream = m->own;
+        } catch (...) {
+            st = ORBFE_ERR_NOMEM;
+        }
+    }
+    if (st != ORBFE_OK && m) {
+        delete m;
+        m = nullptr;
+    }
+    if (status) *status = st;
+    return m;
+}
+
+void orbfe_matcher_destroy(orbfe_matcher* m) {
+    if (!m) return;
+    DeviceGuard dg(m->device);
+    hipStreamSynchronize(m->stream);
+    delete m;
+}
+
+int orbfe_matcher_set_stream(orbfe_matcher* m, void* s) {
+    if (!m) return ORBFE_ERR_ARG;
+    m->stream = s ? static_cast<hipStream_t>(s) : m->own;
+    return ORBFE_OK;
+}
+
+int orbfe_hamming(orbfe_matcher* m, const uint8_t* a, const uint8_t* b, int n, int32_t* dist) {
+    if (n < 0 || (n && (!a || !b || !dist))) return ORBFE_ERR_ARG;
+    if (n == 0) return m ? ORBFE_OK : ORBFE_ERR_ARG;
+    return guarded(m, [&]() {
+        int st;
+        if ((st = m->up(m->q, a, (size_t)n * 32))) return st;
+        if ((st = m->up(m->r, b, (size_t)n * 32))) return st;
+        if ((st = m->out.ensure((size_t)n * sizeof(int)))) return st;
+        hipLaunchKernelGGL(hamming_kernel, dim3((n + 255) / 256), dim3(256), 0, m->stream,
+                           m->q.as<uint4>(), m->r.as<uint4>(), n, m->out.as<int>());
+        if ((st = m->down(dist, m->out, (size_t)n * sizeof(int)))) return st;
+        ORBFE_HIP(hipStreamSynchronize(m->stream));
+        return ORBFE_OK;
+    });
+}
+
+int orbfe_bf_match(orbfe_matcher* m, const uint8_t* q, int nq, const uint8_t* r, int nr,
+                   int32_t* best_idx, int32_t* best_dist, int32_t* second_dist) {
+    if (nq < 0 || nr < 0 || (nq && (!q || !best_idx || !best_dist || !second_dist)) || (nr && !r))
+        return ORBFE_ERR_ARG;
+    if (nq == 0) return m ? ORBFE_OK : ORBFE_ERR_ARG;
+    return guarded(m, [&]() {
+        int st;
+        if ((st = m->up(m->q, q, (size_t)nq * 32))) return st;
+        if ((st = m->up(m->r, r, (size_t)std::max(nr, 1) * 32))) return st;
+        const int counts[2] = {nq, nr};
+        if ((st = m->up(m->nq, counts, sizeof(counts)))) return st;
+        if ((st = m->out.ensure((size_t)nq * 3 * sizeof(int)))) return st;
+        hipLaunchKernelGGL(bf_match_kernel, dim3((nq + kBfBlock - 1) / kBfBlock, 1), dim3(kBfBlock),
+                           0, m->stream, m->q.as<uint8_t>(), 0ll, m->nq.as<int>(), nq,
+                           m->r.as<uint8_t>(), 0ll, m->nq.as<int>() + 1, m->out.as<int>());
+        std::vector<int> tri((size_t)nq * 3);
+        if ((st = m->down(tri.data(), m->out, tri.size() * sizeof(int)))) return st;
+        ORBFE_HIP(hipStreamSynchronize(m->stream));
+        for (int i = 0; i < nq; ++i) {
+            best_idx[i] = tri[3 * i];
+            best_dist[i] = tri[3 * i + 1];
+            second_dist[i] = tri[3 * i + 2];
+        }
+        return ORBFE_OK;
+    });
+}
+
+int orbfe_bf_match_batch_device(orbfe_matcher* m, const uint8_t* d_q, size_t q_pitch,
+                                const int32_t* d_nq, int nq_cap, const uint8_t* d_r,
+                                size_t r_pitch, const int32_t* d_nr, int nb, int32_t* d_out) {
+    if (!m || nb < 0 || nq_cap < 0 || (nb && (!d_q || !d_nq || !d_r || !d_nr || !d_out)))
+        return ORBFE_ERR_ARG;
+    if (nb == 0 || nq_cap == 0) return ORBFE_OK;
+    if ((q_pitch | r_pitch) & 15) return ORBFE_ERR_ARG;
+    return guarded(m, [&]() {
+        hipLaunchKernelGGL(bf_match_kernel, dim3((nq_cap + kBfBlock - 1) / kBfBlock, nb),
+                           dim3(kBfBlock), 0, m->stream, d_q, (long long)q_pitch, d_nq, nq_cap,
+                           d_r, (long long)r_pitch, d_nr, d_out);
+        ORBFE_HIP(hipGetLastError());
+        return ORBFE_OK;
+    });
+}
+
+int orbfe_search_for_initialization(orbfe_matcher* m, float nnratio, int check_ori,
+                                    const orbfe_frame_view* f1, const orbfe_frame_view* f2,
+                                    float* prev_matched, int window, int32_t* matches12,
+                                    int32_t* nmatches) {
+    if (!frame_ok(f1) || !frame_ok(f2) || !nmatches || (f1->n && (!prev_matched || !matches12)))
+        return ORBFE_ERR_ARG;
+    return guarded(m, [&]() {
+        int st;
+        SfiArgs a;
+        if ((st = m->frame(f1, false, a.f1))) return st;
+        if ((st = m->frame(f2, true, a.f2))) return st;
+        if ((st = m->up(m->s5, prev_matched, (size_t)f1->n * 2 * sizeof(float)))) return st;
+        a.prev = m->s5.as<float>();
+        a.window = (float)window;
+        int total = 0;
+        if ((st = m->csr(a, f1->n, sfi_cand_kernel<false>, sfi_cand_kernel<true>, total))) return st;
+        const int n1 = f1->n, n2 = f2->n;
+        if ((st = m->s1.ensure(std::max(n2, 1) * 3 * sizeof(int)))) return st;
+        if ((st = m->s2.ensure(std::max(n1, 1) * 2 * sizeof(int)))) return st;
+        if ((st = m->scal.ensure(16))) return st;
+        SfiResolveArgs r;
+        r.n1 = n1;
+        r.n2 = n2;
+        r.k1 = a.f1.k;
+        r.k2 = a.f2.k;
+        r.off = m->off.as<int>();
+        r.cand = m->cand.as<int2>();
+        r.nnratio = nnratio;
+        r.check_ori = check_ori;
+        r.md = m->s1.as<int>();
+        r.m21 = r.md + std::max(n2, 1);
+        r.claim = r.m21 + std::max(n2, 1);
+        r.m12 = m->s2.as<int>();
+        r.rotbin = r.m12 + std::max(n1, 1);
+        r.prev = m->s5.as<float>();
+        r.nmatches = m->scal.as<int>();
+        hipLaunchKernelGGL(sfi_resolve_kernel, dim3(1), dim3(64), 0, m->stream, r);
+        ORBFE_HIP(hipGetLastError());
+        if ((st = m->down(matches12, m->s2, (size_t)n1 * sizeof(int)))) return st;
+        if ((st = m->down(prev_matched, m->s5, (size_t)n1 * 2 * sizeof(float)))) return st;
+        if ((st = m->down(nmatches, m->scal, sizeof(int)))) return st;
+        ORBFE_HIP(hipStreamSynchronize(m->stream));
+        return ORBFE_OK;
+    });
+}
+
+int orbfe_search_by_projection_local(orbfe_matcher* m, float nnratio,
+                                     const orbfe_frame_view* f, int32_t* frame_mp,
+                                     int32_t* frame_mp_obs, const orbfe_mappoint_view* mps,
+                                     const int32_t* mp_ids, float th, int32_t* nmatches) {
+    if (!frame_ok(f) || !mps || mps->m < 0 || !nmatches || (f->n && (!frame_mp || !frame_mp_obs)))
+        return ORBFE_ERR_ARG;
+    const int M = mps->m;
+    if (M && (!mps->track_in_view || !mps->is_bad || !mps->proj_x || !mps->proj_y ||
+              !mps->proj_xr || !mps->pred_level || !mps->view_cos || !mps->desc || !mps->n_obs))
+        return ORBFE_ERR_ARG;
+    for (int i = 0; i < M; ++i)  // mvScaleFactors[nPredictedLevel] outside the table is UB
+        if (mps->track_in_view[i] && !mps->is_bad[i] &&
+            (mps->pred_level[i] < 0 || mps->pred_level[i] >= f->nlevels))
+            return ORBFE_ERR_UNSUPPORTED;
+    return guarded(m, [&]() {
+        int st;
+        SbpLocalArgs a;
+        if ((st = m->frame(f, false, a.f))) return st;
+        if ((st = m->up(m->m_u0, mps->track_in_view, M))) return st;
+        if ((st = m->up(m->m_u1, mps->is_bad, M))) return st;
+        if ((st = m->up(m->m_f0, mps->proj_x, (size_t)M * 4))) return st;
+        if ((st = m->up(m->m_f1, mps->proj_y, (size_t)M * 4))) return st;
+        if ((st = m->up(m->m_f2, mps->proj_xr, (size_t)M * 4))) return st;
+        if ((st = m->up(m->m_i0, mps->pred_level, (size_t)M * 4))) return st;
+        if ((st = m->up(m->m_f3, mps->view_cos, (size_t)M * 4))) return st;
+        if ((st = m->up(m->m_d, mps->desc, (size_t)M * 32))) return st;
+        if ((st = m->up(m->m_i1, mps->n_obs, (size_t)M * 4))) return st;
+        if ((st = m->up(m->m_f4, f->scale_factors, (size_t)f->nlevels * 4))) return st;
+        if (mp_ids && (st = m->up(m->o_i, mp_ids, (size_t)M * 4))) return st;
+        a.mp = SbpMps{M, m->m_u0.as<uint8_t>(), m->m_u1.as<uint8_t>(), m->m_f0.as<float>(),
+                      m->m_f1.as<float>(), m->m_f2.as<float>(), m->m_i0.as<int>(),
+                      m->m_f3.as<float>(), m->m_d.as<uint4>(), m->m_i1.as<int>()};
+        a.scale = m->m_f4.as<float>();
+        a.th = th;
+        int total = 0;
+        if ((st = m->csr(a, M, sbp_local_cand_kernel<false>, sbp_local_cand_kernel<true>, total)))
+            return st;
+        const int N = f->n;
+        if ((st = m->up(m->s1, frame_mp, (size_t)N * 4))) return st;
+        if ((st = m->up(m->s2, frame_mp_obs, (size_t)N * 4))) return st;
+        if ((st = m->s3.ensure(std::max(N, 1) * sizeof(int)))) return st;
+        if ((st = m->scal.ensure(16))) return st;
+        SbpLocalResolveArgs r;
+        r.m = M;
+        r.nkp = N;
+        r.off = m->off.as<int>();
+        r.cand = m->cand.as<int2>();
+        r.nobs = m->m_i1.as<int>();
+        r.ids = mp_ids ? m->o_i.as<int>() : nullptr;
+        r.nnratio = nnratio;
+        r.fmp = m->s1.as<int>();
+        r.fobs = m->s2.as<int>();
+        r.claim = m->s3.as<int>();
+        r.nmatches = m->scal.as<int>();
+        hipLaunchKernelGGL(sbp_local_resolve_kernel, dim3(1), dim3(64), 0, m->stream, r);
+        ORBFE_HIP(hipGetLastError());
+        if ((st = m->down(frame_mp, m->s1, (size_t)N * 4))) return st;
+        if ((st = m->down(frame_mp_obs, m->s2, (size_t)N * 4))) return st;
+        if ((st = m->down(nmatches, m->scal, sizeof(int)))) return st;
+        ORBFE_HIP(hipStreamSynchronize(m->stream));
+        return ORBFE_OK;
+    });
+}
+
+int orbfe_search_by_projection_last(orbfe_matcher* m, int check_ori,
+                                    const orbfe_frame_view* cur, const float* tcw_cur,
+                                    const orbfe_camera* cam, int32_t* frame_mp,
+                                    int32_t* frame_mp_obs, int n_last,
+                                    const orbfe_keypoint* last_keys,
+                                    const uint8_t* last_mp_valid, const uint8_t* last_outlier,
+                                    const float* last_mp_xyz, const uint8_t* last_mp_desc,
+                                    const int32_t* last_mp_nobs, const int32_t* last_mp_ids,
+                                    const float* tcw_last, float th, int mono,
+                                    int32_t* nmatches) {
+    if (!frame_ok(cur) || !tcw_cur || !tcw_last || !cam || !nmatches || n_last < 0 ||
+        (cur->n && (!frame_mp || !frame_mp_obs)) ||
+        (n_last && (!last_keys || !last_mp_valid || !last_outlier || !last_mp_xyz ||
+                    !last_mp_desc || !last_mp_nobs)))
+        return ORBFE_ERR_ARG;
+    for (int i = 0; i < n_last; ++i)
+        if (last_mp_valid[i] && (last_keys[i].octave < 0 || last_keys[i].octave >= cur->nlevels))
+            return ORBFE_ERR_UNSUPPORTED;
+    return guarded(m, [&]() {
+        int st;
+        SbpLastArgs a;
+        if ((st = m->frame(cur, false, a.cur))) return st;
+        if ((st = m->up(m->fb_k, last_keys, (size_t)n_last * sizeof(orbfe_keypoint)))) return st;
+        if ((st = m->up(m->m_u0, last_mp_valid, n_last))) return st;
+        if ((st = m->up(m->m_u1, last_outlier, n_last))) return st;
+        if ((st = m->up(m->m_f0, last_mp_xyz, (size_t)n_last * 12))) return st;
+        if ((st = m->up(m->m_d, last_mp_desc, (size_t)n_last * 32))) return st;
+        if ((st = m->up(m->m_i1, last_mp_nobs, (size_t)n_last * 4))) return st;
+        if ((st = m->up(m->m_f4, cur->scale_factors, (size_t)cur->nlevels * 4))) return st;
+        if (last_mp_ids && (st = m->up(m->o_i, last_mp_ids, (size_t)n_last * 4))) return st;
+        a.n_last = n_last;
+        a.lk = m->fb_k.as<orbfe_keypoint>();
+        a.valid = m->m_u0.as<uint8_t>();
+        a.outlier = m->m_u1.as<uint8_t>();
+        a.xyz = m->m_f0.as<float>();
+        a.desc = m->m_d.as<uint4>();
+        std::memcpy(a.T, tcw_cur, sizeof(a.T));
+        a.fx = cam->fx;
+        a.fy = cam->fy;
+        a.cx = cam->cx;
+        a.cy = cam->cy;
+        a.bf = cam->bf;
+        a.minx = cur->min_x;
+        a.maxx = cur->max_x;
+        a.miny = cur->min_y;
+        a.maxy = cur->max_y;
+        a.scale = m->m_f4.as<float>();
+        a.th = th;
+        float twc[3], tlc[3];  // 1341-1352: motion direction for stereo/RGB-D
+        camera_center(tcw_cur, twc);
+        rigid(tcw_last, twc, tlc);
+        const bool fwd = tlc[2] > cam->b && !mono;
+        const bool bwd = -tlc[2] > cam->b && !mono;
+        a.mode = fwd ? 1 : bwd ? 2 : 0;
+        int total = 0;
+        if ((st = m->csr(a, n_last, sbp_last_cand_kernel<false>, sbp_last_cand_kernel<true>, total)))
+            return st;
+        const int N = cur->n;
+        if ((st = m->up(m->s1, frame_mp, (size_t)N * 4))) return st;
+        if ((st = m->up(m->s2, frame_mp_obs, (size_t)N * 4))) return st;
+        if ((st = m->s3.ensure(std::max(N, 1) * sizeof(int)))) return st;
+        if ((st = m->s4.ensure(std::max(n_last, 1) * sizeof(int2)))) return st;
+        if ((st = m->scal.ensure(16))) return st;
+        SbpLastResolveArgs r;
+        r.n_last = n_last;
+        r.nkp = N;
+        r.off = m->off.as<int>();
+        r.cand = m->cand.as<int2>();
+        r.nobs = m->m_i1.as<int>();
+        r.ids = last_mp_ids ? m->o_i.as<int>() : nullptr;
+        r.lk = a.lk;
+        r.ck = a.cur.k;
+        r.check_ori = check_ori;
+        r.fmp = m->s1.as<int>();
+        r.fobs = m->s2.as<int>();
+        r.claim = m->s3.as<int>();
+        r.events = m->s4.as<int2>();
+        r.nmatches = m->scal.as<int>();
+        hipLaunchKernelGGL(sbp_last_resolve_kernel, dim3(1), dim3(64), 0, m->stream, r);
+        ORBFE_HIP(hipGetLastError());
+        if ((st = m->down(frame_mp, m->s1, (size_t)N * 4))) return st;
+        if ((st = m->down(frame_mp_obs, m->s2, (size_t)N * 4))) return st;
+        if ((st = m->down(nmatches, m->scal, sizeof(int)))) return st;
+        ORBFE_HIP(hipStreamSynchronize(m->stream));
+        return ORBFE_OK;
+    });
+}
+
+int orbfe_is_in_frustum(orbfe_matcher* m, int n, const float* xyz, const float* normal,
+                        const float* min_dist, const float* max_dist, const float* tcw,
+                        const orbfe_camera* cam, float min_x, float max_x, float min_y,
+                        float max_y, float log_scale_factor, float viewing_cos_limit,
+                        uint8_t* in_view, float* proj_x, float* proj_y, float* proj_xr,
+                        int32_t* pred_level, float* view_cos) {
+    if (n < 0 || !tcw || !cam ||
+        (n && (!xyz || !normal || !min_dist || !max_dist || !in_view || !proj_x || !proj_y ||
+               !proj_xr || !pred_level || !view_cos)))
+        return ORBFE_ERR_ARG;
+    if (n == 0) return m ? ORBFE_OK : ORBFE_ERR_ARG;
+    return guarded(m, [&]() {
+        int st;
+        if ((st = m->up(m->m_f0, xyz, (size_t)n * 12))) return st;
+        if ((st = m->up(m->m_f1, normal, (size_t)n * 12))) return st;
+        if ((st = m->up(m->m_f2, min_dist, (size_t)n * 4))) return st;
+        if ((st = m->up(m->m_f3, max_dist, (size_t)n * 4))) return st;
+        for (DevBuf* b : {&m->o_f0, &m->o_f1, &m->o_f2, &m->o_f3, &m->o_i})
+            if ((st = b->ensure((size_t)n * 4))) return st;
+        if ((st = m->o_u.ensure(n))) return st;
+        // outputs of map points that fail a check keep their previous scratch values
+        if ((st = m->up(m->o_f0, proj_x, (size_t)n * 4))) return st;
+        if ((st = m->up(m->o_f1, proj_y, (size_t)n * 4))) return st;
+        if ((st = m->up(m->o_f2, proj_xr, (size_t)n * 4))) return st;
+        if ((st = m->up(m->o_f3, view_cos, (size_t)n * 4))) return st;
+        if ((st = m->up(m->o_i, pred_level, (size_t)n * 4))) return st;
+        FrustumArgs a;
+        a.n = n;
+        a.xyz = m->m_f0.as<float>();
+        a.normal = m->m_f1.as<float>();
+        a.mind = m->m_f2.as<float>();
+        a.maxd = m->m_f3.as<float>();
+        std::memcpy(a.T, tcw, sizeof(a.T));
+        camera_center(tcw, a.ow);
+        a.fx = cam->fx;
+        a.fy = cam->fy;
+        a.cx = cam->cx;
+        a.cy = cam->cy;
+        a.bf = cam->bf;
+        a.minx = min_x;
+        a.maxx = max_x;
+        a.miny = min_y;
+        a.maxy = max_y;
+        a.log_scale = log_scale_factor;
+        a.cos_limit = viewing_cos_limit;
+        a.in_view = m->o_u.as<uint8_t>();
+        a.px = m->o_f0.as<float>();
+        a.py = m->o_f1.as<float>();
+        a.pxr = m->o_f2.as<float>();
+        a.lvl = m->o_i.as<int>();
+        a.vcos = m->o_f3.as<float>();
+        hipLaunchKernelGGL(frustum_kernel, dim3((n + 255) / 256), dim3(256), 0, m->stream, a);
+        ORBFE_HIP(hipGetLastError());
+        if ((st = m->down(in_view, m->o_u, n))) return st;
+        if ((st = m->down(proj_x, m->o_f0, (size_t)n * 4))) return st;
+        if ((st = m->down(proj_y, m->o_f1, (size_t)n * 4))) return st;
+        if ((st = m->down(proj_xr, m->o_f2, (size_t)n * 4))) return st;
+        if ((st = m->down(pred_level, m->o_i, (size_t)n * 4))) return st;
+        if ((st = m->down(view_cos, m->o_f3, (size_t)n * 4))) return st;
+        ORBFE_HIP(hipStreamSynchronize(m->stream));
+        return ORBFE_OK;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,107 @@
+"""GPU parity of the matchers (liborbfe.so through the C ABI) against the CPU oracle.
+
+Every output is an index, a count or a distance, so every comparison is exact: Hamming
+distances, brute-force (best_idx, best, second), vnMatches12 + nmatches + updated
+vbPrevMatched (SearchForInitialization), the per-keypoint MapPoint assignment +
+Observations + nmatches (both SearchByProjection overloads), and isInFrustum's outputs.
+"""
+import numpy as np
+import pytest
+
+import oracle
+import scenarios as S
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mt():
+    from orbslam_mapsave_amd.native import ORBmatcher
+    m = ORBmatcher(0.9, True, device=0)
+    yield m
+    m.close()
+
+
+def test_hamming_random(mt):
+    rng = np.random.Generator(np.random.PCG64(1))
+    a, b = S.random_desc(rng, 5000), S.random_desc(rng, 5000)
+    assert np.array_equal(mt.DescriptorDistance(a, b), oracle.hamming(a, b))
+    assert mt.DescriptorDistance(a[0], a[0]) == 0
+    assert mt.DescriptorDistance(a[0], ~a[0]) == 256
+
+
+@pytest.mark.parametrize("nq,nr", [(1000, 2000), (1, 1), (300, 7), (513, 1500)])
+def test_bf_match_random(mt, nq, nr):
+    rng = np.random.Generator(np.random.PCG64(nq + nr))
+    q, r = S.random_desc(rng, nq), S.random_desc(rng, nr)
+    got = mt.bf_match(q, r)
+    exp = oracle.bf_match(q, r)
+    for g, e in zip(got, exp):
+        assert np.array_equal(g, e)
+
+
+def test_bf_match_ties(mt):
+    rng = np.random.Generator(np.random.PCG64(3))
+    base = S.random_desc(rng, 4)
+    r = base[rng.integers(0, 4, 700)]       # many exact duplicates: first-wins ties
+    q = S.flip_bits(base[rng.integers(0, 4, 300)], rng, 0.02)
+    for g, e in zip(mt.bf_match(q, r), oracle.bf_match(q, r)):
+        assert np.array_equal(g, e)
+
+
+def test_bf_match_extracted(mt):
+    f1, f2 = S.extract_frame(0, 1000), S.extract_frame(1, 2000)
+    for g, e in zip(mt.bf_match(f1.desc, f2.desc), oracle.bf_match(f1.desc, f2.desc)):
+        assert np.array_equal(g, e)
+
+
+@pytest.mark.parametrize("seed,window,check_ori", [(0, 100, True), (1, 100, True), (2, 50, False),
+                                                   (3, 200, True)])
+def test_search_for_initialization(mt, seed, window, check_ori):
+    from orbslam_mapsave_amd.native import ORBmatcher
+    m = ORBmatcher(0.9, check_ori, device=0)
+    f1, f2, prev = S.sfi_case(seed)
+    g12, gn, gprev = m.SearchForInitialization(f1, f2, prev, window)
+    e12, en, eprev = oracle.search_for_initialization(f1, f2, prev, window, 0.9, check_ori)
+    assert gn == en
+    assert np.array_equal(g12, e12)
+    assert np.array_equal(gprev, eprev)
+    m.close()
+
+
+@pytest.mark.parametrize("seed,th,stereo,prior,m", [(0, 1.0, False, False, 50000),
+                                                    (1, 3.0, True, True, 20000),
+                                                    (2, 5.0, False, True, 5000)])
+def test_search_by_projection_local(seed, th, stereo, prior, m):
+    from orbslam_mapsave_amd.native import ORBmatcher
+    mt = ORBmatcher(0.8, True, device=0)
+    f, mps, fmp, fobs, ids = S.sbp_local_case(seed, m, stereo=stereo, prior=prior)
+    g = mt.SearchByProjection(f, mps, th, fmp, fobs, ids)
+    e = oracle.search_by_projection_local(f, mps, th, 0.8, fmp, fobs, ids)
+    assert g[2] == e[2]
+    assert np.array_equal(g[0], e[0])
+    assert np.array_equal(g[1], e[1])
+    mt.close()
+
+
+@pytest.mark.parametrize("seed,stereo,mono,th", [(0, False, True, 15.0), (1, False, True, 30.0),
+                                                 (2, True, False, 7.0)])
+def test_search_by_projection_last(mt, seed, stereo, mono, th):
+    c = S.sbp_last_case(seed, stereo=stereo)
+    args = (c["cur"], c["tcw_cur"], c["cam"], c["last_keys"], c["last_valid"], c["last_outlier"],
+            c["last_xyz"], c["last_desc"], c["last_nobs"], c["tcw_last"])
+    g = mt.SearchByProjectionLast(*args, th, mono, last_ids=c["last_ids"])
+    e = oracle.search_by_projection_last(*args, th, mono, True, last_ids=c["last_ids"])
+    assert g[2] == e[2]
+    assert np.array_equal(g[0], e[0])
+    assert np.array_equal(g[1], e[1])
+
+
+def test_is_in_frustum(mt):
+    fc = S.frustum_case(0)
+    g = mt.is_in_frustum(**fc)
+    e = oracle.is_in_frustum(**fc)
+    assert np.array_equal(g[0], e[0])
+    sel = e[0] == 1
+    for a, b in zip(g[1:], e[1:]):
+        assert np.array_equal(a[sel], b[sel])
