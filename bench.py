@@ -1,0 +1,236 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X ORB front-end (the hot path of skaegy/ORBSLAM_MapSave).
+
+Default workload (BASELINE.json configs[2], the config its metric "frames/sec ORB
+extract+match, 640x480 @1000 kp" is quoted on): every step, every rank extracts a batch of B
+synthetic 640x480 frames (ORBextractor(1000, 1.2, 8, 32, 7), ORB_RGB640x480.yaml with
+nFeatures=1000) and brute-force Hamming-matches each frame's descriptors against a 2000-kp
+reference frame (best / second / index per query).  Frames are independent, so N ranks shard
+them with no data-path collective ("scaling": "weak").  Inputs are resident in HBM before the
+timed region; outputs stay on the device.
+
+``--config c4`` runs BASELINE configs[3] instead: 1920x1080 @2000 kp, a global batch of 256
+frames sharded round-robin over the ranks, an RCCL all-gather of the descriptor slabs and a
+frame f vs frame f-1 match.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 through torch.distributed.run
+(one process per GPU, RCCL).  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "frames/sec ORB extract+match, 640×480 @1000 kp, 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md "HBM3E peak BW 8.0 TB/s spec"
+STAGES = ("mask", "resize", "fast", "octree", "blur", "describe")
+
+
+def level_sizes(w, h, nlevels=8, scale=1.2):
+    s = np.float32(1.0)
+    out = []
+    for l in range(nlevels):
+        inv = np.float32(1.0) / s
+        out.append((int(np.rint(np.float32(w) * inv)), int(np.rint(np.float32(h) * inv))))
+        s = np.float32(np.float64(s) * np.float64(np.float32(scale)))
+    return out
+
+
+def algorithmic_bytes(stage: str, w: int, h: int, nkp: float) -> float:
+    """Per-frame algorithmic bytes of one stage (DESIGN.md "Roofline")."""
+    P = [a * b for a, b in level_sizes(w, h)]
+    if stage == "resize":   # cascaded: read level l-1, write level l
+        return float(sum(P[:-1]) + sum(P[1:]))
+    if stage == "fast":     # every level read once
+        return float(sum(P))
+    if stage == "blur":     # read + write every level
+        return float(2 * sum(P))
+    if stage == "describe":  # 31x31 angle patch + 512 samples per keypoint, kp + desc out
+        return float(nkp * (961 + 512 + 28 + 32))
+    if stage == "octree":   # the level's FAST candidates (4 B) read, keypoints (4 B) written
+        return float(nkp * 8)
+    return 0.0
+
+
+def cpu_baseline(frames: np.ndarray, ref_desc: np.ndarray, budget_s: float) -> dict:
+    """The CPU oracle (a port of the reference CPU path, oracle/orb_oracle.cpp) on one host
+    thread: extract(1000 kp) + brute-force match vs the 2000-kp reference, frame after frame,
+    until `budget_s` of CPU work."""
+    import oracle  # test infrastructure: the cpu_baseline leg is allowed to load it
+    p = oracle.params(1000, 1.2, 8, 32, 7)
+    done, t0 = 0, time.perf_counter()
+    while True:
+        kps, desc = oracle.extract(p, frames[done % len(frames)])
+        oracle.bf_match(desc, ref_desc)
+        done += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s and done >= 5:
+            break
+    return {"value": round(done / el, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{done} of the bench's 640x480 frames, extract(1000 kp) + BF match vs the "
+                      f"2000-kp reference, 1 thread, oracle/orb_oracle.cpp -O3, {el:.1f} s"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="frames per rank per step")
+    ap.add_argument("--config", default="c3", choices=["c3", "c4"])
+    ap.add_argument("--distinct", type=int, default=32, help="distinct synthetic seeds (cycled)")
+    ap.add_argument("--cpu-budget", type=float, default=15.0,
+                    help="seconds of CPU-baseline work on rank 0 (0 disables)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from orbslam_mapsave_amd.native import ORBextractor, ORBmatcher
+    from orbslam_mapsave_amd.synth import synthetic_batch, synthetic_frame
+
+    if args.config == "c3":
+        W, H, NF, NREF = 640, 480, 1000, 2000
+        B = args.batch
+        workload = ("configs[2]: 640x480 extract (8-level pyramid, FAST-9, oct-tree, rBRIEF, "
+                    "1000 kp) + brute-force Hamming match vs a 2000-kp reference frame")
+    else:
+        W, H, NF, NREF = 1920, 1080, 2000, 2000
+        B = max(1, 256 // world)
+        workload = ("configs[3]: 1920x1080 @2000 kp, global batch 256 sharded round-robin, "
+                    "RCCL all-gather of descriptor slabs, frame f vs f-1 match")
+
+    frames_np = synthetic_batch(B, W, H, first_seed=1000 * rank, distinct=args.distinct)
+    frames = torch.from_numpy(frames_np).to(dev)
+    stream = torch.cuda.current_stream(dev)
+
+    ex = ORBextractor(NF, 1.2, 8, 32, 7, device=local, max_width=W, max_height=H, max_batch=B)
+    ex.set_stream(stream.cuda_stream)
+    mt = ORBmatcher(0.9, True, device=local)
+    mt.set_stream(stream.cuda_stream)
+    cap = ex.capacity()
+    d_kps = torch.empty((B, cap * 28), dtype=torch.uint8, device=dev)
+    d_desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
+    d_n = torch.zeros(B, dtype=torch.int32, device=dev)
+    d_out = torch.empty((B, cap, 3), dtype=torch.int32, device=dev)
+
+    # reference frame (config 3): extracted once on the GPU with the 2x-feature extractor
+    ref_np = synthetic_frame(999_999, W, H)
+    ex_ref = ORBextractor(NREF, 1.2, 8, 32, 7, device=local, max_width=W, max_height=H)
+    ref_kps, ref_desc_np = ex_ref(ref_np)
+    ex_ref.close()
+    ref_desc = torch.from_numpy(np.ascontiguousarray(ref_desc_np)).to(dev)
+    d_nr = torch.full((B,), len(ref_desc_np), dtype=torch.int32, device=dev)
+
+    if args.config == "c4":
+        g_desc = torch.zeros((world * B, cap, 32), dtype=torch.uint8, device=dev)
+        g_n = torch.zeros(world * B, dtype=torch.int32, device=dev)
+        d_prev = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
+        d_prev_n = torch.zeros(B, dtype=torch.int32, device=dev)
+        from orbslam_mapsave_amd.shard import gather_slabs, predecessor_index
+        pred = torch.as_tensor(predecessor_index(rank, world, B), device=dev)
+
+    def step():
+        ex.extract_batch_device(frames.data_ptr(), B, W, H, W, W * H, d_kps.data_ptr(), cap,
+                                d_desc.data_ptr(), d_n.data_ptr())
+        if args.config == "c3":
+            mt.bf_match_batch_device(d_desc.data_ptr(), cap * 32, d_n.data_ptr(), cap,
+                                     ref_desc.data_ptr(), 0, d_nr.data_ptr(), B, d_out.data_ptr())
+        else:
+            gather_slabs(d_desc, d_n, g_desc, g_n, world)
+            torch.index_select(g_desc, 0, pred, out=d_prev)
+            torch.index_select(g_n, 0, pred, out=d_prev_n)
+            mt.bf_match_batch_device(d_desc.data_ptr(), cap * 32, d_n.data_ptr(), cap,
+                                     d_prev.data_ptr(), cap * 32, d_prev_n.data_ptr(), B,
+                                     d_out.data_ptr())
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    ex.profile(True)
+    ex.profile_read()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    dt = time.perf_counter() - t0
+    stages = ex.profile_read()
+    ex.profile(False)
+    nkp = float(d_n.float().mean().item())
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    if rank == 0:
+        K = args.steps
+        value = world * B * K / dt
+        per_step = {s: stages[s][0] / K for s in STAGES}
+        dom = max(STAGES, key=lambda s: stages[s][0])
+        dom_ms, dom_launches = stages[dom]
+        frames_per_launch = B * K * (1 if dom != "resize" else 7) / max(dom_launches, 1)
+        bytes_per_step = algorithmic_bytes(dom, W, H, nkp) * B
+        achieved = bytes_per_step / (dom_ms / K / 1e3) / 1e9 if dom_ms > 0 else 0.0
+        traffic = None
+        tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+        if os.path.exists(tpath):
+            with open(tpath) as fh:
+                traffic = json.load(fh).get(dom)
+        roof = {"bound": "hbm", "kernel": f"{dom}_kernel", "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": traffic,
+                "bytes_per_launch": round(bytes_per_step * K / max(dom_launches, 1)),
+                "avg_launch_ms": round(dom_ms / max(dom_launches, 1), 4)}
+        cpu = None
+        if world == 1 and args.cpu_budget > 0 and args.config == "c3":
+            cpu = cpu_baseline(frames_np[:args.distinct], ref_desc_np, args.cpu_budget)
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
+            "steps": K, "warmup": args.warmup, "ms_per_step": round(dt / K * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak" if args.config == "c3" else "strong",
+            "vs_baseline": None, "dtype": "u8",
+            "data": f"synthetic: seeded textured {W}x{H} u8 frames ({args.distinct} distinct "
+                    f"seeds per rank, cycled), resident in HBM",
+            "config": {"workload": workload, "frames_per_rank_per_step": B,
+                       "global_batch": B * world, "nfeatures": NF, "reference_kp": len(ref_desc_np),
+                       "mean_kp_per_frame": round(nkp, 1),
+                       "parallelism": (f"frame-sharded x{world}, no data-path collective"
+                                       if args.config == "c3" else f"frame-sharded x{world} + RCCL all-gather")},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "stage_ms_per_step": {s: round(v, 4) for s, v in per_step.items()},
+        }
+        if cpu:
+            line["gpu_over_cpu"] = round(value / cpu["value"], 1)
+        print(json.dumps(line), flush=True)
+    ex.close()
+    mt.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -117,6 +117,20 @@ int orbfe_extract_batch_device(orbfe_extractor* h, const uint8_t* d_imgs, int n,
 int orbfe_set_stream(orbfe_extractor* h, void* hip_stream);
 int orbfe_synchronize(orbfe_extractor* h);
 
+/* Per-kernel timing of the extraction pipeline: when enabled, a HIP event pair is recorded on
+ * the handle's stream around every kernel launch.  orbfe_profile_read synchronizes the stream
+ * and returns, per stage (ORBFE_STAGE_*), the summed duration in ms and the launch count since
+ * the previous read.  Used by bench.py for the roofline figure; off by default. */
+#define ORBFE_STAGE_MASK     0
+#define ORBFE_STAGE_RESIZE   1
+#define ORBFE_STAGE_FAST     2
+#define ORBFE_STAGE_OCTREE   3
+#define ORBFE_STAGE_BLUR     4
+#define ORBFE_STAGE_DESCRIBE 5
+#define ORBFE_STAGE_COUNT    6
+int orbfe_profile(orbfe_extractor* h, int enable);
+int orbfe_profile_read(orbfe_extractor* h, double* total_ms, int32_t* launches);
+
 /* Pyramid access — replaces the public member mvImagePyramid (ORBextractor.h:90) read by
  * stereo matching (Frame.cc:589, 679, 696).  Copies level `level` of frame `frame` of the
  * most recent extraction (interior pixels only, rows w bytes apart) into `out`

@@ -61,6 +61,40 @@ int check_device(int device) {
     return ORBFE_OK;
 }
 
+// Event pairs around kernel launches, read back by orbfe_profile_read.
+struct Profiler {
+    bool on = false;
+    std::vector<hipEvent_t> a, b;
+    std::vector<int> kind;
+    size_t used = 0;
+    void begin(hipStream_t s, int k) {
+        if (!on) return;
+        if (used == a.size()) {
+            hipEvent_t e0, e1;
+            if (hipEventCreate(&e0) != hipSuccess) return;
+            if (hipEventCreate(&e1) != hipSuccess) { hipEventDestroy(e0); return; }
+            a.push_back(e0);
+            b.push_back(e1);
+            kind.push_back(k);
+        }
+        kind[used] = k;
+        hipEventRecord(a[used], s);
+    }
+    void end(hipStream_t s) {
+        if (!on || used == a.size()) return;
+        hipEventRecord(b[used], s);
+        ++used;
+    }
+    void release() {
+        for (hipEvent_t e : a) hipEventDestroy(e);
+        for (hipEvent_t e : b) hipEventDestroy(e);
+        a.clear();
+        b.clear();
+        kind.clear();
+        used = 0;
+    }
+};
+
 }  // namespace orbfe
 
 using namespace orbfe;
@@ -78,6 +112,7 @@ struct orbfe_extractor {
     // last run, for the probes
     int last_n = 0;
     LevelPtr last_pyr[kMaxLevels] = {};
+    Profiler prof;
     std::vector<orbfe_keypoint> h_kps;
     std::vector<uint8_t> h_desc;
     std::vector<int32_t> h_n;
@@ -138,10 +173,12 @@ struct orbfe_extractor {
         for (int l = 1; l < L; ++l) {
             const LevelGeo& lv = g.geo.lv[l];
             dim3 block(64, 4), grid((lv.w + 255) / 256, (lv.h + 3) / 4, n);
+            prof.begin(stream, ORBFE_STAGE_RESIZE);
             hipLaunchKernelGGL(resize_kernel, grid, block, 0, stream, lp[l - 1].base,
                                lp[l - 1].fpitch, lp[l - 1].pitch, const_cast<uint8_t*>(lp[l].base),
                                lp[l].fpitch, lp[l].pitch, lv.w, lv.h,
                                xtab.as<int>() + g.xoff[l], ytab.as<int>() + g.yoff[l]);
+            prof.end(stream);
         }
         // K2 FAST per cell
         const int ncells = (int)g.cells.size();
@@ -155,7 +192,9 @@ struct orbfe_extractor {
             fa.cell_cnt = cell_cnt.as<int>();
             fa.cell_keys = cell_keys.as<uint32_t>();
             for (int l = 0; l < L; ++l) fa.pyr[l] = lp[l];
+            prof.begin(stream, ORBFE_STAGE_FAST);
             hipLaunchKernelGGL(fast_kernel, dim3(ncells, n), dim3(kFastBlockSize), 0, stream, fa);
+            prof.end(stream);
         }
         // K3 oct-tree per (frame, level)
         OctArgs oa;
@@ -171,7 +210,9 @@ struct orbfe_extractor {
         oa.oct_cnt = oct_cnt.as<int>();
         oa.ncap_max = g.ncap_max;
         oa.sort_cap = g.sort_cap;
+        prof.begin(stream, ORBFE_STAGE_OCTREE);
         hipLaunchKernelGGL(octree_kernel, dim3(L, n), dim3(kOctBlockSize), g.oct_lds, stream, oa);
+        prof.end(stream);
         // K4 blur
         BlurArgs ba;
         ba.nlevels = L;
@@ -183,7 +224,9 @@ struct orbfe_extractor {
             ba.dst[l] = bp[l];
         }
         for (int i = 0; i < 4; ++i) ba.taps[i] = tab.taps[i];
+        prof.begin(stream, ORBFE_STAGE_BLUR);
         hipLaunchKernelGGL(blur_kernel, dim3(g.tiles_total, n), dim3(256), 0, stream, ba);
+        prof.end(stream);
         // K5 describe
         DescArgs da;
         da.nlevels = L;
@@ -202,8 +245,10 @@ struct orbfe_extractor {
         da.desc = d_desc;
         da.n_out = d_n;
         const int waves = kDescBlockSize / 64;
+        prof.begin(stream, ORBFE_STAGE_DESCRIBE);
         hipLaunchKernelGGL(describe_kernel, dim3((g.geo.out_total + waves - 1) / waves, n),
                            dim3(kDescBlockSize), 0, stream, da);
+        prof.end(stream);
         ORBFE_HIP(hipGetLastError());
         last_n = n;
         for (int l = 0; l < L; ++l) last_pyr[l] = lp[l];
@@ -264,6 +309,7 @@ struct orbfe_extractor {
         for (DevBuf* b : {&cells, &xtab, &ytab, &pyr, &blur, &cell_cnt, &cell_keys, &keys, &act,
                           &oct_out, &oct_cnt, &out_kps, &out_desc, &out_n})
             b->release();
+        prof.release();
         if (own) hipStreamDestroy(own);
     }
 };
@@ -437,15 +483,42 @@ int orbfe_extract_batch_device(orbfe_extractor* h, const uint8_t* d_imgs, int n,
         LevelPtr lp0{d_imgs, (long long)frame_pitch, (int)stride};
         if (d_masks) {
             uint8_t* p0 = h->pyr.as<uint8_t>() + l0.off;
+            h->prof.begin(h->stream, ORBFE_STAGE_MASK);
             hipLaunchKernelGGL(mask_kernel, dim3((w + 255) / 256, hgt, n), dim3(256), 0,
                                h->stream, d_imgs, (long long)frame_pitch, (int)stride, d_masks,
                                (long long)frame_pitch, (int)stride, p0, g.slab, l0.pitch, w, hgt);
+            h->prof.end(h->stream);
             lp0 = LevelPtr{p0, g.slab, l0.pitch};
         }
         return h->run(n, lp0, d_kps, kps_cap, d_desc, d_n_out);
     } catch (...) {
         return ORBFE_ERR_HIP;
     }
+}
+
+int orbfe_profile(orbfe_extractor* h, int enable) {
+    if (!h) return ORBFE_ERR_ARG;
+    h->prof.on = enable != 0;
+    h->prof.used = 0;
+    return ORBFE_OK;
+}
+
+int orbfe_profile_read(orbfe_extractor* h, double* total_ms, int32_t* launches) {
+    if (!h || !total_ms || !launches) return ORBFE_ERR_ARG;
+    DeviceGuard dg(h->device);
+    ORBFE_HIP(hipStreamSynchronize(h->stream));
+    for (int k = 0; k < ORBFE_STAGE_COUNT; ++k) {
+        total_ms[k] = 0;
+        launches[k] = 0;
+    }
+    for (size_t i = 0; i < h->prof.used; ++i) {
+        float ms = 0.f;
+        ORBFE_HIP(hipEventElapsedTime(&ms, h->prof.a[i], h->prof.b[i]));
+        total_ms[h->prof.kind[i]] += ms;
+        launches[h->prof.kind[i]] += 1;
+    }
+    h->prof.used = 0;
+    return ORBFE_OK;
 }
 
 int orbfe_set_stream(orbfe_extractor* h, void* s) {

@@ -29,7 +29,7 @@ EXPORTED = [
     "orbfe_create", "orbfe_destroy", "orbfe_get_levels", "orbfe_get_scale_factor",
     "orbfe_get_scale_tables", "orbfe_get_features_per_level", "orbfe_keypoint_capacity",
     "orbfe_extract", "orbfe_extract_batch", "orbfe_extract_batch_device", "orbfe_set_stream",
-    "orbfe_synchronize", "orbfe_get_level", "orbfe_get_blurred_level", "orbfe_get_fast_keys",
+    "orbfe_synchronize", "orbfe_profile", "orbfe_profile_read", "orbfe_get_level", "orbfe_get_blurred_level", "orbfe_get_fast_keys",
     "orbfe_matcher_create", "orbfe_matcher_destroy", "orbfe_matcher_set_stream", "orbfe_hamming",
     "orbfe_bf_match", "orbfe_bf_match_batch_device", "orbfe_search_for_initialization",
     "orbfe_search_by_projection_local", "orbfe_search_by_projection_last", "orbfe_is_in_frustum",
@@ -174,6 +174,19 @@ class ORBextractor:
 
     def synchronize(self) -> None:
         _check("orbfe_synchronize", lib().orbfe_synchronize(self._h))
+
+    STAGES = ("mask", "resize", "fast", "octree", "blur", "describe")
+
+    def profile(self, enable: bool) -> None:
+        """Record a HIP event pair around every kernel launch (orbfe_profile)."""
+        _check("orbfe_profile", lib().orbfe_profile(self._h, int(enable)))
+
+    def profile_read(self) -> dict:
+        """{stage: (total_ms, launches)} since the previous read (orbfe_profile_read)."""
+        ms = np.zeros(len(self.STAGES), np.float64)
+        n = np.zeros(len(self.STAGES), np.int32)
+        _check("orbfe_profile_read", lib().orbfe_profile_read(self._h, ptr(ms), ptr(n)))
+        return {s: (float(ms[i]), int(n[i])) for i, s in enumerate(self.STAGES)}
 
     # ---- probes of the last extraction
     def _level(self, fn, frame: int, level: int) -> np.ndarray:
