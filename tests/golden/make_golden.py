@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Generates tests/golden/*.npz from the CPU oracle (run from the repo root).
+
+The reference (skaegy/ORBSLAM_MapSave) holds no tests, fixtures or golden vectors for this path
+and cannot be built here (OpenCV/Boost/Eigen absent), so these fixtures are regression pins of
+the oracle's restatement, not reference outputs ("parity unpinned").  They freeze:
+  * A1 tables (scale factors, budgets, umax) for the YAML configs;
+  * pyramid level checksums + one full small level, FAST candidate lists of two levels, final
+    keypoints (28 B) + descriptors (32 B) for seeds 0..4 at 640x480 and seed 0 at 1920x1080;
+  * SearchForInitialization / SearchByProjection (both) / isInFrustum outputs of tests/scenarios.
+"""
+import hashlib
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+
+import oracle  # noqa: E402
+import scenarios as S  # noqa: E402
+from orbslam_mapsave_amd.synth import synthetic_frame, synthetic_mask  # noqa: E402
+
+OUT = os.path.join(ROOT, "tests", "golden")
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def extract_fixture():
+    d = {}
+    p = oracle.params(1000, 1.2, 8, 32, 7)
+    for seed in range(5):
+        img = synthetic_frame(seed, 640, 480)
+        d[f"img_sha_{seed}"] = sha(img)
+        levels = oracle.pyramid(p, img)
+        d[f"pyr_sha_{seed}"] = np.array([sha(l) for l in levels])
+        kps, desc = oracle.extract(p, img)
+        d[f"kps_{seed}"] = kps
+        d[f"desc_{seed}"] = desc
+        if seed == 0:
+            d["level7_0"] = levels[7]
+            d["blur7_0"] = oracle.gaussian_blur(levels[7])
+            d["fast_l0_0"] = oracle.fast_keys(p, levels[0])
+            d["fast_l5_0"] = oracle.fast_keys(p, levels[5])
+    img = synthetic_frame(3, 640, 480)
+    m = synthetic_mask(640, 480, 3)
+    kps, desc = oracle.extract(p, img, m)
+    d["kps_mask3"], d["desc_mask3"] = kps, desc
+    lc = synthetic_frame(7, 640, 480, kind="low_contrast")
+    kps, desc = oracle.extract(p, lc)
+    d["kps_lowc7"], d["desc_lowc7"] = kps, desc
+    p2 = oracle.params(2000, 1.2, 8, 20, 7)
+    big = synthetic_frame(0, 1920, 1080)
+    kps, desc = oracle.extract(p2, big)
+    d["kps_1080_sha"], d["desc_1080_sha"], d["n_1080"] = sha(kps), sha(desc), len(kps)
+    for name, pp in (("p1000", p), ("p2000", oracle.params(2000, 1.2, 8, 20, 7)),
+                     ("rgbd", oracle.params(1000, 1.5, 4, 20, 7))):
+        t = oracle.tables(pp)
+        for k, v in t.items():
+            d[f"tab_{name}_{k}"] = v
+    return d
+
+
+def match_fixture():
+    d = {}
+    f1, f2, prev = S.sfi_case(0)
+    m12, nm, pv = oracle.search_for_initialization(f1, f2, prev, 100, 0.9, True)
+    d["sfi_m12"], d["sfi_nm"], d["sfi_prev_sha"] = m12, nm, sha(pv)
+    f, mps, fmp, fobs, ids = S.sbp_local_case(0, 50000)
+    g = oracle.search_by_projection_local(f, mps, 1.0, 0.8, fmp, fobs, ids)
+    d["sbpl_fmp"], d["sbpl_fobs"], d["sbpl_nm"] = g
+    c = S.sbp_last_case(0)
+    args = (c["cur"], c["tcw_cur"], c["cam"], c["last_keys"], c["last_valid"],
+            c["last_outlier"], c["last_xyz"], c["last_desc"], c["last_nobs"], c["tcw_last"])
+    g = oracle.search_by_projection_last(*args, 15.0, True, True, last_ids=c["last_ids"])
+    d["sbpk_fmp"], d["sbpk_fobs"], d["sbpk_nm"] = g
+    fc = S.frustum_case(0)
+    r = oracle.is_in_frustum(**fc)
+    d["fr_in"], d["fr_lvl"] = r[0], np.where(r[0] == 1, r[4], -99)
+    return d
+
+
+if __name__ == "__main__":
+    np.savez_compressed(os.path.join(OUT, "extract_golden.npz"), **extract_fixture())
+    np.savez_compressed(os.path.join(OUT, "match_golden.npz"), **match_fixture())
+    for f in sorted(os.listdir(OUT)):
+        print(f, os.path.getsize(os.path.join(OUT, f)))
