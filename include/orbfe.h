@@ -197,10 +197,16 @@ int orbfe_bf_match(orbfe_matcher* m, const uint8_t* q, int nq, const uint8_t* r,
                    int32_t* best_idx, int32_t* best_dist, int32_t* second_dist);
 /* Device-resident batched form: `nb` independent (query-set, reference-set) problems;
  * problem b reads d_q + b*q_pitch (nq_b = d_nq[b] rows) against d_r + b*r_pitch
- * (nr_b = d_nr[b] rows) and writes d_out + b*nq_cap*3 as (best_idx, best, second) triples. */
+ * (nr_b = d_nr[b] rows) and writes d_out + b*nq_cap*3 as (best_idx, best, second) triples.
+ * Reference sets hold fewer than 65536 rows. */
 int orbfe_bf_match_batch_device(orbfe_matcher* m, const uint8_t* d_q, size_t q_pitch,
                                 const int32_t* d_nq, int nq_cap, const uint8_t* d_r,
                                 size_t r_pitch, const int32_t* d_nr, int nb, int32_t* d_out);
+
+/* Timing of orbfe_bf_match_batch_device launches (dispatch-bound HIP events, as
+ * orbfe_profile): summed ms and launch count since the previous read. */
+int orbfe_matcher_profile(orbfe_matcher* m, int enable);
+int orbfe_matcher_profile_read(orbfe_matcher* m, double* total_ms, int32_t* launches);
 
 /* ORBmatcher::SearchForInitialization (ORBmatcher.cc:408-523), matcher built as
  * ORBmatcher(nnratio, check_ori) (Tracking.cc:843).  prev_matched: inout F1.n (x,y) pairs

@@ -2,6 +2,7 @@
 // Replaces ORBextractor's public surface (ORBextractor.h:56-90); see the header for the
 // per-function citations.  No CPU compute path exists: every result comes from the kernels.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -61,28 +62,28 @@ int check_device(int device) {
     return ORBFE_OK;
 }
 
-// Event pairs around kernel launches, read back by orbfe_profile_read.
+// Start/stop events bound to kernel dispatches (hipExtLaunchKernel records them from the
+// dispatch packet itself, so a pair brackets exactly one kernel), read by orbfe_profile_read.
 struct Profiler {
     bool on = false;
     std::vector<hipEvent_t> a, b;
     std::vector<int> kind;
     size_t used = 0;
-    void begin(hipStream_t s, int k) {
+    // Returns the event pair for the next launch of stage k (nullptrs when off).
+    void slot(int k, hipEvent_t* e0, hipEvent_t* e1) {
+        *e0 = *e1 = nullptr;
         if (!on) return;
         if (used == a.size()) {
-            hipEvent_t e0, e1;
-            if (hipEventCreate(&e0) != hipSuccess) return;
-            if (hipEventCreate(&e1) != hipSuccess) { hipEventDestroy(e0); return; }
-            a.push_back(e0);
-            b.push_back(e1);
+            hipEvent_t x, y;
+            if (hipEventCreate(&x) != hipSuccess) return;
+            if (hipEventCreate(&y) != hipSuccess) { hipEventDestroy(x); return; }
+            a.push_back(x);
+            b.push_back(y);
             kind.push_back(k);
         }
         kind[used] = k;
-        hipEventRecord(a[used], s);
-    }
-    void end(hipStream_t s) {
-        if (!on || used == a.size()) return;
-        hipEventRecord(b[used], s);
+        *e0 = a[used];
+        *e1 = b[used];
         ++used;
     }
     void release() {
@@ -94,6 +95,14 @@ struct Profiler {
         used = 0;
     }
 };
+
+// Kernel launch through hipExtLaunchKernelGGL with the stage's profiling events.
+#define ORBFE_LAUNCH(prof, stage, kernel, grid, block, shmem, stream, ...)                 \
+    do {                                                                                   \
+        hipEvent_t e0_, e1_;                                                               \
+        (prof).slot(stage, &e0_, &e1_);                                                    \
+        hipExtLaunchKernelGGL(kernel, grid, block, shmem, stream, e0_, e1_, 0, __VA_ARGS__); \
+    } while (0)
 
 }  // namespace orbfe
 
@@ -169,16 +178,21 @@ struct orbfe_extractor {
             bp[l] = LevelPtr{blur.as<uint8_t>() + lv.off, g.slab, lv.pitch};
         }
         lp[0] = l0;
-        // K1 cascaded pyramid
+        // K1 cascaded pyramid: one launch per level, 128 x 32 tiles of every frame
         for (int l = 1; l < L; ++l) {
-            const LevelGeo& lv = g.geo.lv[l];
-            dim3 block(64, 4), grid((lv.w + 255) / 256, (lv.h + 3) / 4, n);
-            prof.begin(stream, ORBFE_STAGE_RESIZE);
-            hipLaunchKernelGGL(resize_kernel, grid, block, 0, stream, lp[l - 1].base,
-                               lp[l - 1].fpitch, lp[l - 1].pitch, const_cast<uint8_t*>(lp[l].base),
-                               lp[l].fpitch, lp[l].pitch, lv.w, lv.h,
-                               xtab.as<int>() + g.xoff[l], ytab.as<int>() + g.yoff[l]);
-            prof.end(stream);
+            ResizeArgs ra;
+            ra.src = lp[l - 1];
+            ra.dst = lp[l];
+            ra.sw = g.geo.lv[l - 1].w;
+            ra.sh = g.geo.lv[l - 1].h;
+            ra.dw = g.geo.lv[l].w;
+            ra.dh = g.geo.lv[l].h;
+            ra.tiles_x = g.rs_tiles_x[l];
+            ra.lds_pitch = g.rs_pitch[l];
+            ra.xt = xtab.as<int>() + g.xoff[l];
+            ra.yt = ytab.as<int>() + g.yoff[l];
+            ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resize_kernel, dim3(g.rs_tiles[l], n), dim3(256),
+                         g.rs_lds[l], stream, ra);
         }
         // K2 FAST per cell
         const int ncells = (int)g.cells.size();
@@ -189,12 +203,13 @@ struct orbfe_extractor {
             fa.cell_cap_total = g.cell_cap_total;
             fa.ini_th = std::min(std::max(tab.p.ini_th_fast, 0), 255);
             fa.min_th = std::min(std::max(tab.p.min_th_fast, 0), 255);
+            fa.roi_pitch = g.roi_pitch;
+            fa.roi_rows = g.roi_rows;
+            fa.cand_max = g.cand_max;
             fa.cell_cnt = cell_cnt.as<int>();
             fa.cell_keys = cell_keys.as<uint32_t>();
             for (int l = 0; l < L; ++l) fa.pyr[l] = lp[l];
-            prof.begin(stream, ORBFE_STAGE_FAST);
-            hipLaunchKernelGGL(fast_kernel, dim3(ncells, n), dim3(kFastBlockSize), 0, stream, fa);
-            prof.end(stream);
+            ORBFE_LAUNCH(prof, ORBFE_STAGE_FAST, fast_kernel, dim3(ncells, n), dim3(kFastBlockSize), g.fast_lds, stream, fa);
         }
         // K3 oct-tree per (frame, level)
         OctArgs oa;
@@ -210,9 +225,7 @@ struct orbfe_extractor {
         oa.oct_cnt = oct_cnt.as<int>();
         oa.ncap_max = g.ncap_max;
         oa.sort_cap = g.sort_cap;
-        prof.begin(stream, ORBFE_STAGE_OCTREE);
-        hipLaunchKernelGGL(octree_kernel, dim3(L, n), dim3(kOctBlockSize), g.oct_lds, stream, oa);
-        prof.end(stream);
+        ORBFE_LAUNCH(prof, ORBFE_STAGE_OCTREE, octree_kernel, dim3(L, n), dim3(kOctBlockSize), g.oct_lds, stream, oa);
         // K4 blur
         BlurArgs ba;
         ba.nlevels = L;
@@ -224,9 +237,7 @@ struct orbfe_extractor {
             ba.dst[l] = bp[l];
         }
         for (int i = 0; i < 4; ++i) ba.taps[i] = tab.taps[i];
-        prof.begin(stream, ORBFE_STAGE_BLUR);
-        hipLaunchKernelGGL(blur_kernel, dim3(g.tiles_total, n), dim3(256), 0, stream, ba);
-        prof.end(stream);
+        ORBFE_LAUNCH(prof, ORBFE_STAGE_BLUR, blur_kernel, dim3(g.tiles_total, n), dim3(256), 0, stream, ba);
         // K5 describe
         DescArgs da;
         da.nlevels = L;
@@ -245,10 +256,8 @@ struct orbfe_extractor {
         da.desc = d_desc;
         da.n_out = d_n;
         const int waves = kDescBlockSize / 64;
-        prof.begin(stream, ORBFE_STAGE_DESCRIBE);
-        hipLaunchKernelGGL(describe_kernel, dim3((g.geo.out_total + waves - 1) / waves, n),
+        ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, describe_kernel, dim3((g.geo.out_total + waves - 1) / waves, n),
                            dim3(kDescBlockSize), 0, stream, da);
-        prof.end(stream);
         ORBFE_HIP(hipGetLastError());
         last_n = n;
         for (int l = 0; l < L; ++l) last_pyr[l] = lp[l];
@@ -481,13 +490,19 @@ int orbfe_extract_batch_device(orbfe_extractor* h, const uint8_t* d_imgs, int n,
         const Plan& g = h->plan;
         const LevelGeo& l0 = g.geo.lv[0];
         LevelPtr lp0{d_imgs, (long long)frame_pitch, (int)stride};
+        const bool aligned = ((uintptr_t)d_imgs % 4 == 0) && stride % 4 == 0 && frame_pitch % 4 == 0;
+        if (!aligned && !d_masks) {  // kernels read level 0 as dwords: stage it in the slab
+            for (int f = 0; f < n; ++f)
+                ORBFE_HIP(hipMemcpy2DAsync(h->pyr.as<uint8_t>() + (size_t)f * g.slab + l0.off, l0.pitch,
+                                           d_imgs + (size_t)f * frame_pitch, stride, w, hgt,
+                                           hipMemcpyDeviceToDevice, h->stream));
+            lp0 = LevelPtr{h->pyr.as<uint8_t>() + l0.off, g.slab, l0.pitch};
+        }
         if (d_masks) {
             uint8_t* p0 = h->pyr.as<uint8_t>() + l0.off;
-            h->prof.begin(h->stream, ORBFE_STAGE_MASK);
-            hipLaunchKernelGGL(mask_kernel, dim3((w + 255) / 256, hgt, n), dim3(256), 0,
+            ORBFE_LAUNCH(h->prof, ORBFE_STAGE_MASK, mask_kernel, dim3((w + 255) / 256, hgt, n), dim3(256), 0,
                                h->stream, d_imgs, (long long)frame_pitch, (int)stride, d_masks,
                                (long long)frame_pitch, (int)stride, p0, g.slab, l0.pitch, w, hgt);
-            h->prof.end(h->stream);
             lp0 = LevelPtr{p0, g.slab, l0.pitch};
         }
         return h->run(n, lp0, d_kps, kps_cap, d_desc, d_n_out);

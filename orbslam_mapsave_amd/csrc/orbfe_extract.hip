@@ -57,39 +57,72 @@ __global__ void mask_kernel(const uint8_t* src, long long src_fpitch, int src_pi
 }
 
 // ---------------------------------------------------------------------------------------------
-// K1 — one pyramid level from the previous one (App. A.1, scalar FixedPtCast<int,uchar,22>).
-// Host-built tables: xt[3*dx] = {sx, min(sx+1,sw-1), a0 | a1<<16}; yt[3*dy] likewise with the
-// source rows clipped to [0, sh-1].  Each thread writes 4 consecutive pixels.
-__global__ __launch_bounds__(256) void resize_kernel(
-    const uint8_t* __restrict__ src, long long src_fpitch, int src_pitch,
-    uint8_t* __restrict__ dst, long long dst_fpitch, int dst_pitch, int dw, int dh,
-    const int* __restrict__ xt, const int* __restrict__ yt) {
-    const int f = blockIdx.z;
-    const int y = blockIdx.y * 4 + threadIdx.y;
-    const int x = (blockIdx.x * 64 + threadIdx.x) * 4;
-    if (y >= dh || x >= dw) return;
-    const int r0 = yt[3 * y], r1 = yt[3 * y + 1], bb = yt[3 * y + 2];
-    const int b0 = bb & 0xffff, b1 = (int)((unsigned)bb >> 16);
-    const uint8_t* s0 = src + f * src_fpitch + (long long)r0 * src_pitch;
-    const uint8_t* s1 = src + f * src_fpitch + (long long)r1 * src_pitch;
-    uint8_t* d = dst + f * dst_fpitch + (long long)y * dst_pitch;
-    uint32_t packed = 0;
-    const int n = min(4, dw - x);
+// K1 — one pyramid level from the previous one (App. A.1, scalar FixedPtCast<int,uchar,22>),
+// one launch per level covering every frame.  A workgroup makes a 128 x 32 output tile: the
+// source rows/cols the tile touches are staged in LDS with dword loads, then each thread makes
+// 4 x 4 pixels from host-built tables xt[3*dx] = {sx, min(sx+1,sw-1), a0 | a1<<16} and
+// yt[3*dy] = {sy0, sy1 clipped, b0 | b1<<16}.
+constexpr int kRsTW = 128, kRsTH = 32;
+__global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
+    const int f = blockIdx.y;
+    const int ox = (blockIdx.x % a.tiles_x) * kRsTW, oy = (blockIdx.x / a.tiles_x) * kRsTH;
+    const int ex = min(ox + kRsTW, a.dw) - 1, ey = min(oy + kRsTH, a.dh) - 1;
+    const int sy0 = a.yt[3 * oy], sy1 = a.yt[3 * ey + 1];
+    const int sx0 = a.xt[3 * ox] & ~3, sx1 = a.xt[3 * ex + 1];
+    const int nrow = sy1 - sy0 + 1, wpr = ((sx1 - sx0) >> 2) + 1, P = a.lds_pitch;
+    const uint8_t* src = a.src.base + f * a.src.fpitch;
+    for (int i = threadIdx.x; i < nrow * wpr; i += 256) {
+        const int r = i / wpr, c = i - r * wpr;
+        const uint8_t* row = src + (long long)(sy0 + r) * a.src.pitch;
+        const int x = sx0 + 4 * c;
+        uint32_t v;
+        if (x + 4 <= a.sw) {
+            v = *reinterpret_cast<const uint32_t*>(row + x);  // pitch % 4 == 0, x % 4 == 0
+        } else {
+            v = 0;
+            for (int q = 0; q < 4 && x + q < a.sw; ++q) v |= (uint32_t)row[x + q] << (8 * q);
+        }
+        *reinterpret_cast<uint32_t*>(rs_lds + r * P + 4 * c) = v;
+    }
+    __syncthreads();
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    const int x = ox + 4 * tx;
+    if (x >= a.dw) return;
+    const int n = min(4, a.dw - x);
+    int x0[4], x1[4], a0[4], a1[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        if (k >= n) break;
-        const int dx = x + k;
-        const int x0 = xt[3 * dx], x1 = xt[3 * dx + 1], aa = xt[3 * dx + 2];
-        const int a0 = aa & 0xffff, a1 = (int)((unsigned)aa >> 16);
-        const int t0 = s0[x0] * a0 + s0[x1] * a1;
-        const int t1 = s1[x0] * a0 + s1[x1] * a1;
-        const int v = min(max((t0 * b0 + t1 * b1 + (1 << 21)) >> 22, 0), 255);
-        packed |= (uint32_t)v << (8 * k);
+        const int dx = min(x + k, a.dw - 1);
+        x0[k] = a.xt[3 * dx] - sx0;
+        x1[k] = a.xt[3 * dx + 1] - sx0;
+        const int aa = a.xt[3 * dx + 2];
+        a0[k] = aa & 0xffff;
+        a1[k] = (int)((unsigned)aa >> 16);
     }
-    if (n == 4) {
-        *reinterpret_cast<uint32_t*>(d + x) = packed;  // dst pitch and x are multiples of 4
-    } else {
-        for (int k = 0; k < n; ++k) d[x + k] = (uint8_t)(packed >> (8 * k));
+    uint8_t* dst = const_cast<uint8_t*>(a.dst.base) + f * a.dst.fpitch;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int y = oy + 4 * ty + j;
+        if (y >= a.dh) break;
+        const int ry0 = a.yt[3 * y] - sy0, ry1 = a.yt[3 * y + 1] - sy0, bb = a.yt[3 * y + 2];
+        const int b0 = bb & 0xffff, b1 = (int)((unsigned)bb >> 16);
+        const uint8_t* s0 = rs_lds + ry0 * P;
+        const uint8_t* s1 = rs_lds + ry1 * P;
+        uint32_t packed = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int t0 = s0[x0[k]] * a0[k] + s0[x1[k]] * a1[k];
+            const int t1 = s1[x0[k]] * a0[k] + s1[x1[k]] * a1[k];
+            const int v = min(max((t0 * b0 + t1 * b1 + (1 << 21)) >> 22, 0), 255);
+            packed |= (uint32_t)v << (8 * k);
+        }
+        uint8_t* d = dst + (long long)y * a.dst.pitch + x;
+        if (n == 4) {
+            *reinterpret_cast<uint32_t*>(d) = packed;
+        } else {
+            for (int k = 0; k < n; ++k) d[k] = (uint8_t)(packed >> (8 * k));
+        }
     }
 }
 
@@ -99,51 +132,54 @@ __global__ __launch_bounds__(256) void resize_kernel(
 // S(p) >= t, and cornerScore<16> returns exactly S(p) for such p (DESIGN.md "FAST").  So S is
 // computed once per pixel and both thresholds of the fallback reuse it.  S ranges over
 // [-256, 254]; only S >= 0 can be a corner, so LDS keeps max(S, -1) + 1 as a byte.
-constexpr int kFastBlock = 256;
-constexpr int kRoiMax = 72;  // cell ROI <= (59+6) x (59+6): wCell < 2*W for every level size
+constexpr int kFastBlock = 64;   // one wave per cell: ballot compaction keeps row-major order
+constexpr int kRoiMax = 72;      // cell ROI <= (59+6) x (59+6): wCell < 2*W for every level size
 
+typedef short short2v __attribute__((ext_vector_type(2)));
+
+// S for the pixel at p (ROI row stride st), with (d, -d) packed in 16-bit halves so one
+// v_pk_min_i16 / v_pk_max_i16 serves both arc polarities:
+// lo = max_k min(d[k..k+8]) = q0, hi = max_k min(-d[k..k+8]) = -q1.
 __device__ __forceinline__ int fast_S(const uint8_t* p, int st) {
     const int v = p[0];
-    int d[16];
-    d[0] = v - p[3 * st];
-    d[1] = v - p[3 * st + 1];
-    d[2] = v - p[2 * st + 2];
-    d[3] = v - p[st + 3];
-    d[4] = v - p[3];
-    d[5] = v - p[-st + 3];
-    d[6] = v - p[-2 * st + 2];
-    d[7] = v - p[-3 * st + 1];
-    d[8] = v - p[-3 * st];
-    d[9] = v - p[-3 * st - 1];
-    d[10] = v - p[-2 * st - 2];
-    d[11] = v - p[-st - 3];
-    d[12] = v - p[-3];
-    d[13] = v - p[st - 3];
-    d[14] = v - p[2 * st - 2];
-    d[15] = v - p[3 * st - 1];
-    int a2[16], b2[16], a4[16], b4[16];
+    const int x[16] = {p[3 * st],      p[3 * st + 1],  p[2 * st + 2],  p[st + 3],
+                       p[3],           p[-st + 3],     p[-2 * st + 2], p[-3 * st + 1],
+                       p[-3 * st],     p[-3 * st - 1], p[-2 * st - 2], p[-st - 3],
+                       p[-3],          p[st - 3],      p[2 * st - 2],  p[3 * st - 1]};
+    short2v e[16], m2[16], m4[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        a2[k] = min(d[k], d[(k + 1) & 15]);
-        b2[k] = max(d[k], d[(k + 1) & 15]);
+        const short d = (short)(v - x[k]);
+        e[k] = short2v{d, (short)-d};
     }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        a4[k] = min(a2[k], a2[(k + 2) & 15]);
-        b4[k] = max(b2[k], b2[(k + 2) & 15]);
-    }
-    int q0 = -1000, q1 = 1000;
+    for (int k = 0; k < 16; ++k) m2[k] = __builtin_elementwise_min(e[k], e[(k + 1) & 15]);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
+    short2v q = short2v{-1000, -1000};
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        const int a9 = min(min(a4[k], a4[(k + 4) & 15]), d[(k + 8) & 15]);
-        const int b9 = max(max(b4[k], b4[(k + 4) & 15]), d[(k + 8) & 15]);
-        q0 = max(q0, a9);
-        q1 = min(q1, b9);
+        const short2v m9 = __builtin_elementwise_min(__builtin_elementwise_min(m4[k], m4[(k + 4) & 15]),
+                                                     e[(k + 8) & 15]);
+        q = __builtin_elementwise_max(q, m9);
     }
-    return max(q0, -q1) - 1;
+    return max((int)q.x, (int)q.y) - 1;
+}
+
+// Necessary condition for a corner at t: a 9-arc always holds two consecutive cardinal points
+// (0/4/8/12), so both must be brighter than v + t or both darker than v - t.
+__device__ __forceinline__ bool fast_maybe(const uint8_t* p, int st, int t) {
+    const int v = p[0];
+    const int c0 = p[3 * st], c4 = p[3], c8 = p[-3 * st], c12 = p[-3];
+    const int hi = v + t, lo = v - t;
+    const int b = (c0 > hi) | ((c4 > hi) << 1) | ((c8 > hi) << 2) | ((c12 > hi) << 3);
+    const int d = (c0 < lo) | ((c4 < lo) << 1) | ((c8 < lo) << 2) | ((c12 < lo) << 3);
+    const int rb = (b & ((b >> 1) | (b << 3))) & 15, rd = (d & ((d >> 1) | (d << 3))) & 15;
+    return (rb | rd) != 0;
 }
 
 // Strict 3x3 NMS inside the cell's detection area at threshold t (cv::FAST nonmax, H1).
+// S holds max(S,-1)+1 per candidate, 0 where the pre-test already ruled a corner out.
 __device__ __forceinline__ bool fast_is_max(const uint8_t* S, int nr, int nc, int r, int c, int t) {
     const int s = (int)S[r * nc + c] - 1;
     if (s < t) return false;
@@ -163,62 +199,118 @@ __device__ __forceinline__ bool fast_is_max(const uint8_t* S, int nr, int nc, in
     return true;
 }
 
+// p / nc for p < 2^13 and nc <= 66 as (p * ceil(2^20 / nc)) >> 20: the error term p / 2^20
+// stays below 1 / nc, so the quotient is exact (no per-pixel integer division).
+struct DivNc {
+    unsigned m;
+    int nc;
+    __device__ __forceinline__ explicit DivNc(int n) : m((1u << 20) / (unsigned)max(n, 1) + 1u), nc(n) {}
+    __device__ __forceinline__ int row(int p) const { return (int)(((unsigned)p * m) >> 20); }
+};
+
+__device__ __forceinline__ int lane_prefix(unsigned long long mask) {
+    return __popcll(mask & ((1ull << (threadIdx.x & 63)) - 1));
+}
+
+// Ordered emission of the NMS survivors at threshold t among the compacted candidates.
+__device__ __forceinline__ int fast_emit(const uint8_t* S, const uint16_t* list, int cnt, int nr,
+                                         int nc, const DivNc& div, int t, const CellDesc& cell,
+                                         uint32_t* out, int cap) {
+    int o = 0;
+    for (int base = 0; base < cnt; base += 64) {
+        const int i = base + (int)threadIdx.x;
+        bool keep = false;
+        int p = 0, r = 0, cc = 0;
+        if (i < cnt) {
+            p = list[i];
+            r = div.row(p);
+            cc = p - r * nc;
+            keep = (int)S[p] - 1 >= t && fast_is_max(S, nr, nc, r, cc, t);
+        }
+        const unsigned long long m = __ballot(keep);
+        if (keep) {
+            const int slot = o + lane_prefix(m);
+            // key relative to (minBorderX, minBorderY): pt + (j*wCell, i*hCell) (819-824)
+            if (slot < cap)
+                out[slot] = pack_key(cell.x0 + 3 + cc - kMinBorder, cell.y0 + 3 + r - kMinBorder,
+                                     (int)S[p] - 1);
+        }
+        o += __popcll(m);
+    }
+    return o;
+}
+
 __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
-    __shared__ uint8_t roi[kRoiMax * kRoiMax];
-    __shared__ uint8_t S[(kRoiMax - 6) * (kRoiMax - 6)];
-    __shared__ int tmp[kFastBlock / 64 + 1];
+    extern __shared__ __attribute__((aligned(16))) unsigned char fast_lds[];
     const int c = blockIdx.x, f = blockIdx.y;
+    const int lane = threadIdx.x;
     const CellDesc cell = a.cells[c];
     const LevelPtr lp = a.pyr[cell.level];
     const int rows = cell.y1 - cell.y0, cols = cell.x1 - cell.x0;
-    const uint8_t* img = lp.base + f * lp.fpitch + (long long)cell.y0 * lp.pitch + cell.x0;
-    for (int i = threadIdx.x; i < rows * cols; i += kFastBlock) {
-        const int r = i / cols, cc = i - r * cols;
-        roi[r * kRoiMax + cc] = img[(long long)r * lp.pitch + cc];
+    const int P = a.roi_pitch;
+    uint8_t* roi_base = fast_lds;
+    uint8_t* S = fast_lds + a.roi_rows * P;
+    uint16_t* list = reinterpret_cast<uint16_t*>(S + ((a.cand_max + 15) & ~15));
+    // dword loads: rows are 4-byte aligned (pitch % 4 == 0, enforced by the host)
+    const int x0a = cell.x0 & ~3, shift = cell.x0 - x0a;
+    const int wpr = (shift + cols + 3) >> 2;
+    const uint8_t* img = lp.base + f * lp.fpitch + (long long)cell.y0 * lp.pitch + x0a;
+    {   // all dword loads of the ROI in flight before the LDS stores (<= 72 rows x 19 dwords)
+        const int nw = rows * wpr;
+        const DivNc dw(wpr);
+        uint32_t buf[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = lane + 64 * k;
+            const int r = dw.row(i), w = i - r * wpr;
+            buf[k] = i < nw ? *reinterpret_cast<const uint32_t*>(img + (long long)r * lp.pitch + 4 * w) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = lane + 64 * k;
+            const int r = dw.row(i), w = i - r * wpr;
+            if (i < nw) *reinterpret_cast<uint32_t*>(roi_base + r * P + 4 * w) = buf[k];
+        }
+        for (int i = lane + 512; i < nw; i += 64) {  // very large cells (tiny levels) only
+            const int r = i / wpr, w = i - r * wpr;
+            *reinterpret_cast<uint32_t*>(roi_base + r * P + 4 * w) =
+                *reinterpret_cast<const uint32_t*>(img + (long long)r * lp.pitch + 4 * w);
+        }
     }
-    __syncthreads();
+    const uint8_t* roi = roi_base + shift;
     const int nr = rows - 6, nc = cols - 6;  // candidates: ROI rows/cols 3 .. n-4
     const int ncand = (nr > 0 && nc > 0) ? nr * nc : 0;
-    for (int i = threadIdx.x; i < ncand; i += kFastBlock) {
-        const int r = i / nc, cc = i - r * nc;
-        // S < 0 is never a corner for t >= 0: clamp to -1 so S + 1 fits a byte
-        S[i] = (uint8_t)(max(fast_S(roi + (r + 3) * kRoiMax + cc + 3, kRoiMax), -1) + 1);
+    const DivNc div(nc);
+    for (int i = lane; i < ncand; i += 64) S[i] = 0;
+    __syncthreads();
+    // pre-test at the lower threshold, compacted in row-major order
+    const int tq = min(a.ini_th, a.min_th);
+    int cnt = 0;
+    for (int base = 0; base < ncand; base += 64) {
+        const int p = base + lane;
+        bool pass = false;
+        if (p < ncand) {
+            const int r = div.row(p), cc = p - r * nc;
+            pass = fast_maybe(roi + (r + 3) * P + cc + 3, P, tq);
+        }
+        const unsigned long long m = __ballot(pass);
+        if (pass) list[cnt + lane_prefix(m)] = (uint16_t)p;
+        cnt += __popcll(m);
     }
     __syncthreads();
-    // ordered compaction: thread t owns candidates [t*chunk, (t+1)*chunk) in row-major order
-    const int chunk = (ncand + kFastBlock - 1) / kFastBlock;
-    const int p0 = min(threadIdx.x * chunk, ncand), p1 = min(p0 + chunk, ncand);
-    int t = a.ini_th;
-    int mine = 0;
-    for (int p = p0; p < p1; ++p) {
-        const int r = p / nc;
-        mine += fast_is_max(S, nr, nc, r, p - r * nc, t);
+#pragma unroll 2
+    for (int i = lane; i < cnt; i += 64) {
+        const int p = list[i];
+        const int r = div.row(p), cc = p - r * nc;
+        // S < 0 is never a corner for t >= 0: clamp to -1 so S + 1 fits a byte
+        S[p] = (uint8_t)(max(fast_S(roi + (r + 3) * P + cc + 3, P), -1) + 1);
     }
-    int total;
-    int before = block_exclusive_scan<kFastBlock>(mine, tmp, total);
-    if (total == 0) {  // no corner survived at iniThFAST: rerun at minThFAST (811-815)
-        t = a.min_th;
-        mine = 0;
-        for (int p = p0; p < p1; ++p) {
-            const int r = p / nc;
-            mine += fast_is_max(S, nr, nc, r, p - r * nc, t);
-        }
-        before = block_exclusive_scan<kFastBlock>(mine, tmp, total);
-    }
+    __syncthreads();
     uint32_t* out = a.cell_keys + f * a.cell_cap_total + cell.slot;
-    const int cap = cell.cap;
-    if (mine) {
-        int o = before;
-        for (int p = p0; p < p1 && o < cap; ++p) {
-            const int r = p / nc, cc = p - r * nc;
-            if (!fast_is_max(S, nr, nc, r, cc, t)) continue;
-            const int s = (int)S[p] - 1;
-            // key relative to (minBorderX, minBorderY): pt + (j*wCell, i*hCell) (819-824)
-            const int xr = cell.x0 + 3 + cc - kMinBorder, yr = cell.y0 + 3 + r - kMinBorder;
-            out[o++] = pack_key(xr, yr, s);
-        }
-    }
-    if (threadIdx.x == 0) a.cell_cnt[f * a.ncells + c] = min(total, cap);
+    int total = fast_emit(S, list, cnt, nr, nc, div, a.ini_th, cell, out, cell.cap);
+    if (total == 0)  // no corner survived at iniThFAST: rerun at minThFAST (811-815)
+        total = fast_emit(S, list, cnt, nr, nc, div, a.min_th, cell, out, cell.cap);
+    if (lane == 0) a.cell_cnt[f * a.ncells + c] = min(total, cell.cap);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -316,8 +408,9 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
         return;
     }
 
-    int2* act[2] = {a.act + f * a.geo.key_total * 2 + L.key_off * 2,
-                    a.act + f * a.geo.key_total * 2 + L.key_off * 2 + L.key_cap};
+    int2* const act0 = a.act + f * a.geo.key_total * 2 + L.key_off * 2;
+    int2* const act1 = act0 + L.key_cap;
+#define ACT(b) ((b) ? act1 : act0)  // runtime-indexed pointer arrays would live in scratch
     int* nact_sh = s.scal;        // scal[0..1]: active counters
     int* flag_sh = s.scal + 2;    // scal[2]: overflow / misc
     int* rmin_sh = s.scal + 3;    // scal[3]: phase-2 cut index
@@ -366,7 +459,7 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
     for (int k = tid; k < nkeys; k += kOctBlock) {
         const int x = key_x(K[k]);
         const int node = s.aux[min((int)((float)x / hX), nini - 1)];
-        if (s.cnt[0][node] >= 2) act[0][atomicAdd(&nact_sh[0], 1)] = make_int2(k, node);
+        if (s.cnt[0][node] >= 2) ACT(0)[atomicAdd(&nact_sh[0], 1)] = make_int2(k, node);
     }
     __syncthreads();
     int cur = 0;
@@ -384,7 +477,7 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
         if (tid == 0) nact_sh[nxt] = 0;
         __syncthreads();
         for (int e = tid; e < nact; e += kOctBlock) {
-            const int2 en = act[cur][e];
+            const int2 en = ACT(cur)[e];
             const uint32_t kk = K[en.x];
             const int q = quadrant(s.box[cur][en.y], s.boy[cur][en.y], key_x(kk), key_y(kk));
             atomicAdd(&s.qc[en.y * 4 + q], 1);
@@ -455,11 +548,11 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
         }
         __syncthreads();
         for (int e = tid; e < nact; e += kOctBlock) {
-            const int2 en = act[cur][e];
+            const int2 en = ACT(cur)[e];
             const uint32_t kk = K[en.x];
             const int q = quadrant(s.box[cur][en.y], s.boy[cur][en.y], key_x(kk), key_y(kk));
             const int np = s.qk[en.y * 4 + q];
-            if (s.cnt[nxt][np] >= 2) act[nxt][atomicAdd(&nact_sh[nxt], 1)] = make_int2(en.x, np);
+            if (s.cnt[nxt][np] >= 2) ACT(nxt)[atomicAdd(&nact_sh[nxt], 1)] = make_int2(en.x, np);
         }
         __syncthreads();
         nact = nact_sh[nxt];
@@ -504,7 +597,7 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
                 __syncthreads();
             }
         for (int e = tid; e < nact; e += kOctBlock) {
-            const int2 en = act[cur][e];
+            const int2 en = ACT(cur)[e];
             const uint32_t kk = K[en.x];
             const int q = quadrant(s.box[cur][en.y], s.boy[cur][en.y], key_x(kk), key_y(kk));
             atomicAdd(&s.qc[en.y * 4 + q], 1);
@@ -595,7 +688,7 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
         }
         __syncthreads();
         for (int e = tid; e < nact; e += kOctBlock) {
-            const int2 en = act[cur][e];
+            const int2 en = ACT(cur)[e];
             int np;
             if (s.aux2[en.y] > 0) {
                 const uint32_t kk = K[en.x];
@@ -604,7 +697,7 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
             } else {
                 np = s.aux[en.y];
             }
-            if (s.cnt[nxt][np] >= 2) act[nxt][atomicAdd(&nact_sh[nxt], 1)] = make_int2(en.x, np);
+            if (s.cnt[nxt][np] >= 2) ACT(nxt)[atomicAdd(&nact_sh[nxt], 1)] = make_int2(en.x, np);
         }
         __syncthreads();
         nact = nact_sh[nxt];
@@ -619,7 +712,7 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
     for (int i = tid; i < size; i += kOctBlock) s.s64[i] = 0ull;
     __syncthreads();
     for (int e = tid; e < nact; e += kOctBlock) {
-        const int2 en = act[cur][e];
+        const int2 en = ACT(cur)[e];
         const uint32_t kk = K[en.x];
         const unsigned long long v =
             ((unsigned long long)key_score(kk) << 32) | (0xffffffffu - (unsigned)en.x);
@@ -633,15 +726,19 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
         out[i] = pack_key(key_x(kk) + kMinBorder, key_y(kk) + kMinBorder, key_score(kk));
     }
     if (tid == 0) *out_cnt = size;
+#undef ACT
 }
 
 // ---------------------------------------------------------------------------------------------
-// K4 — GaussianBlur(7x7, sigma 2, REFLECT_101) integer path: row pass R = sum k_i I, column
-// pass (sum k_j R + 2^15) >> 16 saturated (App. A.2).  64 x 16 output tile per workgroup.
-constexpr int kBlurTW = 64, kBlurTH = 16;
+// K4 — GaussianBlur(7x7, sigma 2, REFLECT_101) integer path: row pass R = sum k_i I (<= 65535,
+// kept as u16), column pass (sum k_j R + 2^15) >> 16 saturated (App. A.2).  128 x 32 output
+// tile per workgroup of 32 x 8 threads; each thread makes 4 x 4 pixels from dword LDS reads.
+constexpr int kBlurTW = 128, kBlurTH = 32;
+constexpr int kBlurIP = kBlurTW + 8;   // input row: image cols [ox-4, ox+TW+4)
+constexpr int kBlurIR = kBlurTH + 6;   // input rows [oy-3, oy+TH+3)
 __global__ __launch_bounds__(256) void blur_kernel(BlurArgs a) {
-    __shared__ uint8_t in[(kBlurTH + 6) * (kBlurTW + 8)];
-    __shared__ int rowp[(kBlurTH + 6) * kBlurTW];
+    __shared__ __attribute__((aligned(16))) uint8_t in[kBlurIR * kBlurIP];
+    __shared__ __attribute__((aligned(16))) uint16_t rowp[kBlurIR * kBlurTW];
     const int f = blockIdx.y;
     int t = blockIdx.x, l = 0;
     while (l + 1 < a.nlevels && t >= a.tile_begin[l + 1]) ++l;
@@ -651,34 +748,91 @@ __global__ __launch_bounds__(256) void blur_kernel(BlurArgs a) {
     const int ox = (t % tx) * kBlurTW, oy = (t / tx) * kBlurTH;
     const LevelPtr sp = a.src[l];
     const uint8_t* src = sp.base + f * sp.fpitch;
-    constexpr int IW = kBlurTW + 6, IH = kBlurTH + 6;
-    for (int i = threadIdx.x; i < IW * IH; i += 256) {
-        const int r = i / IW, c = i - r * IW;
-        int yy = oy + r - 3, xx = ox + c - 3;
-        yy = yy < 0 ? -yy : (yy >= h ? 2 * h - yy - 2 : yy);  // reflect-101 (h, w >= 4)
-        xx = xx < 0 ? -xx : (xx >= w ? 2 * w - xx - 2 : xx);
-        yy = min(max(yy, 0), h - 1);
-        xx = min(max(xx, 0), w - 1);
-        in[r * (kBlurTW + 8) + c] = src[(long long)yy * sp.pitch + xx];
+    const int tid = threadIdx.x;
+    // input rows are reflected by picking the row pointer; only dwords that straddle the left
+    // or right edge are assembled byte by byte (reflect-101, level sizes >= 4)
+    constexpr int WPR = kBlurIP / 4;
+    constexpr int NLD = (kBlurIR * WPR + 255) / 256;  // 6 dwords per thread
+    uint32_t buf[NLD];
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {  // issue every load before the first LDS store
+        const int i = tid + 256 * k;
+        const int r = min(i / WPR, kBlurIR - 1), c = i - (i / WPR) * WPR;
+        int yy = oy - 3 + r;
+        while (yy < 0 || yy >= h) yy = yy < 0 ? -yy : 2 * h - yy - 2;
+        const uint8_t* row = src + (long long)yy * sp.pitch;
+        const int x = ox - 4 + 4 * c;
+        uint32_t v = 0;
+        if (x >= 0 && x + 4 <= w) {
+            v = *reinterpret_cast<const uint32_t*>(row + x);  // pitch % 4 == 0, x % 4 == 0
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                int xx = x + q;
+                while (xx < 0 || xx >= w) xx = xx < 0 ? -xx : 2 * w - xx - 2;
+                v |= (uint32_t)row[xx] << (8 * q);
+            }
+        }
+        buf[k] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+        const int i = tid + 256 * k;
+        if (i < kBlurIR * WPR) *reinterpret_cast<uint32_t*>(in + (i / WPR) * kBlurIP + 4 * (i % WPR)) = buf[k];
     }
     __syncthreads();
     const int k0 = a.taps[0], k1 = a.taps[1], k2 = a.taps[2], k3 = a.taps[3];
-    for (int i = threadIdx.x; i < IH * kBlurTW; i += 256) {
-        const int r = i / kBlurTW, c = i - r * kBlurTW;
-        const uint8_t* p = in + r * (kBlurTW + 8) + c;
-        rowp[i] = k0 * (p[0] + p[6]) + k1 * (p[1] + p[5]) + k2 * (p[2] + p[4]) + k3 * p[3];
+    const int ltx = tid & 31, lty = tid >> 5;
+    for (int r = lty; r < kBlurIR; r += 8) {  // 4 output columns 4*ltx .. +3 <- LDS cols +1 .. +10
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(in + r * kBlurIP + 4 * ltx);
+        const uint32_t w0 = q[0], w1 = q[1], w2 = q[2];
+        int b[12];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            b[i] = (w0 >> (8 * i)) & 255;
+            b[4 + i] = (w1 >> (8 * i)) & 255;
+            b[8 + i] = (w2 >> (8 * i)) & 255;
+        }
+        uint32_t o01, o23;
+        int v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            v[j] = k0 * (b[j + 1] + b[j + 7]) + k1 * (b[j + 2] + b[j + 6]) +
+                   k2 * (b[j + 3] + b[j + 5]) + k3 * b[j + 4];
+        o01 = (uint32_t)v[0] | ((uint32_t)v[1] << 16);
+        o23 = (uint32_t)v[2] | ((uint32_t)v[3] << 16);
+        *reinterpret_cast<uint2*>(rowp + r * kBlurTW + 4 * ltx) = make_uint2(o01, o23);
     }
     __syncthreads();
     const LevelPtr dp = a.dst[l];
     uint8_t* dst = const_cast<uint8_t*>(dp.base) + f * dp.fpitch;
-    for (int i = threadIdx.x; i < kBlurTH * kBlurTW; i += 256) {
-        const int r = i / kBlurTW, c = i - r * kBlurTW;
-        const int y = oy + r, x = ox + c;
-        if (y >= h || x >= w) continue;
-        const int* p = rowp + r * kBlurTW + c;
-        const int acc = k0 * (p[0] + p[6 * kBlurTW]) + k1 * (p[kBlurTW] + p[5 * kBlurTW]) +
-                        k2 * (p[2 * kBlurTW] + p[4 * kBlurTW]) + k3 * p[3 * kBlurTW];
-        dst[(long long)y * dp.pitch + x] = (uint8_t)min(max((acc + (1 << 15)) >> 16, 0), 255);
+    int R[10][4];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint2 u = *reinterpret_cast<const uint2*>(rowp + (4 * lty + i) * kBlurTW + 4 * ltx);
+        R[i][0] = u.x & 0xffff;
+        R[i][1] = u.x >> 16;
+        R[i][2] = u.y & 0xffff;
+        R[i][3] = u.y >> 16;
+    }
+    const int x = ox + 4 * ltx;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int y = oy + 4 * lty + j;
+        if (y >= h) break;
+        uint32_t packed = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int acc = k0 * (R[j][c] + R[j + 6][c]) + k1 * (R[j + 1][c] + R[j + 5][c]) +
+                            k2 * (R[j + 2][c] + R[j + 4][c]) + k3 * R[j + 3][c];
+            packed |= (uint32_t)min((acc + (1 << 15)) >> 16, 255) << (8 * c);
+        }
+        uint8_t* d = dst + (long long)y * dp.pitch + x;
+        if (x + 4 <= w) {
+            *reinterpret_cast<uint32_t*>(d) = packed;
+        } else {
+            for (int c = 0; c < 4 && x + c < w; ++c) d[c] = (uint8_t)(packed >> (8 * c));
+        }
     }
 }
 
@@ -712,16 +866,23 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
     const uint8_t* img = pp.base + f * pp.fpitch + (long long)y * pp.pitch + x;
     const int u = (lane & 31) - 15;
     const int half = lane >> 5;
+    // all 16 rows of the lane's column are loaded before use (rows +-15, cols +-16 stay inside
+    // the level: keypoints are >= 19 px from its border), then masked by umax
+    int val[16];
+#pragma unroll
+    for (int vv = 0; vv < 16; ++vv) {
+        const int v = half ? min(vv + 1, 15) : -vv;
+        val[vv] = img[(long long)v * pp.pitch + u];
+    }
     int m10 = 0, m01 = 0;
     if ((lane & 31) < 31) {
+#pragma unroll
         for (int vv = 0; vv < 16; ++vv) {
             const int v = half ? vv + 1 : -vv;
-            if (half && vv == 15) break;
             const int av = v < 0 ? -v : v;
-            if (u < -c_umax[av] || u > c_umax[av]) continue;
-            const int val = img[(long long)v * pp.pitch + u];
-            m10 += u * val;
-            m01 += v * val;
+            const bool in = !(half && vv == 15) && u >= -c_umax[min(av, 15)] && u <= c_umax[min(av, 15)];
+            m10 += in ? u * val[vv] : 0;
+            m01 += in ? v * val[vv] : 0;
         }
     }
     m10 = wave_sum(m10);
@@ -915,6 +1076,26 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
                 g.xtab.push_back(std::min(sx + 1, sw - 1));
                 g.xtab.push_back((a0 & 0xffff) | (a1 << 16));
             }
+            {   // LDS footprint of a 128 x 32 resize tile of this level
+                int need_rows = 0, need_w = 0;
+                for (int oy = 0; oy < dh; oy += kRsTH) {
+                    const int ey = std::min(oy + kRsTH, dh) - 1;
+                    auto sy = [&](int dy) { return (int)std::floor((float)((dy + 0.5) * scale_y - 0.5)); };
+                    const int r0 = std::min(std::max(sy(oy), 0), sh - 1), r1 = std::min(std::max(sy(ey) + 1, 0), sh - 1);
+                    need_rows = std::max(need_rows, r1 - r0 + 1);
+                }
+                const size_t xb = g.xtab.size() - 3 * (size_t)dw;
+                for (int ox = 0; ox < dw; ox += kRsTW) {
+                    const int ex = std::min(ox + kRsTW, dw) - 1;
+                    const int a0 = g.xtab[xb + 3 * ox] & ~3, a1 = g.xtab[xb + 3 * ex + 1];
+                    need_w = std::max(need_w, ((a1 - a0) >> 2) + 1);
+                }
+                g.rs_tiles_x[l] = (dw + kRsTW - 1) / kRsTW;
+                g.rs_tiles[l] = g.rs_tiles_x[l] * ((dh + kRsTH - 1) / kRsTH);
+                g.rs_pitch[l] = 4 * need_w;
+                g.rs_lds[l] = (size_t)need_rows * 4 * need_w;
+                if (g.rs_lds[l] > 64 * 1024) return ORBFE_ERR_UNSUPPORTED;  // scale factors > ~3
+            }
             g.yoff[l] = (int)g.ytab.size();
             for (int dy = 0; dy < dh; ++dy) {
                 float fy = (float)((dy + 0.5) * scale_y - 0.5);
@@ -928,6 +1109,15 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
         }
     }
     if (w > 4096 || h > 4096) return ORBFE_ERR_UNSUPPORTED;
+    int rmax = 7, cmax = 7;
+    for (const CellDesc& c : g.cells) {
+        rmax = std::max(rmax, c.y1 - c.y0);
+        cmax = std::max(cmax, c.x1 - c.x0);
+    }
+    g.roi_rows = rmax;
+    g.roi_pitch = (cmax + 3 + 3) & ~3;  // + alignment shift, rounded to dwords
+    g.cand_max = (rmax - 6) * (cmax - 6);
+    g.fast_lds = (size_t)rmax * g.roi_pitch + ((g.cand_max + 15) & ~15) + 2 * (size_t)g.cand_max + 16;
     g.geo.key_total = keys;
     g.geo.out_total = out;
     g.slab = slab;

@@ -55,11 +55,20 @@ struct LevelPtr {
     int pitch;             // bytes between rows
 };
 
+struct ResizeArgs {
+    LevelPtr src, dst;
+    int sw, sh, dw, dh;
+    int tiles_x, lds_pitch;
+    const int* xt;
+    const int* yt;
+};
+
 struct FastArgs {
     const CellDesc* cells;
     int ncells;
     long long cell_cap_total;
     int ini_th, min_th;
+    int roi_pitch, roi_rows, cand_max;  // dynamic-LDS carve of fast_kernel
     int* cell_cnt;         // [frame][cell]
     uint32_t* cell_keys;   // [frame][cell_cap_total]
     LevelPtr pyr[kMaxLevels];
@@ -122,6 +131,10 @@ struct Plan {
     int ncap_max = 0, sort_cap = 0, tiles_total = 0;
     int tile_begin[kMaxLevels] = {};
     size_t oct_lds = 0;
+    int roi_pitch = 0, roi_rows = 0, cand_max = 0;
+    size_t fast_lds = 0;
+    int rs_tiles_x[kMaxLevels] = {}, rs_tiles[kMaxLevels] = {}, rs_pitch[kMaxLevels] = {};
+    size_t rs_lds[kMaxLevels] = {};
 };
 
 int make_tables(const orbfe_params& p, HostTables& t);
@@ -130,17 +143,16 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g);
 // kernels (orbfe_extract.hip)
 __global__ void mask_kernel(const uint8_t*, long long, int, const uint8_t*, long long, int,
                             uint8_t*, long long, int, int, int);
-__global__ void resize_kernel(const uint8_t*, long long, int, uint8_t*, long long, int, int, int,
-                              const int*, const int*);
+__global__ void resize_kernel(ResizeArgs);
 __global__ void fast_kernel(FastArgs);
 __global__ void octree_kernel(OctArgs);
 __global__ void blur_kernel(BlurArgs);
 __global__ void describe_kernel(DescArgs);
 extern __constant__ int c_umax[16];
 
-constexpr int kFastBlockSize = 256;
+constexpr int kFastBlockSize = 64;
 constexpr int kOctBlockSize = 512;
 constexpr int kDescBlockSize = 256;
-constexpr int kBlurTileW = 64, kBlurTileH = 16;
+constexpr int kBlurTileW = 128, kBlurTileH = 32;
 
 }  // namespace orbfe

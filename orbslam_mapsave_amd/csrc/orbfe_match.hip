@@ -46,17 +46,26 @@ __global__ __launch_bounds__(256) void hamming_kernel(const uint4* a, const uint
     if (i < n) dist[i] = hamming_rows(a + 2 * i, b + 2 * i);
 }
 
-// Brute force: problem b = blockIdx.y; each lane owns one query; 256 references per LDS tile.
+// Brute force: problem b = blockIdx.y; a block serves 64 queries (one per lane) and its 4 waves
+// split the references into contiguous quarters.  Keys pack (distance << 16 | reference index):
+// with the first-wins rule of ORBmatcher.cc:102-114 (strict <, start at 256) the best key is
+// min(keys) and the second distance is the second-smallest key's, so each reference costs
+// 8 XOR + 8 bit-counts + one shift-or + min/max/min -- no compare chain.  An initial key of
+// 256 << 16 keeps distance-256 references out, as the strict compare does.  Partitions merge
+// with second = min(second_a, second_b, max(best_a, best_b)).  nr < 65536.
 constexpr int kBfBlock = 256;
+constexpr int kBfTile = 64;  // references per wave per tile
 __global__ __launch_bounds__(kBfBlock) void bf_match_kernel(const uint8_t* q, long long q_pitch,
                                                             const int* nq_arr, int nq_cap,
                                                             const uint8_t* r, long long r_pitch,
                                                             const int* nr_arr, int* out) {
-    __shared__ uint4 tile[kBfBlock * 2];
+    __shared__ uint4 tile[4][kBfTile * 2];
+    __shared__ unsigned part[4][64][2];
     const int b = blockIdx.y;
     const int nq = nq_arr[b], nr = nr_arr[b];
-    const int qi = blockIdx.x * kBfBlock + threadIdx.x;
-    if (blockIdx.x * kBfBlock >= nq) return;
+    if ((int)blockIdx.x * 64 >= nq) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int qi = blockIdx.x * 64 + lane;
     const uint4* Q = reinterpret_cast<const uint4*>(q + b * q_pitch);
     const uint4* R = reinterpret_cast<const uint4*>(r + b * r_pitch);
     uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
@@ -64,31 +73,43 @@ __global__ __launch_bounds__(kBfBlock) void bf_match_kernel(const uint8_t* q, lo
         a0 = Q[2 * qi];
         a1 = Q[2 * qi + 1];
     }
-    int best = 256, second = 256, bi = -1;
-    for (int base = 0; base < nr; base += kBfBlock) {
-        const int cnt = min(kBfBlock, nr - base);
-        __syncthreads();
-        if (threadIdx.x < cnt) {
-            tile[2 * threadIdx.x] = R[2 * (base + threadIdx.x)];
-            tile[2 * threadIdx.x + 1] = R[2 * (base + threadIdx.x) + 1];
+    const int quarter = (((nr + 3) / 4) + kBfTile - 1) / kBfTile * kBfTile;
+    const int j0 = w * quarter, j1 = min(nr, j0 + quarter);
+    const unsigned kInit = 256u << 16;
+    unsigned best = kInit, second = kInit;
+    const int ntiles = (quarter + kBfTile - 1) / kBfTile;  // same count in every wave
+    for (int t = 0; t < ntiles; ++t) {
+        const int base = j0 + t * kBfTile;
+        const int cnt = max(0, min(kBfTile, j1 - base));
+        if (lane < cnt) {
+            tile[w][2 * lane] = R[2 * (base + lane)];
+            tile[w][2 * lane + 1] = R[2 * (base + lane) + 1];
         }
         __syncthreads();
-        for (int j = 0; j < cnt; ++j) {  // in reference order: first-wins ties (ORBmatcher.cc:102-114)
-            const int d = hamming256(a0, a1, tile[2 * j], tile[2 * j + 1]);
-            if (d < best) {
-                second = best;
-                best = d;
-                bi = base + j;
-            } else if (d < second) {
-                second = d;
-            }
+#pragma unroll 4
+        for (int j = 0; j < cnt; ++j) {
+            const unsigned d = (unsigned)hamming256(a0, a1, tile[w][2 * j], tile[w][2 * j + 1]);
+            const unsigned key = (d << 16) | (unsigned)(base + j);
+            const unsigned hi = max(best, key);
+            best = min(best, key);
+            second = min(second, hi);
         }
+        __syncthreads();
     }
-    if (qi < nq) {
+    part[w][lane][0] = best;
+    part[w][lane][1] = second;
+    __syncthreads();
+    if (w == 0 && qi < nq) {
+#pragma unroll
+        for (int o = 1; o < 4; ++o) {
+            const unsigned ob = part[o][lane][0], os = part[o][lane][1];
+            second = min(min(second, os), max(best, ob));
+            best = min(best, ob);
+        }
         int* o = out + ((long long)b * nq_cap + qi) * 3;
-        o[0] = bi;
-        o[1] = best;
-        o[2] = second;
+        o[0] = (best >> 16) >= 256 ? -1 : (int)(best & 0xffff);
+        o[1] = (int)(best >> 16);
+        o[2] = (int)(second >> 16);
     }
 }
 

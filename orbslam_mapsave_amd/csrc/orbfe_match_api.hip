@@ -23,6 +23,7 @@ struct orbfe_matcher {
     DevBuf m_f0, m_f1, m_f2, m_f3, m_f4, m_u0, m_u1, m_i0, m_i1, m_d;  // per-map-point inputs
     DevBuf o_u, o_f0, o_f1, o_f2, o_f3, o_i;        // frustum outputs
     DevBuf scal;
+    Profiler prof;
 
     ~orbfe_matcher() {
         for (DevBuf* b : {&fa_k, &fa_d, &fa_ur, &fa_cs, &fa_ci, &fa_co, &fb_k, &fb_d, &fb_ur,
@@ -30,6 +31,7 @@ struct orbfe_matcher {
                           &s2, &s3, &s4, &s5, &m_f0, &m_f1, &m_f2, &m_f3, &m_f4, &m_u0, &m_u1,
                           &m_i0, &m_i1, &m_d, &o_u, &o_f0, &o_f1, &o_f2, &o_f3, &o_i, &scal})
             b->release();
+        prof.release();
         if (own) hipStreamDestroy(own);
     }
 
@@ -194,7 +196,8 @@ int orbfe_bf_match(orbfe_matcher* m, const uint8_t* q, int nq, const uint8_t* r,
         const int counts[2] = {nq, nr};
         if ((st = m->up(m->nq, counts, sizeof(counts)))) return st;
         if ((st = m->out.ensure((size_t)nq * 3 * sizeof(int)))) return st;
-        hipLaunchKernelGGL(bf_match_kernel, dim3((nq + kBfBlock - 1) / kBfBlock, 1), dim3(kBfBlock),
+        if (nr >= 65536) return ORBFE_ERR_UNSUPPORTED;
+        hipLaunchKernelGGL(bf_match_kernel, dim3((nq + 63) / 64, 1), dim3(kBfBlock),
                            0, m->stream, m->q.as<uint8_t>(), 0ll, m->nq.as<int>(), nq,
                            m->r.as<uint8_t>(), 0ll, m->nq.as<int>() + 1, m->out.as<int>());
         std::vector<int> tri((size_t)nq * 3);
@@ -217,12 +220,35 @@ int orbfe_bf_match_batch_device(orbfe_matcher* m, const uint8_t* d_q, size_t q_p
     if (nb == 0 || nq_cap == 0) return ORBFE_OK;
     if ((q_pitch | r_pitch) & 15) return ORBFE_ERR_ARG;
     return guarded(m, [&]() {
-        hipLaunchKernelGGL(bf_match_kernel, dim3((nq_cap + kBfBlock - 1) / kBfBlock, nb),
-                           dim3(kBfBlock), 0, m->stream, d_q, (long long)q_pitch, d_nq, nq_cap,
-                           d_r, (long long)r_pitch, d_nr, d_out);
+        ORBFE_LAUNCH(m->prof, 0, bf_match_kernel, dim3((nq_cap + 63) / 64, nb),
+                     dim3(kBfBlock), 0, m->stream, d_q, (long long)q_pitch, d_nq, nq_cap, d_r,
+                     (long long)r_pitch, d_nr, d_out);
         ORBFE_HIP(hipGetLastError());
         return ORBFE_OK;
     });
+}
+
+int orbfe_matcher_profile(orbfe_matcher* m, int enable) {
+    if (!m) return ORBFE_ERR_ARG;
+    m->prof.on = enable != 0;
+    m->prof.used = 0;
+    return ORBFE_OK;
+}
+
+int orbfe_matcher_profile_read(orbfe_matcher* m, double* total_ms, int32_t* launches) {
+    if (!m || !total_ms || !launches) return ORBFE_ERR_ARG;
+    DeviceGuard dg(m->device);
+    ORBFE_HIP(hipStreamSynchronize(m->stream));
+    *total_ms = 0;
+    *launches = 0;
+    for (size_t i = 0; i < m->prof.used; ++i) {
+        float ms = 0.f;
+        ORBFE_HIP(hipEventElapsedTime(&ms, m->prof.a[i], m->prof.b[i]));
+        *total_ms += ms;
+        *launches += 1;
+    }
+    m->prof.used = 0;
+    return ORBFE_OK;
 }
 
 int orbfe_search_for_initialization(orbfe_matcher* m, float nnratio, int check_ori,

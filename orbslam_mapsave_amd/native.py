@@ -30,7 +30,8 @@ EXPORTED = [
     "orbfe_get_scale_tables", "orbfe_get_features_per_level", "orbfe_keypoint_capacity",
     "orbfe_extract", "orbfe_extract_batch", "orbfe_extract_batch_device", "orbfe_set_stream",
     "orbfe_synchronize", "orbfe_profile", "orbfe_profile_read", "orbfe_get_level", "orbfe_get_blurred_level", "orbfe_get_fast_keys",
-    "orbfe_matcher_create", "orbfe_matcher_destroy", "orbfe_matcher_set_stream", "orbfe_hamming",
+    "orbfe_matcher_create", "orbfe_matcher_destroy", "orbfe_matcher_set_stream",
+    "orbfe_matcher_profile", "orbfe_matcher_profile_read", "orbfe_hamming",
     "orbfe_bf_match", "orbfe_bf_match_batch_device", "orbfe_search_for_initialization",
     "orbfe_search_by_projection_local", "orbfe_search_by_projection_last", "orbfe_is_in_frustum",
 ]
@@ -266,6 +267,16 @@ class ORBmatcher:
         _check("orbfe_bf_match_batch_device", lib().orbfe_bf_match_batch_device(
             self._h, C.c_void_p(d_q), C.c_size_t(q_pitch), C.c_void_p(d_nq), nq_cap,
             C.c_void_p(d_r), C.c_size_t(r_pitch), C.c_void_p(d_nr), nb, C.c_void_p(d_out)))
+
+    def profile(self, enable: bool) -> None:
+        _check("orbfe_matcher_profile", lib().orbfe_matcher_profile(self._h, int(enable)))
+
+    def profile_read(self) -> tuple[float, int]:
+        """(total ms, launches) of bf_match_batch_device since the previous read."""
+        ms = np.zeros(1, np.float64)
+        n = np.zeros(1, np.int32)
+        _check("orbfe_matcher_profile_read", lib().orbfe_matcher_profile_read(self._h, ptr(ms), ptr(n)))
+        return float(ms[0]), int(n[0])
 
     def set_stream(self, stream_handle: int | None) -> None:
         _check("orbfe_matcher_set_stream", lib().orbfe_matcher_set_stream(

@@ -1,0 +1,77 @@
+// GPU parity check of the C++ adapter (include/orbfe_orbslam.hpp) against the CPU oracle, as
+// C++ host code of the reference would use it.  Built by __graft_entry__.build(); run by
+// tests/test_gpu_cpp.py on the MI355X.  Prints "ADAPTER PASS" on success.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../../include/orbfe_orbslam.hpp"
+#include "../../oracle/orb_oracle.h"
+
+static std::vector<uint8_t> make_image(int w, int h, unsigned seed) {
+    std::vector<uint8_t> img((size_t)w * h);
+    unsigned s = seed * 2654435761u + 12345u;
+    auto rnd = [&]() { s = s * 1664525u + 1013904223u; return (s >> 8) & 0xffff; };
+    for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x)
+            img[(size_t)y * w + x] = (uint8_t)(128 + 60 * std::sin(x * 0.05) * std::cos(y * 0.07));
+    for (int r = 0; r < 150; ++r) {  // random rectangles: corners for FAST
+        const int x0 = rnd() % w, y0 = rnd() % h, rw = 5 + rnd() % 50, rh = 5 + rnd() % 50;
+        const uint8_t g = (uint8_t)(rnd() & 255);
+        for (int y = y0; y < std::min(h, y0 + rh); ++y)
+            for (int x = x0; x < std::min(w, x0 + rw); ++x) img[(size_t)y * w + x] = g;
+    }
+    return img;
+}
+
+int main() {
+    const int W = 640, H = 480;
+    int fails = 0;
+    orbfe::ORBextractor ex(1000, 1.2f, 8, 32, 7);
+    orbfe_params p{1000, 1.2f, 8, 32, 7};
+    for (unsigned seed = 0; seed < 3; ++seed) {
+        std::vector<uint8_t> img = make_image(W, H, seed);
+        std::vector<orbfe_keypoint> kps;
+        std::vector<uint8_t> desc;
+        ex(img.data(), W, H, W, nullptr, 0, kps, desc);
+        std::vector<orbfe_keypoint> okps(2000);
+        std::vector<uint8_t> odesc(2000 * 32);
+        int n = 0;
+        if (oracle_extract(&p, img.data(), W, H, W, nullptr, 0, okps.data(), 2000, odesc.data(), &n)) return 2;
+        const bool same = (int)kps.size() == n && !std::memcmp(kps.data(), okps.data(), n * sizeof(orbfe_keypoint)) &&
+                          !std::memcmp(desc.data(), odesc.data(), (size_t)n * 32);
+        std::printf("seed %u: %zu keypoints (oracle %d) %s\n", seed, kps.size(), n, same ? "bit-exact" : "MISMATCH");
+        fails += !same;
+    }
+    // scale tables through the getters
+    std::vector<float> sf = ex.GetScaleFactors(), osf(8);
+    oracle_tables(&p, osf.data(), nullptr, nullptr, nullptr, nullptr, nullptr);
+    fails += std::memcmp(sf.data(), osf.data(), 8 * sizeof(float)) != 0;
+    // SearchForInitialization on two extracted frames
+    orbfe::ORBextractor ini(2000, 1.2f, 8, 32, 7);
+    orbfe::FrameData F1, F2;
+    std::vector<uint8_t> i1 = make_image(W, H, 7), i2 = make_image(W, H, 7);
+    std::memmove(i2.data() + 3, i2.data(), i2.size() - 3);  // shifted view
+    ini(i1.data(), W, H, W, nullptr, 0, F1.keys_un, F1.descriptors);
+    ini(i2.data(), W, H, W, nullptr, 0, F2.keys_un, F2.descriptors);
+    for (orbfe::FrameData* F : {&F1, &F2}) {
+        F->max_x = W;
+        F->max_y = H;
+        F->scale_factors = sf;
+    }
+    orbfe::ORBmatcher matcher(0.9f, true);
+    std::vector<float> prev, oprev;
+    for (const orbfe_keypoint& k : F1.keys_un) { prev.push_back(k.x); prev.push_back(k.y); }
+    oprev = prev;
+    std::vector<int> m12, om12(F1.keys_un.size());
+    const int nm = matcher.SearchForInitialization(F1, F2, prev, m12, 100);
+    int onm = 0;
+    const orbfe_frame_view v1 = F1.view(), v2 = F2.view();
+    oracle_search_for_initialization(0.9f, 1, &v1, &v2, oprev.data(), 100, om12.data(), &onm);
+    const bool sfi_same = nm == onm && m12 == om12 && prev == oprev;
+    std::printf("SearchForInitialization: %d matches (oracle %d) %s\n", nm, onm, sfi_same ? "exact" : "MISMATCH");
+    fails += !sfi_same;
+    std::printf(fails ? "ADAPTER FAIL\n" : "ADAPTER PASS\n");
+    return fails ? 1 : 0;
+}
