@@ -283,33 +283,36 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
     const DivNc div(nc);
     for (int i = lane; i < ncand; i += 64) S[i] = 0;
     __syncthreads();
-    // pre-test at the lower threshold, compacted in row-major order
-    const int tq = min(a.ini_th, a.min_th);
-    int cnt = 0;
-    for (int base = 0; base < ncand; base += 64) {
-        const int p = base + lane;
-        bool pass = false;
-        if (p < ncand) {
-            const int r = div.row(p), cc = p - r * nc;
-            pass = fast_maybe(roi + (r + 3) * P + cc + 3, P, tq);
-        }
-        const unsigned long long m = __ballot(pass);
-        if (pass) list[cnt + lane_prefix(m)] = (uint16_t)p;
-        cnt += __popcll(m);
-    }
-    __syncthreads();
-#pragma unroll 2
-    for (int i = lane; i < cnt; i += 64) {
-        const int p = list[i];
-        const int r = div.row(p), cc = p - r * nc;
-        // S < 0 is never a corner for t >= 0: clamp to -1 so S + 1 fits a byte
-        S[p] = (uint8_t)(max(fast_S(roi + (r + 3) * P + cc + 3, P), -1) + 1);
-    }
-    __syncthreads();
+    // Pass at iniThFAST: only pixels passing the pre-test at that threshold can have S >= t,
+    // and every other pixel counts as 0 in the NMS, so S is computed for those alone.
     uint32_t* out = a.cell_keys + f * a.cell_cap_total + cell.slot;
-    int total = fast_emit(S, list, cnt, nr, nc, div, a.ini_th, cell, out, cell.cap);
-    if (total == 0)  // no corner survived at iniThFAST: rerun at minThFAST (811-815)
-        total = fast_emit(S, list, cnt, nr, nc, div, a.min_th, cell, out, cell.cap);
+    int total = 0;
+    for (int pass = 0; pass < 2 && total == 0; ++pass) {
+        const int t = pass ? a.min_th : a.ini_th;  // rerun at minThFAST when empty (811-815)
+        int cnt = 0;
+        for (int base = 0; base < ncand; base += 64) {
+            const int p = base + lane;
+            bool ok = false;
+            if (p < ncand) {
+                const int r = div.row(p), cc = p - r * nc;
+                ok = fast_maybe(roi + (r + 3) * P + cc + 3, P, t);
+            }
+            const unsigned long long m = __ballot(ok);
+            if (ok) list[cnt + lane_prefix(m)] = (uint16_t)p;  // row-major order
+            cnt += __popcll(m);
+        }
+        __syncthreads();
+#pragma unroll 2
+        for (int i = lane; i < cnt; i += 64) {
+            const int p = list[i];
+            const int r = div.row(p), cc = p - r * nc;
+            // S < 0 is never a corner for t >= 0: clamp to -1 so S + 1 fits a byte
+            S[p] = (uint8_t)(max(fast_S(roi + (r + 3) * P + cc + 3, P), -1) + 1);
+        }
+        __syncthreads();
+        total = fast_emit(S, list, cnt, nr, nc, div, t, cell, out, cell.cap);
+        __syncthreads();
+    }
     if (lane == 0) a.cell_cnt[f * a.ncells + c] = min(total, cell.cap);
 }
 
