@@ -9,6 +9,20 @@
 
 namespace orbfe {
 
+// XCD-aware block remap (cdna_hip_programming.md T1): blocks are dealt round-robin over the 8
+// XCDs (blocks b and b + 8 share one), so give each XCD a contiguous range of the linear
+// (x fastest, then y) grid: the tiles, cells and keypoints of one frame then share one XCD's
+// L2 instead of pulling the frame's lines into all eight.  Bijective for any grid size; speed
+// only, never correctness.
+__device__ __forceinline__ void xcd_block(int& bx, int& by) {
+    const unsigned nx = gridDim.x, n = nx * gridDim.y;
+    const unsigned id = blockIdx.y * nx + blockIdx.x;
+    const unsigned q = n >> 3, r = n & 7, x = id & 7;
+    const unsigned l = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (id >> 3);
+    by = (int)(l / nx);
+    bx = (int)(l - (unsigned)by * nx);
+}
+
 // cvRound(float): round half to even (v_rndne_f32), App. A.5.
 __device__ __forceinline__ int rne(float v) { return (int)__builtin_rintf(v); }
 

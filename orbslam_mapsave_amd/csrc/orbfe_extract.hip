@@ -65,8 +65,9 @@ __global__ void mask_kernel(const uint8_t* src, long long src_fpitch, int src_pi
 constexpr int kRsTW = 128, kRsTH = 32;
 __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
-    const int f = blockIdx.y;
-    const int ox = (blockIdx.x % a.tiles_x) * kRsTW, oy = (blockIdx.x / a.tiles_x) * kRsTH;
+    int bx, f;
+    xcd_block(bx, f);
+    const int ox = (bx % a.tiles_x) * kRsTW, oy = (bx / a.tiles_x) * kRsTH;
     const int ex = min(ox + kRsTW, a.dw) - 1, ey = min(oy + kRsTH, a.dh) - 1;
     const int sy0 = a.yt[3 * oy], sy1 = a.yt[3 * ey + 1];
     const int sx0 = a.xt[3 * ox] & ~3, sx1 = a.xt[3 * ex + 1];
@@ -137,66 +138,51 @@ constexpr int kRoiMax = 72;      // cell ROI <= (59+6) x (59+6): wCell < 2*W for
 
 typedef short short2v __attribute__((ext_vector_type(2)));
 
-// S for the pixel at p (ROI row stride st), with (d, -d) packed in 16-bit halves so one
-// v_pk_min_i16 / v_pk_max_i16 serves both arc polarities:
+// S for the pixel at p (ROI row stride st).  Both arc polarities run in one packed f16 pair
+// e = (d, -d), d = v - circle: a byte b enters as the exact f16 1024 + b (bits 0x6400 + b, one
+// v_mad_u32_u24 for both halves), so every d in [-255, 255] and every min / max of them is an
+// exact f16 integer.  9-arcs come from 3-arcs with v_pk_minimum3_f16:
 // lo = max_k min(d[k..k+8]) = q0, hi = max_k min(-d[k..k+8]) = -q1.
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ half2v fast_h2(uint32_t b) {
+    return __builtin_bit_cast(half2v, b * 0x10001u + 0x64006400u);
+}
 __device__ __forceinline__ int fast_S(const uint8_t* p, int st) {
-    const int v = p[0];
-    const int x[16] = {p[3 * st],      p[3 * st + 1],  p[2 * st + 2],  p[st + 3],
-                       p[3],           p[-st + 3],     p[-2 * st + 2], p[-3 * st + 1],
-                       p[-3 * st],     p[-3 * st - 1], p[-2 * st - 2], p[-st - 3],
-                       p[-3],          p[st - 3],      p[2 * st - 2],  p[3 * st - 1]};
-    short2v e[16], m2[16], m4[16];
+    const half2v V = fast_h2(p[0]);
+    const half2v Vs = half2v{V.x, -V.y};
+    const uint32_t x[16] = {p[3 * st],      p[3 * st + 1],  p[2 * st + 2],  p[st + 3],
+                            p[3],           p[-st + 3],     p[-2 * st + 2], p[-3 * st + 1],
+                            p[-3 * st],     p[-3 * st - 1], p[-2 * st - 2], p[-st - 3],
+                            p[-3],          p[st - 3],      p[2 * st - 2],  p[3 * st - 1]};
+    half2v e[16], m3[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        const short d = (short)(v - x[k]);
-        e[k] = short2v{d, (short)-d};
+        const half2v X = fast_h2(x[k]);
+        e[k] = Vs + half2v{-X.x, X.y};
     }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) m2[k] = __builtin_elementwise_min(e[k], e[(k + 1) & 15]);
+    for (int k = 0; k < 16; ++k)
+        m3[k] = __builtin_elementwise_minimum(__builtin_elementwise_minimum(e[k], e[(k + 1) & 15]),
+                                              e[(k + 2) & 15]);
+    half2v q = __builtin_elementwise_minimum(__builtin_elementwise_minimum(m3[0], m3[3]), m3[6]);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
-    short2v q = short2v{-1000, -1000};
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const short2v m9 = __builtin_elementwise_min(__builtin_elementwise_min(m4[k], m4[(k + 4) & 15]),
-                                                     e[(k + 8) & 15]);
-        q = __builtin_elementwise_max(q, m9);
+    for (int k = 1; k < 16; ++k) {
+        const half2v m9 = __builtin_elementwise_minimum(
+            __builtin_elementwise_minimum(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15]);
+        q = __builtin_elementwise_maximum(q, m9);
     }
-    return max((int)q.x, (int)q.y) - 1;
+    return (int)(float)__builtin_elementwise_maximum(q.x, q.y) - 1;
 }
 
 // Necessary condition for a corner at t: a 9-arc always holds two consecutive cardinal points
-// (0/4/8/12), so both must be brighter than v + t or both darker than v - t.
-__device__ __forceinline__ bool fast_maybe(const uint8_t* p, int st, int t) {
-    const int v = p[0];
-    const int c0 = p[3 * st], c4 = p[3], c8 = p[-3 * st], c12 = p[-3];
-    const int hi = v + t, lo = v - t;
-    const int b = (c0 > hi) | ((c4 > hi) << 1) | ((c8 > hi) << 2) | ((c12 > hi) << 3);
-    const int d = (c0 < lo) | ((c4 < lo) << 1) | ((c8 < lo) << 2) | ((c12 < lo) << 3);
-    const int rb = (b & ((b >> 1) | (b << 3))) & 15, rd = (d & ((d >> 1) | (d << 3))) & 15;
-    return (rb | rd) != 0;
-}
-
-// Strict 3x3 NMS inside the cell's detection area at threshold t (cv::FAST nonmax, H1).
-// S holds max(S,-1)+1 per candidate, 0 where the pre-test already ruled a corner out.
-__device__ __forceinline__ bool fast_is_max(const uint8_t* S, int nr, int nc, int r, int c, int t) {
-    const int s = (int)S[r * nc + c] - 1;
-    if (s < t) return false;
-#pragma unroll
-    for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-        for (int dx = -1; dx <= 1; ++dx) {
-            if (!dy && !dx) continue;
-            const int rr = r + dy, cc = c + dx;
-            int nv = 0;
-            if (rr >= 0 && rr < nr && cc >= 0 && cc < nc) {
-                const int ns = (int)S[rr * nc + cc] - 1;
-                nv = ns >= t ? ns : 0;
-            }
-            if (!(s > nv)) return false;
-        }
-    return true;
+// (0/4/8/12), so both must be brighter than v + t or both darker than v - t.  w points at the
+// top-left of the pixel's 7 x 7 window (row stride st).
+__device__ __forceinline__ bool fast_maybe(const uint8_t* w, int st, int t) {
+    const int v = w[3 * st + 3];
+    const int c0 = w[6 * st + 3], c4 = w[3 * st + 6], c8 = w[3], c12 = w[3 * st];
+    const int bright = max(max(min(c0, c4), min(c4, c8)), max(min(c8, c12), min(c12, c0)));
+    const int dark = min(min(max(c0, c4), max(c4, c8)), min(max(c8, c12), max(c12, c0)));
+    return bright > v + t || dark < v - t;
 }
 
 // p / nc for p < 2^13 and nc <= 66 as (p * ceil(2^20 / nc)) >> 20: the error term p / 2^20
@@ -213,27 +199,38 @@ __device__ __forceinline__ int lane_prefix(unsigned long long mask) {
 }
 
 // Ordered emission of the NMS survivors at threshold t among the compacted candidates.
-__device__ __forceinline__ int fast_emit(const uint8_t* S, const uint16_t* list, int cnt, int nr,
-                                         int nc, const DivNc& div, int t, const CellDesc& cell,
+//
+// Candidates are ROI offsets o = r * P + c of their window's top-left (row-major order), and
+// the score plane S shares the ROI pitch with a zero border, so candidate (r, c) scores at
+// S[o + P + 1] and its 8 neighbours sit at fixed offsets.  S holds max(S, -1) + 1, 0 where the
+// pre-test ruled a corner out.  cv::FAST's strict 3x3 NMS (H1) keeps s when s >= t and
+// s > nv for every neighbour, nv = (ns >= t ? ns : 0): for s >= max(t, 1) that is exactly
+// max(ns) < s, and for s = t = 0 it never holds — so one byte compare against the neighbour
+// maximum decides it.
+__device__ __forceinline__ int fast_emit(const uint8_t* S, const uint16_t* list, int cnt, int P,
+                                         unsigned inv_p, int t, const CellDesc& cell,
                                          uint32_t* out, int cap) {
+    const int tb = max(t, 1) + 1;
     int o = 0;
     for (int base = 0; base < cnt; base += 64) {
         const int i = base + (int)threadIdx.x;
         bool keep = false;
-        int p = 0, r = 0, cc = 0;
+        int off = 0, sb = 0;
         if (i < cnt) {
-            p = list[i];
-            r = div.row(p);
-            cc = p - r * nc;
-            keep = (int)S[p] - 1 >= t && fast_is_max(S, nr, nc, r, cc, t);
+            off = list[i];
+            const uint8_t* q = S + off + P + 1;
+            sb = q[0];
+            const int nb = max(max(max(q[-P - 1], q[-P]), max(q[-P + 1], q[-1])),
+                               max(max(q[1], q[P - 1]), max(q[P], q[P + 1])));
+            keep = sb >= tb && nb < sb;
         }
         const unsigned long long m = __ballot(keep);
         if (keep) {
             const int slot = o + lane_prefix(m);
+            const int r = (int)__umulhi((unsigned)off, inv_p), cc = off - r * P;
             // key relative to (minBorderX, minBorderY): pt + (j*wCell, i*hCell) (819-824)
             if (slot < cap)
-                out[slot] = pack_key(cell.x0 + 3 + cc - kMinBorder, cell.y0 + 3 + r - kMinBorder,
-                                     (int)S[p] - 1);
+                out[slot] = pack_key(cell.x0 + 3 + cc - kMinBorder, cell.y0 + 3 + r - kMinBorder, sb - 1);
         }
         o += __popcll(m);
     }
@@ -242,7 +239,8 @@ __device__ __forceinline__ int fast_emit(const uint8_t* S, const uint16_t* list,
 
 __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char fast_lds[];
-    const int c = blockIdx.x, f = blockIdx.y;
+    int c, f;
+    xcd_block(c, f);
     const int lane = threadIdx.x;
     const CellDesc cell = a.cells[c];
     const LevelPtr lp = a.pyr[cell.level];
@@ -250,7 +248,7 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
     const int P = a.roi_pitch;
     uint8_t* roi_base = fast_lds;
     uint8_t* S = fast_lds + a.roi_rows * P;
-    uint16_t* list = reinterpret_cast<uint16_t*>(S + ((a.cand_max + 15) & ~15));
+    uint16_t* list = reinterpret_cast<uint16_t*>(S + (((a.roi_rows - 4) * P + 15) & ~15));
     // dword loads: rows are 4-byte aligned (pitch % 4 == 0, enforced by the host)
     const int x0a = cell.x0 & ~3, shift = cell.x0 - x0a;
     const int wpr = (shift + cols + 3) >> 2;
@@ -281,7 +279,12 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
     const int nr = rows - 6, nc = cols - 6;  // candidates: ROI rows/cols 3 .. n-4
     const int ncand = (nr > 0 && nc > 0) ? nr * nc : 0;
     const DivNc div(nc);
-    for (int i = lane; i < ncand; i += 64) S[i] = 0;
+    // score plane: ROI pitch, rows -1 .. nr of the candidates, zero border
+    for (int i = lane; i < (ncand ? ((nr + 2) * P) >> 2 : 0); i += 64) reinterpret_cast<uint32_t*>(S)[i] = 0u;
+    const unsigned inv_p = 0xffffffffu / (unsigned)P + 1u;  // r = umulhi(o, inv_p) for o < 2^16
+    const int rpi = nc <= 64 ? 64 / max(nc, 1) : 0;  // candidate rows per 64-lane sweep
+    const int lr = rpi ? lane / max(nc, 1) : 0, lc = lane - lr * nc;
+    const bool lane_on = lr < rpi;
     __syncthreads();
     // Pass at iniThFAST: only pixels passing the pre-test at that threshold can have S >= t,
     // and every other pixel counts as 0 in the NMS, so S is computed for those alone.
@@ -290,27 +293,36 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
     for (int pass = 0; pass < 2 && total == 0; ++pass) {
         const int t = pass ? a.min_th : a.ini_th;  // rerun at minThFAST when empty (811-815)
         int cnt = 0;
-        for (int base = 0; base < ncand; base += 64) {
-            const int p = base + lane;
-            bool ok = false;
-            if (p < ncand) {
-                const int r = div.row(p), cc = p - r * nc;
-                ok = fast_maybe(roi + (r + 3) * P + cc + 3, P, t);
+        if (rpi) {  // lanes cover rpi whole candidate rows: no per-pixel index arithmetic
+            const uint8_t* w = roi + lr * P + lc;
+            for (int r0 = 0; r0 < nr; r0 += rpi, w += rpi * P) {
+                const bool ok = lane_on && r0 + lr < nr && fast_maybe(w, P, t);
+                const unsigned long long m = __ballot(ok);
+                if (ok) list[cnt + lane_prefix(m)] = (uint16_t)((r0 + lr) * P + lc);  // row-major
+                cnt += __popcll(m);
             }
-            const unsigned long long m = __ballot(ok);
-            if (ok) list[cnt + lane_prefix(m)] = (uint16_t)p;  // row-major order
-            cnt += __popcll(m);
+        } else {
+            for (int base = 0; base < ncand; base += 64) {
+                const int p = base + lane;
+                bool ok = false;
+                if (p < ncand) {
+                    const int r = div.row(p), cc = p - r * nc;
+                    ok = fast_maybe(roi + r * P + cc, P, t);
+                }
+                const unsigned long long m = __ballot(ok);
+                if (ok) list[cnt + lane_prefix(m)] = (uint16_t)(div.row(p) * (P - nc) + p);  // r*P+c
+                cnt += __popcll(m);
+            }
         }
         __syncthreads();
 #pragma unroll 2
         for (int i = lane; i < cnt; i += 64) {
-            const int p = list[i];
-            const int r = div.row(p), cc = p - r * nc;
+            const int o = list[i];
             // S < 0 is never a corner for t >= 0: clamp to -1 so S + 1 fits a byte
-            S[p] = (uint8_t)(max(fast_S(roi + (r + 3) * P + cc + 3, P), -1) + 1);
+            S[o + P + 1] = (uint8_t)(max(fast_S(roi + o + 3 * P + 3, P), -1) + 1);
         }
         __syncthreads();
-        total = fast_emit(S, list, cnt, nr, nc, div, t, cell, out, cell.cap);
+        total = fast_emit(S, list, cnt, P, inv_p, t, cell, out, cell.cap);
         __syncthreads();
     }
     if (lane == 0) a.cell_cnt[f * a.ncells + c] = min(total, cell.cap);
@@ -742,8 +754,8 @@ constexpr int kBlurIR = kBlurTH + 6;   // input rows [oy-3, oy+TH+3)
 __global__ __launch_bounds__(256) void blur_kernel(BlurArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t in[kBlurIR * kBlurIP];
     __shared__ __attribute__((aligned(16))) uint16_t rowp[kBlurIR * kBlurTW];
-    const int f = blockIdx.y;
-    int t = blockIdx.x, l = 0;
+    int t, f, l = 0;
+    xcd_block(t, f);
     while (l + 1 < a.nlevels && t >= a.tile_begin[l + 1]) ++l;
     t -= a.tile_begin[l];
     const int w = a.w[l], h = a.h[l];
@@ -844,11 +856,12 @@ __global__ __launch_bounds__(256) void blur_kernel(BlurArgs a) {
 // output keypoint scaled to level 0 (1098-1104).
 constexpr int kDescBlock = 256;
 __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
-    const int f = blockIdx.y;
+    int bx, f;
+    xcd_block(bx, f);
     const int lane = threadIdx.x & 63;
-    const int slot = blockIdx.x * (kDescBlock / 64) + (threadIdx.x >> 6);
+    const int slot = bx * (kDescBlock / 64) + (threadIdx.x >> 6);
     const int* cnt = a.oct_cnt + f * a.nlevels;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (bx == 0 && threadIdx.x == 0) {
         int n = 0;
         for (int l = 0; l < a.nlevels; ++l) n += max(cnt[l], 0);
         a.n_out[f] = min(n, a.kps_cap);
@@ -1120,7 +1133,10 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
     g.roi_rows = rmax;
     g.roi_pitch = (cmax + 3 + 3) & ~3;  // + alignment shift, rounded to dwords
     g.cand_max = (rmax - 6) * (cmax - 6);
-    g.fast_lds = (size_t)rmax * g.roi_pitch + ((g.cand_max + 15) & ~15) + 2 * (size_t)g.cand_max + 16;
+    // ROI + zero-bordered score plane at the ROI pitch + candidate list of u16 ROI offsets
+    if ((long long)rmax * g.roi_pitch >= 65536) return ORBFE_ERR_UNSUPPORTED;
+    g.fast_lds = (size_t)rmax * g.roi_pitch + (((rmax - 4) * g.roi_pitch + 15) & ~15) +
+                 2 * (size_t)g.cand_max + 16;
     g.geo.key_total = keys;
     g.geo.out_total = out;
     g.slab = slab;
