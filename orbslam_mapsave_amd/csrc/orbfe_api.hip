@@ -159,7 +159,7 @@ struct orbfe_extractor {
         if ((st = cell_cnt.ensure(N * std::max<size_t>(1, g.cells.size()) * sizeof(int)))) return st;
         if ((st = cell_keys.ensure(N * std::max<long long>(1, g.cell_cap_total) * sizeof(uint32_t)))) return st;
         if ((st = keys.ensure(N * std::max<long long>(1, g.geo.key_total) * sizeof(uint32_t)))) return st;
-        if ((st = act.ensure(N * 2 * std::max<long long>(1, g.geo.key_total) * sizeof(int2)))) return st;
+        if ((st = act.ensure(N * 2 * std::max<long long>(1, g.geo.key_total) * sizeof(int4)))) return st;
         if ((st = oct_out.ensure(N * g.geo.out_total * sizeof(uint32_t)))) return st;
         if ((st = oct_cnt.ensure(N * g.geo.nlevels * sizeof(int)))) return st;
         frames_cap = n;
@@ -220,7 +220,7 @@ struct orbfe_extractor {
         oa.cell_cnt = cell_cnt.as<int>();
         oa.cell_keys = cell_keys.as<uint32_t>();
         oa.keys = keys.as<uint32_t>();
-        oa.act = act.as<int2>();
+        oa.act = act.as<int4>();
         oa.oct_out = oct_out.as<uint32_t>();
         oa.oct_cnt = oct_cnt.as<int>();
         oa.ncap_max = g.ncap_max;

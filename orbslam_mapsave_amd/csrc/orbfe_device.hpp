@@ -76,6 +76,19 @@ __device__ __forceinline__ int wave_inclusive_sum(int x) {
     return x;
 }
 
+// Slot of this lane's item in a block-shared list: one LDS atomic per wave (called by every
+// lane of the wave); -1 for lanes without an item.  Order among waves is unspecified.
+__device__ __forceinline__ int wave_append(bool pred, int* counter) {
+    const unsigned long long m = __ballot(pred);
+    if (!m) return -1;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(counter, __popcll(m));
+    base = __shfl(base, leader, 64);
+    return pred ? base + __popcll(m & ((1ull << lane) - 1)) : -1;
+}
+
 __device__ __forceinline__ int wave_sum(int x) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);

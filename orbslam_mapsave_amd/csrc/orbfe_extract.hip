@@ -341,13 +341,19 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
 // list position of its node.  Single-key nodes remember their key and drop out of the key set.
 // Final: per node the max response, first (lowest original index) on ties (741-759).
 constexpr int kOctBlock = 512;
+constexpr int OCT_UNROLL = 4;
 
 struct OctLds {  // carve of the dynamic LDS region (sizes in elements)
-    int* box[2];    // x0 | x1 << 16
-    int* boy[2];    // y0 | y1 << 16
-    int* cnt[2];
-    int* seq[2];
-    int* key[2];
+    // two node lists (b = 0 / 1), 5 arrays of NC each: box x0 | x1 << 16, boy y0 | y1 << 16,
+    // key count, creation seq, key (single-key nodes); addressed by arithmetic, since a
+    // runtime-indexed pointer array would live in scratch
+    int* lists;
+    int nc;
+    __device__ __forceinline__ int* box(int b) const { return lists + (b * 5 + 0) * nc; }
+    __device__ __forceinline__ int* boy(int b) const { return lists + (b * 5 + 1) * nc; }
+    __device__ __forceinline__ int* cnt(int b) const { return lists + (b * 5 + 2) * nc; }
+    __device__ __forceinline__ int* seq(int b) const { return lists + (b * 5 + 3) * nc; }
+    __device__ __forceinline__ int* key(int b) const { return lists + (b * 5 + 4) * nc; }
     int* qc;        // 4 per node: keys per quadrant
     int* qk;        // 4 per node: a key of the quadrant, then the child's new list position
     int* aux;       // per node: scan offsets / kept position / processed flag
@@ -373,6 +379,45 @@ __device__ __forceinline__ void child_box(int box, int boy, int q, int& cbx, int
     cby = cy0 | (cy1 << 16);
 }
 
+// Sweeps over a live-key list: every thread loads OCT_UNROLL entries before using any.
+template <class F>
+__device__ __forceinline__ void oct_sweep(const int4* list, int nact, F&& body) {
+    for (int e0 = threadIdx.x; e0 < nact; e0 += OCT_UNROLL * kOctBlock) {
+        int4 ens[OCT_UNROLL];
+#pragma unroll
+        for (int u = 0; u < OCT_UNROLL; ++u) {
+            const int e = e0 + u * kOctBlock;
+            ens[u] = e < nact ? list[e] : make_int4(0, 0, -1, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < OCT_UNROLL; ++u)
+            if (ens[u].z >= 0) body(ens[u]);
+    }
+}
+
+// As oct_sweep; body sets the entry's node in the next list, and entries whose node still
+// holds >= 2 keys are appended to it.
+template <class F>
+__device__ __forceinline__ void oct_sweep_append(const int4* list, int4* next, int nact,
+                                                 const int* next_cnt, int* next_n, F&& body) {
+    for (int e0 = threadIdx.x; e0 < nact; e0 += OCT_UNROLL * kOctBlock) {
+        int4 ens[OCT_UNROLL];
+#pragma unroll
+        for (int u = 0; u < OCT_UNROLL; ++u) {
+            const int e = e0 + u * kOctBlock;
+            ens[u] = e < nact ? list[e] : make_int4(0, 0, -1, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < OCT_UNROLL; ++u) {
+            int np = 0;
+            if (ens[u].z >= 0) body(ens[u], np);
+            const bool live = ens[u].z >= 0 && next_cnt[np] >= 2;
+            const int slot = wave_append(live, next_n);
+            if (live) next[slot] = make_int4(ens[u].x, ens[u].y, np, 0);
+        }
+    }
+}
+
 __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     const int level = blockIdx.x, f = blockIdx.y;
@@ -384,13 +429,9 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
         int* p = reinterpret_cast<int*>(lds_raw);
         s.s64 = reinterpret_cast<unsigned long long*>(p);
         p += 2 * a.sort_cap;
-        for (int b = 0; b < 2; ++b) {
-            s.box[b] = p; p += NC;
-            s.boy[b] = p; p += NC;
-            s.cnt[b] = p; p += NC;
-            s.seq[b] = p; p += NC;
-            s.key[b] = p; p += NC;
-        }
+        s.lists = p;
+        s.nc = NC;
+        p += 10 * NC;
         s.qc = p; p += 4 * NC;
         s.qk = p; p += 4 * NC;
         s.aux = p; p += NC;
@@ -423,8 +464,10 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
         return;
     }
 
-    int2* const act0 = a.act + f * a.geo.key_total * 2 + L.key_off * 2;
-    int2* const act1 = act0 + L.key_cap;
+    // live keys {packed key, key index, node}: the key travels with its entry, so a sweep is
+    // one 16-byte load per key with OCT_UNROLL of them in flight per thread
+    int4* const act0 = a.act + f * a.geo.key_total * 2 + L.key_off * 2;
+    int4* const act1 = act0 + L.key_cap;
 #define ACT(b) ((b) ? act1 : act0)  // runtime-indexed pointer arrays would live in scratch
     int* nact_sh = s.scal;        // scal[0..1]: active counters
     int* flag_sh = s.scal + 2;    // scal[2]: overflow / misc
@@ -459,11 +502,11 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
             if (ne) {
                 const int pos = total + off;
                 const int x0 = (int)(hX * (float)i), x1 = (int)(hX * (float)(i + 1));
-                s.box[0][pos] = x0 | (x1 << 16);
-                s.boy[0][pos] = 0 | (H << 16);
-                s.cnt[0][pos] = s.qc[i];
-                s.seq[0][pos] = i;
-                s.key[0][pos] = s.qc[i] == 1 ? s.qk[i] : -1;
+                s.box(0)[pos] = x0 | (x1 << 16);
+                s.boy(0)[pos] = 0 | (H << 16);
+                s.cnt(0)[pos] = s.qc[i];
+                s.seq(0)[pos] = i;
+                s.key(0)[pos] = s.qc[i] == 1 ? s.qk[i] : -1;
                 s.aux[i] = pos;
             }
             total += chunk_total;
@@ -471,10 +514,13 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
         size = total;
     }
     __syncthreads();
-    for (int k = tid; k < nkeys; k += kOctBlock) {
-        const int x = key_x(K[k]);
-        const int node = s.aux[min((int)((float)x / hX), nini - 1)];
-        if (s.cnt[0][node] >= 2) ACT(0)[atomicAdd(&nact_sh[0], 1)] = make_int2(k, node);
+    for (int k0 = 0; k0 < nkeys; k0 += kOctBlock) {
+        const int k = k0 + tid;
+        const uint32_t kk = k < nkeys ? K[k] : 0u;
+        const int node = k < nkeys ? s.aux[min((int)((float)key_x(kk) / hX), nini - 1)] : 0;
+        const bool live = k < nkeys && s.cnt(0)[node] >= 2;
+        const int slot = wave_append(live, &nact_sh[0]);
+        if (live) ACT(0)[slot] = make_int4((int)kk, k, node, 0);
     }
     __syncthreads();
     int cur = 0;
@@ -491,12 +537,14 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
         for (int i = tid; i < 4 * size; i += kOctBlock) s.qc[i] = 0;
         if (tid == 0) nact_sh[nxt] = 0;
         __syncthreads();
-        for (int e = tid; e < nact; e += kOctBlock) {
-            const int2 en = ACT(cur)[e];
-            const uint32_t kk = K[en.x];
-            const int q = quadrant(s.box[cur][en.y], s.boy[cur][en.y], key_x(kk), key_y(kk));
-            atomicAdd(&s.qc[en.y * 4 + q], 1);
-            s.qk[en.y * 4 + q] = en.x;
+        {
+            const int *bx = s.box(cur), *by = s.boy(cur);
+            int *qc = s.qc, *qk = s.qk;
+            oct_sweep(ACT(cur), nact, [=](const int4 en) {
+                const int q = quadrant(bx[en.z], by[en.z], key_x(en.x), key_y(en.x));
+                atomicAdd(&qc[en.z * 4 + q], 1);
+                qk[en.z * 4 + q] = en.y;
+            });
         }
         __syncthreads();
         // per node: children (divided) or kept (single); aux = child offset, aux2 = kept offset
@@ -505,7 +553,7 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
             const int i = base + tid;
             int nch = 0, keep = 0, ne = 0;
             if (i < size) {
-                if (s.cnt[cur][i] >= 2) {
+                if (s.cnt(cur)[i] >= 2) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         const int qn = s.qc[i * 4 + q];
@@ -535,7 +583,7 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
         }
         __syncthreads();
         for (int i = tid; i < size; i += kOctBlock) {
-            if (s.cnt[cur][i] >= 2) {
+            if (s.cnt(cur)[i] >= 2) {
                 int cp = s.aux[i];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -543,31 +591,31 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
                     if (!qn) continue;
                     const int np = csize - 1 - cp;
                     int cbx, cby;
-                    child_box(s.box[cur][i], s.boy[cur][i], q, cbx, cby);
-                    s.box[nxt][np] = cbx;
-                    s.boy[nxt][np] = cby;
-                    s.cnt[nxt][np] = qn;
-                    s.seq[nxt][np] = seq_base + cp;
-                    s.key[nxt][np] = qn == 1 ? s.qk[i * 4 + q] : -1;
+                    child_box(s.box(cur)[i], s.boy(cur)[i], q, cbx, cby);
+                    s.box(nxt)[np] = cbx;
+                    s.boy(nxt)[np] = cby;
+                    s.cnt(nxt)[np] = qn;
+                    s.seq(nxt)[np] = seq_base + cp;
+                    s.key(nxt)[np] = qn == 1 ? s.qk[i * 4 + q] : -1;
                     s.qk[i * 4 + q] = np;
                     ++cp;
                 }
             } else {
                 const int np = csize + s.aux2[i];
-                s.box[nxt][np] = s.box[cur][i];
-                s.boy[nxt][np] = s.boy[cur][i];
-                s.cnt[nxt][np] = s.cnt[cur][i];
-                s.seq[nxt][np] = s.seq[cur][i];
-                s.key[nxt][np] = s.key[cur][i];
+                s.box(nxt)[np] = s.box(cur)[i];
+                s.boy(nxt)[np] = s.boy(cur)[i];
+                s.cnt(nxt)[np] = s.cnt(cur)[i];
+                s.seq(nxt)[np] = s.seq(cur)[i];
+                s.key(nxt)[np] = s.key(cur)[i];
             }
         }
         __syncthreads();
-        for (int e = tid; e < nact; e += kOctBlock) {
-            const int2 en = ACT(cur)[e];
-            const uint32_t kk = K[en.x];
-            const int q = quadrant(s.box[cur][en.y], s.boy[cur][en.y], key_x(kk), key_y(kk));
-            const int np = s.qk[en.y * 4 + q];
-            if (s.cnt[nxt][np] >= 2) ACT(nxt)[atomicAdd(&nact_sh[nxt], 1)] = make_int2(en.x, np);
+        {
+            const int *bx = s.box(cur), *by = s.boy(cur), *qk = s.qk;
+            oct_sweep_append(ACT(cur), ACT(nxt), nact, s.cnt(nxt), &nact_sh[nxt], [=](const int4 en, int& np) {
+                const int q = quadrant(bx[en.z], by[en.z], key_x(en.x), key_y(en.x));
+                np = qk[en.z * 4 + q];
+            });
         }
         __syncthreads();
         nact = nact_sh[nxt];
@@ -588,10 +636,10 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
         for (int i = tid; i < 4 * size; i += kOctBlock) s.qc[i] = 0;
         __syncthreads();
         for (int i = tid; i < size; i += kOctBlock)
-            if (s.cnt[cur][i] >= 2) {
+            if (s.cnt(cur)[i] >= 2) {
                 const int slot = atomicAdd(&flag_sh[0], 1);
-                s.s64[slot] = ((unsigned long long)s.cnt[cur][i] << 40) |
-                              ((unsigned long long)(unsigned)s.seq[cur][i] << 14) | (unsigned)i;
+                s.s64[slot] = ((unsigned long long)s.cnt(cur)[i] << 40) |
+                              ((unsigned long long)(unsigned)s.seq(cur)[i] << 14) | (unsigned)i;
             }
         __syncthreads();
         const int m = flag_sh[0];
@@ -611,12 +659,14 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
                 }
                 __syncthreads();
             }
-        for (int e = tid; e < nact; e += kOctBlock) {
-            const int2 en = ACT(cur)[e];
-            const uint32_t kk = K[en.x];
-            const int q = quadrant(s.box[cur][en.y], s.boy[cur][en.y], key_x(kk), key_y(kk));
-            atomicAdd(&s.qc[en.y * 4 + q], 1);
-            s.qk[en.y * 4 + q] = en.x;
+        {
+            const int *bx = s.box(cur), *by = s.boy(cur);
+            int *qc = s.qc, *qk = s.qk;
+            oct_sweep(ACT(cur), nact, [=](const int4 en) {
+                const int q = quadrant(bx[en.z], by[en.z], key_x(en.x), key_y(en.x));
+                atomicAdd(&qc[en.z * 4 + q], 1);
+                qk[en.z * 4 + q] = en.y;
+            });
         }
         __syncthreads();
         // cut: first j in sorted order with size + sum_{<=j}(nch-1) >= N (else all m)
@@ -682,37 +732,36 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
                     if (!qn) continue;
                     const int np = csize - 1 - cp;
                     int cbx, cby;
-                    child_box(s.box[cur][i], s.boy[cur][i], q, cbx, cby);
-                    s.box[nxt][np] = cbx;
-                    s.boy[nxt][np] = cby;
-                    s.cnt[nxt][np] = qn;
-                    s.seq[nxt][np] = seq_base + cp;
-                    s.key[nxt][np] = qn == 1 ? s.qk[i * 4 + q] : -1;
+                    child_box(s.box(cur)[i], s.boy(cur)[i], q, cbx, cby);
+                    s.box(nxt)[np] = cbx;
+                    s.boy(nxt)[np] = cby;
+                    s.cnt(nxt)[np] = qn;
+                    s.seq(nxt)[np] = seq_base + cp;
+                    s.key(nxt)[np] = qn == 1 ? s.qk[i * 4 + q] : -1;
                     s.qk[i * 4 + q] = np;
                     ++cp;
                 }
             } else {
                 const int np = csize + (-s.aux2[i] - 1);
-                s.box[nxt][np] = s.box[cur][i];
-                s.boy[nxt][np] = s.boy[cur][i];
-                s.cnt[nxt][np] = s.cnt[cur][i];
-                s.seq[nxt][np] = s.seq[cur][i];
-                s.key[nxt][np] = s.key[cur][i];
+                s.box(nxt)[np] = s.box(cur)[i];
+                s.boy(nxt)[np] = s.boy(cur)[i];
+                s.cnt(nxt)[np] = s.cnt(cur)[i];
+                s.seq(nxt)[np] = s.seq(cur)[i];
+                s.key(nxt)[np] = s.key(cur)[i];
                 s.aux[i] = np;
             }
         }
         __syncthreads();
-        for (int e = tid; e < nact; e += kOctBlock) {
-            const int2 en = ACT(cur)[e];
-            int np;
-            if (s.aux2[en.y] > 0) {
-                const uint32_t kk = K[en.x];
-                const int q = quadrant(s.box[cur][en.y], s.boy[cur][en.y], key_x(kk), key_y(kk));
-                np = s.qk[en.y * 4 + q];
-            } else {
-                np = s.aux[en.y];
-            }
-            if (s.cnt[nxt][np] >= 2) ACT(nxt)[atomicAdd(&nact_sh[nxt], 1)] = make_int2(en.x, np);
+        {
+            const int *bx = s.box(cur), *by = s.boy(cur), *qk = s.qk, *aux = s.aux, *aux2 = s.aux2;
+            oct_sweep_append(ACT(cur), ACT(nxt), nact, s.cnt(nxt), &nact_sh[nxt], [=](const int4 en, int& np) {
+                if (aux2[en.z] > 0) {
+                    const int q = quadrant(bx[en.z], by[en.z], key_x(en.x), key_y(en.x));
+                    np = qk[en.z * 4 + q];
+                } else {
+                    np = aux[en.z];
+                }
+            });
         }
         __syncthreads();
         nact = nact_sh[nxt];
@@ -726,16 +775,17 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
     // ---- 5. retain the best key per node (740-759), emit in list order
     for (int i = tid; i < size; i += kOctBlock) s.s64[i] = 0ull;
     __syncthreads();
-    for (int e = tid; e < nact; e += kOctBlock) {
-        const int2 en = ACT(cur)[e];
-        const uint32_t kk = K[en.x];
-        const unsigned long long v =
-            ((unsigned long long)key_score(kk) << 32) | (0xffffffffu - (unsigned)en.x);
-        atomicMax(&s.s64[en.y], v);
+    {
+        unsigned long long* best = s.s64;
+        oct_sweep(ACT(cur), nact, [=](const int4 en) {
+            const unsigned long long v =
+                ((unsigned long long)key_score(en.x) << 32) | (0xffffffffu - (unsigned)en.y);
+            atomicMax(&best[en.z], v);
+        });
     }
     __syncthreads();
     for (int i = tid; i < size; i += kOctBlock) {
-        const int k = s.cnt[cur][i] == 1 ? s.key[cur][i]
+        const int k = s.cnt(cur)[i] == 1 ? s.key(cur)[i]
                                           : (int)(0xffffffffu - (unsigned)(s.s64[i] & 0xffffffffu));
         const uint32_t kk = K[k];
         out[i] = pack_key(key_x(kk) + kMinBorder, key_y(kk) + kMinBorder, key_score(kk));
@@ -748,12 +798,13 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
 // K4 — GaussianBlur(7x7, sigma 2, REFLECT_101) integer path: row pass R = sum k_i I (<= 65535,
 // kept as u16), column pass (sum k_j R + 2^15) >> 16 saturated (App. A.2).  128 x 32 output
 // tile per workgroup of 32 x 8 threads; each thread makes 4 x 4 pixels from dword LDS reads.
-constexpr int kBlurTW = 128, kBlurTH = 32;
+constexpr int kBlurTW = kBlurTileW, kBlurTH = kBlurTileH;
+constexpr int kBlurRPT = kBlurTH / 8;  // output rows per thread (256 threads = 8 x 32)
 constexpr int kBlurIP = kBlurTW + 8;   // input row: image cols [ox-4, ox+TW+4)
 constexpr int kBlurIR = kBlurTH + 6;   // input rows [oy-3, oy+TH+3)
 __global__ __launch_bounds__(256) void blur_kernel(BlurArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t in[kBlurIR * kBlurIP];
-    __shared__ __attribute__((aligned(16))) uint16_t rowp[kBlurIR * kBlurTW];
+    __shared__ __attribute__((aligned(16))) uint16_t rowp[kBlurIR * kBlurTW];  // row pairs, u16x2
     int t, f, l = 0;
     xcd_block(t, f);
     while (l + 1 < a.nlevels && t >= a.tile_begin[l + 1]) ++l;
@@ -767,7 +818,7 @@ __global__ __launch_bounds__(256) void blur_kernel(BlurArgs a) {
     // input rows are reflected by picking the row pointer; only dwords that straddle the left
     // or right edge are assembled byte by byte (reflect-101, level sizes >= 4)
     constexpr int WPR = kBlurIP / 4;
-    constexpr int NLD = (kBlurIR * WPR + 255) / 256;  // 6 dwords per thread
+    constexpr int NLD = (kBlurIR * WPR + 255) / 256;  // dwords per thread
     uint32_t buf[NLD];
 #pragma unroll
     for (int k = 0; k < NLD; ++k) {  // issue every load before the first LDS store
@@ -796,52 +847,74 @@ __global__ __launch_bounds__(256) void blur_kernel(BlurArgs a) {
         if (i < kBlurIR * WPR) *reinterpret_cast<uint32_t*>(in + (i / WPR) * kBlurIP + 4 * (i % WPR)) = buf[k];
     }
     __syncthreads();
+    // Row pass on bytes: output col c = dot4(bytes c+1..c+4, k0 k1 k2 k3) + dot4(bytes c+5..c+8,
+    // k2 k1 k0 0) (v_dot4_u32_u8), exact in u16 (max 255 * 257).  A work item makes 4 columns
+    // of two consecutive input rows and stores them as dwords (row 2i in the low half, row 2i+1
+    // in the high half), so the column pass reads row pairs for v_dot2_u32_u16.
     const int k0 = a.taps[0], k1 = a.taps[1], k2 = a.taps[2], k3 = a.taps[3];
-    const int ltx = tid & 31, lty = tid >> 5;
-    for (int r = lty; r < kBlurIR; r += 8) {  // 4 output columns 4*ltx .. +3 <- LDS cols +1 .. +10
-        const uint32_t* q = reinterpret_cast<const uint32_t*>(in + r * kBlurIP + 4 * ltx);
-        const uint32_t w0 = q[0], w1 = q[1], w2 = q[2];
-        int b[12];
+    const uint32_t KLO = (uint32_t)(k0 | (k1 << 8) | (k2 << 16) | (k3 << 24));
+    const uint32_t KHI = (uint32_t)(k2 | (k1 << 8) | (k0 << 16));
+    constexpr int NPAIR = kBlurIR / 2;
+    for (int it = tid; it < NPAIR * (kBlurTW / 4); it += 256) {
+        const int pr = it >> 5, q = it & 31;
+        uint32_t h[2][4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            b[i] = (w0 >> (8 * i)) & 255;
-            b[4 + i] = (w1 >> (8 * i)) & 255;
-            b[8 + i] = (w2 >> (8 * i)) & 255;
+        for (int e = 0; e < 2; ++e) {
+            const uint32_t* row = reinterpret_cast<const uint32_t*>(in + (2 * pr + e) * kBlurIP) + q;
+            const uint32_t w0 = row[0], w1 = row[1], w2 = row[2];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t lo = j < 3 ? __builtin_amdgcn_alignbyte(w1, w0, j + 1) : w1;
+                const uint32_t hi = j < 3 ? __builtin_amdgcn_alignbyte(w2, w1, j + 1) : w2;
+                h[e][j] = __builtin_amdgcn_udot4(hi, KHI, __builtin_amdgcn_udot4(lo, KLO, 0u, false), false);
+            }
         }
-        uint32_t o01, o23;
-        int v[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            v[j] = k0 * (b[j + 1] + b[j + 7]) + k1 * (b[j + 2] + b[j + 6]) +
-                   k2 * (b[j + 3] + b[j + 5]) + k3 * b[j + 4];
-        o01 = (uint32_t)v[0] | ((uint32_t)v[1] << 16);
-        o23 = (uint32_t)v[2] | ((uint32_t)v[3] << 16);
-        *reinterpret_cast<uint2*>(rowp + r * kBlurTW + 4 * ltx) = make_uint2(o01, o23);
+        *reinterpret_cast<uint4*>(rowp + (pr * kBlurTW + 4 * q) * 2) =
+            make_uint4(h[0][0] | (h[1][0] << 16), h[0][1] | (h[1][1] << 16),
+                       h[0][2] | (h[1][2] << 16), h[0][3] | (h[1][3] << 16));
     }
     __syncthreads();
+    // Column pass: output row j (input rows j .. j+6) as four v_dot2_u32_u16 over row pairs,
+    // the rounding constant folded into the first; rows j even / odd pair differently.
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    const us2 T01 = us2{(unsigned short)k0, (unsigned short)k1}, T23 = us2{(unsigned short)k2, (unsigned short)k3},
+              T21 = us2{(unsigned short)k2, (unsigned short)k1}, T12 = us2{(unsigned short)k1, (unsigned short)k2},
+              T32 = us2{(unsigned short)k3, (unsigned short)k2}, T10 = us2{(unsigned short)k1, (unsigned short)k0},
+              T0L = us2{(unsigned short)k0, 0}, T0H = us2{0, (unsigned short)k0};
     const LevelPtr dp = a.dst[l];
     uint8_t* dst = const_cast<uint8_t*>(dp.base) + f * dp.fpitch;
-    int R[10][4];
+    const int ltx = tid & 31, lty = tid >> 5;
+    uint4 Pq[kBlurRPT / 2 + 3];
 #pragma unroll
-    for (int i = 0; i < 10; ++i) {
-        const uint2 u = *reinterpret_cast<const uint2*>(rowp + (4 * lty + i) * kBlurTW + 4 * ltx);
-        R[i][0] = u.x & 0xffff;
-        R[i][1] = u.x >> 16;
-        R[i][2] = u.y & 0xffff;
-        R[i][3] = u.y >> 16;
-    }
+    for (int i = 0; i < kBlurRPT / 2 + 3; ++i)
+        Pq[i] = *reinterpret_cast<const uint4*>(rowp + (((kBlurRPT / 2) * lty + i) * kBlurTW + 4 * ltx) * 2);
     const int x = ox + 4 * ltx;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int y = oy + 4 * lty + j;
+    for (int j = 0; j < kBlurRPT; ++j) {
+        const int y = oy + kBlurRPT * lty + j;
         if (y >= h) break;
-        uint32_t packed = 0;
+        const int b = j >> 1;
+        uint32_t acc[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            const int acc = k0 * (R[j][c] + R[j + 6][c]) + k1 * (R[j + 1][c] + R[j + 5][c]) +
-                            k2 * (R[j + 2][c] + R[j + 4][c]) + k3 * R[j + 3][c];
-            packed |= (uint32_t)min((acc + (1 << 15)) >> 16, 255) << (8 * c);
+            const uint32_t p0 = (&Pq[b].x)[c], p1 = (&Pq[b + 1].x)[c], p2 = (&Pq[b + 2].x)[c],
+                           p3 = (&Pq[b + 3].x)[c];
+            uint32_t v;
+            if ((j & 1) == 0) {
+                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T01, 1u << 15, false);
+                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), T23, v, false);
+                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), T21, v, false);
+                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), T0L, v, false);
+            } else {
+                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T0H, 1u << 15, false);
+                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), T12, v, false);
+                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), T32, v, false);
+                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), T10, v, false);
+            }
+            acc[c] = min(v, 0xffffffu);  // byte 2 = min(acc >> 16, 255)
         }
+        const uint32_t packed = __builtin_amdgcn_perm(acc[1], acc[0], 0x0c0c0602u) |
+                                __builtin_amdgcn_perm(acc[3], acc[2], 0x06020c0cu);
         uint8_t* d = dst + (long long)y * dp.pitch + x;
         if (x + 4 <= w) {
             *reinterpret_cast<uint32_t*>(d) = packed;

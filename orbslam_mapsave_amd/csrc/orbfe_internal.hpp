@@ -82,7 +82,7 @@ struct OctArgs {
     const int* cell_cnt;
     const uint32_t* cell_keys;
     uint32_t* keys;        // [frame][key_total] compacted per level
-    int2* act;             // [frame][2 * key_total] live keys (key index, node)
+    int4* act;             // [frame][2 * key_total] live keys (packed key, key index, node, -)
     uint32_t* oct_out;     // [frame][out_total]
     int* oct_cnt;          // [frame][nlevels]
     int ncap_max, sort_cap;
