@@ -255,8 +255,8 @@ struct orbfe_extractor {
         da.kps = d_kps;
         da.desc = d_desc;
         da.n_out = d_n;
-        const int waves = kDescBlockSize / 64;
-        ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, describe_kernel, dim3((g.geo.out_total + waves - 1) / waves, n),
+        const int per_block = (kDescBlockSize / 64) * kDescGroupSize;  // slots per workgroup
+        ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, describe_kernel, dim3((g.geo.out_total + per_block - 1) / per_block, n),
                            dim3(kDescBlockSize), 0, stream, da);
         ORBFE_HIP(hipGetLastError());
         last_n = n;

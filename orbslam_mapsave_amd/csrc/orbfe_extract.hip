@@ -925,91 +925,208 @@ __global__ __launch_bounds__(256) void blur_kernel(BlurArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// K5 — one wave per keypoint: IC angle on the unblurred level, rBRIEF on the blurred level,
-// output keypoint scaled to level 0 (1098-1104).
-constexpr int kDescBlock = 256;
+// K5 — IC angle (76-103) on the unblurred level, rBRIEF (107-146) on the blurred level and
+// the keypoint scaled to level 0 (1098-1104).  A wave owns kDescGroup consecutive oct-tree
+// output slots of one frame:
+//   1. per keypoint, the whole wave sums the 31 x 31 disc: lane = (row v, half) loads 16
+//      pixels with one 16-byte load and weighs them with v_dot4_u32_u8 against per-lane
+//      constant byte masks: m10 = sum (u + 16) I - 16 sum I, m01 = v sum I (integers, exact);
+//   2. lane j computes keypoint j's fastAtan2 and its double-precision cos / sin once, so the
+//      trig costs one wave instruction stream per group instead of one per keypoint;
+//   3. per keypoint, lane k evaluates the rotated pattern pairs k + 64 r (pattern held in
+//      registers across the group) and 4 ballots make the 256-bit descriptor.
+constexpr int kDescBlock = kDescBlockSize;
+constexpr int kDescGroup = kDescGroupSize;
+constexpr int kDescWinR = 18;                        // rotated pattern radius bound (< 18.5)
+constexpr int kDescWinRows = 2 * kDescWinR + 1;      // 37
+constexpr int kDescWinP = 48;                        // bytes per window row (3 x 16)
+constexpr int kDescWinBytes = kDescWinRows * kDescWinP;
+typedef uint4 __attribute__((aligned(1))) uint4_u;  // unaligned 16-byte global load
+typedef float float2v __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
     int bx, f;
     xcd_block(bx, f);
     const int lane = threadIdx.x & 63;
-    const int slot = bx * (kDescBlock / 64) + (threadIdx.x >> 6);
     const int* cnt = a.oct_cnt + f * a.nlevels;
     if (bx == 0 && threadIdx.x == 0) {
         int n = 0;
         for (int l = 0; l < a.nlevels; ++l) n += max(cnt[l], 0);
         a.n_out[f] = min(n, a.kps_cap);
     }
-    if (slot >= a.out_total) return;
-    int l = 0;
-    while (l + 1 < a.nlevels && slot >= a.out_off[l + 1]) ++l;
-    const int idx = slot - a.out_off[l];
-    if (idx >= cnt[l]) return;
-    int o = idx;
-    for (int q = 0; q < l; ++q) o += max(cnt[q], 0);
-    if (o >= a.kps_cap) return;
-    const uint32_t kk = a.oct_out[f * a.out_total + slot];
-    const int x = key_x(kk), y = key_y(kk), score = key_score(kk);
+    const int s0 = (bx * (kDescBlock / 64) + (threadIdx.x >> 6)) * kDescGroup;
+    if (s0 >= a.out_total) return;
 
-    // IC angle: lane handles column u = (lane & 31) - 15, rows v <= 0 (half 0) or v > 0.
-    const LevelPtr pp = a.pyr[l];
-    const uint8_t* img = pp.base + f * pp.fpitch + (long long)y * pp.pitch + x;
-    const int u = (lane & 31) - 15;
-    const int half = lane >> 5;
-    // all 16 rows of the lane's column are loaded before use (rows +-15, cols +-16 stay inside
-    // the level: keypoints are >= 19 px from its border), then masked by umax
-    int val[16];
-#pragma unroll
-    for (int vv = 0; vv < 16; ++vv) {
-        const int v = half ? min(vv + 1, 15) : -vv;
-        val[vv] = img[(long long)v * pp.pitch + u];
-    }
-    int m10 = 0, m01 = 0;
-    if ((lane & 31) < 31) {
-#pragma unroll
-        for (int vv = 0; vv < 16; ++vv) {
-            const int v = half ? vv + 1 : -vv;
-            const int av = v < 0 ? -v : v;
-            const bool in = !(half && vv == 15) && u >= -c_umax[min(av, 15)] && u <= c_umax[min(av, 15)];
-            m10 += in ? u * val[vv] : 0;
-            m01 += in ? v * val[vv] : 0;
+    // lane j < kDescGroup: slot s0 + j -> level, key, output index
+    int my_l = 0, my_key = 0, my_o = 0;
+    bool valid = false;
+    if (lane < kDescGroup && s0 + lane < a.out_total) {
+        const int slot = s0 + lane;
+        int l = 0;
+        while (l + 1 < a.nlevels && slot >= a.out_off[l + 1]) ++l;
+        const int idx = slot - a.out_off[l];
+        if (idx < cnt[l]) {
+            int o = idx;
+            for (int q = 0; q < l; ++q) o += max(cnt[q], 0);
+            if (o < a.kps_cap) {
+                valid = true;
+                my_l = l;
+                my_o = o;
+                my_key = (int)a.oct_out[f * a.out_total + slot];
+            }
         }
     }
-    m10 = wave_sum(m10);
-    m01 = wave_sum(m01);
-    const float angle = fast_atan2((float)m01, (float)m10);
+    const unsigned long long vmask = __ballot(valid);
+    if (!vmask) return;
 
-    // rBRIEF: lane handles pairs lane + 64 r; bit k of byte i = pair 8 i + k (122-143)
-    const float ang = angle * (float)(3.14159265358979323846 / 180.f);
-    const float ca = (float)cos((double)ang), sb = (float)sin((double)ang);
-    const LevelPtr bp = a.blur[l];
-    const uint8_t* c = bp.base + f * bp.fpitch + (long long)y * bp.pitch + x;
-    const long long st = bp.pitch;
-    unsigned long long words[4];
+    // 1. IC moments.  Lane (r = lane >> 1, hh = lane & 1): row v = r - 15, columns
+    //    u = -15 + 16 hh .. +15 (u = 16 never lies in the disc).
+    const int r = lane >> 1, hh = lane & 1, v = r - 15;
+    const int av = v < 0 ? -v : v;
+    const int ulim = r < 31 ? c_umax[min(av, 15)] : -1;
+    uint32_t wu[4], w1[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int pair = lane + 64 * r;
-        const float px0 = (float)c_pattern[4 * pair], py0 = (float)c_pattern[4 * pair + 1];
-        const float px1 = (float)c_pattern[4 * pair + 2], py1 = (float)c_pattern[4 * pair + 3];
-        const int i0 = c[rne(px0 * sb + py0 * ca) * st + rne(px0 * ca - py0 * sb)];
-        const int i1 = c[rne(px1 * sb + py1 * ca) * st + rne(px1 * ca - py1 * sb)];
-        words[r] = __ballot(i0 < i1);
+    for (int d = 0; d < 4; ++d) {
+        uint32_t x = 0, y = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int u = -15 + 16 * hh + 4 * d + b;
+            const bool in = (u < 0 ? -u : u) <= ulim;
+            x |= (in ? (uint32_t)(u + 16) : 0u) << (8 * b);
+            y |= (in ? 1u : 0u) << (8 * b);
+        }
+        wu[d] = x;
+        w1[d] = y;
     }
-    const long long outi = (long long)f * a.kps_cap + o;
-    if (lane < 4) {
-        unsigned long long wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
-        reinterpret_cast<unsigned long long*>(a.desc + outi * 32)[lane] = wv;
+    // every keypoint's 16-byte row load is issued before the first reduction
+    uint4 px[kDescGroup];
+#pragma unroll
+    for (int j = 0; j < kDescGroup; ++j) {
+        px[j] = make_uint4(0u, 0u, 0u, 0u);
+        if (((vmask >> j) & 1) && r < 31) {
+            const int kl = __builtin_amdgcn_readlane(my_l, j);
+            const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane(my_key, j);
+            const LevelPtr pp = a.pyr[kl];
+            const uint8_t* row = pp.base + f * pp.fpitch + (long long)(key_y(kk) + v) * pp.pitch +
+                                 key_x(kk) - 15 + 16 * hh;
+            px[j] = *reinterpret_cast<const uint4_u*>(row);
+        }
     }
-    if (lane == 0) {
+    int M10 = 0, M01 = 0;
+#pragma unroll
+    for (int j = 0; j < kDescGroup; ++j) {
+        const uint4 p4 = px[j];
+        const int su = (int)__builtin_amdgcn_udot4(p4.x, wu[0], __builtin_amdgcn_udot4(p4.y, wu[1],
+                       __builtin_amdgcn_udot4(p4.z, wu[2], __builtin_amdgcn_udot4(p4.w, wu[3], 0u, false), false), false), false);
+        const int s = (int)__builtin_amdgcn_udot4(p4.x, w1[0], __builtin_amdgcn_udot4(p4.y, w1[1],
+                      __builtin_amdgcn_udot4(p4.z, w1[2], __builtin_amdgcn_udot4(p4.w, w1[3], 0u, false), false), false), false);
+        const int m10 = wave_sum(su - 16 * s), m01 = wave_sum(v * s);
+        if (lane == j) {
+            M10 = m10;
+            M01 = m01;
+        }
+    }
+
+    // 2. angle and its rotation, one keypoint per lane
+    const float angle = fast_atan2((float)M01, (float)M10);
+    const float ang = angle * (float)(3.14159265358979323846 / 180.f);
+    float ca = 1.f, sa = 0.f;
+    if (valid) {
+        ca = (float)cos((double)ang);
+        sa = (float)sin((double)ang);
+    }
+
+    // 3. rBRIEF: lane handles pairs lane + 64 q; bit k of byte i = pair 8 i + k (122-143).
+    // Rotated pattern points stay within 13 sqrt 2 < 18.5 px of the keypoint, so keypoint j's
+    // 37-row window of the blurred level (48 bytes per row from x0 = (x - 18) & ~3) is copied
+    // into LDS with coalesced 16-byte loads (111 chunks, lanes c and c + 64), and the 512
+    // scattered byte reads become ds_read_u8.  Windows are double-buffered per wave: the
+    // loads of keypoint j + 1 are in flight while keypoint j is sampled.
+    //
+    // A rotated point is (py, px) = (px sin + py cos, px cos - py sin), each product and the
+    // sum rounded separately as the reference writes it (v_pk_mul_f32 / v_pk_add_f32 do both
+    // coordinates with the same IEEE roundings; px * -sin == -(px * sin)).  cvRound is the
+    // magic-number add (|v| < 2^22, round-to-nearest-even): bits(v + 1.5 * 2^23) =
+    // 0x4b400000 + rne(v); v_mul_u32_u24 takes its low 24 bits, 0x400000 + rne(v), so one
+    // per-keypoint constant turns the pair into the window index (18 + ry) * 48 + cx + rx.
+    uint32_t my_blo = 0, my_bhi = 0, my_kc = 0;
+    if (valid) {
+        const LevelPtr bp = a.blur[my_l];
+        const int x = key_x((uint32_t)my_key), y = key_y((uint32_t)my_key);
+        const int x0 = (x - kDescWinR) & ~3;
+        const uint64_t base = (uint64_t)(bp.base + f * bp.fpitch + (long long)(y - kDescWinR) * bp.pitch + x0);
+        my_blo = (uint32_t)base;
+        my_bhi = (uint32_t)(base >> 32);
+        my_kc = (uint32_t)(kDescWinR * kDescWinP + (x - x0)) - 0x400000u * kDescWinP - 0x4b400000u;
+    }
+    int my_st = valid ? a.blur[my_l].pitch : 0;
+    float pat[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) pat[4 * q + c] = (float)c_pattern[4 * (lane + 64 * q) + c];
+    const float2v MG = float2v{12582912.f, 12582912.f};
+    __shared__ __attribute__((aligned(16))) uint8_t win_all[kDescBlock / 64][2][kDescWinBytes];
+    uint8_t(*win)[kDescWinBytes] = win_all[threadIdx.x >> 6];
+    // chunk c = lane (+ 64): row c / 3, 16-byte part c % 3
+    const int ca_row = lane / 3, ca_part = lane - 3 * (lane / 3);
+    const int cb = lane + 64, cb_row = cb / 3, cb_part = cb - 3 * (cb / 3);
+    const bool cb_on = cb < kDescWinRows * 3;
+    uint4 ra = make_uint4(0u, 0u, 0u, 0u), rb = ra;
+    auto load_win = [&](int j) {
+        const uint64_t base = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)my_blo, j) |
+                              ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)my_bhi, j) << 32);
+        const long long st = __builtin_amdgcn_readlane(my_st, j);
+        const uint8_t* w0 = reinterpret_cast<const uint8_t*>(base);
+        ra = *reinterpret_cast<const uint4*>(w0 + ca_row * st + 16 * ca_part);
+        if (cb_on) rb = *reinterpret_cast<const uint4*>(w0 + cb_row * st + 16 * cb_part);
+    };
+    load_win(__ffsll((long long)vmask) - 1);
+    int buf = 0;
+    for (unsigned long long m = vmask; m; m &= m - 1, buf ^= 1) {
+        const int j = __ffsll((long long)m) - 1;
+        uint8_t* wb = win[buf];
+        *reinterpret_cast<uint4*>(wb + ca_row * kDescWinP + 16 * ca_part) = ra;
+        if (cb_on) *reinterpret_cast<uint4*>(wb + cb_row * kDescWinP + 16 * cb_part) = rb;
+        __builtin_amdgcn_wave_barrier();
+        const unsigned long long rest = m & (m - 1);
+        if (rest) load_win(__ffsll((long long)rest) - 1);  // next keypoint's window in flight
+        const float cj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ca), j));
+        const float sj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, sa), j));
+        const uint32_t kc = (uint32_t)__builtin_amdgcn_readlane((int)my_kc, j);
+        const float2v SC = float2v{sj, cj}, CSn = float2v{cj, -sj};
+        int i0[4], i1[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float2v r0 = (pat[4 * q] * SC + pat[4 * q + 1] * CSn) + MG;
+            const float2v r1 = (pat[4 * q + 2] * SC + pat[4 * q + 3] * CSn) + MG;
+            // (__builtin_bit_cast of an ext-vector element reads element 0 in this clang:
+            // go through __float_as_uint on copied scalars)
+            const float r0y = r0.x, r0x = r0.y, r1y = r1.x, r1x = r1.y;
+            i0[q] = wb[__umul24(__float_as_uint(r0y), (uint32_t)kDescWinP) + __float_as_uint(r0x) + kc];
+            i1[q] = wb[__umul24(__float_as_uint(r1y), (uint32_t)kDescWinP) + __float_as_uint(r1x) + kc];
+        }
+        unsigned long long words[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) words[q] = __ballot(i0[q] < i1[q]);
+        const long long outi = (long long)f * a.kps_cap + __builtin_amdgcn_readlane(my_o, j);
+        if (lane < 4) {
+            const unsigned long long wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
+            reinterpret_cast<unsigned long long*>(a.desc + outi * 32)[lane] = wv;
+        }
+    }
+    if (valid) {
+        const uint32_t kk = (uint32_t)my_key;
+        const int kl = my_l, x = key_x(kk), y = key_y(kk);
         orbfe_keypoint kp;
-        const float sc = a.scale[l];
-        kp.x = l ? (float)x * sc : (float)x;
-        kp.y = l ? (float)y * sc : (float)y;
-        kp.size = a.size[l];
+        const float sc = a.scale[kl];
+        kp.x = kl ? (float)x * sc : (float)x;
+        kp.y = kl ? (float)y * sc : (float)y;
+        kp.size = a.size[kl];
         kp.angle = angle;
-        kp.response = (float)score;
-        kp.octave = l;
+        kp.response = (float)key_score(kk);
+        kp.octave = kl;
         kp.class_id = -1;
-        a.kps[outi] = kp;
+        a.kps[(long long)f * a.kps_cap + my_o] = kp;
     }
 }
 

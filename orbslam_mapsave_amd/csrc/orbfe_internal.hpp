@@ -153,6 +153,7 @@ extern __constant__ int c_umax[16];
 constexpr int kFastBlockSize = 64;
 constexpr int kOctBlockSize = 512;
 constexpr int kDescBlockSize = 256;
+constexpr int kDescGroupSize = 8;  // oct-tree output slots per describe wave
 constexpr int kBlurTileW = 128, kBlurTileH = 32;
 
 }  // namespace orbfe
