@@ -26,27 +26,35 @@ shutil.copy(os.path.join(SRC, "trace", "run_kernel_stats.csv"), os.path.join(DST
 for f in ("bench.json", "trace_bench.json"):
     shutil.copy(os.path.join(SRC, f), os.path.join(DST, f))
 
-# per-kernel launches of the timed bench shape (largest grid of each kernel)
+# Bench-shape launches: the timed launches of bench.py process one sub-batch of FRAMES frames
+# (grid y = frames for every kernel); the parity launches before timing use fewer.  The kernel
+# trace has the grid per dimension; the PMC csv only the total, so the bench shapes found in the
+# trace (kernel, total grid) select the PMC dispatches.  Multi-launch stages (resize: one launch
+# per level) are averaged over all their bench-shape launches, as bench.py's avg_launch_ms is.
+FRAMES = int(os.environ.get("BENCH_SUBBATCH", "128"))
+trace_rows = list(csv.DictReader(open(os.path.join(SRC, "trace", "run_kernel_trace.csv"))))
+shapes = collections.defaultdict(set)
+for r in trace_rows:
+    if int(r["Grid_Size_Y"]) == FRAMES:
+        shapes[short(r["Kernel_Name"])].add(
+            int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"]))
+
 def pmc(kind):
     rows = list(csv.DictReader(open(os.path.join(SRC, f"pmc_{kind}", "run_counter_collection.csv"))))
-    best = {}
-    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    per = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(float)))
     for r in rows:
         n = short(r["Kernel_Name"])
         if not n.endswith("kernel") or "at::" in r["Kernel_Name"]:
             continue
-        g = int(r["Grid_Size"])
-        best[n] = max(best.get(n, 0), g)
-        acc[n][g].append((r["Counter_Name"], float(r["Counter_Value"]), int(r["Dispatch_Id"])))
+        if int(r["Grid_Size"]) not in shapes.get(n, ()):
+            continue
+        per[n][int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
     out = {}
-    for n, g in best.items():
-        per = collections.defaultdict(lambda: collections.defaultdict(float))
-        for c, v, d in acc[n][g]:
-            per[d][c] += v
-        disp = list(per.values())
-        out[n] = {c: sum(d[c] for d in disp) / len(disp) for c in disp[0]}
-        out[n]["dispatches"] = len(disp)
-        out[n]["grid"] = g
+    for n, disp in per.items():
+        d = list(disp.values())
+        out[n] = {c: sum(x[c] for x in d) / len(d) for c in d[0]}
+        out[n]["dispatches"] = len(d)
+        out[n]["grids"] = sorted(shapes[n])
     return out
 
 fetch, write, sq = pmc("fetch"), pmc("write"), pmc("sq")
@@ -57,7 +65,7 @@ for n in sorted(fetch):
     s = sq.get(n, {})
     wc = s.get("SQ_WAVE_CYCLES", 0) or 1
     waves = s.get("SQ_WAVES", 1) or 1
-    summary[n] = {"grid": fetch[n]["grid"], "fetch_bytes_raw": f, "write_bytes": w,
+    summary[n] = {"grids": fetch[n]["grids"], "dispatches": fetch[n]["dispatches"], "fetch_bytes_raw": f, "write_bytes": w,
                   "hbm_bytes_est": 2 * f + w,
                   "active_pct": round(100 * s.get("SQ_ACTIVE_INST_ANY", 0) / wc, 1),
                   "wait_pct": round(100 * s.get("SQ_WAIT_ANY", 0) / wc, 1),
@@ -71,21 +79,15 @@ json.dump(traffic, open(os.path.join(ROOT, "profiles", "traffic_c3.json"), "w"),
 for n, v in summary.items():
     print(n, v)
 
-# Average duration of the bench-shaped launches (largest grid per kernel) from the kernel trace;
-# this is the figure bench.py's live roofline.avg_launch_ms must agree with.
-rows = list(csv.DictReader(open(os.path.join(SRC, "trace", "run_kernel_trace.csv"))))
-grid = collections.defaultdict(int)
-for r in rows:
-    g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
-    grid[short(r["Kernel_Name"])] = max(grid[short(r["Kernel_Name"])], g)
+# Average duration of the bench-shape launches from the kernel trace; the figure bench.py's
+# live roofline.avg_launch_ms must agree with.
 dur = collections.defaultdict(list)
-for r in rows:
+for r in trace_rows:
     n = short(r["Kernel_Name"])
-    g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
-    if g == grid[n]:
+    if int(r["Grid_Size_Y"]) == FRAMES and n.endswith("kernel"):
         dur[n].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-launch = {n: {"launches": len(v), "grid": grid[n], "avg_ms": round(sum(v) / len(v) / 1e6, 5)}
-          for n, v in dur.items() if n.endswith("kernel")}
+launch = {n: {"launches": len(v), "grids": sorted(shapes[n]), "avg_ms": round(sum(v) / len(v) / 1e6, 5)}
+          for n, v in dur.items()}
 json.dump(launch, open(os.path.join(DST, "bench_shape_launches.json"), "w"), indent=1)
 for n, v in sorted(launch.items()):
     print(n, v)
