@@ -58,6 +58,21 @@ typedef struct orbfe_keypoint {
     int32_t class_id;
 } orbfe_keypoint;
 
+/* Pixel formats of the frames handed to the colour entry points: the four cvtColor codes of
+ * Tracking::GrabImageStereo / GrabImageRGBD / GrabImageMonocular (Tracking.cc:286-310,
+ * 350-363, 409-422), chosen there by channels() and mbRGB (Camera.RGB, Tracking.cc:192). */
+#define ORBFE_PIX_GRAY 0   /* CV_8UC1, no conversion                                          */
+#define ORBFE_PIX_RGB  1   /* CV_8UC3, CV_RGB2GRAY  (mbRGB = 1)                               */
+#define ORBFE_PIX_BGR  2   /* CV_8UC3, CV_BGR2GRAY  (mbRGB = 0)                               */
+#define ORBFE_PIX_RGBA 3   /* CV_8UC4, CV_RGBA2GRAY                                           */
+#define ORBFE_PIX_BGRA 4   /* CV_8UC4, CV_BGRA2GRAY                                           */
+
+/* Zeroed rectangle of the human mask: rows [y0, y1) x cols [x0, x1) of an all-ones mask
+ * (OpDetector::SkeletonSquareMask, DetectHumanPose.cpp:484-489). */
+typedef struct orbfe_rect {
+    int32_t x0, y0, x1, y1;
+} orbfe_rect;
+
 typedef struct orbfe_extractor orbfe_extractor;
 typedef struct orbfe_matcher   orbfe_matcher;
 
@@ -98,6 +113,24 @@ int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int w, int hgt, size_t
                   const uint8_t* mask, size_t mask_stride, orbfe_keypoint* kps, int kps_cap,
                   uint8_t* desc, int* n_out);
 
+/* Colour front-end: cvtColor(img, gray, CV_*2GRAY) of Tracking::GrabImage* (Tracking.cc:409-422
+ * and the stereo / RGB-D twins) fused with Frame::ExtractORBMask -> operator()(gray, mask)
+ * (Frame.cc:366-371, ORBextractor.cc:1053).  `pix` is an ORBFE_PIX_* format, `stride` the row
+ * stride of img in bytes (>= w * channels).  The mask is given as a u8 plane (`mask`, NULL for
+ * none) and/or as the zeroed rectangle `rect` (NULL for none) of OpDetector's square mask;
+ * a pixel survives when both keep it.  rect with x1 < x0 or y1 < y0 (where the reference's
+ * rowRange/colRange assert) returns ORBFE_ERR_UNSUPPORTED.  Gray values follow OpenCV's 8U
+ * integer path.  Otherwise as orbfe_extract. */
+int orbfe_extract_color(orbfe_extractor* h, const uint8_t* img, int pix, int w, int hgt,
+                        size_t stride, const uint8_t* mask, size_t mask_stride,
+                        const orbfe_rect* rect, orbfe_keypoint* kps, int kps_cap, uint8_t* desc,
+                        int* n_out);
+
+/* The human-mask rectangle from 25 OpenPose joints (x, y, score) — the bounding box of the
+ * joints grown by 30 px and clamped to the image, exactly as OpDetector::SkeletonSquareMask
+ * computes it (DetectHumanPose.cpp:453-489).  Host-only helper (no device work). */
+int orbfe_human_mask_rect(const float* joints, int njoints, int w, int hgt, orbfe_rect* out);
+
 /* Throughput form of orbfe_extract over n same-size frames (host buffers).  Frame f's
  * keypoints go to kps[f*kps_cap ...], descriptors to desc[f*kps_cap*32 ...], count n_out[f].
  * masks may be NULL (no masks) or an array of n pointers (entries may be NULL). */
@@ -113,6 +146,16 @@ int orbfe_extract_batch_device(orbfe_extractor* h, const uint8_t* d_imgs, int n,
                                orbfe_keypoint* d_kps, int kps_cap, uint8_t* d_desc,
                                int32_t* d_n_out);
 
+/* Device-resident colour form: frame f at d_imgs + f*frame_pitch in format `pix`; d_masks NULL
+ * or n u8 planes (mask_stride, mask_frame_pitch); d_rects NULL or n device orbfe_rect.  Level 0
+ * (the gray, masked image) is made by one fused kernel before the pipeline. */
+int orbfe_extract_color_batch_device(orbfe_extractor* h, const uint8_t* d_imgs, int pix, int n,
+                                     int w, int hgt, size_t stride, size_t frame_pitch,
+                                     const uint8_t* d_masks, size_t mask_stride,
+                                     size_t mask_frame_pitch, const orbfe_rect* d_rects,
+                                     orbfe_keypoint* d_kps, int kps_cap, uint8_t* d_desc,
+                                     int32_t* d_n_out);
+
 /* Stream control: `hip_stream` is a hipStream_t (NULL => the handle's own stream). */
 int orbfe_set_stream(orbfe_extractor* h, void* hip_stream);
 int orbfe_synchronize(orbfe_extractor* h);
@@ -121,7 +164,7 @@ int orbfe_synchronize(orbfe_extractor* h);
  * the handle's stream around every kernel launch.  orbfe_profile_read synchronizes the stream
  * and returns, per stage (ORBFE_STAGE_*), the summed duration in ms and the launch count since
  * the previous read.  Used by bench.py for the roofline figure; off by default. */
-#define ORBFE_STAGE_MASK     0
+#define ORBFE_STAGE_MASK     0   /* K0: colour conversion + mask (level 0) */
 #define ORBFE_STAGE_RESIZE   1
 #define ORBFE_STAGE_FAST     2
 #define ORBFE_STAGE_OCTREE   3
@@ -145,6 +188,34 @@ int orbfe_get_blurred_level(orbfe_extractor* h, int frame, int level, uint8_t* o
                             int* hgt);
 int orbfe_get_fast_keys(orbfe_extractor* h, int frame, int level, orbfe_keypoint* out, int cap,
                         int* n_out);
+
+/* ---- stereo ------------------------------------------------------------------------------ */
+
+/* Frame::ComputeStereoMatches (Frame.cc:584-756), called by the stereo Frame ctor right after
+ * the two extractions (Frame.cc:78-103).  kl/dl: mvKeys + mDescriptors of the left image (nl,
+ * distorted keypoints as extracted); kr/dr: mvKeysRight + mDescriptorsRight (nr).  The pyramids
+ * read are mpORBextractorLeft/Right->mvImagePyramid: frame `frame` of the most recent
+ * extraction of `left` / `right` (same image size and scale parameters).  bf = mbf, b = mb.
+ * Writes mvuRight / mvDepth (nl floats each, -1 = no match).  Inputs on which the reference
+ * indexes vRowIndices out of range or trips a rowRange/colRange assert return
+ * ORBFE_ERR_UNSUPPORTED.  Synchronous; runs on left's stream after right's stream. */
+int orbfe_compute_stereo_matches(orbfe_extractor* left, orbfe_extractor* right, int frame,
+                                 const orbfe_keypoint* kl, const uint8_t* dl, int nl,
+                                 const orbfe_keypoint* kr, const uint8_t* dr, int nr, float bf,
+                                 float b, float* u_right, float* depth);
+
+/* Device-resident batch form over frames 0..n-1 of the two handles' most recent
+ * orbfe_extract*_batch_device calls: keypoint / descriptor / count slabs as those calls write
+ * them (kps_cap keypoints per frame); u_right / depth are n x kps_cap floats.  The device frames
+ * the extractions read must still be valid (level 0 is read in place).  Asynchronous on left's
+ * stream (ordered after right's stream); orbfe_stereo_status reports UB inputs afterwards. */
+int orbfe_compute_stereo_matches_device(orbfe_extractor* left, orbfe_extractor* right, int n,
+                                        const orbfe_keypoint* d_kl, const uint8_t* d_dl,
+                                        const int32_t* d_nl, const orbfe_keypoint* d_kr,
+                                        const uint8_t* d_dr, const int32_t* d_nr, int kps_cap,
+                                        float bf, float b, float* d_u_right, float* d_depth);
+/* Synchronizes left's stream; ORBFE_OK or ORBFE_ERR_UNSUPPORTED for the last stereo call. */
+int orbfe_stereo_status(orbfe_extractor* left);
 
 /* ---- matchers ------------------------------------------------------------------------------- */
 

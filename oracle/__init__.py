@@ -65,6 +65,34 @@ def capacity(p: Params) -> int:
     return int(p.nfeatures) + 4 * int(p.nlevels) + 64
 
 
+def cvt_gray(img: np.ndarray, pix: int) -> np.ndarray:
+    """cvtColor(img, CV_*2GRAY) 8U (oracle_cvt_gray); pix as ORBFE_PIX_*."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w, cn = img.shape
+    out = np.zeros((h, w), np.uint8)
+    _check("oracle_cvt_gray", lib().oracle_cvt_gray(ptr(img), pix, w, h, C.c_size_t(w * cn),
+                                                    ptr(out)))
+    return out
+
+
+def compute_stereo_matches(p: Params, im_l: np.ndarray, im_r: np.ndarray, kl, dl, kr, dr,
+                           bf: float, b: float):
+    """Frame::ComputeStereoMatches (oracle_compute_stereo_matches) -> (mvuRight, mvDepth)."""
+    im_l = np.ascontiguousarray(im_l, np.uint8)
+    im_r = np.ascontiguousarray(im_r, np.uint8)
+    h, w = im_l.shape
+    kl = np.ascontiguousarray(kl, KEYPOINT_DTYPE)
+    kr = np.ascontiguousarray(kr, KEYPOINT_DTYPE)
+    dl = np.ascontiguousarray(dl, np.uint8)
+    dr = np.ascontiguousarray(dr, np.uint8)
+    ur = np.zeros(len(kl), np.float32)
+    dp = np.zeros(len(kl), np.float32)
+    _check("oracle_compute_stereo_matches", lib().oracle_compute_stereo_matches(
+        C.byref(p), ptr(im_l), ptr(im_r), w, h, ptr(kl), ptr(dl), len(kl), ptr(kr), ptr(dr),
+        len(kr), C.c_float(bf), C.c_float(b), ptr(ur), ptr(dp)))
+    return ur, dp
+
+
 def extract(p: Params, img: np.ndarray, mask: np.ndarray | None = None):
     img = np.ascontiguousarray(img, np.uint8)
     h, w = img.shape

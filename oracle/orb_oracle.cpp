@@ -763,6 +763,151 @@ int oracle_extract_batch(const orbfe_params* p, const uint8_t* imgs, int n, int 
     return ORBFE_OK;
 }
 
+// cvtColor(src, dst, CV_{RGB,BGR,RGBA,BGRA}2GRAY) for 8U, as called by Tracking::GrabImage*
+// (Tracking.cc:286-310, 350-363, 409-422).  OpenCV 3.3.1 RGB2Gray<uchar> (App. A, DESIGN H9):
+// three 256-entry tables built by repeated addition, coefficients R2Y 4899, G2Y 9617, B2Y 1868
+// (yuv_shift 14), the rounding constant folded into the table of source channel 2;
+// blueIdx = 0 for BGR(A), 2 for RGB(A) picks which weight goes to channel 0.
+int oracle_cvt_gray(const uint8_t* src, int pix, int w, int h, size_t stride, uint8_t* dst) {
+    int scn, blue_idx;
+    switch (pix) {
+        case ORBFE_PIX_RGB: scn = 3; blue_idx = 2; break;
+        case ORBFE_PIX_BGR: scn = 3; blue_idx = 0; break;
+        case ORBFE_PIX_RGBA: scn = 4; blue_idx = 2; break;
+        case ORBFE_PIX_BGRA: scn = 4; blue_idx = 0; break;
+        default: return ORBFE_ERR_ARG;
+    }
+    if (!src || !dst || w <= 0 || h <= 0) return ORBFE_ERR_ARG;
+    const int coeffs[3] = {4899, 9617, 1868};  // R2Y, G2Y, B2Y
+    int tab[256 * 3];
+    int b = 0, g = 0, r = 1 << 13;
+    const int db = coeffs[blue_idx ^ 2], dg = coeffs[1], dr = coeffs[blue_idx];
+    for (int i = 0; i < 256; ++i, b += db, g += dg, r += dr) {
+        tab[i] = b;
+        tab[i + 256] = g;
+        tab[i + 512] = r;
+    }
+    for (int y = 0; y < h; ++y) {
+        const uint8_t* s = src + (size_t)y * stride;
+        for (int x = 0; x < w; ++x, s += scn)
+            dst[(size_t)y * w + x] = (uint8_t)((tab[s[0]] + tab[s[1] + 256] + tab[s[2] + 512]) >> 14);
+    }
+    return ORBFE_OK;
+}
+
+// Frame::ComputeStereoMatches (Frame.cc:584-756) on the two pyramids of imL / imR (built as
+// ORBextractor::ComputePyramid does).  kl/kr are mvKeys / mvKeysRight (distorted, as extracted).
+int oracle_compute_stereo_matches(const orbfe_params* p, const uint8_t* imL, const uint8_t* imR,
+                                  int w, int h, const orbfe_keypoint* kl, const uint8_t* dl,
+                                  int nl, const orbfe_keypoint* kr, const uint8_t* dr, int nr,
+                                  float bf, float b, float* u_right, float* depth) {
+    Tables t;
+    if (!make_tables(p, t) || !imL || !imR || w <= 0 || h <= 0 || nl < 0 || nr < 0 ||
+        (nl && (!kl || !dl || !u_right || !depth)) || (nr && (!kr || !dr)))
+        return ORBFE_ERR_ARG;
+    std::vector<Plane> pl, pr;
+    build_pyramid(t, imL, w, h, w, nullptr, 0, pl);
+    build_pyramid(t, imR, w, h, w, nullptr, 0, pr);
+    for (int i = 0; i < nl; ++i) u_right[i] = depth[i] = -1.0f;  // 586-587
+    const int n_rows = pl[0].h;                                   // 589
+    // row table (591-606): right keypoint iR is listed in rows floor(y-r) .. ceil(y+r)
+    std::vector<std::vector<int>> rows(n_rows);
+    for (int ir = 0; ir < nr; ++ir) {
+        const float ky = kr[ir].y;
+        const float r = 2.0f * t.scale[kr[ir].octave];
+        const int maxr = (int)std::ceil(ky + r);
+        const int minr = (int)std::floor(ky - r);
+        for (int yi = minr; yi <= maxr; ++yi) {
+            if (yi < 0 || yi >= n_rows) return ORBFE_ERR_UNSUPPORTED;  // out-of-range vector index
+            rows[yi].push_back(ir);
+        }
+    }
+    const float min_z = b, min_d = -3, max_d = bf / min_z;  // 609-611
+    std::vector<std::pair<int, int>> dist_idx;              // vDistIdx
+    for (int il = 0; il < nl; ++il) {
+        const orbfe_keypoint& kpl = kl[il];
+        const int level_l = kpl.octave;
+        const float vl = kpl.y, ul = kpl.x;
+        const size_t row = (size_t)vl;  // vRowIndices[vL]: float -> size_t
+        if (row >= (size_t)n_rows) return ORBFE_ERR_UNSUPPORTED;
+        const std::vector<int>& cand = rows[row];
+        if (cand.empty()) continue;
+        const float min_u = ul - max_d, max_u = ul - min_d;
+        if (max_u < 0) continue;
+        int best_dist = kThHigh;
+        int best_ir = 0;
+        for (int ir : cand) {  // 641-660
+            const orbfe_keypoint& kpr = kr[ir];
+            if (kpr.octave < level_l - 1 || kpr.octave > level_l + 1) continue;
+            const float ur = kpr.x;
+            if (ur >= min_u && ur <= max_u) {
+                const int d = descriptor_distance(dl + 32 * (size_t)il, dr + 32 * (size_t)ir);
+                if (d < best_dist) { best_dist = d; best_ir = ir; }
+            }
+        }
+        if (best_dist >= kThHigh) continue;
+        // sub-pixel match by correlation (663-735)
+        const float ur0 = kr[best_ir].x;
+        const float sf = t.inv[level_l];
+        const float sul = std::round(kpl.x * sf), svl = std::round(kpl.y * sf);
+        const float sur0 = std::round(ur0 * sf);
+        const int W5 = 5, L5 = 5;
+        const Plane& PL = pl[level_l];
+        const Plane& PR = pr[level_l];
+        const int r0 = (int)(svl - W5), c0 = (int)(sul - W5);
+        if (r0 < 0 || r0 + 2 * W5 + 1 > PL.h || c0 < 0 || c0 + 2 * W5 + 1 > PL.w)
+            return ORBFE_ERR_UNSUPPORTED;  // rowRange / colRange assert (CV_Assert)
+        const float iniu = sur0 + L5 - W5, endu = sur0 + L5 + W5 + 1;  // 684-685
+        if (iniu < 0 || endu >= PR.w) continue;
+        const int rc0 = (int)(sur0 - L5 - W5);
+        if (rc0 < 0 || (int)(sur0 + L5 + W5 + 1) > PR.w) return ORBFE_ERR_UNSUPPORTED;
+        float il_win[11][11];
+        for (int y = 0; y < 11; ++y)
+            for (int x = 0; x < 11; ++x) il_win[y][x] = (float)PL.at(r0 + y, c0 + x);
+        const float ilc = il_win[W5][W5];
+        for (int y = 0; y < 11; ++y)
+            for (int x = 0; x < 11; ++x) il_win[y][x] = il_win[y][x] - ilc;
+        int best_sad = INT_MAX, best_inc = 0;
+        float dists[2 * L5 + 1];
+        for (int inc = -L5; inc <= L5; ++inc) {
+            const int cc0 = (int)(sur0 + inc - W5);
+            const float irc = (float)PR.at(r0 + W5, cc0 + W5);
+            double acc = 0.0;  // cv::norm(NORM_L1) of two CV_32F Mats accumulates in double
+            for (int y = 0; y < 11; ++y)
+                for (int x = 0; x < 11; ++x)
+                    acc += std::fabs(il_win[y][x] - ((float)PR.at(r0 + y, cc0 + x) - irc));
+            const float dist = (float)acc;
+            if (dist < best_sad) { best_sad = (int)dist; best_inc = inc; }
+            dists[L5 + inc] = dist;
+        }
+        if (best_inc == -L5 || best_inc == L5) continue;
+        const float d1 = dists[L5 + best_inc - 1], d2 = dists[L5 + best_inc], d3 = dists[L5 + best_inc + 1];
+        const float delta = (d1 - d3) / (2.0f * (d1 + d3 - 2.0f * d2));
+        if (delta < -1 || delta > 1) continue;
+        float best_ur = t.scale[level_l] * ((float)sur0 + (float)best_inc + delta);
+        float disparity = (ul - best_ur);
+        if (disparity >= 0 && disparity < max_d) {
+            if (disparity <= 0) {
+                disparity = 0.01;
+                best_ur = ul - 0.01;
+            }
+            depth[il] = bf / disparity;
+            u_right[il] = best_ur;
+            dist_idx.push_back(std::make_pair(best_sad, il));
+        }
+    }
+    if (dist_idx.empty()) return ORBFE_OK;  // the reference reads vDistIdx[0] of an empty vector
+    std::sort(dist_idx.begin(), dist_idx.end());
+    const float median = dist_idx[dist_idx.size() / 2].first;
+    const float th_dist = 1.5f * 1.4f * median;
+    for (int i = (int)dist_idx.size() - 1; i >= 0; --i) {
+        if (dist_idx[i].first < th_dist) break;
+        u_right[dist_idx[i].second] = -1;
+        depth[dist_idx[i].second] = -1;
+    }
+    return ORBFE_OK;
+}
+
 int oracle_pyramid(const orbfe_params* p, const uint8_t* img, int w, int h, size_t stride,
                    const uint8_t* mask, size_t mask_stride, uint8_t* out) {
     Tables t;

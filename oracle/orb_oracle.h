@@ -35,6 +35,16 @@ int oracle_extract_batch(const orbfe_params* p, const uint8_t* imgs, int n, int 
                          size_t frame_pitch, orbfe_keypoint* kps, int kps_cap, uint8_t* desc,
                          int32_t* n_out, int nthreads);
 
+/* cvtColor(*2GRAY) 8U of Tracking::GrabImage* (pix = ORBFE_PIX_RGB/BGR/RGBA/BGRA); dst is
+ * w x h dense. */
+int oracle_cvt_gray(const uint8_t* src, int pix, int w, int h, size_t stride, uint8_t* dst);
+
+/* Frame::ComputeStereoMatches (Frame.cc:584-756) over the pyramids of the two images. */
+int oracle_compute_stereo_matches(const orbfe_params* p, const uint8_t* imL, const uint8_t* imR,
+                                  int w, int h, const orbfe_keypoint* kl, const uint8_t* dl,
+                                  int nl, const orbfe_keypoint* kr, const uint8_t* dr, int nr,
+                                  float bf, float b, float* u_right, float* depth);
+
 /* Stage probes. */
 int oracle_pyramid(const orbfe_params* p, const uint8_t* img, int w, int h, size_t stride,
                    const uint8_t* mask, size_t mask_stride, uint8_t* out /* levels packed,

@@ -46,6 +46,16 @@ struct DevBuf {
     }
 };
 
+// Bytes per pixel of an ORBFE_PIX_* format (0 for an unknown format).
+int pix_channels(int pix) {
+    switch (pix) {
+        case ORBFE_PIX_GRAY: return 1;
+        case ORBFE_PIX_RGB: case ORBFE_PIX_BGR: return 3;
+        case ORBFE_PIX_RGBA: case ORBFE_PIX_BGRA: return 4;
+        default: return 0;
+    }
+}
+
 // Returns ORBFE_OK when `device` is a usable gfx950 agent (the only target this library is
 // built for); the library has no CPU fallback.
 int check_device(int device) {
@@ -118,6 +128,10 @@ struct orbfe_extractor {
     DevBuf cells, xtab, ytab;
     DevBuf pyr, blur, cell_cnt, cell_keys, keys, act, oct_out, oct_cnt;
     DevBuf out_kps, out_desc, out_n;  // staging for the host-pointer entry points
+    DevBuf stage, rects;              // host colour frames / rectangle masks (level-0 inputs)
+    DevBuf st_off, st_items, st_sad, st_status;           // stereo workspaces (left handle)
+    DevBuf st_kl, st_dl, st_kr, st_dr, st_n, st_ur, st_dp;  // stereo host-path staging
+    std::vector<int4> h_rects;
     // last run, for the probes
     int last_n = 0;
     LevelPtr last_pyr[kMaxLevels] = {};
@@ -264,9 +278,39 @@ struct orbfe_extractor {
         return ORBFE_OK;
     }
 
+    // K0: level 0 of every frame from the caller's frames (gray or colour), full masks laid out
+    // like the frames' rows (mask_fpitch / mask_pitch) and/or per-frame zeroed rectangles.
+    int launch_level0(int n, const uint8_t* src, long long src_fpitch, int src_pitch, int pix,
+                      const uint8_t* mask, long long mask_fpitch, int mask_pitch,
+                      const int4* d_rects) {
+        const Plan& g = plan;
+        const LevelGeo& l0 = g.geo.lv[0];
+        Level0Args a;
+        a.src = src;
+        a.src_fpitch = src_fpitch;
+        a.src_pitch = src_pitch;
+        a.cn = pix_channels(pix);
+        const bool rgb_first = pix == ORBFE_PIX_RGB || pix == ORBFE_PIX_RGBA;
+        a.c0 = rgb_first ? 4899 : 1868;  // R2Y : B2Y (yuv_shift 14)
+        a.c2 = rgb_first ? 1868 : 4899;
+        a.aligned = ((uintptr_t)src % 4 == 0) && src_pitch % 4 == 0 && src_fpitch % 4 == 0;
+        a.mask = mask;
+        a.mask_fpitch = mask_fpitch;
+        a.mask_pitch = mask_pitch;
+        a.rects = d_rects;
+        a.dst = pyr.as<uint8_t>() + l0.off;
+        a.dst_fpitch = g.slab;
+        a.dst_pitch = l0.pitch;
+        a.w = g.w;
+        a.h = g.h;
+        ORBFE_LAUNCH(prof, ORBFE_STAGE_MASK, level0_kernel, dim3((g.w + 1023) / 1024, g.h, n), dim3(256),
+                     0, stream, a);
+        return ORBFE_OK;
+    }
+
     // Host-pointer path: upload, run into the staging slabs, download.
-    int run_host(const uint8_t* const* imgs, int n, int w, int h, size_t stride,
-                 const uint8_t* const* masks, size_t mstride) {
+    int run_host(const uint8_t* const* imgs, int n, int w, int h, size_t stride, int pix,
+                 const uint8_t* const* masks, size_t mstride, const orbfe_rect* host_rects) {
         int st;
         if ((st = set_plan(w, h))) return st;
         if ((st = ensure_frames(n))) return st;
@@ -277,27 +321,50 @@ struct orbfe_extractor {
         if ((st = out_desc.ensure((size_t)n * cap * 32))) return st;
         if ((st = out_n.ensure((size_t)n * sizeof(int32_t)))) return st;
         bool any_mask = false;
-        for (int f = 0; f < n; ++f) {
-            uint8_t* dst = pyr.as<uint8_t>() + (size_t)f * g.slab + l0.off;
-            ORBFE_HIP(hipMemcpy2DAsync(dst, l0.pitch, imgs[f], stride, w, h,
-                                       hipMemcpyHostToDevice, stream));
-            if (masks && masks[f]) any_mask = true;
-        }
-        if (any_mask) {
-            // the blur slab is free until K4: stage the masks there, then zero masked pixels
+        if (masks)
+            for (int f = 0; f < n; ++f) any_mask |= masks[f] != nullptr;
+        const int cn = pix_channels(pix);
+        if (pix == ORBFE_PIX_GRAY && !any_mask && !host_rects) {
             for (int f = 0; f < n; ++f) {
-                uint8_t* mdst = blur.as<uint8_t>() + (size_t)f * g.slab + l0.off;
-                if (masks[f]) {
-                    ORBFE_HIP(hipMemcpy2DAsync(mdst, l0.pitch, masks[f], mstride, w, h,
-                                               hipMemcpyHostToDevice, stream));
-                } else {
-                    ORBFE_HIP(hipMemset2DAsync(mdst, l0.pitch, 1, w, h, stream));
+                uint8_t* dst = pyr.as<uint8_t>() + (size_t)f * g.slab + l0.off;
+                ORBFE_HIP(hipMemcpy2DAsync(dst, l0.pitch, imgs[f], stride, w, h,
+                                           hipMemcpyHostToDevice, stream));
+            }
+        } else {
+            // frames -> `stage` (rows padded to 4 B so K0 reads them with vector loads)
+            const size_t spitch = ((size_t)w * cn + 3) & ~(size_t)3;
+            const size_t sfp = spitch * h;
+            if ((st = stage.ensure(n * sfp))) return st;
+            for (int f = 0; f < n; ++f)
+                ORBFE_HIP(hipMemcpy2DAsync(stage.as<uint8_t>() + f * sfp, spitch, imgs[f], stride,
+                                           (size_t)w * cn, h, hipMemcpyHostToDevice, stream));
+            // masks -> the blur slab, which is free until K4
+            if (any_mask) {
+                for (int f = 0; f < n; ++f) {
+                    uint8_t* mdst = blur.as<uint8_t>() + (size_t)f * g.slab + l0.off;
+                    if (masks[f]) {
+                        ORBFE_HIP(hipMemcpy2DAsync(mdst, l0.pitch, masks[f], mstride, w, h,
+                                                   hipMemcpyHostToDevice, stream));
+                    } else {
+                        ORBFE_HIP(hipMemset2DAsync(mdst, l0.pitch, 1, w, h, stream));
+                    }
                 }
             }
-            uint8_t* p0 = pyr.as<uint8_t>() + l0.off;
-            hipLaunchKernelGGL(mask_kernel, dim3((w + 255) / 256, h, n), dim3(256), 0, stream,
-                               p0, g.slab, l0.pitch, blur.as<uint8_t>() + l0.off, g.slab,
-                               l0.pitch, p0, g.slab, l0.pitch, w, h);
+            const int4* d_rects = nullptr;
+            if (host_rects) {
+                if ((st = rects.ensure(n * sizeof(int4)))) return st;
+                h_rects.resize(n);
+                for (int f = 0; f < n; ++f)
+                    h_rects[f] = int4{host_rects[f].x0, host_rects[f].y0, host_rects[f].x1,
+                                      host_rects[f].y1};
+                ORBFE_HIP(hipMemcpyAsync(rects.p, h_rects.data(), n * sizeof(int4),
+                                         hipMemcpyHostToDevice, stream));
+                d_rects = rects.as<int4>();
+            }
+            if ((st = launch_level0(n, stage.as<uint8_t>(), (long long)sfp, (int)spitch, pix,
+                                    any_mask ? blur.as<uint8_t>() + l0.off : nullptr, g.slab,
+                                    l0.pitch, d_rects)))
+                return st;
         }
         LevelPtr lp0{pyr.as<uint8_t>() + l0.off, g.slab, l0.pitch};
         if ((st = run(n, lp0, out_kps.as<orbfe_keypoint>(), cap, out_desc.as<uint8_t>(),
@@ -316,7 +383,8 @@ struct orbfe_extractor {
 
     ~orbfe_extractor() {
         for (DevBuf* b : {&cells, &xtab, &ytab, &pyr, &blur, &cell_cnt, &cell_keys, &keys, &act,
-                          &oct_out, &oct_cnt, &out_kps, &out_desc, &out_n})
+                          &oct_out, &oct_cnt, &out_kps, &out_desc, &out_n, &stage, &rects, &st_off, &st_items,
+                          &st_sad, &st_status, &st_kl, &st_dl, &st_kr, &st_dr, &st_n, &st_ur, &st_dp})
             b->release();
         prof.release();
         if (own) hipStreamDestroy(own);
@@ -411,11 +479,11 @@ int orbfe_keypoint_capacity(const orbfe_extractor* h) {
 }
 
 static int extract_host_common(orbfe_extractor* h, const uint8_t* const* imgs, int n, int w,
-                               int hgt, size_t stride, const uint8_t* const* masks,
-                               size_t mask_stride, orbfe_keypoint* kps, int kps_cap,
-                               uint8_t* desc, int32_t* n_out) {
+                               int hgt, size_t stride, int pix, const uint8_t* const* masks,
+                               size_t mask_stride, const orbfe_rect* rects, orbfe_keypoint* kps,
+                               int kps_cap, uint8_t* desc, int32_t* n_out) {
     DeviceGuard dg(h->device);
-    int st = h->run_host(imgs, n, w, hgt, stride, masks, mask_stride);
+    int st = h->run_host(imgs, n, w, hgt, stride, pix, masks, mask_stride, rects);
     if (st != ORBFE_OK) return st;
     const int cap = h->kp_capacity();
     int worst = ORBFE_OK;
@@ -435,18 +503,31 @@ static int extract_host_common(orbfe_extractor* h, const uint8_t* const* imgs, i
     return worst;
 }
 
+static bool rect_ok(const orbfe_rect* r) { return !r || (r->x0 <= r->x1 && r->y0 <= r->y1); }
+
 int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int w, int hgt, size_t stride,
                   const uint8_t* mask, size_t mask_stride, orbfe_keypoint* kps, int kps_cap,
                   uint8_t* desc, int* n_out) {
+    return orbfe_extract_color(h, img, ORBFE_PIX_GRAY, w, hgt, stride, mask, mask_stride, nullptr,
+                               kps, kps_cap, desc, n_out);
+}
+
+int orbfe_extract_color(orbfe_extractor* h, const uint8_t* img, int pix, int w, int hgt,
+                        size_t stride, const uint8_t* mask, size_t mask_stride,
+                        const orbfe_rect* rect, orbfe_keypoint* kps, int kps_cap, uint8_t* desc,
+                        int* n_out) {
     if (!h) return ORBFE_ERR_ARG;
     if (!img || w <= 0 || hgt <= 0) return ORBFE_OK;  // empty image: no-op (1045-1046)
-    if (!kps || !n_out || kps_cap < 0 || stride < (size_t)w || (mask && mask_stride < (size_t)w))
+    const int cn = pix_channels(pix);
+    if (!cn || !kps || !n_out || kps_cap < 0 || stride < (size_t)w * cn ||
+        (mask && mask_stride < (size_t)w))
         return ORBFE_ERR_ARG;
+    if (!rect_ok(rect)) return ORBFE_ERR_UNSUPPORTED;
     try {
         const uint8_t* m[1] = {mask};
         int32_t cnt = 0;
-        const int st = extract_host_common(h, &img, 1, w, hgt, stride, mask ? m : nullptr,
-                                           mask_stride, kps, kps_cap, desc, &cnt);
+        const int st = extract_host_common(h, &img, 1, w, hgt, stride, pix, mask ? m : nullptr,
+                                           mask_stride, rect, kps, kps_cap, desc, &cnt);
         *n_out = cnt;
         return st;
     } catch (const std::bad_alloc&) {
@@ -465,8 +546,8 @@ int orbfe_extract_batch(orbfe_extractor* h, const uint8_t* const* imgs, int n, i
     for (int f = 0; f < n; ++f)
         if (!imgs[f]) return ORBFE_ERR_ARG;
     try {
-        return extract_host_common(h, imgs, n, w, hgt, stride, masks, mask_stride, kps, kps_cap,
-                                   desc, n_out);
+        return extract_host_common(h, imgs, n, w, hgt, stride, ORBFE_PIX_GRAY, masks, mask_stride,
+                                   nullptr, kps, kps_cap, desc, n_out);
     } catch (const std::bad_alloc&) {
         return ORBFE_ERR_NOMEM;
     } catch (...) {
@@ -478,9 +559,23 @@ int orbfe_extract_batch_device(orbfe_extractor* h, const uint8_t* d_imgs, int n,
                                size_t stride, size_t frame_pitch, const uint8_t* d_masks,
                                orbfe_keypoint* d_kps, int kps_cap, uint8_t* d_desc,
                                int32_t* d_n_out) {
-    if (!h || n < 0 || !d_imgs || !d_kps || !d_desc || !d_n_out) return ORBFE_ERR_ARG;
+    return orbfe_extract_color_batch_device(h, d_imgs, ORBFE_PIX_GRAY, n, w, hgt, stride,
+                                            frame_pitch, d_masks, stride, frame_pitch, nullptr,
+                                            d_kps, kps_cap, d_desc, d_n_out);
+}
+
+int orbfe_extract_color_batch_device(orbfe_extractor* h, const uint8_t* d_imgs, int pix, int n,
+                                     int w, int hgt, size_t stride, size_t frame_pitch,
+                                     const uint8_t* d_masks, size_t mask_stride,
+                                     size_t mask_frame_pitch, const orbfe_rect* d_rects,
+                                     orbfe_keypoint* d_kps, int kps_cap, uint8_t* d_desc,
+                                     int32_t* d_n_out) {
+    const int cn = pix_channels(pix);
+    if (!h || n < 0 || !d_imgs || !d_kps || !d_desc || !d_n_out || !cn) return ORBFE_ERR_ARG;
     if (n == 0 || w <= 0 || hgt <= 0) return ORBFE_OK;
-    if (stride < (size_t)w || (n > 1 && frame_pitch < stride * hgt)) return ORBFE_ERR_ARG;
+    if (stride < (size_t)w * cn || (n > 1 && frame_pitch < stride * hgt)) return ORBFE_ERR_ARG;
+    if (d_masks && (mask_stride < (size_t)w || (n > 1 && mask_frame_pitch < mask_stride * hgt)))
+        return ORBFE_ERR_ARG;
     try {
         DeviceGuard dg(h->device);
         int st;
@@ -491,24 +586,191 @@ int orbfe_extract_batch_device(orbfe_extractor* h, const uint8_t* d_imgs, int n,
         const LevelGeo& l0 = g.geo.lv[0];
         LevelPtr lp0{d_imgs, (long long)frame_pitch, (int)stride};
         const bool aligned = ((uintptr_t)d_imgs % 4 == 0) && stride % 4 == 0 && frame_pitch % 4 == 0;
-        if (!aligned && !d_masks) {  // kernels read level 0 as dwords: stage it in the slab
-            for (int f = 0; f < n; ++f)
-                ORBFE_HIP(hipMemcpy2DAsync(h->pyr.as<uint8_t>() + (size_t)f * g.slab + l0.off, l0.pitch,
-                                           d_imgs + (size_t)f * frame_pitch, stride, w, hgt,
-                                           hipMemcpyDeviceToDevice, h->stream));
+        if (pix != ORBFE_PIX_GRAY || d_masks || d_rects || !aligned) {
+            // K0 writes level 0 into the slab (the kernels read level 0 as dwords)
+            if ((st = h->launch_level0(n, d_imgs, (long long)frame_pitch, (int)stride, pix, d_masks,
+                                       (long long)mask_frame_pitch, (int)mask_stride,
+                                       reinterpret_cast<const int4*>(d_rects))))
+                return st;
             lp0 = LevelPtr{h->pyr.as<uint8_t>() + l0.off, g.slab, l0.pitch};
-        }
-        if (d_masks) {
-            uint8_t* p0 = h->pyr.as<uint8_t>() + l0.off;
-            ORBFE_LAUNCH(h->prof, ORBFE_STAGE_MASK, mask_kernel, dim3((w + 255) / 256, hgt, n), dim3(256), 0,
-                               h->stream, d_imgs, (long long)frame_pitch, (int)stride, d_masks,
-                               (long long)frame_pitch, (int)stride, p0, g.slab, l0.pitch, w, hgt);
-            lp0 = LevelPtr{p0, g.slab, l0.pitch};
         }
         return h->run(n, lp0, d_kps, kps_cap, d_desc, d_n_out);
     } catch (...) {
         return ORBFE_ERR_HIP;
     }
+}
+
+// ---- stereo (Frame::ComputeStereoMatches, Frame.cc:584-756) ----------------------------------
+// Launches S1-S3 of orbfe_stereo.hip on the left handle's stream for frames [f0, f0 + n) of
+// the two handles' most recent extractions; keypoint slabs are `kps_cap` apart per frame.
+static int stereo_launch(orbfe_extractor* L, orbfe_extractor* R, int f0, int n,
+                         const orbfe_keypoint* d_kl, const uint8_t* d_dl, const int32_t* d_nl,
+                         const orbfe_keypoint* d_kr, const uint8_t* d_dr, const int32_t* d_nr,
+                         int kps_cap, float bf, float b, float* d_ur, float* d_dp) {
+    const Plan& g = L->plan;
+    const int nlev = L->tab.p.nlevels;
+    StereoArgs a;
+    a.nrows = g.h;
+    float smax = 1.f;
+    for (int l = 0; l < nlev; ++l) smax = std::max(smax, L->tab.scale[l]);
+    a.row_cap = (int)std::ceil(4.0f * smax) + 3;  // rows floor(y-r)..ceil(y+r), r = 2 scale
+    a.kps_cap = kps_cap;
+    a.nlevels = nlev;
+    a.kl = d_kl;
+    a.dl = reinterpret_cast<const uint4*>(d_dl);
+    a.nl = d_nl;
+    a.kr = d_kr;
+    a.dr = reinterpret_cast<const uint4*>(d_dr);
+    a.nr = d_nr;
+    for (int l = 0; l < nlev; ++l) {
+        a.scale[l] = L->tab.scale[l];
+        a.inv[l] = L->tab.inv[l];
+        a.pl[l] = L->last_pyr[l];
+        a.pr[l] = R->last_pyr[l];
+        a.pl[l].base += f0 * a.pl[l].fpitch;
+        a.pr[l].base += f0 * a.pr[l].fpitch;
+        a.lw[l] = g.geo.lv[l].w;
+        a.lh[l] = g.geo.lv[l].h;
+    }
+    a.bf = bf;
+    a.b = b;
+    int st;
+    if ((st = L->st_off.ensure((size_t)n * (g.h + 1) * sizeof(int)))) return st;
+    if ((st = L->st_items.ensure((size_t)n * kps_cap * a.row_cap * sizeof(int)))) return st;
+    if ((st = L->st_sad.ensure((size_t)n * kps_cap * sizeof(int)))) return st;
+    if ((st = L->st_status.ensure(sizeof(int)))) return st;
+    a.row_off = L->st_off.as<int>();
+    a.row_items = L->st_items.as<int>();
+    a.u_right = d_ur;
+    a.depth = d_dp;
+    a.sad = L->st_sad.as<int>();
+    a.status = L->st_status.as<int>();
+    // the right handle's extraction must be complete on its own stream
+    if (R->stream != L->stream) {
+        hipEvent_t ev;
+        ORBFE_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        ORBFE_HIP(hipEventRecord(ev, R->stream));
+        ORBFE_HIP(hipStreamWaitEvent(L->stream, ev, 0));
+        ORBFE_HIP(hipEventDestroy(ev));
+    }
+    ORBFE_HIP(hipMemsetAsync(a.status, 0, sizeof(int), L->stream));
+    hipLaunchKernelGGL(stereo_rows_kernel, dim3(n), dim3(kStereoRowsBlock), 0, L->stream, a);
+    hipLaunchKernelGGL(stereo_match_kernel, dim3((kps_cap + 3) / 4, n), dim3(kStereoBlock), 0,
+                       L->stream, a);
+    hipLaunchKernelGGL(stereo_filter_kernel, dim3(n), dim3(kStereoFilterBlock), 0, L->stream, a);
+    ORBFE_HIP(hipGetLastError());
+    return ORBFE_OK;
+}
+
+static int stereo_pair_ok(const orbfe_extractor* L, const orbfe_extractor* R, int f_end) {
+    if (!L || !R || !L->planned || !R->planned || L->device != R->device) return ORBFE_ERR_ARG;
+    if (L->plan.w != R->plan.w || L->plan.h != R->plan.h ||
+        L->tab.p.nlevels != R->tab.p.nlevels || L->tab.p.scale_factor != R->tab.p.scale_factor)
+        return ORBFE_ERR_ARG;
+    if (f_end > L->last_n || f_end > R->last_n) return ORBFE_ERR_ARG;
+    if (L->plan.h > kStereoMaxRows) return ORBFE_ERR_UNSUPPORTED;
+    return ORBFE_OK;
+}
+
+int orbfe_compute_stereo_matches(orbfe_extractor* left, orbfe_extractor* right, int frame,
+                                 const orbfe_keypoint* kl, const uint8_t* dl, int nl,
+                                 const orbfe_keypoint* kr, const uint8_t* dr, int nr, float bf,
+                                 float b, float* u_right, float* depth) {
+    if (frame < 0 || nl < 0 || nr < 0 || (nl && (!kl || !dl || !u_right || !depth)) ||
+        (nr && (!kr || !dr)))
+        return ORBFE_ERR_ARG;
+    int st = stereo_pair_ok(left, right, frame + 1);
+    if (st) return st;
+    if (nl == 0) return ORBFE_OK;
+    if (nr >= 65536) return ORBFE_ERR_UNSUPPORTED;  // candidate keys pack iR in 16 bits
+    try {
+        DeviceGuard dg(left->device);
+        orbfe_extractor* L = left;
+        const int cap = std::max(nl, nr);
+        hipStream_t s = L->stream;
+        if ((st = L->st_kl.ensure((size_t)cap * sizeof(orbfe_keypoint)))) return st;
+        if ((st = L->st_kr.ensure((size_t)cap * sizeof(orbfe_keypoint)))) return st;
+        if ((st = L->st_dl.ensure((size_t)cap * 32))) return st;
+        if ((st = L->st_dr.ensure((size_t)cap * 32))) return st;
+        if ((st = L->st_n.ensure(2 * sizeof(int32_t)))) return st;
+        if ((st = L->st_ur.ensure((size_t)cap * sizeof(float)))) return st;
+        if ((st = L->st_dp.ensure((size_t)cap * sizeof(float)))) return st;
+        const int32_t counts[2] = {nl, nr};
+        ORBFE_HIP(hipMemcpyAsync(L->st_kl.p, kl, (size_t)nl * sizeof(orbfe_keypoint), hipMemcpyHostToDevice, s));
+        ORBFE_HIP(hipMemcpyAsync(L->st_dl.p, dl, (size_t)nl * 32, hipMemcpyHostToDevice, s));
+        if (nr) {
+            ORBFE_HIP(hipMemcpyAsync(L->st_kr.p, kr, (size_t)nr * sizeof(orbfe_keypoint), hipMemcpyHostToDevice, s));
+            ORBFE_HIP(hipMemcpyAsync(L->st_dr.p, dr, (size_t)nr * 32, hipMemcpyHostToDevice, s));
+        }
+        ORBFE_HIP(hipMemcpyAsync(L->st_n.p, counts, sizeof(counts), hipMemcpyHostToDevice, s));
+        if ((st = stereo_launch(L, right, frame, 1, L->st_kl.as<orbfe_keypoint>(), L->st_dl.as<uint8_t>(),
+                                L->st_n.as<int32_t>(), L->st_kr.as<orbfe_keypoint>(),
+                                L->st_dr.as<uint8_t>(), L->st_n.as<int32_t>() + 1, cap, bf, b,
+                                L->st_ur.as<float>(), L->st_dp.as<float>())))
+            return st;
+        int status = 0;
+        ORBFE_HIP(hipMemcpyAsync(u_right, L->st_ur.p, (size_t)nl * sizeof(float), hipMemcpyDeviceToHost, s));
+        ORBFE_HIP(hipMemcpyAsync(depth, L->st_dp.p, (size_t)nl * sizeof(float), hipMemcpyDeviceToHost, s));
+        ORBFE_HIP(hipMemcpyAsync(&status, L->st_status.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        ORBFE_HIP(hipStreamSynchronize(s));
+        return status;
+    } catch (const std::bad_alloc&) {
+        return ORBFE_ERR_NOMEM;
+    } catch (...) {
+        return ORBFE_ERR_HIP;
+    }
+}
+
+int orbfe_compute_stereo_matches_device(orbfe_extractor* left, orbfe_extractor* right, int n,
+                                        const orbfe_keypoint* d_kl, const uint8_t* d_dl,
+                                        const int32_t* d_nl, const orbfe_keypoint* d_kr,
+                                        const uint8_t* d_dr, const int32_t* d_nr, int kps_cap,
+                                        float bf, float b, float* d_u_right, float* d_depth) {
+    if (n < 0 || kps_cap <= 0 || !d_kl || !d_dl || !d_nl || !d_kr || !d_dr || !d_nr ||
+        !d_u_right || !d_depth)
+        return ORBFE_ERR_ARG;
+    int st = stereo_pair_ok(left, right, n);
+    if (st || n == 0) return st;
+    if (kps_cap >= 65536) return ORBFE_ERR_UNSUPPORTED;
+    try {
+        DeviceGuard dg(left->device);
+        return stereo_launch(left, right, 0, n, d_kl, d_dl, d_nl, d_kr, d_dr, d_nr, kps_cap, bf,
+                             b, d_u_right, d_depth);
+    } catch (...) {
+        return ORBFE_ERR_HIP;
+    }
+}
+
+int orbfe_stereo_status(orbfe_extractor* left) {
+    if (!left) return ORBFE_ERR_ARG;
+    if (!left->st_status.p) return ORBFE_OK;
+    DeviceGuard dg(left->device);
+    int status = 0;
+    ORBFE_HIP(hipMemcpyAsync(&status, left->st_status.p, sizeof(int), hipMemcpyDeviceToHost, left->stream));
+    ORBFE_HIP(hipStreamSynchronize(left->stream));
+    return status;
+}
+
+int orbfe_human_mask_rect(const float* joints, int njoints, int w, int hgt, orbfe_rect* out) {
+    if (!joints || njoints < 0 || w <= 0 || hgt <= 0 || !out) return ORBFE_ERR_ARG;
+    // OpDetector::SkeletonSquareMask (DetectHumanPose.cpp:453-489): the bounding box of the
+    // joints' (x, y) (a float ternary truncated by static_cast<int>), grown by 30 px, clamped.
+    int xmin = w - 1, ymin = hgt - 1, xmax = 0, ymax = 0;
+    for (int i = 0; i < njoints; ++i) {
+        const float x = joints[3 * i], y = joints[3 * i + 1];
+        xmin = static_cast<int>(x < xmin ? x : (float)xmin);
+        xmax = static_cast<int>(x > xmax ? x : (float)xmax);
+        ymin = static_cast<int>(y < ymin ? y : (float)ymin);
+        ymax = static_cast<int>(y > ymax ? y : (float)ymax);
+    }
+    xmin -= 30; xmax += 30;
+    ymin -= 30; ymax += 30;
+    out->x0 = xmin <= 0 ? 0 : xmin;
+    out->y0 = ymin <= 0 ? 0 : ymin;
+    out->x1 = xmax >= w - 1 ? w - 1 : xmax;
+    out->y1 = ymax >= hgt - 1 ? hgt - 1 : ymax;
+    // rowRange(y0, y1).colRange(x0, x1) asserts start <= end (CV_Assert stays in release)
+    return rect_ok(out) ? ORBFE_OK : ORBFE_ERR_UNSUPPORTED;
 }
 
 int orbfe_profile(orbfe_extractor* h, int enable) {

@@ -3,7 +3,8 @@
 //
 // Pipeline for a batch of B same-size frames (one launch per stage, every launch covers the
 // whole batch; DESIGN.md "Kernels" has the roofline and bytes of each):
-//   K0 mask_kernel      Mat::copyTo(dst, mask) (1053)                       [only with a mask]
+//   K0 level0_kernel    cvtColor(*2GRAY) (Tracking.cc:409-422) + Mat::copyTo(dst, mask) (1053)
+//                       [only for colour input or a mask]
 //   K1 resize_kernel    cascaded cv::resize INTER_LINEAR 8U, levels 1..L-1 (1123)
 //   K2 fast_kernel      per-cell FAST-9 score + cell-local 3x3 NMS + iniTh->minTh fallback
 //                       (764-831); one workgroup per (frame, cell)
@@ -41,19 +42,90 @@ constexpr int kMinBorder = 16;  // EDGE_THRESHOLD - 3 (772)
 constexpr int kCellW = 30;      // W (768)
 
 // ---------------------------------------------------------------------------------------------
-// K0 — masked copy into pyramid level 0 (Mat::copyTo with a mask, App. A.7).
-__global__ void mask_kernel(const uint8_t* src, long long src_fpitch, int src_pitch,
-                            const uint8_t* mask, long long mask_fpitch,
-                            int mask_pitch, uint8_t* dst, long long dst_fpitch,
-                            int dst_pitch, int w, int h) {
-    const int f = blockIdx.z;
-    const int y = blockIdx.y;
-    const uint8_t* s = src + f * src_fpitch + (long long)y * src_pitch;
-    const uint8_t* m = mask + f * mask_fpitch + (long long)y * mask_pitch;
-    uint8_t* d = dst + f * dst_fpitch + (long long)y * dst_pitch;
-    for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < w; x += gridDim.x * blockDim.x)
-        d[x] = m[x] ? s[x] : 0;
-    (void)h;
+// K0 — pyramid level 0 from the caller's frame: cvtColor(CV_{RGB,BGR,RGBA,BGRA}2GRAY) of
+// Tracking::GrabImage* (Tracking.cc:286-310, 350-363, 409-422), then Mat::copyTo(image, mask)
+// (ORBextractor.cc:1053, App. A.7) with the mask given as a full u8 plane and/or the zeroed
+// rectangle of OpDetector::SkeletonSquareMask (DetectHumanPose.cpp:484-489).  Gray is
+// OpenCV's 8U integer path RGB2Gray<uchar>: (c0*s0 + 9617*s1 + c2*s2 + 2^13) >> 14 with
+// {c0, c2} = {B2Y 1868, R2Y 4899} for BGR order and swapped for RGB.  Each thread makes 4
+// pixels and stores one dword (level-0 rows are padded to 64 B; pixels >= w are written 0).
+// Sources whose rows are 4-byte aligned are read with dword / 3-dword / uint4 loads.
+template <int CN>
+__device__ __forceinline__ void load4(const uint8_t* row, int x, int w, bool aligned, uint8_t (&px)[4][4]) {
+    if (aligned && x + 4 <= w) {
+        if constexpr (CN == 1) {
+            const uint32_t v = *reinterpret_cast<const uint32_t*>(row + x);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) px[i][0] = (uint8_t)(v >> (8 * i));
+        } else if constexpr (CN == 3) {
+            const uint32_t* q = reinterpret_cast<const uint32_t*>(row + 3 * x);
+            const uint32_t v0 = q[0], v1 = q[1], v2 = q[2];
+            const uint8_t b[12] = {(uint8_t)v0, (uint8_t)(v0 >> 8), (uint8_t)(v0 >> 16), (uint8_t)(v0 >> 24),
+                                   (uint8_t)v1, (uint8_t)(v1 >> 8), (uint8_t)(v1 >> 16), (uint8_t)(v1 >> 24),
+                                   (uint8_t)v2, (uint8_t)(v2 >> 8), (uint8_t)(v2 >> 16), (uint8_t)(v2 >> 24)};
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) px[i][c] = b[3 * i + c];
+        } else {
+            const uint4 v = *reinterpret_cast<const uint4*>(row + 4 * x);
+            const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) px[i][c] = (uint8_t)(vv[i] >> (8 * c));
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int c = 0; c < CN; ++c) px[i][c] = (x + i < w) ? row[CN * (x + i) + c] : 0;
+}
+
+template <int CN>
+__device__ __forceinline__ void level0_row(const Level0Args& a, int f, int y, int x) {
+    const uint8_t* row = a.src + f * a.src_fpitch + (long long)y * a.src_pitch;
+    uint8_t px[4][4];
+    load4<CN>(row, x, a.w, a.aligned, px);
+    bool keep[4] = {true, true, true, true};
+    if (a.mask) {
+        const uint8_t* m = a.mask + f * a.mask_fpitch + (long long)y * a.mask_pitch;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) keep[i] = (x + i < a.w) && m[x + i] != 0;
+    }
+    if (a.rects) {
+        const int4 r = a.rects[f];
+        if (y >= r.y && y < r.w) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (x + i >= r.x && x + i < r.z) keep[i] = false;
+        }
+    }
+    uint32_t out = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        int g;
+        if constexpr (CN == 1) {
+            g = px[i][0];
+        } else {
+            g = (a.c0 * px[i][0] + 9617 * px[i][1] + a.c2 * px[i][2] + (1 << 13)) >> 14;
+        }
+        if (!keep[i] || x + i >= a.w) g = 0;
+        out |= (uint32_t)g << (8 * i);
+    }
+    *reinterpret_cast<uint32_t*>(a.dst + f * a.dst_fpitch + (long long)y * a.dst_pitch + x) = out;
+}
+
+__global__ __launch_bounds__(256) void level0_kernel(Level0Args a) {
+    const int f = blockIdx.z, y = blockIdx.y;
+    const int x = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
+    if (x >= a.w) return;
+    switch (a.cn) {
+        case 1: level0_row<1>(a, f, y, x); break;
+        case 3: level0_row<3>(a, f, y, x); break;
+        default: level0_row<4>(a, f, y, x); break;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -55,6 +55,20 @@ struct LevelPtr {
     int pitch;             // bytes between rows
 };
 
+struct Level0Args {
+    const uint8_t* src;    // caller frames (cn bytes per pixel)
+    long long src_fpitch;
+    int src_pitch, cn, c0, c2;   // channels; gray weights of channel 0 and 2 (RGB2Gray<uchar>)
+    bool aligned;          // src rows 4-byte aligned: vector loads
+    const uint8_t* mask;   // NULL or u8 plane per frame
+    long long mask_fpitch;
+    int mask_pitch;
+    const int4* rects;     // NULL or per frame (x0, y0, x1, y1) zeroed rectangle
+    uint8_t* dst;          // pyramid level 0
+    long long dst_fpitch;
+    int dst_pitch, w, h;
+};
+
 struct ResizeArgs {
     LevelPtr src, dst;
     int sw, sh, dw, dh;
@@ -141,8 +155,7 @@ int make_tables(const orbfe_params& p, HostTables& t);
 int plan_geometry(const HostTables& t, int w, int h, Plan& g);
 
 // kernels (orbfe_extract.hip)
-__global__ void mask_kernel(const uint8_t*, long long, int, const uint8_t*, long long, int,
-                            uint8_t*, long long, int, int, int);
+__global__ void level0_kernel(Level0Args);
 __global__ void resize_kernel(ResizeArgs);
 __global__ void fast_kernel(FastArgs);
 __global__ void octree_kernel(OctArgs);

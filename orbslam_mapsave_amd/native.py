@@ -28,8 +28,10 @@ _lib: C.CDLL | None = None
 EXPORTED = [
     "orbfe_create", "orbfe_destroy", "orbfe_get_levels", "orbfe_get_scale_factor",
     "orbfe_get_scale_tables", "orbfe_get_features_per_level", "orbfe_keypoint_capacity",
-    "orbfe_extract", "orbfe_extract_batch", "orbfe_extract_batch_device", "orbfe_set_stream",
-    "orbfe_synchronize", "orbfe_profile", "orbfe_profile_read", "orbfe_get_level", "orbfe_get_blurred_level", "orbfe_get_fast_keys",
+    "orbfe_extract", "orbfe_extract_color", "orbfe_human_mask_rect", "orbfe_extract_batch",
+    "orbfe_extract_batch_device", "orbfe_extract_color_batch_device", "orbfe_set_stream",
+    "orbfe_synchronize", "orbfe_compute_stereo_matches", "orbfe_compute_stereo_matches_device",
+    "orbfe_stereo_status", "orbfe_profile", "orbfe_profile_read", "orbfe_get_level", "orbfe_get_blurred_level", "orbfe_get_fast_keys",
     "orbfe_matcher_create", "orbfe_matcher_destroy", "orbfe_matcher_set_stream",
     "orbfe_matcher_profile", "orbfe_matcher_profile_read", "orbfe_hamming",
     "orbfe_bf_match", "orbfe_bf_match_batch_device", "orbfe_search_for_initialization",
@@ -63,6 +65,20 @@ def lib() -> C.CDLL:
 def _check(fn: str, st: int) -> None:
     if st != ORBFE_OK:
         raise OrbfeError(fn, st)
+
+
+# ORBFE_PIX_* (include/orbfe.h): the cvtColor codes of Tracking::GrabImage*
+PIX_GRAY, PIX_RGB, PIX_BGR, PIX_RGBA, PIX_BGRA = range(5)
+PIX_CHANNELS = {PIX_GRAY: 1, PIX_RGB: 3, PIX_BGR: 3, PIX_RGBA: 4, PIX_BGRA: 4}
+
+
+def human_mask_rect(joints: np.ndarray, w: int, h: int) -> tuple[int, int, int, int]:
+    """OpDetector::SkeletonSquareMask's zeroed rectangle from (n, 3) joints
+    (DetectHumanPose.cpp:453-489), via orbfe_human_mask_rect."""
+    j = np.ascontiguousarray(joints, np.float32).reshape(-1, 3)
+    out = (C.c_int32 * 4)()
+    _check("orbfe_human_mask_rect", lib().orbfe_human_mask_rect(ptr(j), len(j), w, h, out))
+    return tuple(out)
 
 
 class ORBextractor:
@@ -141,6 +157,71 @@ class ORBextractor:
             self._h, ptr(image), w, h, C.c_size_t(w), ptr(m), C.c_size_t(w), ptr(kps), cap,
             ptr(desc), C.byref(n)))
         return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def extract_color(self, image: np.ndarray, pix: int, mask: np.ndarray | None = None,
+                      rect: tuple[int, int, int, int] | None = None):
+        """``cvtColor(image, gray, CV_*2GRAY)`` (Tracking.cc:409-422) fused with
+        ``operator()(gray, mask)``; `pix` is one of PIX_*; `rect` = (x0, y0, x1, y1) zeroed
+        rectangle of the human mask (DetectHumanPose.cpp:484-489)."""
+        image = np.ascontiguousarray(image, np.uint8)
+        if image.size == 0:
+            return None, None
+        h, w = image.shape[:2]
+        cn = 1 if image.ndim == 2 else image.shape[2]
+        if cn != PIX_CHANNELS[pix]:
+            raise ValueError(f"pix {pix} needs {PIX_CHANNELS[pix]} channels, image has {cn}")
+        m = None if mask is None or np.size(mask) == 0 else np.ascontiguousarray(mask, np.uint8)
+        r = None if rect is None else (C.c_int32 * 4)(*rect)
+        cap = self.capacity()
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = C.c_int(0)
+        _check("orbfe_extract_color", lib().orbfe_extract_color(
+            self._h, ptr(image), pix, w, h, C.c_size_t(w * cn), ptr(m), C.c_size_t(w),
+            r, ptr(kps), cap, ptr(desc), C.byref(n)))
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def extract_color_batch_device(self, d_imgs: int, pix: int, n: int, w: int, h: int,
+                                   stride: int, frame_pitch: int, d_kps: int, kps_cap: int,
+                                   d_desc: int, d_n_out: int, d_masks: int | None = None,
+                                   mask_stride: int = 0, mask_frame_pitch: int = 0,
+                                   d_rects: int | None = None) -> None:
+        """Device-resident colour batch (orbfe_extract_color_batch_device); async."""
+        _check("orbfe_extract_color_batch_device", lib().orbfe_extract_color_batch_device(
+            self._h, C.c_void_p(d_imgs), pix, n, w, h, C.c_size_t(stride),
+            C.c_size_t(frame_pitch), C.c_void_p(d_masks) if d_masks else None,
+            C.c_size_t(mask_stride), C.c_size_t(mask_frame_pitch),
+            C.c_void_p(d_rects) if d_rects else None, C.c_void_p(d_kps), kps_cap,
+            C.c_void_p(d_desc), C.c_void_p(d_n_out)))
+
+    def ComputeStereoMatches(self, right: "ORBextractor", kl: np.ndarray, dl: np.ndarray,
+                             kr: np.ndarray, dr: np.ndarray, bf: float, b: float,
+                             frame: int = 0):
+        """Frame::ComputeStereoMatches (Frame.cc:584-756) with this handle as
+        mpORBextractorLeft and `right` as mpORBextractorRight (their last extractions' pyramids).
+        Returns (mvuRight, mvDepth) float32 arrays of len(kl)."""
+        kl = np.ascontiguousarray(kl, KEYPOINT_DTYPE)
+        kr = np.ascontiguousarray(kr, KEYPOINT_DTYPE)
+        dl = np.ascontiguousarray(dl, np.uint8)
+        dr = np.ascontiguousarray(dr, np.uint8)
+        ur = np.full(len(kl), -1, np.float32)
+        dp = np.full(len(kl), -1, np.float32)
+        _check("orbfe_compute_stereo_matches", lib().orbfe_compute_stereo_matches(
+            self._h, right._h, frame, ptr(kl), ptr(dl), len(kl), ptr(kr), ptr(dr), len(kr),
+            C.c_float(bf), C.c_float(b), ptr(ur), ptr(dp)))
+        return ur, dp
+
+    def compute_stereo_matches_device(self, right: "ORBextractor", n: int, d_kl: int, d_dl: int,
+                                      d_nl: int, d_kr: int, d_dr: int, d_nr: int, kps_cap: int,
+                                      bf: float, b: float, d_ur: int, d_dp: int) -> None:
+        """Batched device form (orbfe_compute_stereo_matches_device); async."""
+        _check("orbfe_compute_stereo_matches_device", lib().orbfe_compute_stereo_matches_device(
+            self._h, right._h, n, C.c_void_p(d_kl), C.c_void_p(d_dl), C.c_void_p(d_nl),
+            C.c_void_p(d_kr), C.c_void_p(d_dr), C.c_void_p(d_nr), kps_cap, C.c_float(bf),
+            C.c_float(b), C.c_void_p(d_ur), C.c_void_p(d_dp)))
+
+    def stereo_status(self) -> None:
+        _check("orbfe_stereo_status", lib().orbfe_stereo_status(self._h))
 
     def extract_batch(self, images: np.ndarray, masks: np.ndarray | None = None):
         """Host batch: (n, h, w) uint8 -> (kps (n, cap), desc (n, cap, 32), counts (n,))."""

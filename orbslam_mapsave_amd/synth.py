@@ -105,3 +105,35 @@ def synthetic_batch(n: int, w: int = 640, h: int = 480, first_seed: int = 0,
     d = n if distinct is None else max(1, min(distinct, n))
     frames = [synthetic_frame(first_seed + i, w, h) for i in range(d)]
     return np.stack([frames[i % d] for i in range(n)])
+
+
+def synthetic_color_frame(seed: int, w: int = 640, h: int = 480, channels: int = 3) -> np.ndarray:
+    """(h, w, channels) uint8 colour frame: three correlated textured planes (the gray texture
+    plus a per-channel tint and a second texture), alpha random for 4 channels."""
+    base = synthetic_frame(seed, w, h).astype(np.float32)
+    other = synthetic_frame(seed + 50_000, w, h).astype(np.float32)
+    rng = np.random.Generator(np.random.PCG64(seed + 7))
+    planes = []
+    for c in range(3):
+        a, b, t = rng.uniform(0.5, 1.0), rng.uniform(0.0, 0.4), rng.uniform(-30, 30)
+        planes.append(np.clip(np.rint(a * base + b * other + t), 0, 255).astype(np.uint8))
+    if channels == 4:
+        planes.append(rng.integers(0, 256, (h, w), dtype=np.uint8))
+    return np.ascontiguousarray(np.stack(planes, -1))
+
+
+def synthetic_stereo_pair(seed: int, w: int = 640, h: int = 480, d0: float = 4.0,
+                          d1: float = 40.0) -> tuple[np.ndarray, np.ndarray]:
+    """A rectified pair: the right image samples the left one at x + d(x, y) with a disparity
+    ramp d from d0 (top) to d1 (bottom) plus a gentle x tilt (a slanted plane), bilinear, so
+    matches are sub-pixel and the ORB keypoints of both images correspond."""
+    left = synthetic_frame(seed, w, h + 0).astype(np.float32)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    d = d0 + (d1 - d0) * yy / max(h - 1, 1) + 3.0 * xx / max(w - 1, 1)
+    sx = np.clip(xx + d, 0, w - 1)
+    x0 = np.floor(sx).astype(np.int64)
+    x1 = np.minimum(x0 + 1, w - 1)
+    t = sx - x0
+    rows = np.arange(h)[:, None]
+    right = left[rows, x0] * (1 - t) + left[rows, x1] * t
+    return left.astype(np.uint8), np.clip(np.rint(right), 0, 255).astype(np.uint8)
