@@ -311,6 +311,27 @@ int orbfe_search_by_projection_last(orbfe_matcher* m, int check_ori,
                                     const float* tcw_last, float th, int mono,
                                     int32_t* nmatches);
 
+/* Relocalisation ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF,
+ * const set<MapPoint*>& sAlreadyFound, th, ORBdist) (ORBmatcher.cc:1475-1602), called by
+ * Tracking::Relocalization with ORBmatcher(0.9, true), th/ORBdist = 10/100 and 3/64
+ * (Tracking.cc:1664, 1723, 1737).  The keyframe is given as its n_kf map-point slots
+ * (pKF->GetMapPointMatches(); kf_mp_valid[i] == 0 <=> NULL) with isBad(), sAlreadyFound
+ * membership, world position (n_kf x 3), descriptor (n_kf x 32), mfMinDistance /
+ * mfMaxDistance and the rotation angle pKF->mvKeysUn[i].angle.  frame_mp: inout cur->n ids
+ * (-1 = NULL; a slot holding a point is never re-assigned); a match writes kf_mp_ids[i] (or i).
+ * log_scale_factor = mfLogScaleFactor.  A predicted scale level outside the pyramid (where the
+ * fork indexes mvScaleFactors out of range; MapPoint::PredictScale has no clamp) returns
+ * ORBFE_ERR_UNSUPPORTED. */
+int orbfe_search_by_projection_keyframe(orbfe_matcher* m, int check_ori,
+                                        const orbfe_frame_view* cur, const float* tcw_cur,
+                                        const orbfe_camera* cam, float log_scale_factor,
+                                        int32_t* frame_mp, int n_kf, const float* kf_key_angle,
+                                        const uint8_t* kf_mp_valid, const uint8_t* kf_mp_bad,
+                                        const uint8_t* already_found, const float* kf_mp_xyz,
+                                        const uint8_t* kf_mp_desc, const float* kf_mp_min_dist,
+                                        const float* kf_mp_max_dist, const int32_t* kf_mp_ids,
+                                        float th, int orb_dist, int32_t* nmatches);
+
 /* Frame::isInFrustum (Frame.cc:387-443) + MapPoint::PredictScale (MapPoint.cc:633-642) over
  * m MapPoints: world pos (m x 3), normal (m x 3), mfMinDistance/mfMaxDistance.  Writes the
  * tracking scratch fields (mbTrackInView, mTrackProjX/Y/XR, mnTrackScaleLevel,

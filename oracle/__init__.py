@@ -267,6 +267,34 @@ def search_by_projection_last(cur: Frame, tcw_cur, cam: Camera, last_keys, last_
     return fmp, fobs, nm.value
 
 
+def _sbp_kf_args(c):
+    return [np.ascontiguousarray(c["tcw_cur"], np.float32).reshape(12),
+            np.ascontiguousarray(c["kf_angle"], np.float32),
+            np.ascontiguousarray(c["kf_valid"], np.uint8),
+            np.ascontiguousarray(c["kf_bad"], np.uint8),
+            np.ascontiguousarray(c["found"], np.uint8),
+            np.ascontiguousarray(c["kf_xyz"], np.float32).reshape(-1, 3),
+            np.ascontiguousarray(c["kf_desc"], np.uint8).reshape(-1, 32),
+            np.ascontiguousarray(c["kf_min"], np.float32),
+            np.ascontiguousarray(c["kf_max"], np.float32),
+            None if c.get("kf_ids") is None else np.ascontiguousarray(c["kf_ids"], np.int32)]
+
+
+def search_by_projection_keyframe(c: dict, th=10.0, orb_dist=100, check_ori=True):
+    """Relocalisation SearchByProjection(Frame&, KeyFrame*, ...) (ORBmatcher.cc:1475-1602);
+    `c` holds the keys of tests/scenarios.sbp_keyframe_case.  Returns (frame_mp, nmatches)."""
+    cur = c["cur"]
+    fmp = np.ascontiguousarray(c["frame_mp"], np.int32).copy()
+    a = _sbp_kf_args(c)
+    nm = C.c_int32(0)
+    cv = cur.view()
+    _check("oracle_search_by_projection_keyframe", lib().oracle_search_by_projection_keyframe(
+        int(check_ori), C.byref(cv), ptr(a[0]), C.byref(c["cam"]), C.c_float(c["log_scale"]),
+        ptr(fmp), len(a[1]), *(ptr(x) for x in a[1:]), C.c_float(th), int(orb_dist),
+        C.byref(nm)))
+    return fmp, nm.value
+
+
 def is_in_frustum(xyz, normal, min_dist, max_dist, tcw, cam: Camera, bounds, log_scale,
                   cos_limit=0.5):
     xyz = np.ascontiguousarray(xyz, np.float32).reshape(-1, 3)

@@ -1207,6 +1207,69 @@ int oracle_search_by_projection_last(int check_ori, const orbfe_frame_view* cur,
     return ORBFE_OK;
 }
 
+// Relocalisation SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th, ORBdist)
+// (ORBmatcher.cc:1475-1602).  The keyframe is its n_kf map-point slots (GetMapPointMatches).
+int oracle_search_by_projection_keyframe(int check_ori, const orbfe_frame_view* cur,
+                                         const float* tcw_cur, const orbfe_camera* cam,
+                                         float log_scale_factor, int32_t* frame_mp, int n_kf,
+                                         const float* kf_key_angle, const uint8_t* kf_mp_valid,
+                                         const uint8_t* kf_mp_bad, const uint8_t* already_found,
+                                         const float* kf_mp_xyz, const uint8_t* kf_mp_desc,
+                                         const float* kf_mp_min_dist,
+                                         const float* kf_mp_max_dist, const int32_t* kf_mp_ids,
+                                         float th, int orb_dist, int32_t* nmatches) {
+    Grid g;
+    build_grid(cur, g);
+    float ow[3];
+    camera_center(tcw_cur, ow);  // Ow = -Rcw^T tcw (1479-1481)
+    int nm = 0;
+    std::vector<int> hist[kHistLen];
+    std::vector<int> cand;
+    for (int i = 0; i < n_kf; ++i) {
+        if (!kf_mp_valid[i] || kf_mp_bad[i] || already_found[i]) continue;
+        const float* P = kf_mp_xyz + 3 * (size_t)i;
+        float pc[3];
+        rigid(tcw_cur, P, pc);
+        const float invz = (float)(1.0 / pc[2]);
+        const float u = cam->fx * pc[0] * invz + cam->cx;
+        const float v = cam->fy * pc[1] * invz + cam->cy;
+        if (u < cur->min_x || u > cur->max_x) continue;
+        if (v < cur->min_y || v > cur->max_y) continue;
+        const float po[3] = {P[0] - ow[0], P[1] - ow[1], P[2] - ow[2]};
+        const float dist3d = (float)std::sqrt((double)po[0] * po[0] + (double)po[1] * po[1] +
+                                              (double)po[2] * po[2]);  // cv::norm (double)
+        const float max_d = 1.2f * kf_mp_max_dist[i], min_d = 0.8f * kf_mp_min_dist[i];
+        if (dist3d < min_d || dist3d > max_d) continue;
+        const float ratio = kf_mp_max_dist[i] / dist3d;  // PredictScale (MapPoint.cc:633-642)
+        const int lvl = (int)std::ceil((float)std::log((double)ratio) / log_scale_factor);
+        if (lvl < 0 || lvl >= cur->nlevels) return ORBFE_ERR_UNSUPPORTED;  // mvScaleFactors[lvl]
+        const float radius = th * cur->scale_factors[lvl];
+        features_in_area(cur, g, u, v, radius, lvl - 1, lvl + 1, cand);
+        if (cand.empty()) continue;
+        int best = 256, bi = -1;
+        for (int i2 : cand) {
+            if (frame_mp[i2] >= 0) continue;
+            const int d = descriptor_distance(kf_mp_desc + 32 * (size_t)i, cur->desc + 32 * (size_t)i2);
+            if (d < best) { best = d; bi = i2; }
+        }
+        if (best <= orb_dist) {
+            frame_mp[bi] = kf_mp_ids ? kf_mp_ids[i] : i;
+            ++nm;
+            if (check_ori) hist[rot_bin(kf_key_angle[i], cur->keys_un[bi].angle)].push_back(bi);
+        }
+    }
+    if (check_ori) {
+        int a, b, c;
+        three_maxima(hist, a, b, c);
+        for (int i = 0; i < kHistLen; ++i) {
+            if (i == a || i == b || i == c) continue;
+            for (int i2 : hist[i]) { frame_mp[i2] = -1; --nm; }
+        }
+    }
+    *nmatches = nm;
+    return ORBFE_OK;
+}
+
 // A17 — Frame::isInFrustum (Frame.cc:387-443) + MapPoint::PredictScale (MapPoint.cc:633-642).
 int oracle_is_in_frustum(int n, const float* xyz, const float* normal, const float* min_dist,
                          const float* max_dist, const float* tcw, const orbfe_camera* cam,

@@ -87,6 +87,15 @@ int oracle_search_by_projection_last(int check_ori, const orbfe_frame_view* cur,
                                      const int32_t* last_mp_nobs, const int32_t* last_mp_ids,
                                      const float* tcw_last, float th, int mono,
                                      int32_t* nmatches);
+int oracle_search_by_projection_keyframe(int check_ori, const orbfe_frame_view* cur,
+                                         const float* tcw_cur, const orbfe_camera* cam,
+                                         float log_scale_factor, int32_t* frame_mp, int n_kf,
+                                         const float* kf_key_angle, const uint8_t* kf_mp_valid,
+                                         const uint8_t* kf_mp_bad, const uint8_t* already_found,
+                                         const float* kf_mp_xyz, const uint8_t* kf_mp_desc,
+                                         const float* kf_mp_min_dist,
+                                         const float* kf_mp_max_dist, const int32_t* kf_mp_ids,
+                                         float th, int orb_dist, int32_t* nmatches);
 int oracle_is_in_frustum(int n, const float* xyz, const float* normal, const float* min_dist,
                          const float* max_dist, const float* tcw, const orbfe_camera* cam,
                          float min_x, float max_x, float min_y, float max_y,

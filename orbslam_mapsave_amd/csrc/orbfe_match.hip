@@ -545,6 +545,7 @@ __global__ __launch_bounds__(256) void sbp_last_cand_kernel(SbpLastArgs a) {
 
 struct SbpLastResolveArgs {
     int n_last, nkp;
+    int max_dist;      // accept best <= max_dist: TH_HIGH (1411) or ORBdist (1545)
     const int* off;
     const int2* cand;
     const int* nobs;
@@ -576,8 +577,8 @@ __global__ __launch_bounds__(64) void sbp_last_resolve_kernel(SbpLastResolveArgs
             if (a.fmp[c.x] >= 0 && a.fobs[c.x] > 0) continue;  // 1406-1408
             if (c.y < best) { best = c.y; bi = c.x; }
         }
-        const bool acc = valid && best <= kThHigh;
-        const int nobs = acc ? a.nobs[i] : 0;
+        const bool acc = valid && best <= a.max_dist;
+        const int nobs = acc ? (a.nobs ? a.nobs[i] : 1) : 0;
         if (acc && nobs > 0) atomicMin(&a.claim[bi], lane);
         __syncthreads();
         bool conf = false;
@@ -623,6 +624,79 @@ __global__ __launch_bounds__(64) void sbp_last_resolve_kernel(SbpLastResolveArgs
         nm -= wave_sum(removed);
     }
     if (lane == 0) *a.nmatches = nm;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Relocalisation SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th, ORBdist)
+// (ORBmatcher.cc:1475-1602): candidates of every keyframe map point in parallel; the greedy
+// assignment (a slot taken by an earlier map point blocks later ones, 1529-1530) is
+// sbp_last_resolve_kernel with every map point counted as observed (nobs = 1) and
+// max_dist = ORBdist.
+struct SbpKfArgs {
+    DevFrame cur;
+    int n;
+    const uint8_t* valid;     // GetMapPointMatches()[i] != NULL
+    const uint8_t* bad;       // isBad()
+    const uint8_t* found;     // sAlreadyFound.count()
+    const float* xyz;
+    const float* mind;        // mfMinDistance
+    const float* maxd;        // mfMaxDistance
+    const uint4* desc;
+    float T[12];
+    float ow[3];              // -Rcw^T tcw (host, double accumulation)
+    float fx, fy, cx, cy;
+    float minx, maxx, miny, maxy;
+    const float* scale;
+    int nlevels;
+    float log_scale, th;
+    int* status;
+    int* cnt;
+    const int* off;
+    int2* cand;
+};
+
+template <bool FILL>
+__global__ __launch_bounds__(256) void sbp_kf_cand_kernel(SbpKfArgs a) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n) return;
+    int n = 0;
+    if (a.valid[i] && !a.bad[i] && !a.found[i]) {
+        const float* P = a.xyz + 3 * i;
+        float pc[3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+            pc[r] = ((a.T[4 * r] * P[0] + a.T[4 * r + 1] * P[1]) + a.T[4 * r + 2] * P[2]) + a.T[4 * r + 3];
+        const float invz = (float)(1.0 / (double)pc[2]);  // 1.0/x3Dc.at<float>(2): double divide
+        const float u = a.fx * pc[0] * invz + a.cx;
+        const float v = a.fy * pc[1] * invz + a.cy;
+        bool ok = !(u < a.minx || u > a.maxx) && !(v < a.miny || v > a.maxy);
+        float dist = 0.f;
+        if (ok) {
+            const float po0 = P[0] - a.ow[0], po1 = P[1] - a.ow[1], po2 = P[2] - a.ow[2];
+            dist = (float)sqrt((double)po0 * po0 + (double)po1 * po1 + (double)po2 * po2);
+            const float dmax = 1.2f * a.maxd[i], dmin = 0.8f * a.mind[i];  // MapPoint.cc:621-631
+            ok = !(dist < dmin || dist > dmax);
+        }
+        if (ok) {
+            const float ratio = a.maxd[i] / dist;
+            const int lvl = (int)ceilf((float)log((double)ratio) / a.log_scale);
+            if (lvl < 0 || lvl >= a.nlevels) {
+                atomicExch(a.status, ORBFE_ERR_UNSUPPORTED);  // mvScaleFactors[lvl] out of range
+            } else {
+                const float radius = a.th * a.scale[lvl];
+                const uint4 q0 = a.desc[2 * i], q1 = a.desc[2 * i + 1];
+                int2* out = FILL ? a.cand + a.off[i] : nullptr;
+                features_in_area(a.cur, u, v, radius, lvl - 1, lvl + 1, [&](int i2) {
+                    if (FILL) {
+                        const uint4* d = a.cur.desc + 2 * i2;
+                        out[n] = make_int2(i2, hamming256(q0, q1, d[0], d[1]));
+                    }
+                    ++n;
+                });
+            }
+        }
+    }
+    if (!FILL) a.cnt[i] = n;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -427,6 +427,7 @@ int orbfe_search_by_projection_last(orbfe_matcher* m, int check_ori,
         SbpLastResolveArgs r;
         r.n_last = n_last;
         r.nkp = N;
+        r.max_dist = kThHigh;
         r.off = m->off.as<int>();
         r.cand = m->cand.as<int2>();
         r.nobs = m->m_i1.as<int>();
@@ -443,6 +444,102 @@ int orbfe_search_by_projection_last(orbfe_matcher* m, int check_ori,
         ORBFE_HIP(hipGetLastError());
         if ((st = m->down(frame_mp, m->s1, (size_t)N * 4))) return st;
         if ((st = m->down(frame_mp_obs, m->s2, (size_t)N * 4))) return st;
+        if ((st = m->down(nmatches, m->scal, sizeof(int)))) return st;
+        ORBFE_HIP(hipStreamSynchronize(m->stream));
+        return ORBFE_OK;
+    });
+}
+
+int orbfe_search_by_projection_keyframe(orbfe_matcher* m, int check_ori,
+                                        const orbfe_frame_view* cur, const float* tcw_cur,
+                                        const orbfe_camera* cam, float log_scale_factor,
+                                        int32_t* frame_mp, int n_kf, const float* kf_key_angle,
+                                        const uint8_t* kf_mp_valid, const uint8_t* kf_mp_bad,
+                                        const uint8_t* already_found, const float* kf_mp_xyz,
+                                        const uint8_t* kf_mp_desc, const float* kf_mp_min_dist,
+                                        const float* kf_mp_max_dist, const int32_t* kf_mp_ids,
+                                        float th, int orb_dist, int32_t* nmatches) {
+    if (!frame_ok(cur) || !tcw_cur || !cam || !nmatches || n_kf < 0 || (cur->n && !frame_mp) ||
+        (n_kf && (!kf_key_angle || !kf_mp_valid || !kf_mp_bad || !already_found || !kf_mp_xyz ||
+                  !kf_mp_desc || !kf_mp_min_dist || !kf_mp_max_dist)))
+        return ORBFE_ERR_ARG;
+    return guarded(m, [&]() {
+        int st;
+        SbpKfArgs a;
+        if ((st = m->frame(cur, false, a.cur))) return st;
+        if ((st = m->up(m->m_u0, kf_mp_valid, n_kf))) return st;
+        if ((st = m->up(m->m_u1, kf_mp_bad, n_kf))) return st;
+        if ((st = m->up(m->o_u, already_found, n_kf))) return st;
+        if ((st = m->up(m->m_f0, kf_mp_xyz, (size_t)n_kf * 12))) return st;
+        if ((st = m->up(m->m_f1, kf_mp_min_dist, (size_t)n_kf * 4))) return st;
+        if ((st = m->up(m->m_f2, kf_mp_max_dist, (size_t)n_kf * 4))) return st;
+        if ((st = m->up(m->m_f3, kf_key_angle, (size_t)n_kf * 4))) return st;
+        if ((st = m->up(m->m_d, kf_mp_desc, (size_t)n_kf * 32))) return st;
+        if ((st = m->up(m->m_f4, cur->scale_factors, (size_t)cur->nlevels * 4))) return st;
+        if (kf_mp_ids && (st = m->up(m->o_i, kf_mp_ids, (size_t)n_kf * 4))) return st;
+        if ((st = m->scal.ensure(16))) return st;
+        ORBFE_HIP(hipMemsetAsync(m->scal.p, 0, 16, m->stream));
+        a.n = n_kf;
+        a.valid = m->m_u0.as<uint8_t>();
+        a.bad = m->m_u1.as<uint8_t>();
+        a.found = m->o_u.as<uint8_t>();
+        a.xyz = m->m_f0.as<float>();
+        a.mind = m->m_f1.as<float>();
+        a.maxd = m->m_f2.as<float>();
+        a.desc = m->m_d.as<uint4>();
+        std::memcpy(a.T, tcw_cur, sizeof(a.T));
+        camera_center(tcw_cur, a.ow);
+        a.fx = cam->fx;
+        a.fy = cam->fy;
+        a.cx = cam->cx;
+        a.cy = cam->cy;
+        a.minx = cur->min_x;
+        a.maxx = cur->max_x;
+        a.miny = cur->min_y;
+        a.maxy = cur->max_y;
+        a.scale = m->m_f4.as<float>();
+        a.nlevels = cur->nlevels;
+        a.log_scale = log_scale_factor;
+        a.th = th;
+        a.status = m->scal.as<int>() + 1;
+        int total = 0;
+        if ((st = m->csr(a, n_kf, sbp_kf_cand_kernel<false>, sbp_kf_cand_kernel<true>, total)))
+            return st;
+        int status = 0;  // csr() synchronized the stream after the count pass
+        ORBFE_HIP(hipMemcpy(&status, m->scal.as<int>() + 1, sizeof(int), hipMemcpyDeviceToHost));
+        if (status) return status;
+        // a slot already holding a map point blocks (1529-1530): fobs = 1 where fmp >= 0
+        const int N = cur->n;
+        std::vector<int32_t> fobs(N);
+        for (int k = 0; k < N; ++k) fobs[k] = frame_mp[k] >= 0 ? 1 : 0;
+        if ((st = m->up(m->s1, frame_mp, (size_t)N * 4))) return st;
+        if ((st = m->up(m->s2, fobs.data(), (size_t)N * 4))) return st;
+        if ((st = m->s3.ensure(std::max(N, 1) * sizeof(int)))) return st;
+        if ((st = m->s4.ensure(std::max(n_kf, 1) * sizeof(int2)))) return st;
+        // the rotation-bin angle of map point i is pKF->mvKeysUn[i].angle (1549)
+        if ((st = m->fb_k.ensure(std::max<size_t>(16, (size_t)n_kf * sizeof(orbfe_keypoint))))) return st;
+        std::vector<orbfe_keypoint> kk(n_kf);
+        for (int i = 0; i < n_kf; ++i) kk[i] = orbfe_keypoint{0.f, 0.f, 0.f, kf_key_angle[i], 0.f, 0, -1};
+        if ((st = m->up(m->fb_k, kk.data(), (size_t)n_kf * sizeof(orbfe_keypoint)))) return st;
+        SbpLastResolveArgs r;
+        r.n_last = n_kf;
+        r.nkp = N;
+        r.max_dist = orb_dist;
+        r.off = m->off.as<int>();
+        r.cand = m->cand.as<int2>();
+        r.nobs = nullptr;
+        r.ids = kf_mp_ids ? m->o_i.as<int>() : nullptr;
+        r.lk = m->fb_k.as<orbfe_keypoint>();
+        r.ck = a.cur.k;
+        r.check_ori = check_ori;
+        r.fmp = m->s1.as<int>();
+        r.fobs = m->s2.as<int>();
+        r.claim = m->s3.as<int>();
+        r.events = m->s4.as<int2>();
+        r.nmatches = m->scal.as<int>();
+        hipLaunchKernelGGL(sbp_last_resolve_kernel, dim3(1), dim3(64), 0, m->stream, r);
+        ORBFE_HIP(hipGetLastError());
+        if ((st = m->down(frame_mp, m->s1, (size_t)N * 4))) return st;
         if ((st = m->down(nmatches, m->scal, sizeof(int)))) return st;
         ORBFE_HIP(hipStreamSynchronize(m->stream));
         return ORBFE_OK;

@@ -35,7 +35,8 @@ EXPORTED = [
     "orbfe_matcher_create", "orbfe_matcher_destroy", "orbfe_matcher_set_stream",
     "orbfe_matcher_profile", "orbfe_matcher_profile_read", "orbfe_hamming",
     "orbfe_bf_match", "orbfe_bf_match_batch_device", "orbfe_search_for_initialization",
-    "orbfe_search_by_projection_local", "orbfe_search_by_projection_last", "orbfe_is_in_frustum",
+    "orbfe_search_by_projection_local", "orbfe_search_by_projection_last",
+    "orbfe_search_by_projection_keyframe", "orbfe_is_in_frustum",
 ]
 
 
@@ -417,6 +418,32 @@ class ORBmatcher:
             ptr(a[5]), ptr(a[6]), ptr(ids), ptr(a[7]), C.c_float(th), int(bMono),
             C.byref(nm)))
         return fmp, fobs, nm.value
+
+    def SearchByProjectionKeyFrame(self, cur: Frame, tcw_cur, cam: Camera, log_scale: float,
+                                   kf_angle, kf_valid, kf_bad, already_found, kf_xyz, kf_desc,
+                                   kf_min_dist, kf_max_dist, th: float, ORBdist: int,
+                                   frame_mp=None, kf_ids=None):
+        """Relocalisation overload SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th,
+        ORBdist) (ORBmatcher.cc:1475-1602).  Returns (frame_mp, nmatches)."""
+        fmp = (np.full(cur.n, -1, np.int32) if frame_mp is None
+               else np.ascontiguousarray(frame_mp, np.int32).copy())
+        a = [np.ascontiguousarray(tcw_cur, np.float32).reshape(12),
+             np.ascontiguousarray(kf_angle, np.float32),
+             np.ascontiguousarray(kf_valid, np.uint8),
+             np.ascontiguousarray(kf_bad, np.uint8),
+             np.ascontiguousarray(already_found, np.uint8),
+             np.ascontiguousarray(kf_xyz, np.float32).reshape(-1, 3),
+             np.ascontiguousarray(kf_desc, np.uint8).reshape(-1, 32),
+             np.ascontiguousarray(kf_min_dist, np.float32),
+             np.ascontiguousarray(kf_max_dist, np.float32)]
+        ids = None if kf_ids is None else np.ascontiguousarray(kf_ids, np.int32)
+        nm = C.c_int32(0)
+        cv = cur.view()
+        _check("orbfe_search_by_projection_keyframe", lib().orbfe_search_by_projection_keyframe(
+            self._h, int(self.mbCheckOrientation), C.byref(cv), ptr(a[0]), C.byref(cam),
+            C.c_float(log_scale), ptr(fmp), len(a[1]), *(ptr(x) for x in a[1:]), ptr(ids),
+            C.c_float(th), int(ORBdist), C.byref(nm)))
+        return fmp, nm.value
 
     def is_in_frustum(self, xyz, normal, min_dist, max_dist, tcw, cam: Camera, bounds,
                       log_scale: float, cos_limit: float = 0.5):

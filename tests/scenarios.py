@@ -131,3 +131,31 @@ def frustum_case(seed: int = 0, m: int = 20000):
 
 def random_desc(rng, n) -> np.ndarray:
     return rng.integers(0, 256, (n, 32), dtype=np.uint8)
+
+
+def sbp_keyframe_case(seed: int = 0, motion=(0.01, 0.03)):
+    """Relocalisation (Tracking.cc:1723/1737): a candidate keyframe whose keypoints hold map
+    points along their rays (keyframe pose = identity); the current frame sees the scene after
+    a small motion and already holds some map points (from SearchByBoW + PnP).  mfMaxDistance
+    = 0.97 * dist * scale[octave] keeps the predicted level inside the pyramid."""
+    rng = np.random.Generator(np.random.PCG64(seed + 21))
+    kf = extract_frame(seed, 1000)
+    cur = extract_frame(seed, 1000, shift=(1, 2))
+    n = kf.n
+    z = rng.uniform(2.0, 8.0, n)
+    xyz = np.stack([(kf.keys["x"] - CX) / FX * z, (kf.keys["y"] - CY) / FY * z, z], 1)
+    dist = np.linalg.norm(xyz, axis=1)
+    scale = np.float32(1.2) ** np.arange(8, dtype=np.float32)
+    maxd = (0.97 * dist * scale[kf.keys["octave"]]).astype(np.float32)
+    mind = (maxd / scale[7]).astype(np.float32)
+    valid = (rng.uniform(size=n) < 0.9).astype(np.uint8)
+    bad = (rng.uniform(size=n) < 0.03).astype(np.uint8)
+    found = (rng.uniform(size=n) < 0.2).astype(np.uint8)
+    desc = flip_bits(kf.desc, rng, 0.06)
+    frame_mp = np.where(rng.uniform(size=cur.n) < 0.15, rng.integers(0, 10_000, cur.n), -1)
+    return dict(cur=cur, tcw_cur=pose(rng, *motion), cam=camera(),
+                log_scale=float(np.log(np.float32(1.2)).astype(np.float32)),
+                frame_mp=frame_mp.astype(np.int32), kf_angle=kf.keys["angle"].astype(np.float32),
+                kf_valid=valid, kf_bad=bad, found=found, kf_xyz=xyz.astype(np.float32),
+                kf_desc=desc, kf_min=mind, kf_max=maxd,
+                kf_ids=(np.arange(n) + 20_000).astype(np.int32))
