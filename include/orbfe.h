@@ -332,6 +332,20 @@ int orbfe_search_by_projection_keyframe(orbfe_matcher* m, int check_ori,
                                         const float* kf_mp_max_dist, const int32_t* kf_mp_ids,
                                         float th, int orb_dist, int32_t* nmatches);
 
+/* MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:483-548) for n_mp map points at once
+ * (LocalMapping calls it for every new / fused point, LocalMapping.cc:268, 489).  The
+ * descriptors of map point i's observations in non-bad keyframes, in mObservations order, are
+ * rows obs_off[i] .. obs_off[i+1]-1 of obs_desc (obs_off has n_mp + 1 entries, < 65536
+ * observations per point).  best[i] = the chosen row relative to obs_off[i] (least median
+ * distance to the others, first on ties), -1 for a point without observations (mDescriptor
+ * untouched); desc_out (n_mp x 32, may be NULL) receives mDescriptor. */
+int orbfe_distinctive_descriptors(orbfe_matcher* m, int n_mp, const int32_t* obs_off,
+                                  const uint8_t* obs_desc, int32_t* best, uint8_t* desc_out);
+/* Device form of the same (asynchronous on the matcher's stream); d_desc_out may be NULL. */
+int orbfe_distinctive_descriptors_device(orbfe_matcher* m, int n_mp, const int32_t* d_obs_off,
+                                         const uint8_t* d_obs_desc, int32_t* d_best,
+                                         uint8_t* d_desc_out);
+
 /* Frame::isInFrustum (Frame.cc:387-443) + MapPoint::PredictScale (MapPoint.cc:633-642) over
  * m MapPoints: world pos (m x 3), normal (m x 3), mfMinDistance/mfMaxDistance.  Writes the
  * tracking scratch fields (mbTrackInView, mTrackProjX/Y/XR, mnTrackScaleLevel,

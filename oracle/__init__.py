@@ -295,6 +295,18 @@ def search_by_projection_keyframe(c: dict, th=10.0, orb_dist=100, check_ori=True
     return fmp, nm.value
 
 
+def distinctive_descriptors(obs_off: np.ndarray, obs_desc: np.ndarray):
+    """MapPoint::ComputeDistinctiveDescriptors over a CSR of observation descriptors."""
+    off = np.ascontiguousarray(obs_off, np.int32)
+    d = np.ascontiguousarray(obs_desc, np.uint8).reshape(-1, 32)
+    n = len(off) - 1
+    best = np.zeros(n, np.int32)
+    out = np.zeros((n, 32), np.uint8)
+    _check("oracle_distinctive_descriptors",
+           lib().oracle_distinctive_descriptors(n, ptr(off), ptr(d), ptr(best), ptr(out)))
+    return best, out
+
+
 def is_in_frustum(xyz, normal, min_dist, max_dist, tcw, cam: Camera, bounds, log_scale,
                   cos_limit=0.5):
     xyz = np.ascontiguousarray(xyz, np.float32).reshape(-1, 3)

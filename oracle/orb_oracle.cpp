@@ -1270,6 +1270,39 @@ int oracle_search_by_projection_keyframe(int check_ori, const orbfe_frame_view* 
     return ORBFE_OK;
 }
 
+// MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:483-548) for n_mp map points; the
+// observation descriptors of point i are rows obs_off[i] .. obs_off[i+1]-1.
+int oracle_distinctive_descriptors(int n_mp, const int32_t* obs_off, const uint8_t* obs_desc,
+                                   int32_t* best, uint8_t* desc_out) {
+    if (n_mp < 0 || (n_mp && (!obs_off || !best))) return ORBFE_ERR_ARG;
+    for (int i = 0; i < n_mp; ++i) {
+        const int o = obs_off[i];
+        const size_t N = (size_t)(obs_off[i + 1] - o);
+        best[i] = -1;
+        if (N == 0) continue;  // no observation: mDescriptor untouched (498-499, 510-511)
+        std::vector<float> dmat(N * N);
+        for (size_t a = 0; a < N; ++a) {
+            dmat[a * N + a] = 0;
+            for (size_t b = a + 1; b < N; ++b) {
+                const int d = descriptor_distance(obs_desc + 32 * (size_t)(o + a), obs_desc + 32 * (size_t)(o + b));
+                dmat[a * N + b] = (float)d;
+                dmat[b * N + a] = (float)d;
+            }
+        }
+        int best_median = INT_MAX, best_idx = 0;
+        std::vector<int> row(N);
+        for (size_t a = 0; a < N; ++a) {
+            for (size_t b = 0; b < N; ++b) row[b] = (int)dmat[a * N + b];
+            std::sort(row.begin(), row.end());
+            const int median = row[(size_t)(0.5 * (N - 1))];
+            if (median < best_median) { best_median = median; best_idx = (int)a; }
+        }
+        best[i] = best_idx;
+        if (desc_out) std::memcpy(desc_out + 32 * (size_t)i, obs_desc + 32 * (size_t)(o + best_idx), 32);
+    }
+    return ORBFE_OK;
+}
+
 // A17 — Frame::isInFrustum (Frame.cc:387-443) + MapPoint::PredictScale (MapPoint.cc:633-642).
 int oracle_is_in_frustum(int n, const float* xyz, const float* normal, const float* min_dist,
                          const float* max_dist, const float* tcw, const orbfe_camera* cam,

@@ -96,6 +96,8 @@ int oracle_search_by_projection_keyframe(int check_ori, const orbfe_frame_view* 
                                          const float* kf_mp_min_dist,
                                          const float* kf_mp_max_dist, const int32_t* kf_mp_ids,
                                          float th, int orb_dist, int32_t* nmatches);
+int oracle_distinctive_descriptors(int n_mp, const int32_t* obs_off, const uint8_t* obs_desc,
+                                   int32_t* best, uint8_t* desc_out);
 int oracle_is_in_frustum(int n, const float* xyz, const float* normal, const float* min_dist,
                          const float* max_dist, const float* tcw, const orbfe_camera* cam,
                          float min_x, float max_x, float min_y, float max_y,

@@ -700,6 +700,55 @@ __global__ __launch_bounds__(256) void sbp_kf_cand_kernel(SbpKfArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:483-548): one wave per map point.  Lane
+// i owns observation i (i = lane, lane + 64, ...); the median of its distance row
+// (sorted row[(size_t)(0.5 (N-1))], self distance 0 included) is the smallest v with
+// #{j : d(i, j) <= v} > (N-1)/2, found by bisection over v in [0, 256] with the row recomputed
+// from the descriptors (staged in LDS when N <= kDdStage).  The winner is the first i with the
+// smallest median: min over (median << 16 | i).
+constexpr int kDdBlock = 256;
+constexpr int kDdStage = 64;  // descriptors per wave staged in LDS
+__global__ __launch_bounds__(kDdBlock) void distinctive_kernel(int n_mp, const int* off,
+                                                               const uint4* desc, int* best,
+                                                               uint4* desc_out) {
+    __shared__ uint4 s_d[kDdBlock / 64][2 * kDdStage];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int mp = blockIdx.x * (kDdBlock / 64) + wid;
+    if (mp >= n_mp) return;
+    const int o = off[mp], N = off[mp + 1] - o;
+    if (N <= 0) {
+        if (lane == 0) best[mp] = -1;
+        return;
+    }
+    const uint4* d = desc + 2 * (size_t)o;
+    const bool staged = N <= kDdStage;
+    if (staged) {
+        for (int k = lane; k < 2 * N; k += 64) s_d[wid][k] = d[k];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    }
+    const uint4* src = staged ? s_d[wid] : d;
+    const int k = (int)(0.5 * (double)(N - 1));  // vDists[0.5*(N-1)]
+    uint32_t key = 0xffffffffu;
+    for (int i = lane; i < N; i += 64) {
+        const uint4 a0 = src[2 * i], a1 = src[2 * i + 1];
+        int lo = 0, hi = 256;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            int c = 0;
+            for (int j = 0; j < N; ++j) c += hamming256(a0, a1, src[2 * j], src[2 * j + 1]) <= mid;
+            if (c > k) hi = mid; else lo = mid + 1;
+        }
+        key = min(key, ((uint32_t)lo << 16) | (uint32_t)i);
+    }
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) key = min(key, (uint32_t)__shfl_xor((int)key, s, 64));
+    const int bi = (int)(key & 0xffff);
+    if (lane == 0) best[mp] = bi;
+    if (desc_out && lane < 2) desc_out[2 * (size_t)mp + lane] = d[2 * bi + lane];
+}
+
+// ---------------------------------------------------------------------------------------------
 // Frame::isInFrustum (Frame.cc:387-443) with MapPoint::PredictScale (MapPoint.cc:633-642).
 struct FrustumArgs {
     int n;

@@ -546,6 +546,46 @@ int orbfe_search_by_projection_keyframe(orbfe_matcher* m, int check_ori,
     });
 }
 
+int orbfe_distinctive_descriptors_device(orbfe_matcher* m, int n_mp, const int32_t* d_obs_off,
+                                         const uint8_t* d_obs_desc, int32_t* d_best,
+                                         uint8_t* d_desc_out) {
+    if (n_mp < 0 || (n_mp && (!d_obs_off || !d_obs_desc || !d_best))) return ORBFE_ERR_ARG;
+    return guarded(m, [&]() {
+        if (n_mp == 0) return ORBFE_OK;
+        hipLaunchKernelGGL(distinctive_kernel, dim3((n_mp + 3) / 4), dim3(kDdBlock), 0, m->stream,
+                           n_mp, d_obs_off, reinterpret_cast<const uint4*>(d_obs_desc), d_best,
+                           reinterpret_cast<uint4*>(d_desc_out));
+        ORBFE_HIP(hipGetLastError());
+        return ORBFE_OK;
+    });
+}
+
+int orbfe_distinctive_descriptors(orbfe_matcher* m, int n_mp, const int32_t* obs_off,
+                                  const uint8_t* obs_desc, int32_t* best, uint8_t* desc_out) {
+    if (n_mp < 0 || (n_mp && (!obs_off || !best))) return ORBFE_ERR_ARG;
+    if (n_mp == 0) return m ? ORBFE_OK : ORBFE_ERR_ARG;
+    if (obs_off[0] < 0) return ORBFE_ERR_ARG;
+    for (int i = 0; i < n_mp; ++i)
+        if (obs_off[i + 1] < obs_off[i] || obs_off[i + 1] - obs_off[i] >= 65536) return ORBFE_ERR_ARG;
+    const size_t nobs = (size_t)obs_off[n_mp];
+    if (nobs && !obs_desc) return ORBFE_ERR_ARG;
+    return guarded(m, [&]() {
+        int st;
+        if ((st = m->up(m->o_i, obs_off, (size_t)(n_mp + 1) * 4))) return st;
+        if ((st = m->up(m->m_d, obs_desc, nobs * 32))) return st;
+        if ((st = m->s1.ensure((size_t)n_mp * 4))) return st;
+        if ((st = m->q.ensure((size_t)n_mp * 32))) return st;
+        hipLaunchKernelGGL(distinctive_kernel, dim3((n_mp + 3) / 4), dim3(kDdBlock), 0, m->stream,
+                           n_mp, m->o_i.as<int>(), m->m_d.as<uint4>(), m->s1.as<int>(),
+                           desc_out ? m->q.as<uint4>() : nullptr);
+        ORBFE_HIP(hipGetLastError());
+        if ((st = m->down(best, m->s1, (size_t)n_mp * 4))) return st;
+        if (desc_out && (st = m->down(desc_out, m->q, (size_t)n_mp * 32))) return st;
+        ORBFE_HIP(hipStreamSynchronize(m->stream));
+        return ORBFE_OK;
+    });
+}
+
 int orbfe_is_in_frustum(orbfe_matcher* m, int n, const float* xyz, const float* normal,
                         const float* min_dist, const float* max_dist, const float* tcw,
                         const orbfe_camera* cam, float min_x, float max_x, float min_y,

@@ -36,7 +36,8 @@ EXPORTED = [
     "orbfe_matcher_profile", "orbfe_matcher_profile_read", "orbfe_hamming",
     "orbfe_bf_match", "orbfe_bf_match_batch_device", "orbfe_search_for_initialization",
     "orbfe_search_by_projection_local", "orbfe_search_by_projection_last",
-    "orbfe_search_by_projection_keyframe", "orbfe_is_in_frustum",
+    "orbfe_search_by_projection_keyframe", "orbfe_distinctive_descriptors",
+    "orbfe_distinctive_descriptors_device", "orbfe_is_in_frustum",
 ]
 
 
@@ -444,6 +445,18 @@ class ORBmatcher:
             C.c_float(log_scale), ptr(fmp), len(a[1]), *(ptr(x) for x in a[1:]), ptr(ids),
             C.c_float(th), int(ORBdist), C.byref(nm)))
         return fmp, nm.value
+
+    def ComputeDistinctiveDescriptors(self, obs_off: np.ndarray, obs_desc: np.ndarray):
+        """MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:483-548) over a CSR of the
+        points' observation descriptors -> (best row per point or -1, mDescriptor (n, 32))."""
+        off = np.ascontiguousarray(obs_off, np.int32)
+        d = np.ascontiguousarray(obs_desc, np.uint8).reshape(-1, 32)
+        n = len(off) - 1
+        best = np.zeros(n, np.int32)
+        out = np.zeros((n, 32), np.uint8)
+        _check("orbfe_distinctive_descriptors", lib().orbfe_distinctive_descriptors(
+            self._h, n, ptr(off), ptr(d), ptr(best), ptr(out)))
+        return best, out
 
     def is_in_frustum(self, xyz, normal, min_dist, max_dist, tcw, cam: Camera, bounds,
                       log_scale: float, cos_limit: float = 0.5):
