@@ -4,4 +4,5 @@
 #include "orbfe_stereo.hip"
 #include "orbfe_api.hip"
 #include "orbfe_match.hip"
+#include "orbfe_greedy.hip"
 #include "orbfe_match_api.hip"

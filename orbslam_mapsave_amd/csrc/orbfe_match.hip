@@ -7,10 +7,12 @@
 //   grid_kernel          Frame::AssignFeaturesToGrid (Frame.cc:341-356) as a CSR
 //   *_cand_kernel        GetFeaturesInArea (Frame.cc:445-498) + distances for every query in
 //                        parallel (counts, scan, fill)
-//   *_resolve_kernel     the reference's sequential greedy semantics (H7): one wave decides 64
-//                        consecutive queries against the committed state, commits the prefix
-//                        that no earlier lane of the chunk can have influenced, and resumes at
-//                        the first conflicting lane.  Bit-identical to the in-order loop.
+//   sfi_resolve_kernel   SearchForInitialization's sequential greedy semantics (H7): one wave
+//                        decides 64 consecutive queries against the committed state, commits
+//                        the prefix no earlier lane of the chunk can have influenced, and
+//                        resumes at the first conflicting lane.  Bit-identical to the loop.
+//   (the SearchByProjection overloads resolve in orbfe_greedy.hip: parallel Jacobi rounds
+//    to the unique fixed point of the in-order loop)
 //   frustum_kernel       Frame::isInFrustum (387-443) + MapPoint::PredictScale (MapPoint.cc:633)
 #include <hip/hip_runtime.h>
 
@@ -426,65 +428,6 @@ __global__ __launch_bounds__(256) void sbp_local_cand_kernel(SbpLocalArgs a) {
     if (!FILL) a.cnt[i] = n;
 }
 
-struct SbpLocalResolveArgs {
-    int m, nkp;
-    const int* off;
-    const int2* cand;
-    const int* nobs;
-    const int* ids;      // NULL: index
-    float nnratio;
-    int* fmp;            // nkp inout
-    int* fobs;           // nkp inout
-    int* claim;          // nkp scratch
-    int* nmatches;
-};
-
-__global__ __launch_bounds__(64) void sbp_local_resolve_kernel(SbpLocalResolveArgs a) {
-    const int lane = lane_id();
-    for (int i = lane; i < a.nkp; i += 64) a.claim[i] = 64;
-    __syncthreads();
-    int nm = 0;
-    for (int base = 0; base < a.m;) {
-        const int i = base + lane;
-        const bool valid = i < a.m;
-        const int e0 = valid ? a.off[i] : 0, e1 = valid ? a.off[i + 1] : 0;
-        int best = 256, bl = -1, second = 256, sl = -1, bi = -1;
-        for (int e = e0; e < e1; ++e) {
-            const int2 c = a.cand[e];
-            if (a.fmp[c.x] >= 0 && a.fobs[c.x] > 0) continue;  // already observed (87-89)
-            const int d = c.y & 0xffff, lv = c.y >> 16;
-            if (d < best) { second = best; best = d; sl = bl; bl = lv; bi = c.x; }
-            else if (d < second) { sl = lv; second = d; }
-        }
-        bool acc = valid && best <= kThHigh;
-        if (acc && bl == sl && best > a.nnratio * second) acc = false;  // ratio, same level only
-        const int nobs = acc ? a.nobs[i] : 0;
-        if (acc && nobs > 0) atomicMin(&a.claim[bi], lane);
-        __syncthreads();
-        bool conf = false;
-        for (int e = e0; e < e1 && !conf; ++e) {
-            const int idx = a.cand[e].x;
-            conf = a.claim[idx] < lane && !(a.fmp[idx] >= 0 && a.fobs[idx] > 0);
-        }
-        const int stop = first_lane(conf);
-        const bool commit = acc && lane < stop;
-        __syncthreads();
-        if (commit) atomicMax(&a.claim[bi], 1000 + lane);  // last committed writer wins
-        __syncthreads();
-        if (commit && a.claim[bi] == 1000 + lane) {
-            a.fmp[bi] = a.ids ? a.ids[i] : i;
-            a.fobs[bi] = nobs;
-        }
-        nm += commit;
-        __syncthreads();
-        if (acc) a.claim[bi] = 64;
-        __syncthreads();
-        base += stop;
-    }
-    nm = wave_sum(nm);
-    if (lane == 0) *a.nmatches = nm;
-}
-
 // ---------------------------------------------------------------------------------------------
 // SearchByProjection(Frame& Cur, const Frame& Last, th, bMono) (ORBmatcher.cc:1331-1473)
 struct SbpLastArgs {
@@ -543,95 +486,11 @@ __global__ __launch_bounds__(256) void sbp_last_cand_kernel(SbpLastArgs a) {
     if (!FILL) a.cnt[i] = n;
 }
 
-struct SbpLastResolveArgs {
-    int n_last, nkp;
-    int max_dist;      // accept best <= max_dist: TH_HIGH (1411) or ORBdist (1545)
-    const int* off;
-    const int2* cand;
-    const int* nobs;
-    const int* ids;
-    const orbfe_keypoint* lk;
-    const orbfe_keypoint* ck;
-    int check_ori;
-    int* fmp;
-    int* fobs;
-    int* claim;
-    int2* events;   // (i2, bin) in acceptance order, capacity n_last
-    int* nmatches;
-};
-
-__global__ __launch_bounds__(64) void sbp_last_resolve_kernel(SbpLastResolveArgs a) {
-    __shared__ int hist[kHistLen];
-    const int lane = lane_id();
-    for (int i = lane; i < a.nkp; i += 64) a.claim[i] = 64;
-    if (lane < kHistLen) hist[lane] = 0;
-    __syncthreads();
-    int nev = 0;
-    for (int base = 0; base < a.n_last;) {
-        const int i = base + lane;
-        const bool valid = i < a.n_last;
-        const int e0 = valid ? a.off[i] : 0, e1 = valid ? a.off[i + 1] : 0;
-        int best = 256, bi = -1;
-        for (int e = e0; e < e1; ++e) {
-            const int2 c = a.cand[e];
-            if (a.fmp[c.x] >= 0 && a.fobs[c.x] > 0) continue;  // 1406-1408
-            if (c.y < best) { best = c.y; bi = c.x; }
-        }
-        const bool acc = valid && best <= a.max_dist;
-        const int nobs = acc ? (a.nobs ? a.nobs[i] : 1) : 0;
-        if (acc && nobs > 0) atomicMin(&a.claim[bi], lane);
-        __syncthreads();
-        bool conf = false;
-        for (int e = e0; e < e1 && !conf; ++e) {
-            const int idx = a.cand[e].x;
-            conf = a.claim[idx] < lane && !(a.fmp[idx] >= 0 && a.fobs[idx] > 0);
-        }
-        const int stop = first_lane(conf);
-        const bool commit = acc && lane < stop;
-        __syncthreads();
-        if (commit) atomicMax(&a.claim[bi], 1000 + lane);
-        __syncthreads();
-        if (commit && a.claim[bi] == 1000 + lane) {
-            a.fmp[bi] = a.ids ? a.ids[i] : i;
-            a.fobs[bi] = nobs;
-        }
-        const unsigned long long cm = __ballot(commit);
-        if (commit) {
-            const int slot = nev + __popcll(cm & ((1ull << lane) - 1));
-            const int bin = a.check_ori ? rot_bin(a.lk[i].angle, a.ck[bi].angle) : 0;
-            a.events[slot] = make_int2(bi, bin);
-            if (a.check_ori) atomicAdd(&hist[bin], 1);
-        }
-        nev += __popcll(cm);
-        __syncthreads();
-        if (acc) a.claim[bi] = 64;
-        __syncthreads();
-        base += stop;
-    }
-    int nm = nev;
-    if (a.check_ori) {  // 1451-1470: every event in a non-top bin clears its keypoint
-        int t1, t2, t3;
-        three_maxima(hist, t1, t2, t3);
-        int removed = 0;
-        for (int e = lane; e < nev; e += 64) {
-            const int2 ev = a.events[e];
-            if (ev.y != t1 && ev.y != t2 && ev.y != t3) {
-                a.fmp[ev.x] = -1;
-                a.fobs[ev.x] = 0;
-                ++removed;
-            }
-        }
-        nm -= wave_sum(removed);
-    }
-    if (lane == 0) *a.nmatches = nm;
-}
-
 // ---------------------------------------------------------------------------------------------
 // Relocalisation SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th, ORBdist)
 // (ORBmatcher.cc:1475-1602): candidates of every keyframe map point in parallel; the greedy
-// assignment (a slot taken by an earlier map point blocks later ones, 1529-1530) is
-// sbp_last_resolve_kernel with every map point counted as observed (nobs = 1) and
-// max_dist = ORBdist.
+// assignment (a slot taken by an earlier map point blocks later ones, 1529-1530) is resolved
+// by orbfe_greedy.hip with every held point blocking and max_dist = ORBdist.
 struct SbpKfArgs {
     DevFrame cur;
     int n;

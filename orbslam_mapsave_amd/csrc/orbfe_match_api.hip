@@ -23,13 +23,16 @@ struct orbfe_matcher {
     DevBuf m_f0, m_f1, m_f2, m_f3, m_f4, m_u0, m_u1, m_i0, m_i1, m_d;  // per-map-point inputs
     DevBuf o_u, o_f0, o_f1, o_f2, o_f3, o_i;        // frustum outputs
     DevBuf scal;
+    DevBuf g_t0, g_t1, g_t2, g_dec, g_chg, g_last, g_bins, g_hist;  // greedy resolver
     Profiler prof;
+    int last_rounds = 0;  // rounds the most recent greedy resolution took (diagnostics)
 
     ~orbfe_matcher() {
         for (DevBuf* b : {&fa_k, &fa_d, &fa_ur, &fa_cs, &fa_ci, &fa_co, &fb_k, &fb_d, &fb_ur,
                           &fb_cs, &fb_ci, &fb_co, &q, &r, &nq, &nr, &out, &cnt, &off, &cand, &s1,
                           &s2, &s3, &s4, &s5, &m_f0, &m_f1, &m_f2, &m_f3, &m_f4, &m_u0, &m_u1,
-                          &m_i0, &m_i1, &m_d, &o_u, &o_f0, &o_f1, &o_f2, &o_f3, &o_i, &scal})
+                          &m_i0, &m_i1, &m_d, &o_u, &o_f0, &o_f1, &o_f2, &o_f3, &o_i, &scal,
+                          &g_t0, &g_t1, &g_t2, &g_dec, &g_chg, &g_last, &g_bins, &g_hist})
             b->release();
         prof.release();
         if (own) hipStreamDestroy(own);
@@ -96,6 +99,56 @@ struct orbfe_matcher {
         if ((st = cand.ensure(std::max(total, 1) * sizeof(int2)))) return st;
         a.cand = cand.as<int2>();
         hipLaunchKernelGGL(fk, dim3(blocks), dim3(256), 0, stream, a);
+        ORBFE_HIP(hipGetLastError());
+        return ORBFE_OK;
+    }
+
+    // Exact parallel resolution of the greedy assignment (orbfe_greedy.hip).  `g` carries the
+    // problem (m points, nkp slots, CSR candidates, decision mode, slot arrays fmp/fobs that
+    // hold the state before the call and receive the result); the scratch is owned here.
+    int greedy(GreedyArgs& g) {
+        int st;
+        const int M = g.m, N = g.nkp;
+        if ((st = g_t0.ensure(std::max(N, 1) * sizeof(int)))) return st;
+        if ((st = g_t1.ensure(std::max(N, 1) * sizeof(int)))) return st;
+        if ((st = g_t2.ensure(std::max(N, 1) * sizeof(int)))) return st;
+        if ((st = g_last.ensure(std::max(N, 1) * sizeof(int)))) return st;
+        if ((st = g_dec.ensure(std::max(M, 1) * sizeof(int)))) return st;
+        if ((st = g_bins.ensure(std::max(M, 1) * sizeof(int)))) return st;
+        if ((st = g_chg.ensure((size_t)(M + 2) * sizeof(int)))) return st;
+        if ((st = g_hist.ensure(32 * sizeof(int)))) return st;
+        if ((st = scal.ensure(16))) return st;
+        g.T[0] = g_t0.as<int>();
+        g.T[1] = g_t1.as<int>();
+        g.T[2] = g_t2.as<int>();
+        g.dec = g_dec.as<int>();
+        g.chg = g_chg.as<int>();
+        g.last = g_last.as<int>();
+        g.bins = g_bins.as<int>();
+        g.hist = g_hist.as<int>();
+        g.nm = scal.as<int>();
+        const int blocks = std::max(1, (std::max(std::max(M, N), 32) + kGreedyBlock - 1) / kGreedyBlock);
+        const int mblocks = std::max(1, (M + kGreedyBlock - 1) / kGreedyBlock);
+        const int nblocks = std::max(1, (N + kGreedyBlock - 1) / kGreedyBlock);
+        ORBFE_HIP(hipMemsetAsync(g.chg, 0, (size_t)(M + 2) * sizeof(int), stream));
+        hipLaunchKernelGGL(greedy_init_kernel, dim3(blocks), dim3(kGreedyBlock), 0, stream, g);
+        // rounds in batches; a round after a change-free round exits at once
+        int r = 0, batch = 4;
+        while (true) {
+            for (int b = 0; b < batch && r <= M; ++b, ++r)
+                hipLaunchKernelGGL(greedy_round_kernel, dim3(blocks), dim3(kGreedyBlock), 0, stream, g, r);
+            int c = 0;
+            ORBFE_HIP(hipMemcpyAsync(&c, g.chg + (r - 1), sizeof(int), hipMemcpyDeviceToHost, stream));
+            ORBFE_HIP(hipStreamSynchronize(stream));
+            if (c == 0) break;
+            if (r > M) return ORBFE_ERR_HIP;  // cannot happen: the correct prefix grows every round
+            batch = std::min(batch * 2, 64);
+        }
+        last_rounds = r;
+        hipLaunchKernelGGL(greedy_accept_kernel, dim3(mblocks), dim3(kGreedyBlock), 0, stream, g);
+        hipLaunchKernelGGL(greedy_slots_kernel, dim3(nblocks), dim3(kGreedyBlock), 0, stream, g);
+        if (g.check_ori)
+            hipLaunchKernelGGL(greedy_ori_kernel, dim3(mblocks), dim3(kGreedyBlock), 0, stream, g);
         ORBFE_HIP(hipGetLastError());
         return ORBFE_OK;
     }
@@ -339,20 +392,18 @@ int orbfe_search_by_projection_local(orbfe_matcher* m, float nnratio,
         if ((st = m->up(m->s2, frame_mp_obs, (size_t)N * 4))) return st;
         if ((st = m->s3.ensure(std::max(N, 1) * sizeof(int)))) return st;
         if ((st = m->scal.ensure(16))) return st;
-        SbpLocalResolveArgs r;
-        r.m = M;
-        r.nkp = N;
-        r.off = m->off.as<int>();
-        r.cand = m->cand.as<int2>();
-        r.nobs = m->m_i1.as<int>();
-        r.ids = mp_ids ? m->o_i.as<int>() : nullptr;
-        r.nnratio = nnratio;
-        r.fmp = m->s1.as<int>();
-        r.fobs = m->s2.as<int>();
-        r.claim = m->s3.as<int>();
-        r.nmatches = m->scal.as<int>();
-        hipLaunchKernelGGL(sbp_local_resolve_kernel, dim3(1), dim3(64), 0, m->stream, r);
-        ORBFE_HIP(hipGetLastError());
+        GreedyArgs g{};
+        g.m = M;
+        g.nkp = N;
+        g.mode = kGreedyLocal;
+        g.nnratio = nnratio;
+        g.off = m->off.as<int>();
+        g.cand = m->cand.as<int2>();
+        g.nobs = m->m_i1.as<int>();
+        g.fmp0 = g.fmp = m->s1.as<int>();
+        g.fobs0 = g.fobs = m->s2.as<int>();
+        g.ids = mp_ids ? m->o_i.as<int>() : nullptr;
+        if ((st = m->greedy(g))) return st;
         if ((st = m->down(frame_mp, m->s1, (size_t)N * 4))) return st;
         if ((st = m->down(frame_mp_obs, m->s2, (size_t)N * 4))) return st;
         if ((st = m->down(nmatches, m->scal, sizeof(int)))) return st;
@@ -424,24 +475,25 @@ int orbfe_search_by_projection_last(orbfe_matcher* m, int check_ori,
         if ((st = m->s3.ensure(std::max(N, 1) * sizeof(int)))) return st;
         if ((st = m->s4.ensure(std::max(n_last, 1) * sizeof(int2)))) return st;
         if ((st = m->scal.ensure(16))) return st;
-        SbpLastResolveArgs r;
-        r.n_last = n_last;
-        r.nkp = N;
-        r.max_dist = kThHigh;
-        r.off = m->off.as<int>();
-        r.cand = m->cand.as<int2>();
-        r.nobs = m->m_i1.as<int>();
-        r.ids = last_mp_ids ? m->o_i.as<int>() : nullptr;
-        r.lk = a.lk;
-        r.ck = a.cur.k;
-        r.check_ori = check_ori;
-        r.fmp = m->s1.as<int>();
-        r.fobs = m->s2.as<int>();
-        r.claim = m->s3.as<int>();
-        r.events = m->s4.as<int2>();
-        r.nmatches = m->scal.as<int>();
-        hipLaunchKernelGGL(sbp_last_resolve_kernel, dim3(1), dim3(64), 0, m->stream, r);
-        ORBFE_HIP(hipGetLastError());
+        if ((st = m->o_f3.ensure(std::max<size_t>(16, (size_t)n_last * 4)))) return st;
+        std::vector<float> qa(n_last);
+        for (int i = 0; i < n_last; ++i) qa[i] = last_keys[i].angle;
+        if ((st = m->up(m->o_f3, qa.data(), (size_t)n_last * 4))) return st;
+        GreedyArgs g{};
+        g.m = n_last;
+        g.nkp = N;
+        g.mode = kGreedyMaxD;
+        g.max_dist = kThHigh;
+        g.off = m->off.as<int>();
+        g.cand = m->cand.as<int2>();
+        g.nobs = m->m_i1.as<int>();
+        g.fmp0 = g.fmp = m->s1.as<int>();
+        g.fobs0 = g.fobs = m->s2.as<int>();
+        g.check_ori = check_ori;
+        g.q_angle = m->o_f3.as<float>();
+        g.k = a.cur.k;
+        g.ids = last_mp_ids ? m->o_i.as<int>() : nullptr;
+        if ((st = m->greedy(g))) return st;
         if ((st = m->down(frame_mp, m->s1, (size_t)N * 4))) return st;
         if ((st = m->down(frame_mp_obs, m->s2, (size_t)N * 4))) return st;
         if ((st = m->down(nmatches, m->scal, sizeof(int)))) return st;
@@ -508,37 +560,24 @@ int orbfe_search_by_projection_keyframe(orbfe_matcher* m, int check_ori,
         int status = 0;  // csr() synchronized the stream after the count pass
         ORBFE_HIP(hipMemcpy(&status, m->scal.as<int>() + 1, sizeof(int), hipMemcpyDeviceToHost));
         if (status) return status;
-        // a slot already holding a map point blocks (1529-1530): fobs = 1 where fmp >= 0
+        // a slot already holding a map point blocks (1529-1530), whatever its observations
         const int N = cur->n;
-        std::vector<int32_t> fobs(N);
-        for (int k = 0; k < N; ++k) fobs[k] = frame_mp[k] >= 0 ? 1 : 0;
         if ((st = m->up(m->s1, frame_mp, (size_t)N * 4))) return st;
-        if ((st = m->up(m->s2, fobs.data(), (size_t)N * 4))) return st;
-        if ((st = m->s3.ensure(std::max(N, 1) * sizeof(int)))) return st;
-        if ((st = m->s4.ensure(std::max(n_kf, 1) * sizeof(int2)))) return st;
-        // the rotation-bin angle of map point i is pKF->mvKeysUn[i].angle (1549)
-        if ((st = m->fb_k.ensure(std::max<size_t>(16, (size_t)n_kf * sizeof(orbfe_keypoint))))) return st;
-        std::vector<orbfe_keypoint> kk(n_kf);
-        for (int i = 0; i < n_kf; ++i) kk[i] = orbfe_keypoint{0.f, 0.f, 0.f, kf_key_angle[i], 0.f, 0, -1};
-        if ((st = m->up(m->fb_k, kk.data(), (size_t)n_kf * sizeof(orbfe_keypoint)))) return st;
-        SbpLastResolveArgs r;
-        r.n_last = n_kf;
-        r.nkp = N;
-        r.max_dist = orb_dist;
-        r.off = m->off.as<int>();
-        r.cand = m->cand.as<int2>();
-        r.nobs = nullptr;
-        r.ids = kf_mp_ids ? m->o_i.as<int>() : nullptr;
-        r.lk = m->fb_k.as<orbfe_keypoint>();
-        r.ck = a.cur.k;
-        r.check_ori = check_ori;
-        r.fmp = m->s1.as<int>();
-        r.fobs = m->s2.as<int>();
-        r.claim = m->s3.as<int>();
-        r.events = m->s4.as<int2>();
-        r.nmatches = m->scal.as<int>();
-        hipLaunchKernelGGL(sbp_last_resolve_kernel, dim3(1), dim3(64), 0, m->stream, r);
-        ORBFE_HIP(hipGetLastError());
+        GreedyArgs g{};
+        g.m = n_kf;
+        g.nkp = N;
+        g.mode = kGreedyMaxD;
+        g.max_dist = orb_dist;
+        g.off = m->off.as<int>();
+        g.cand = m->cand.as<int2>();
+        g.nobs = nullptr;
+        g.fmp0 = g.fmp = m->s1.as<int>();
+        g.fobs0 = g.fobs = nullptr;
+        g.check_ori = check_ori;
+        g.q_angle = m->m_f3.as<float>();  // pKF->mvKeysUn[i].angle (1549)
+        g.k = a.cur.k;
+        g.ids = kf_mp_ids ? m->o_i.as<int>() : nullptr;
+        if ((st = m->greedy(g))) return st;
         if ((st = m->down(frame_mp, m->s1, (size_t)N * 4))) return st;
         if ((st = m->down(nmatches, m->scal, sizeof(int)))) return st;
         ORBFE_HIP(hipStreamSynchronize(m->stream));
