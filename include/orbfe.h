@@ -311,6 +311,30 @@ int orbfe_search_by_projection_last(orbfe_matcher* m, int check_ori,
                                     const float* tcw_last, float th, int mono,
                                     int32_t* nmatches);
 
+/* Tracking::SearchLocalPoints (Tracking.cc:1403-1455) on device-resident data: for every local
+ * map point that is neither bad (d_bad) nor already matched in the frame (d_skip[i] != 0 <=>
+ * mnLastFrameSeen == mCurrentFrame.mnId), Frame::isInFrustum(pMP, viewing_cos_limit) with
+ * MapPoint::PredictScale (Frame.cc:387-443, MapPoint.cc:633-642), then
+ * ORBmatcher(nnratio).SearchByProjection(F, vpLocalMapPoints, th) (ORBmatcher.cc:45-129).
+ * `frame` is a view whose keys_un / desc / u_right are DEVICE pointers (scale_factors stays a
+ * host table).  Map-point arrays (xyz, normal n x 3; mfMinDistance / mfMaxDistance; descriptor
+ * n x 32; Observations(); ids or NULL) are device arrays.  d_in_view receives mbTrackInView
+ * (0 for skipped or bad points); d_frame_mp / d_frame_mp_obs are updated in place.
+ * counts[0] = nmatches, counts[1] = nToMatch (host).  A predicted level outside the pyramid
+ * returns ORBFE_ERR_UNSUPPORTED (such points are not matched).  Synchronous on return. */
+int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* frame,
+                                     const float* tcw, const orbfe_camera* cam,
+                                     float log_scale_factor, float viewing_cos_limit, int n_mp,
+                                     const float* d_xyz, const float* d_normal,
+                                     const float* d_min_dist, const float* d_max_dist,
+                                     const uint8_t* d_desc, const int32_t* d_nobs,
+                                     const uint8_t* d_bad, const uint8_t* d_skip,
+                                     const int32_t* d_mp_ids, float nnratio, float th,
+                                     int32_t* d_frame_mp, int32_t* d_frame_mp_obs,
+                                     uint8_t* d_in_view, int32_t* counts);
+/* Jacobi rounds the most recent SearchByProjection resolution took (diagnostics). */
+int orbfe_matcher_last_rounds(const orbfe_matcher* m);
+
 /* Relocalisation ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF,
  * const set<MapPoint*>& sAlreadyFound, th, ORBdist) (ORBmatcher.cc:1475-1602), called by
  * Tracking::Relocalization with ORBmatcher(0.9, true), th/ORBdist = 10/100 and 3/64

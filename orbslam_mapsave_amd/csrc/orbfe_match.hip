@@ -393,6 +393,8 @@ struct SbpLocalArgs {
     SbpMps mp;
     const float* scale;  // per level
     float th;
+    int nlevels;         // levels of `scale`; a predicted level outside is UB in the reference
+    int* status;         // NULL, or set to ORBFE_ERR_UNSUPPORTED for such a point
     int* cnt;
     const int* off;
     int2* cand;          // (idx, dist | octave << 16)
@@ -407,6 +409,11 @@ __global__ __launch_bounds__(256) void sbp_local_cand_kernel(SbpLocalArgs a) {
         return;
     }
     const int pl = a.mp.lvl[i];
+    if (pl < 0 || pl >= a.nlevels) {  // F.mvScaleFactors[nPredictedLevel] out of range
+        if (a.status) atomicExch(a.status, ORBFE_ERR_UNSUPPORTED);
+        if (!FILL) a.cnt[i] = 0;
+        return;
+    }
     float r = a.mp.vcos[i] > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos (131-137)
     if (a.th != 1.0) r *= a.th;
     const float rs = r * a.scale[pl];
@@ -625,31 +632,36 @@ struct FrustumArgs {
     float* pxr;
     int* lvl;
     float* vcos;
+    // Tracking::SearchLocalPoints (Tracking.cc:1403-1438): points already matched in the frame
+    // (skip) get mbTrackInView = false, bad points are not projected; in-view points are
+    // counted (nToMatch).  All NULL for the plain isInFrustum entry point.
+    const uint8_t* skip;
+    const uint8_t* bad;
+    int* n_in_view;
 };
 
-__global__ __launch_bounds__(256) void frustum_kernel(FrustumArgs a) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= a.n) return;
-    a.in_view[i] = 0;
+__device__ __forceinline__ bool frustum_point(const FrustumArgs& a, int i) {
+    a.in_view[i] = 0;  // isInFrustum starts with mbTrackInView = false (Frame.cc:389)
+    if ((a.skip && a.skip[i]) || (a.bad && a.bad[i])) return false;
     const float* P = a.xyz + 3 * i;
     float pc[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r)
         pc[r] = ((a.T[4 * r] * P[0] + a.T[4 * r + 1] * P[1]) + a.T[4 * r + 2] * P[2]) + a.T[4 * r + 3];
-    if (pc[2] < 0.0f) return;
+    if (pc[2] < 0.0f) return false;
     const float invz = 1.0f / pc[2];
     const float u = a.fx * pc[0] * invz + a.cx;
     const float v = a.fy * pc[1] * invz + a.cy;
-    if (u < a.minx || u > a.maxx) return;
-    if (v < a.miny || v > a.maxy) return;
+    if (u < a.minx || u > a.maxx) return false;
+    if (v < a.miny || v > a.maxy) return false;
     const float dmax = 1.2f * a.maxd[i], dmin = 0.8f * a.mind[i];
     const float po0 = P[0] - a.ow[0], po1 = P[1] - a.ow[1], po2 = P[2] - a.ow[2];
     const float dist = (float)sqrt((double)po0 * po0 + (double)po1 * po1 + (double)po2 * po2);
-    if (dist < dmin || dist > dmax) return;
+    if (dist < dmin || dist > dmax) return false;
     const float* nv = a.normal + 3 * i;
     const double dot = (double)po0 * nv[0] + (double)po1 * nv[1] + (double)po2 * nv[2];
     const float vc = (float)(dot / dist);
-    if (vc < a.cos_limit) return;
+    if (vc < a.cos_limit) return false;
     const float ratio = a.maxd[i] / dist;
     const int lvl = (int)ceilf((float)log((double)ratio) / a.log_scale);
     a.in_view[i] = 1;
@@ -658,6 +670,17 @@ __global__ __launch_bounds__(256) void frustum_kernel(FrustumArgs a) {
     a.py[i] = v;
     a.lvl[i] = lvl;
     a.vcos[i] = vc;
+    return true;
+}
+
+__global__ __launch_bounds__(256) void frustum_kernel(FrustumArgs a) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    bool in = false;
+    if (i < a.n) in = frustum_point(a, i);
+    if (a.n_in_view) {
+        const unsigned long long b = __ballot(in);
+        if ((threadIdx.x & 63) == 0 && b) atomicAdd(a.n_in_view, __popcll(b));
+    }
 }
 
 }  // namespace orbfe

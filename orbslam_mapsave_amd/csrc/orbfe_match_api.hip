@@ -83,6 +83,31 @@ struct orbfe_matcher {
         return ORBFE_OK;
     }
 
+    // Device-resident frame view (keys_un / desc / u_right are device pointers): builds the grid.
+    int frame_device(const orbfe_frame_view* v, DevFrame& F) {
+        const int n = v->n;
+        int st;
+        if ((st = fa_cs.ensure((kGridCells + 1) * sizeof(int)))) return st;
+        if ((st = fa_ci.ensure(std::max(n, 1) * sizeof(int)))) return st;
+        if ((st = fa_co.ensure(std::max(n, 1) * sizeof(int)))) return st;
+        hipLaunchKernelGGL(grid_kernel, dim3(1), dim3(kGridBlock), 0, stream, v->keys_un, n,
+                           v->min_x, v->min_y, v->grid_w_inv, v->grid_h_inv, fa_co.as<int>(),
+                           fa_cs.as<int>(), fa_ci.as<int>());
+        F.k = v->keys_un;
+        F.desc = reinterpret_cast<const uint4*>(v->desc);
+        F.ur = v->u_right;
+        F.n = n;
+        F.minx = v->min_x;
+        F.maxx = v->max_x;
+        F.miny = v->min_y;
+        F.maxy = v->max_y;
+        F.gwi = v->grid_w_inv;
+        F.ghi = v->grid_h_inv;
+        F.cstart = fa_cs.as<int>();
+        F.citems = fa_ci.as<int>();
+        return ORBFE_OK;
+    }
+
     // count -> scan -> fill for a candidate kernel family; returns the candidate total.
     template <class Args, class CountK, class FillK>
     int csr(Args& a, int nq, CountK ck, FillK fk, int& total) {
@@ -384,6 +409,8 @@ int orbfe_search_by_projection_local(orbfe_matcher* m, float nnratio,
                       m->m_f3.as<float>(), m->m_d.as<uint4>(), m->m_i1.as<int>()};
         a.scale = m->m_f4.as<float>();
         a.th = th;
+        a.nlevels = f->nlevels;
+        a.status = nullptr;  // levels were checked on the host
         int total = 0;
         if ((st = m->csr(a, M, sbp_local_cand_kernel<false>, sbp_local_cand_kernel<true>, total)))
             return st;
@@ -625,6 +652,98 @@ int orbfe_distinctive_descriptors(orbfe_matcher* m, int n_mp, const int32_t* obs
     });
 }
 
+int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* frame,
+                                     const float* tcw, const orbfe_camera* cam,
+                                     float log_scale_factor, float viewing_cos_limit, int n_mp,
+                                     const float* d_xyz, const float* d_normal,
+                                     const float* d_min_dist, const float* d_max_dist,
+                                     const uint8_t* d_desc, const int32_t* d_nobs,
+                                     const uint8_t* d_bad, const uint8_t* d_skip,
+                                     const int32_t* d_mp_ids, float nnratio, float th,
+                                     int32_t* d_frame_mp, int32_t* d_frame_mp_obs,
+                                     uint8_t* d_in_view, int32_t* counts) {
+    if (!frame_ok(frame) || !tcw || !cam || n_mp < 0 || !counts ||
+        (frame->n && (!d_frame_mp || !d_frame_mp_obs)) ||
+        (n_mp && (!d_xyz || !d_normal || !d_min_dist || !d_max_dist || !d_desc || !d_nobs ||
+                  !d_bad || !d_in_view)))
+        return ORBFE_ERR_ARG;
+    return guarded(m, [&]() {
+        int st;
+        const int M = n_mp, N = frame->n;
+        if ((st = m->scal.ensure(16))) return st;
+        if ((st = m->m_f4.ensure(std::max<size_t>(16, (size_t)frame->nlevels * 4)))) return st;
+        ORBFE_HIP(hipMemcpyAsync(m->m_f4.p, frame->scale_factors, (size_t)frame->nlevels * 4,
+                                 hipMemcpyHostToDevice, m->stream));
+        for (DevBuf* b : {&m->o_f0, &m->o_f1, &m->o_f2, &m->o_f3, &m->o_i})
+            if ((st = b->ensure(std::max<size_t>(16, (size_t)M * 4)))) return st;
+        int* d_cnt = m->scal.as<int>() + 1;     // nToMatch
+        int* d_status = m->scal.as<int>() + 2;  // UB level
+        ORBFE_HIP(hipMemsetAsync(m->scal.p, 0, 16, m->stream));
+        // Tracking::SearchLocalPoints: isInFrustum(pMP, 0.5) over the local map (1425-1438)
+        FrustumArgs fa;
+        fa.n = M;
+        fa.xyz = d_xyz;
+        fa.normal = d_normal;
+        fa.mind = d_min_dist;
+        fa.maxd = d_max_dist;
+        std::memcpy(fa.T, tcw, sizeof(fa.T));
+        camera_center(tcw, fa.ow);
+        fa.fx = cam->fx;
+        fa.fy = cam->fy;
+        fa.cx = cam->cx;
+        fa.cy = cam->cy;
+        fa.bf = cam->bf;
+        fa.minx = frame->min_x;
+        fa.maxx = frame->max_x;
+        fa.miny = frame->min_y;
+        fa.maxy = frame->max_y;
+        fa.log_scale = log_scale_factor;
+        fa.cos_limit = viewing_cos_limit;
+        fa.in_view = d_in_view;
+        fa.px = m->o_f0.as<float>();
+        fa.py = m->o_f1.as<float>();
+        fa.pxr = m->o_f2.as<float>();
+        fa.lvl = m->o_i.as<int>();
+        fa.vcos = m->o_f3.as<float>();
+        fa.skip = d_skip;
+        fa.bad = d_bad;
+        fa.n_in_view = d_cnt;
+        if (M) hipLaunchKernelGGL(frustum_kernel, dim3((M + 255) / 256), dim3(256), 0, m->stream, fa);
+        // SearchByProjection(F, vpLocalMapPoints, th) (1440-1453, ORBmatcher.cc:45-129)
+        SbpLocalArgs a;
+        if ((st = m->frame_device(frame, a.f))) return st;
+        a.mp = SbpMps{M, d_in_view, d_bad, fa.px, fa.py, fa.pxr, fa.lvl, fa.vcos,
+                      reinterpret_cast<const uint4*>(d_desc), d_nobs};
+        a.scale = m->m_f4.as<float>();
+        a.th = th;
+        a.nlevels = frame->nlevels;
+        a.status = d_status;
+        int total = 0;
+        if ((st = m->csr(a, M, sbp_local_cand_kernel<false>, sbp_local_cand_kernel<true>, total)))
+            return st;
+        GreedyArgs g{};
+        g.m = M;
+        g.nkp = N;
+        g.mode = kGreedyLocal;
+        g.nnratio = nnratio;
+        g.off = m->off.as<int>();
+        g.cand = m->cand.as<int2>();
+        g.nobs = d_nobs;
+        g.fmp0 = g.fmp = d_frame_mp;
+        g.fobs0 = g.fobs = d_frame_mp_obs;
+        g.ids = d_mp_ids;
+        if ((st = m->greedy(g))) return st;  // synchronizes per batch of rounds
+        int host[3] = {0, 0, 0};
+        ORBFE_HIP(hipMemcpyAsync(host, m->scal.p, sizeof(host), hipMemcpyDeviceToHost, m->stream));
+        ORBFE_HIP(hipStreamSynchronize(m->stream));
+        counts[0] = host[0];  // nmatches
+        counts[1] = host[1];  // nToMatch
+        return host[2] ? host[2] : ORBFE_OK;
+    });
+}
+
+int orbfe_matcher_last_rounds(const orbfe_matcher* m) { return m ? m->last_rounds : ORBFE_ERR_ARG; }
+
 int orbfe_is_in_frustum(orbfe_matcher* m, int n, const float* xyz, const float* normal,
                         const float* min_dist, const float* max_dist, const float* tcw,
                         const orbfe_camera* cam, float min_x, float max_x, float min_y,
@@ -676,6 +795,8 @@ int orbfe_is_in_frustum(orbfe_matcher* m, int n, const float* xyz, const float* 
         a.pxr = m->o_f2.as<float>();
         a.lvl = m->o_i.as<int>();
         a.vcos = m->o_f3.as<float>();
+        a.skip = a.bad = nullptr;
+        a.n_in_view = nullptr;
         hipLaunchKernelGGL(frustum_kernel, dim3((n + 255) / 256), dim3(256), 0, m->stream, a);
         ORBFE_HIP(hipGetLastError());
         if ((st = m->down(in_view, m->o_u, n))) return st;

@@ -17,8 +17,8 @@ import os
 
 import numpy as np
 
-from .abi import (KEYPOINT_DTYPE, ORBFE_ERR_CAPACITY, ORBFE_OK, Camera, Frame, MapPoints,
-                  OrbfeError, Params, ptr)
+from .abi import (KEYPOINT_DTYPE, ORBFE_ERR_CAPACITY, ORBFE_OK, Camera, Frame, FrameView,
+                  MapPoints, OrbfeError, Params, ptr)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "liborbfe.so")
@@ -37,7 +37,8 @@ EXPORTED = [
     "orbfe_bf_match", "orbfe_bf_match_batch_device", "orbfe_search_for_initialization",
     "orbfe_search_by_projection_local", "orbfe_search_by_projection_last",
     "orbfe_search_by_projection_keyframe", "orbfe_distinctive_descriptors",
-    "orbfe_distinctive_descriptors_device", "orbfe_is_in_frustum",
+    "orbfe_distinctive_descriptors_device", "orbfe_search_local_points_device",
+    "orbfe_matcher_last_rounds", "orbfe_is_in_frustum",
 ]
 
 
@@ -457,6 +458,35 @@ class ORBmatcher:
         _check("orbfe_distinctive_descriptors", lib().orbfe_distinctive_descriptors(
             self._h, n, ptr(off), ptr(d), ptr(best), ptr(out)))
         return best, out
+
+    def search_local_points_device(self, n_kp: int, d_keys: int, d_desc: int,
+                                   d_u_right: int | None, width: int, height: int,
+                                   scale_factors: np.ndarray, tcw, cam: Camera,
+                                   log_scale: float, cos_limit: float, n_mp: int, d_xyz: int,
+                                   d_normal: int, d_min: int, d_max: int, d_mdesc: int,
+                                   d_nobs: int, d_bad: int, d_skip: int | None,
+                                   d_ids: int | None, nnratio: float, th: float, d_fmp: int,
+                                   d_fobs: int, d_in_view: int) -> tuple[int, int]:
+        """Tracking::SearchLocalPoints on device-resident frame + local map
+        (orbfe_search_local_points_device) -> (nmatches, nToMatch)."""
+        sf = np.ascontiguousarray(scale_factors, np.float32)
+        gw = np.float32(64) / np.float32(width)
+        gh = np.float32(48) / np.float32(height)
+        fv = FrameView(n_kp, C.c_void_p(d_keys), C.c_void_p(d_desc),
+                       C.c_void_p(d_u_right) if d_u_right else None, 0.0, float(width), 0.0,
+                       float(height), float(gw), float(gh), ptr(sf), len(sf))
+        t = np.ascontiguousarray(tcw, np.float32).reshape(12)
+        counts = np.zeros(2, np.int32)
+        vp = lambda p: C.c_void_p(p) if p else None  # noqa: E731
+        _check("orbfe_search_local_points_device", lib().orbfe_search_local_points_device(
+            self._h, C.byref(fv), ptr(t), C.byref(cam), C.c_float(log_scale),
+            C.c_float(cos_limit), n_mp, vp(d_xyz), vp(d_normal), vp(d_min), vp(d_max),
+            vp(d_mdesc), vp(d_nobs), vp(d_bad), vp(d_skip), vp(d_ids), C.c_float(nnratio),
+            C.c_float(th), vp(d_fmp), vp(d_fobs), vp(d_in_view), ptr(counts)))
+        return int(counts[0]), int(counts[1])
+
+    def last_rounds(self) -> int:
+        return lib().orbfe_matcher_last_rounds(self._h)
 
     def is_in_frustum(self, xyz, normal, min_dist, max_dist, tcw, cam: Camera, bounds,
                       log_scale: float, cos_limit: float = 0.5):

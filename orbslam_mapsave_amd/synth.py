@@ -137,3 +137,57 @@ def synthetic_stereo_pair(seed: int, w: int = 640, h: int = 480, d0: float = 4.0
     rows = np.arange(h)[:, None]
     right = left[rows, x0] * (1 - t) + left[rows, x1] * t
     return left.astype(np.uint8), np.clip(np.rint(right), 0, 255).astype(np.uint8)
+
+
+def synthetic_local_map(keys: np.ndarray, desc: np.ndarray, m: int = 50_000, seed: int = 0,
+                        w: int = 640, h: int = 480, fx: float = 500.0, fy: float = 500.0,
+                        cx: float = 320.0, cy: float = 240.0, nlevels: int = 8,
+                        scale: float = 1.2) -> dict:
+    """BASELINE config 5 as world-space map points seen by a camera at the
+    identity pose: 60% project within 2 px of a real keypoint with its descriptor ~8% bit-flipped
+    and a predicted level of the keypoint's octave + {0, 1}; the rest project uniformly with
+    random descriptors and levels.  mfMaxDistance = dist * scale^(level - 1/2) makes
+    MapPoint::PredictScale return that level; mfMinDistance = mfMaxDistance / scale^(nlevels-1).
+    Normals make viewing cosines ~U[0.5, 1] (10% above 0.998); a few points lie behind the
+    camera or outside the image; Observations() in 1..5 (5% zero), 2% bad, 3% already matched
+    (skip)."""
+    rng = np.random.Generator(np.random.PCG64(seed + 5))
+    n = len(keys)
+    true = rng.uniform(size=m) < 0.6
+    src = rng.integers(0, max(n, 1), m)
+    kx = keys["x"][src] if n else np.zeros(m)
+    ky = keys["y"][src] if n else np.zeros(m)
+    ko = keys["octave"][src] if n else np.zeros(m, np.int32)
+    u = np.where(true, kx + rng.uniform(-2, 2, m), rng.uniform(0, w, m))
+    v = np.where(true, ky + rng.uniform(-2, 2, m), rng.uniform(0, h, m))
+    lvl = np.clip(np.where(true, ko + rng.integers(0, 2, m), rng.integers(0, nlevels, m)), 0,
+                  nlevels - 1)
+    z = rng.uniform(2.0, 8.0, m)
+    off = rng.uniform(size=m)
+    u = np.where(off < 0.03, u + 2 * w, u)                       # outside the image
+    z = np.where((off >= 0.03) & (off < 0.05), -z, z)            # behind the camera
+    xyz = np.stack([(u - cx) / fx * np.abs(z), (v - cy) / fy * np.abs(z), z], 1)
+    dist = np.linalg.norm(xyz, axis=1)
+    s = np.float64(np.float32(scale))
+    maxd = dist * s ** (lvl - 0.5)
+    mind = maxd / s ** (nlevels - 1)
+    d = xyz / dist[:, None]
+    cosv = np.where(rng.uniform(size=m) < 0.1, rng.uniform(0.9985, 1.0, m), rng.uniform(0.5, 1, m))
+    perp = np.cross(d, rng.normal(size=(m, 3)))
+    perp /= np.linalg.norm(perp, axis=1, keepdims=True)
+    normal = d * cosv[:, None] + perp * np.sqrt(1 - cosv ** 2)[:, None]
+    bits = np.unpackbits(desc[src] if n else np.zeros((m, 32), np.uint8), axis=1)
+    flipped = np.packbits(bits ^ (rng.uniform(size=bits.shape) < 0.08).astype(np.uint8), axis=1)
+    mdesc = np.where(true[:, None], flipped, rng.integers(0, 256, (m, 32), dtype=np.uint8))
+    nobs = rng.integers(1, 6, m)
+    nobs[rng.uniform(size=m) < 0.05] = 0
+    fmp = np.where(rng.uniform(size=n) < 0.1, rng.integers(0, 1000, n), -1)
+    return dict(xyz=xyz.astype(np.float32), normal=normal.astype(np.float32),
+                min_dist=mind.astype(np.float32), max_dist=maxd.astype(np.float32),
+                desc=np.ascontiguousarray(mdesc, np.uint8), nobs=nobs.astype(np.int32),
+                bad=(rng.uniform(size=m) < 0.02).astype(np.uint8),
+                skip=(rng.uniform(size=m) < 0.03).astype(np.uint8),
+                ids=(np.arange(m) + 100_000).astype(np.int32),
+                frame_mp=fmp.astype(np.int32),
+                frame_mp_obs=np.where(fmp >= 0, rng.integers(0, 3, n), 0).astype(np.int32),
+                tcw=np.hstack([np.eye(3), np.zeros((3, 1))]).astype(np.float32))

@@ -1,0 +1,70 @@
+"""Tracking::SearchLocalPoints on device-resident data (BASELINE config 5): isInFrustum over a
+50k-point local map + SearchByProjection(F, vpLocalMapPoints, th), through
+orbfe_search_local_points_device, bit-exact against the oracle's isInFrustum and
+SearchByProjection composed the way Tracking.cc:1403-1455 composes them.
+"""
+import numpy as np
+import pytest
+
+import oracle
+import scenarios as S
+from orbslam_mapsave_amd.abi import MapPoints
+from orbslam_mapsave_amd.synth import synthetic_local_map
+
+LOG_SCALE = float(np.log(np.float32(1.2)).astype(np.float32))
+
+
+def oracle_search_local_points(frame, lm, cam, th=1.0, nnratio=0.8):
+    inv, px, py, pxr, pl, vc = oracle.is_in_frustum(
+        lm["xyz"], lm["normal"], lm["min_dist"], lm["max_dist"], lm["tcw"], cam,
+        (0.0, float(S.W), 0.0, float(S.H)), LOG_SCALE, 0.5)
+    inv[(lm["skip"] > 0) | (lm["bad"] > 0)] = 0  # skipped points: mbTrackInView = false (1419)
+    mps = MapPoints(px, py, pl, vc, lm["desc"], lm["nobs"], track_in_view=inv,
+                    is_bad=lm["bad"], proj_xr=pxr)
+    fmp, fobs, nm = oracle.search_by_projection_local(frame, mps, th, nnratio, lm["frame_mp"],
+                                                      lm["frame_mp_obs"], lm["ids"])
+    return inv, fmp, fobs, nm, int(inv.sum())
+
+
+def test_local_map_generator_predicts_levels():
+    f = S.extract_frame(0, 1000)
+    lm = synthetic_local_map(f.keys, f.desc, 20000, seed=0)
+    inv, px, py, pxr, pl, vc = oracle.is_in_frustum(
+        lm["xyz"], lm["normal"], lm["min_dist"], lm["max_dist"], lm["tcw"], S.camera(),
+        (0.0, float(S.W), 0.0, float(S.H)), LOG_SCALE, 0.5)
+    assert 0.85 < inv.mean() < 0.97
+    assert pl[inv > 0].min() >= 0 and pl[inv > 0].max() <= 7
+    inv2, fmp, fobs, nm, nto = oracle_search_local_points(f, lm, S.camera())
+    assert nm > 300
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,m,th,stereo", [(0, 50000, 1.0, False), (1, 50000, 3.0, False),
+                                              (2, 20000, 1.0, True), (3, 1000, 5.0, False)])
+def test_gpu_search_local_points(seed, m, th, stereo):
+    import torch
+    from orbslam_mapsave_amd.native import ORBmatcher
+    f = S.extract_frame(seed, 1000, u_right=stereo)
+    lm = synthetic_local_map(f.keys, f.desc, m, seed=seed)
+    cam = S.camera()
+    inv, fmp, fobs, nm, nto = oracle_search_local_points(f, lm, cam, th)
+    dev = torch.device("cuda", 0)
+    T = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in lm.items()}
+    d_keys = torch.from_numpy(f.keys.view(np.uint8).copy()).to(dev)
+    d_desc = torch.from_numpy(f.desc).to(dev)
+    d_ur = torch.from_numpy(f.u_right).to(dev) if f.u_right is not None else None
+    d_inv = torch.zeros(m, dtype=torch.uint8, device=dev)
+    mt = ORBmatcher(0.8, False, device=0)
+    gnm, gnto = mt.search_local_points_device(
+        f.n, d_keys.data_ptr(), d_desc.data_ptr(), d_ur.data_ptr() if d_ur is not None else None,
+        S.W, S.H, f.scale_factors, lm["tcw"], cam, LOG_SCALE, 0.5, m, T["xyz"].data_ptr(),
+        T["normal"].data_ptr(), T["min_dist"].data_ptr(), T["max_dist"].data_ptr(),
+        T["desc"].data_ptr(), T["nobs"].data_ptr(), T["bad"].data_ptr(), T["skip"].data_ptr(),
+        T["ids"].data_ptr(), 0.8, th, T["frame_mp"].data_ptr(), T["frame_mp_obs"].data_ptr(),
+        d_inv.data_ptr())
+    assert (gnm, gnto) == (nm, nto)
+    assert np.array_equal(d_inv.cpu().numpy(), inv)
+    assert np.array_equal(T["frame_mp"].cpu().numpy(), fmp)
+    assert np.array_equal(T["frame_mp_obs"].cpu().numpy(), fobs)
+    print(f"rounds={mt.last_rounds()} nmatches={nm} nToMatch={nto}")
+    mt.close()
