@@ -395,6 +395,7 @@ struct SbpLocalArgs {
     float th;
     int nlevels;         // levels of `scale`; a predicted level outside is UB in the reference
     int* status;         // NULL, or set to ORBFE_ERR_UNSUPPORTED for such a point
+    long long cand_cap;  // fill writes only lists that end within the capacity
     int* cnt;
     const int* off;
     int2* cand;          // (idx, dist | octave << 16)
@@ -418,6 +419,7 @@ __global__ __launch_bounds__(256) void sbp_local_cand_kernel(SbpLocalArgs a) {
     if (a.th != 1.0) r *= a.th;
     const float rs = r * a.scale[pl];
     const float pxr = a.mp.pxr[i];
+    if (FILL && a.off[i + 1] > a.cand_cap) return;
     const uint4 q0 = a.mp.desc[2 * i], q1 = a.mp.desc[2 * i + 1];
     int n = 0;
     int2* out = FILL ? a.cand + a.off[i] : nullptr;

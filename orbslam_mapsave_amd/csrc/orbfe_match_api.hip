@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
+#include <functional>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -131,7 +133,9 @@ struct orbfe_matcher {
     // Exact parallel resolution of the greedy assignment (orbfe_greedy.hip).  `g` carries the
     // problem (m points, nkp slots, CSR candidates, decision mode, slot arrays fmp/fobs that
     // hold the state before the call and receive the result); the scratch is owned here.
-    int greedy(GreedyArgs& g) {
+    // `total` / `cap` (optional): a candidate total that is only known on the device; it is
+    // checked at the first synchronization, before any slot is written (ORBFE_ERR_CAPACITY).
+    int greedy(GreedyArgs& g, int first_batch = 8, const int* total = nullptr, size_t cap = 0) {
         int st;
         const int M = g.m, N = g.nkp;
         if ((st = g_t0.ensure(std::max(N, 1) * sizeof(int)))) return st;
@@ -158,18 +162,24 @@ struct orbfe_matcher {
         ORBFE_HIP(hipMemsetAsync(g.chg, 0, (size_t)(M + 2) * sizeof(int), stream));
         hipLaunchKernelGGL(greedy_init_kernel, dim3(blocks), dim3(kGreedyBlock), 0, stream, g);
         // rounds in batches; a round after a change-free round exits at once
-        int r = 0, batch = 4;
+        int r = 0, batch = first_batch;
+        std::vector<int> chg_h;
         while (true) {
+            const int r0 = r;
             for (int b = 0; b < batch && r <= M; ++b, ++r)
                 hipLaunchKernelGGL(greedy_round_kernel, dim3(blocks), dim3(kGreedyBlock), 0, stream, g, r);
-            int c = 0;
-            ORBFE_HIP(hipMemcpyAsync(&c, g.chg + (r - 1), sizeof(int), hipMemcpyDeviceToHost, stream));
+            chg_h.assign(r - r0, 0);
+            ORBFE_HIP(hipMemcpyAsync(chg_h.data(), g.chg + r0, (r - r0) * sizeof(int), hipMemcpyDeviceToHost, stream));
             ORBFE_HIP(hipStreamSynchronize(stream));
-            if (c == 0) break;
+            if (total && (size_t)*total > cap) return ORBFE_ERR_CAPACITY;
+            const auto z = std::find(chg_h.begin(), chg_h.end(), 0);
+            if (z != chg_h.end()) {
+                last_rounds = r0 + (int)(z - chg_h.begin()) + 1;  // the change-free round included
+                break;
+            }
             if (r > M) return ORBFE_ERR_HIP;  // cannot happen: the correct prefix grows every round
             batch = std::min(batch * 2, 64);
         }
-        last_rounds = r;
         hipLaunchKernelGGL(greedy_accept_kernel, dim3(mblocks), dim3(kGreedyBlock), 0, stream, g);
         hipLaunchKernelGGL(greedy_slots_kernel, dim3(nblocks), dim3(kGreedyBlock), 0, stream, g);
         if (g.check_ori)
@@ -411,6 +421,7 @@ int orbfe_search_by_projection_local(orbfe_matcher* m, float nnratio,
         a.th = th;
         a.nlevels = f->nlevels;
         a.status = nullptr;  // levels were checked on the host
+        a.cand_cap = LLONG_MAX;
         int total = 0;
         if ((st = m->csr(a, M, sbp_local_cand_kernel<false>, sbp_local_cand_kernel<true>, total)))
             return st;
@@ -678,6 +689,8 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
             if ((st = b->ensure(std::max<size_t>(16, (size_t)M * 4)))) return st;
         int* d_cnt = m->scal.as<int>() + 1;     // nToMatch
         int* d_status = m->scal.as<int>() + 2;  // UB level
+        bool retried = false;
+        std::function<int()> attempt = [&]() -> int {
         ORBFE_HIP(hipMemsetAsync(m->scal.p, 0, 16, m->stream));
         // Tracking::SearchLocalPoints: isInFrustum(pMP, 0.5) over the local map (1425-1438)
         FrustumArgs fa;
@@ -718,9 +731,23 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
         a.th = th;
         a.nlevels = frame->nlevels;
         a.status = d_status;
+        // candidates without a host round trip: the fill is bounded by the current capacity
+        // (16 per point to start); the total is checked after the first greedy batch and the
+        // call is redone once with the exact capacity if it did not fit
+        const size_t cap = std::max(m->cand.bytes / sizeof(int2), (size_t)16 * std::max(M, 1));
+        if ((st = m->cand.ensure(cap * sizeof(int2)))) return st;
+        if ((st = m->cnt.ensure(std::max(M, 1) * sizeof(int)))) return st;
+        if ((st = m->off.ensure((M + 1) * sizeof(int)))) return st;
+        a.cnt = m->cnt.as<int>();
+        a.off = m->off.as<int>();
+        a.cand = m->cand.as<int2>();
+        a.cand_cap = (long long)cap;
+        const int qb = std::max(1, (M + 255) / 256);
+        hipLaunchKernelGGL(sbp_local_cand_kernel<false>, dim3(qb), dim3(256), 0, m->stream, a);
+        hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, m->stream, m->cnt.as<int>(), M, m->off.as<int>());
+        hipLaunchKernelGGL(sbp_local_cand_kernel<true>, dim3(qb), dim3(256), 0, m->stream, a);
         int total = 0;
-        if ((st = m->csr(a, M, sbp_local_cand_kernel<false>, sbp_local_cand_kernel<true>, total)))
-            return st;
+        ORBFE_HIP(hipMemcpyAsync(&total, m->off.as<int>() + M, sizeof(int), hipMemcpyDeviceToHost, m->stream));
         GreedyArgs g{};
         g.m = M;
         g.nkp = N;
@@ -732,13 +759,23 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
         g.fmp0 = g.fmp = d_frame_mp;
         g.fobs0 = g.fobs = d_frame_mp_obs;
         g.ids = d_mp_ids;
-        if ((st = m->greedy(g))) return st;  // synchronizes per batch of rounds
+        // synchronizes per batch of rounds; ORBFE_ERR_CAPACITY (nothing written yet) when the
+        // candidates did not fit: grow to the exact total and run again
+        st = m->greedy(g, 8, &total, cap);
+        if (st == ORBFE_ERR_CAPACITY && !retried) {
+            if ((st = m->cand.ensure((size_t)total * sizeof(int2)))) return st;
+            retried = true;
+            return attempt();
+        }
+        if (st) return st;
         int host[3] = {0, 0, 0};
         ORBFE_HIP(hipMemcpyAsync(host, m->scal.p, sizeof(host), hipMemcpyDeviceToHost, m->stream));
         ORBFE_HIP(hipStreamSynchronize(m->stream));
         counts[0] = host[0];  // nmatches
         counts[1] = host[1];  // nToMatch
         return host[2] ? host[2] : ORBFE_OK;
+        };
+        return attempt();
     });
 }
 
