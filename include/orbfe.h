@@ -73,8 +73,9 @@ typedef struct orbfe_rect {
     int32_t x0, y0, x1, y1;
 } orbfe_rect;
 
-typedef struct orbfe_extractor orbfe_extractor;
-typedef struct orbfe_matcher   orbfe_matcher;
+typedef struct orbfe_extractor  orbfe_extractor;
+typedef struct orbfe_matcher    orbfe_matcher;
+typedef struct orbfe_vocabulary orbfe_vocabulary;
 
 /* ---- extractor ---------------------------------------------------------------------------- */
 
@@ -380,6 +381,55 @@ int orbfe_is_in_frustum(orbfe_matcher* m, int n, const float* xyz, const float* 
                         float max_y, float log_scale_factor, float viewing_cos_limit,
                         uint8_t* in_view, float* proj_x, float* proj_y, float* proj_xr,
                         int32_t* pred_level, float* view_cos);
+
+/* ---- bag of words (DBoW2, vendored in the reference as Thirdparty/DBoW2) ----------------- */
+
+/* ORBVocabulary::loadFromTextFile (TemplatedVocabulary.h:1351-1436), called by System::System
+ * on ORBvoc.txt: header "k L scoring weighting", one line per node "parent isLeaf d0..d31
+ * weight".  The tree is kept in HBM of `device`.  Blank lines are skipped. */
+orbfe_vocabulary* orbfe_vocabulary_load_text(const char* path, int device, int* status);
+/* The same from node arrays: node 0 is the root (its entries are ignored); parent[i] < i;
+ * is_word flags the leaves that are words (word ids in node order); desc n_nodes x 32. */
+orbfe_vocabulary* orbfe_vocabulary_create(int k, int L, int scoring, int weighting, int n_nodes,
+                                          const int32_t* parent, const uint8_t* is_word,
+                                          const uint8_t* desc, const double* weight, int device,
+                                          int* status);
+void orbfe_vocabulary_destroy(orbfe_vocabulary* v);
+/* info[6] = {k, L, scoring, weighting, nodes, words}. */
+int orbfe_vocabulary_info(const orbfe_vocabulary* v, int32_t* info);
+int orbfe_vocabulary_set_stream(orbfe_vocabulary* v, void* hip_stream);
+
+/* Frame::ComputeBoW / KeyFrame::ComputeBoW (Frame.cc:513-520) = TemplatedVocabulary::transform(
+ * features, BowVector, FeatureVector, levelsup) (TemplatedVocabulary.h:1140-1196) over n
+ * descriptors (n <= 4096).  BowVector: nw ascending word ids + values (double, normalised as the
+ * vocabulary's scoring requires); FeatureVector: nn ascending node ids (level L - levelsup),
+ * CSR offsets node_off[nn + 1] into feat (feature indices, ascending within a node).  Every
+ * output array holds at least n entries (node_off n + 1).  Synchronous. */
+int orbfe_bow_transform(orbfe_vocabulary* v, const uint8_t* desc, int n, int levelsup,
+                        int32_t* word_ids, double* values, int32_t* nw, int32_t* node_ids,
+                        int32_t* node_off, int32_t* feat, int32_t* nn);
+/* Batched device form: frame f's descriptors at d_desc + f*cap*32 (d_n[f] rows, cap <= 4096);
+ * outputs per frame at f*cap (node_off at f*(cap+1)), counts in d_nw[f] / d_nn[f].
+ * Asynchronous on the vocabulary's stream (orbfe_vocabulary_set_stream). */
+int orbfe_bow_transform_batch_device(orbfe_vocabulary* v, int nframes, const uint8_t* d_desc,
+                                     const int32_t* d_n, int cap, int levelsup,
+                                     int32_t* d_word_ids, double* d_values, int32_t* d_nw,
+                                     int32_t* d_node_ids, int32_t* d_node_off, int32_t* d_feat,
+                                     int32_t* d_nn);
+
+/* ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPointMatches)
+ * (ORBmatcher.cc:159-291) with ORBmatcher(nnratio, check_ori) (Tracking.cc:1011 / 1621 use 0.7 /
+ * 0.75, checkOri true).  Keyframe: n_kf descriptors, keypoint angles (mvKeysUn), kf_mp_ok[i] =
+ * GetMapPointMatches()[i] != NULL && !isBad(), its FeatureVector (kf_nn nodes, CSR).  Frame: n_f
+ * descriptors, angles (mvKeys) and FeatureVector.  matches[f] = the keyframe feature whose map
+ * point lands in vpMapPointMatches[f], or -1; *nmatches as returned. */
+int orbfe_search_by_bow(orbfe_matcher* m, float nnratio, int check_ori, int n_kf,
+                        const uint8_t* kf_desc, const float* kf_angle, const uint8_t* kf_mp_ok,
+                        int kf_nn, const int32_t* kf_node_ids, const int32_t* kf_node_off,
+                        const int32_t* kf_feat, int n_f, const uint8_t* f_desc,
+                        const float* f_angle, int f_nn, const int32_t* f_node_ids,
+                        const int32_t* f_node_off, const int32_t* f_feat, int32_t* matches,
+                        int32_t* nmatches);
 
 #ifdef __cplusplus
 }

@@ -307,6 +307,64 @@ def distinctive_descriptors(obs_off: np.ndarray, obs_desc: np.ndarray):
     return best, out
 
 
+class Vocabulary:
+    """DBoW2 text vocabulary loaded by the oracle (oracle_vocab_load_text)."""
+
+    def __init__(self, path: str):
+        L = lib()
+        L.oracle_vocab_load_text.restype = C.c_void_p
+        L.oracle_vocab_load_text.argtypes = [C.c_char_p, C.c_void_p]
+        L.oracle_vocab_free.argtypes = [C.c_void_p]
+        st = C.c_int(0)
+        h = L.oracle_vocab_load_text(path.encode(), C.byref(st))
+        if not h:
+            raise OrbfeError("oracle_vocab_load_text", st.value)
+        self._h = C.c_void_p(h)
+        info = np.zeros(6, np.int32)
+        _check("oracle_vocab_info", L.oracle_vocab_info(self._h, ptr(info)))
+        self.k, self.L, self.scoring, self.weighting, self.nodes, self.words = map(int, info)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().oracle_vocab_free(self._h)
+            self._h = None
+
+    def transform(self, desc: np.ndarray, levelsup: int = 4):
+        """-> (word_ids, values, node_ids, node_off, feat): BowVector and FeatureVector."""
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = len(d)
+        wid = np.zeros(max(n, 1), np.int32)
+        val = np.zeros(max(n, 1), np.float64)
+        nid = np.zeros(max(n, 1), np.int32)
+        off = np.zeros(n + 2, np.int32)
+        feat = np.zeros(max(n, 1), np.int32)
+        nw, nn = C.c_int32(0), C.c_int32(0)
+        _check("oracle_bow_transform", lib().oracle_bow_transform(
+            self._h, ptr(d), n, levelsup, ptr(wid), ptr(val), C.byref(nw), ptr(nid), ptr(off),
+            ptr(feat), C.byref(nn)))
+        return (wid[:nw.value].copy(), val[:nw.value].copy(), nid[:nn.value].copy(),
+                off[:nn.value + 1].copy(), feat[:off[nn.value]].copy())
+
+
+def search_by_bow(kf_desc, kf_angle, kf_mp_ok, kf_fv, f_desc, f_angle, f_fv, nnratio=0.75,
+                  check_ori=True):
+    """ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...) -> (matches per frame feature, n)."""
+    kd = np.ascontiguousarray(kf_desc, np.uint8).reshape(-1, 32)
+    fd = np.ascontiguousarray(f_desc, np.uint8).reshape(-1, 32)
+    ka = np.ascontiguousarray(kf_angle, np.float32)
+    fa = np.ascontiguousarray(f_angle, np.float32)
+    ok = np.ascontiguousarray(kf_mp_ok, np.uint8)
+    kn, ko, kfe = (np.ascontiguousarray(x, np.int32) for x in kf_fv)
+    fn, fo, ffe = (np.ascontiguousarray(x, np.int32) for x in f_fv)
+    out = np.zeros(len(fd), np.int32)
+    nm = C.c_int32(0)
+    _check("oracle_search_by_bow", lib().oracle_search_by_bow(
+        C.c_float(nnratio), int(check_ori), ptr(kd), ptr(ka), ptr(ok), ptr(kn), ptr(ko),
+        ptr(kfe), len(kn), len(fd), ptr(fd), ptr(fa), ptr(fn), ptr(fo), ptr(ffe), len(fn),
+        ptr(out), C.byref(nm)))
+    return out, nm.value
+
+
 def is_in_frustum(xyz, normal, min_dist, max_dist, tcw, cam: Camera, bounds, log_scale,
                   cos_limit=0.5):
     xyz = np.ascontiguousarray(xyz, np.float32).reshape(-1, 3)

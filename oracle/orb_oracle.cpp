@@ -26,6 +26,10 @@
 #include <climits>
 #include <cmath>
 #include <cstring>
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <string>
 #include <list>
 #include <thread>
 #include <vector>
@@ -1300,6 +1304,229 @@ int oracle_distinctive_descriptors(int n_mp, const int32_t* obs_off, const uint8
         best[i] = best_idx;
         if (desc_out) std::memcpy(desc_out + 32 * (size_t)i, obs_desc + 32 * (size_t)(o + best_idx), 32);
     }
+    return ORBFE_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// DBoW2 (vendored in the reference: Thirdparty/DBoW2) — TemplatedVocabulary<FORB> text format,
+// transform, BowVector / FeatureVector, and ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...).
+}  // extern "C"
+
+struct oracle_vocab {
+    int k = 0, L = 0, scoring = 0, weighting = 0;
+    struct Node {
+        int parent = 0;
+        std::vector<int> children;
+        uint8_t desc[32] = {};
+        double weight = 0;
+        int word_id = 0;  // Node() default (TemplatedVocabulary.h:329)
+    };
+    std::vector<Node> nodes;
+    int nwords = 0;
+};
+
+namespace {
+// loadFromTextFile (TemplatedVocabulary.h:1351-1436): header "k L scoring weighting", then one
+// line per node "parent isLeaf d0 .. d31 weight", node ids in file order from 1.  Blank lines
+// are skipped (the reference turns a trailing blank line into a phantom child
+// of the root with an uninitialised descriptor).
+bool vocab_parse(const char* path, oracle_vocab& v) {
+    FILE* f = std::fopen(path, "r");
+    if (!f) return false;
+    std::string line;
+    auto getline = [&](std::string& out) -> bool {
+        out.clear();
+        int c;
+        bool any = false;
+        while ((c = std::fgetc(f)) != EOF) {
+            any = true;
+            if (c == '\n') break;
+            out.push_back((char)c);
+        }
+        return any;
+    };
+    if (!getline(line)) { std::fclose(f); return false; }
+    int n1 = -1, n2 = -1;
+    if (std::sscanf(line.c_str(), "%d %d %d %d", &v.k, &v.L, &n1, &n2) != 4 || v.k < 0 ||
+        v.k > 20 || v.L < 1 || v.L > 10 || n1 < 0 || n1 > 5 || n2 < 0 || n2 > 3) {
+        std::fclose(f);
+        return false;
+    }
+    v.scoring = n1;
+    v.weighting = n2;
+    v.nodes.assign(1, oracle_vocab::Node());
+    while (getline(line)) {
+        const char* p = line.c_str();
+        char* e;
+        while (*p == ' ' || *p == '\t' || *p == '\r') ++p;
+        if (!*p) continue;
+        oracle_vocab::Node nd;
+        nd.parent = (int)std::strtol(p, &e, 10); p = e;
+        const int leaf = (int)std::strtol(p, &e, 10); p = e;
+        for (int i = 0; i < 32; ++i) { nd.desc[i] = (uint8_t)std::strtol(p, &e, 10); p = e; }
+        nd.weight = std::strtod(p, &e);
+        const int id = (int)v.nodes.size();
+        if (nd.parent < 0 || nd.parent >= id) { std::fclose(f); return false; }
+        if (leaf > 0) nd.word_id = v.nwords++;
+        v.nodes.push_back(nd);
+        v.nodes[nd.parent].children.push_back(id);
+    }
+    std::fclose(f);
+    return true;
+}
+
+// transform(feature, word_id, weight, &nid, levelsup) (TemplatedVocabulary.h:1233-1270)
+void vocab_descend(const oracle_vocab& v, const uint8_t* d, int levelsup, int& word, double& w,
+                   int& nid) {
+    const int nid_level = v.L - levelsup;
+    if (nid_level <= 0) nid = 0;
+    int final_id = 0, level = 0;
+    do {
+        ++level;
+        const std::vector<int>& ch = v.nodes[final_id].children;
+        final_id = ch[0];
+        int best = descriptor_distance(d, v.nodes[final_id].desc);
+        for (size_t c = 1; c < ch.size(); ++c) {
+            const int dd = descriptor_distance(d, v.nodes[ch[c]].desc);
+            if (dd < best) { best = dd; final_id = ch[c]; }
+        }
+        if (level == nid_level) nid = final_id;
+    } while (!v.nodes[final_id].children.empty());
+    word = v.nodes[final_id].word_id;
+    w = v.nodes[final_id].weight;
+}
+}  // namespace
+
+extern "C" {
+oracle_vocab* oracle_vocab_load_text(const char* path, int* status) {
+    oracle_vocab* v = new oracle_vocab();
+    const bool ok = path && vocab_parse(path, *v);
+    if (status) *status = ok ? ORBFE_OK : ORBFE_ERR_ARG;
+    if (!ok) { delete v; return nullptr; }
+    return v;
+}
+void oracle_vocab_free(oracle_vocab* v) { delete v; }
+int oracle_vocab_info(const oracle_vocab* v, int32_t* info /* k, L, scoring, weighting, nodes, words */) {
+    if (!v || !info) return ORBFE_ERR_ARG;
+    info[0] = v->k; info[1] = v->L; info[2] = v->scoring; info[3] = v->weighting;
+    info[4] = (int32_t)v->nodes.size(); info[5] = v->nwords;
+    return ORBFE_OK;
+}
+
+// TemplatedVocabulary::transform(features, BowVector, FeatureVector, levelsup)
+// (TemplatedVocabulary.h:1140-1196) as called by Frame::ComputeBoW (Frame.cc:513-520).
+int oracle_bow_transform(const oracle_vocab* v, const uint8_t* desc, int n, int levelsup,
+                         int32_t* word_ids, double* values, int32_t* nw, int32_t* node_ids,
+                         int32_t* node_off, int32_t* feat, int32_t* nn) {
+    if (!v || n < 0 || (n && !desc) || !nw || !nn) return ORBFE_ERR_ARG;
+    std::map<int, double> bow;
+    std::map<int, std::vector<int>> fv;
+    if (v->nwords > 0) {
+        const bool must = v->scoring != 5;  // DotProductScoring only skips normalisation
+        for (int i = 0; i < n; ++i) {
+            int word = 0, nid = 0;
+            double w = 0;
+            vocab_descend(*v, desc + 32 * (size_t)i, levelsup, word, w, nid);
+            if (w > 0) {
+                if (v->weighting == 0 || v->weighting == 1) {  // TF_IDF, TF: addWeight
+                    auto it = bow.find(word);
+                    if (it != bow.end()) it->second += w; else bow[word] = w;
+                } else {                                         // IDF, BINARY: addIfNotExist
+                    bow.emplace(word, w);
+                }
+                fv[nid].push_back(i);
+            }
+        }
+        if ((v->weighting == 0 || v->weighting == 1) && !bow.empty() && !must) {
+            const double nd = (double)bow.size();
+            for (auto& kv : bow) kv.second /= nd;
+        }
+        if (must) {  // BowVector::normalize: L2 for L2Scoring, L1 otherwise
+            double norm = 0.0;
+            if (v->scoring == 1) {
+                for (auto& kv : bow) norm += kv.second * kv.second;
+                norm = std::sqrt(norm);
+            } else {
+                for (auto& kv : bow) norm += std::fabs(kv.second);
+            }
+            if (norm > 0.0)
+                for (auto& kv : bow) kv.second /= norm;
+        }
+    }
+    *nw = (int32_t)bow.size();
+    *nn = (int32_t)fv.size();
+    int i = 0;
+    for (auto& kv : bow) {
+        if (word_ids) word_ids[i] = kv.first;
+        if (values) values[i] = kv.second;
+        ++i;
+    }
+    int j = 0, o = 0;
+    for (auto& kv : fv) {
+        if (node_ids) node_ids[j] = kv.first;
+        if (node_off) node_off[j] = o;
+        for (int f : kv.second) {
+            if (feat) feat[o] = f;
+            ++o;
+        }
+        ++j;
+    }
+    if (node_off) node_off[j] = o;
+    return ORBFE_OK;
+}
+
+// ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPointMatches)
+// (ORBmatcher.cc:159-291).  kf_mp_ok[i] = (GetMapPointMatches()[i] != NULL && !isBad());
+// matches[f] = the keyframe feature matched to frame feature f, or -1.
+int oracle_search_by_bow(float nnratio, int check_ori, const uint8_t* kf_desc,
+                         const float* kf_angle, const uint8_t* kf_mp_ok,
+                         const int32_t* kf_node_ids, const int32_t* kf_node_off,
+                         const int32_t* kf_feat, int kf_nn, int n_f, const uint8_t* f_desc,
+                         const float* f_angle, const int32_t* f_node_ids,
+                         const int32_t* f_node_off, const int32_t* f_feat, int f_nn,
+                         int32_t* matches, int32_t* nmatches) {
+    if (kf_nn < 0 || f_nn < 0 || n_f < 0 || !nmatches || (n_f && !matches)) return ORBFE_ERR_ARG;
+    for (int i = 0; i < n_f; ++i) matches[i] = -1;
+    int nm = 0;
+    std::vector<int> hist[kHistLen];
+    int a = 0, b = 0;
+    while (a < kf_nn && b < f_nn) {
+        if (kf_node_ids[a] == f_node_ids[b]) {
+            for (int x = kf_node_off[a]; x < kf_node_off[a + 1]; ++x) {
+                const int ikf = kf_feat[x];
+                if (!kf_mp_ok[ikf]) continue;
+                const uint8_t* dkf = kf_desc + 32 * (size_t)ikf;
+                int best1 = 256, bidx = -1, best2 = 256;
+                for (int y = f_node_off[b]; y < f_node_off[b + 1]; ++y) {
+                    const int jf = f_feat[y];
+                    if (matches[jf] >= 0) continue;
+                    const int d = descriptor_distance(dkf, f_desc + 32 * (size_t)jf);
+                    if (d < best1) { best2 = best1; best1 = d; bidx = jf; }
+                    else if (d < best2) { best2 = d; }
+                }
+                if (best1 <= kThLow && (float)best1 < nnratio * (float)best2) {
+                    matches[bidx] = ikf;
+                    if (check_ori) hist[rot_bin(kf_angle[ikf], f_angle[bidx])].push_back(bidx);
+                    ++nm;
+                }
+            }
+            ++a;
+            ++b;
+        } else if (kf_node_ids[a] < f_node_ids[b]) {
+            while (a < kf_nn && kf_node_ids[a] < f_node_ids[b]) ++a;  // lower_bound
+        } else {
+            while (b < f_nn && f_node_ids[b] < kf_node_ids[a]) ++b;
+        }
+    }
+    if (check_ori) {
+        int i1, i2, i3;
+        three_maxima(hist, i1, i2, i3);
+        for (int i = 0; i < kHistLen; ++i) {
+            if (i == i1 || i == i2 || i == i3) continue;
+            for (int jf : hist[i]) { matches[jf] = -1; --nm; }
+        }
+    }
+    *nmatches = nm;
     return ORBFE_OK;
 }
 

@@ -98,6 +98,21 @@ int oracle_search_by_projection_keyframe(int check_ori, const orbfe_frame_view* 
                                          float th, int orb_dist, int32_t* nmatches);
 int oracle_distinctive_descriptors(int n_mp, const int32_t* obs_off, const uint8_t* obs_desc,
                                    int32_t* best, uint8_t* desc_out);
+/* DBoW2 (Thirdparty/DBoW2 of the reference): text vocabulary, transform, SearchByBoW. */
+typedef struct oracle_vocab oracle_vocab;
+oracle_vocab* oracle_vocab_load_text(const char* path, int* status);
+void oracle_vocab_free(oracle_vocab* v);
+int oracle_vocab_info(const oracle_vocab* v, int32_t* info);
+int oracle_bow_transform(const oracle_vocab* v, const uint8_t* desc, int n, int levelsup,
+                         int32_t* word_ids, double* values, int32_t* nw, int32_t* node_ids,
+                         int32_t* node_off, int32_t* feat, int32_t* nn);
+int oracle_search_by_bow(float nnratio, int check_ori, const uint8_t* kf_desc,
+                         const float* kf_angle, const uint8_t* kf_mp_ok,
+                         const int32_t* kf_node_ids, const int32_t* kf_node_off,
+                         const int32_t* kf_feat, int kf_nn, int n_f, const uint8_t* f_desc,
+                         const float* f_angle, const int32_t* f_node_ids,
+                         const int32_t* f_node_off, const int32_t* f_feat, int f_nn,
+                         int32_t* matches, int32_t* nmatches);
 int oracle_is_in_frustum(int n, const float* xyz, const float* normal, const float* min_dist,
                          const float* max_dist, const float* tcw, const orbfe_camera* cam,
                          float min_x, float max_x, float min_y, float max_y,

@@ -1,0 +1,715 @@
+// orbfe_bow.hip — DBoW2 on the GPU: the vocabulary tree of TemplatedVocabulary<FORB>
+// (reference Thirdparty/DBoW2, loaded from the ORBvoc.txt text format) and
+// Frame::ComputeBoW -> transform(features, BowVector, FeatureVector, levelsup)
+// (Frame.cc:513-520, TemplatedVocabulary.h:1140-1270).
+//
+//   bow_descend_kernel   one thread per descriptor walks the tree: at each level the children
+//                        in insertion order, FORB::distance (Hamming), strict '<' so the first
+//                        closest child wins; records the node at level L - levelsup and the
+//                        leaf's word id / weight (weight 0 = stopped word, dropped)
+//   bow_assemble_kernel  one workgroup per frame: LDS bitonic sorts of (word, feature) and
+//                        (node, feature) give the BowVector (ascending words; TF / TF-IDF
+//                        weights summed by repeated addition in feature order, IDF / BINARY
+//                        first value) and the FeatureVector (ascending nodes, features in
+//                        order); normalisation (L1, or L2 for L2 scoring; / nd for dot product
+//                        scoring) in double with the norm accumulated in word order, as
+//                        BowVector::normalize does
+//
+// The vocabulary lives in HBM as a CSR of children (child_off / child_ids in insertion order),
+// 32-byte node descriptors, word ids and double weights (≈ 40 B per node: ~45 MB for the
+// 1.1M-node ORBvoc).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../include/orbfe.h"
+#include "orbfe_device.hpp"
+
+namespace orbfe {
+
+constexpr int kBowMaxFeatures = 4096;  // features per frame the assembly sorts in LDS
+constexpr int kBowBlock = 1024;
+
+struct VocabDev {
+    int L, nodes, nwords, scoring, weighting;
+    const int* child_off;  // nodes + 1
+    const int* child_ids;
+    const uint4* desc;     // 2 per node
+    const int* word;       // word id (0 for nodes that are not words, as Node())
+    const double* weight;
+};
+
+struct BowArgs {
+    VocabDev v;
+    int levelsup, cap;          // cap: features per frame slot (descriptor / output stride)
+    const uint4* desc;          // [frame][cap] x 2
+    const int* n;               // [frame] features
+    int* f_word;                // [frame][cap] scratch: word, node, weight per feature
+    int* f_node;
+    double* f_w;
+    int* word_ids;              // [frame][cap]
+    double* values;             // [frame][cap]
+    int* nw;                    // [frame]
+    int* node_ids;              // [frame][cap]
+    int* node_off;              // [frame][cap + 1]
+    int* feat;                  // [frame][cap]
+    int* nn;                    // [frame]
+};
+
+__global__ __launch_bounds__(256) void bow_descend_kernel(BowArgs a) {
+    const int f = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n[f]) return;
+    const size_t o = (size_t)f * a.cap + i;
+    const uint4 q0 = a.desc[2 * o], q1 = a.desc[2 * o + 1];
+    const VocabDev& v = a.v;
+    const int nid_level = v.L - a.levelsup;
+    int nid = 0, node = 0, level = 0;
+    do {
+        ++level;
+        const int c0 = v.child_off[node], c1 = v.child_off[node + 1];
+        node = v.child_ids[c0];
+        int best = hamming256(q0, q1, v.desc[2 * node], v.desc[2 * node + 1]);
+        for (int c = c0 + 1; c < c1; ++c) {
+            const int id = v.child_ids[c];
+            const int d = hamming256(q0, q1, v.desc[2 * id], v.desc[2 * id + 1]);
+            if (d < best) {
+                best = d;
+                node = id;
+            }
+        }
+        if (level == nid_level) nid = node;
+    } while (v.child_off[node + 1] > v.child_off[node]);
+    a.f_word[o] = v.word[node];
+    a.f_node[o] = nid;
+    a.f_w[o] = v.weight[node];
+}
+
+// LDS bitonic sort of n_pad 64-bit keys by all threads of the block.
+__device__ __forceinline__ void bitonic_sort_u64(unsigned long long* k, int n_pad) {
+    for (int size = 2; size <= n_pad; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = threadIdx.x; t < n_pad / 2; t += blockDim.x) {
+                const int lo = 2 * t - (t & (stride - 1));
+                const int hi = lo + stride;
+                const bool up = ((lo & size) == 0);
+                const unsigned long long x = k[lo], y = k[hi];
+                if ((x > y) == up) {
+                    k[lo] = y;
+                    k[hi] = x;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBowBlock) void bow_assemble_kernel(BowArgs a) {
+    __shared__ unsigned long long keys[kBowMaxFeatures];
+    __shared__ double vals[kBowMaxFeatures];
+    __shared__ int pos[kBowMaxFeatures];
+    __shared__ int tmp[kBowBlock / 64 + 1];
+    __shared__ double s_norm;
+    const int f = blockIdx.x;
+    const int n = a.n[f];
+    const size_t fo = (size_t)f * a.cap;
+    int n_pad = 1;
+    while (n_pad < n) n_pad <<= 1;
+    const VocabDev& v = a.v;
+    const bool must = v.scoring != 5;                 // DotProductScoring does not normalise
+    const bool tf = v.weighting == 0 || v.weighting == 1;  // addWeight vs addIfNotExist
+    // ---- BowVector: sort (word, feature) of the kept features
+    for (int t = threadIdx.x; t < n_pad; t += kBowBlock)
+        keys[t] = (t < n && a.f_w[fo + t] > 0)
+                      ? ((unsigned long long)(unsigned)a.f_word[fo + t] << 32) | (unsigned)t
+                      : ~0ull;
+    __syncthreads();
+    bitonic_sort_u64(keys, n_pad);
+    // run heads -> compact index by a block scan over runs of kBowBlock-strided chunks
+    int base = 0;
+    for (int c = 0; c < n_pad; c += kBowBlock) {
+        const int t = c + threadIdx.x;
+        bool head = false;
+        if (t < n_pad && keys[t] != ~0ull)
+            head = t == 0 || (keys[t] >> 32) != (keys[t - 1] >> 32);
+        int total;
+        const int ex = block_exclusive_scan<kBowBlock>(head ? 1 : 0, tmp, total);
+        if (head) pos[t] = base + ex;
+        base += total;
+        __syncthreads();
+    }
+    const int nw = base;
+    // value of each word: weights summed in feature order (TF / TF-IDF) or the first (IDF /
+    // BINARY); a run's features are sorted by index, i.e. in insertion order
+    for (int c = 0; c < n_pad; c += kBowBlock) {
+        const int t = c + threadIdx.x;
+        if (t < n_pad && keys[t] != ~0ull && (t == 0 || (keys[t] >> 32) != (keys[t - 1] >> 32))) {
+            const unsigned wd = (unsigned)(keys[t] >> 32);
+            const double w = a.f_w[fo + (unsigned)(keys[t] & 0xffffffffu)];
+            double s = w;
+            if (tf)
+                for (int u = t + 1; u < n_pad && keys[u] != ~0ull && (unsigned)(keys[u] >> 32) == wd; ++u) s += w;
+            vals[pos[t]] = s;
+            a.word_ids[fo + pos[t]] = (int)wd;
+        }
+    }
+    __syncthreads();
+    __shared__ int s_div;
+    if (threadIdx.x == 0) {
+        double norm = 0.0;
+        int div = 0;
+        if (must) {  // BowVector::normalize, norm accumulated in ascending word order
+            if (v.scoring == 1) {
+                for (int i = 0; i < nw; ++i) norm += vals[i] * vals[i];
+                norm = sqrt(norm);
+            } else {
+                for (int i = 0; i < nw; ++i) norm += fabs(vals[i]);
+            }
+            div = norm > 0.0;
+        } else if (tf && nw > 0) {
+            norm = (double)nw;  // TF / TF-IDF without normalisation: / nd (1174-1180)
+            div = 1;
+        }
+        s_norm = norm;
+        s_div = div;
+        a.nw[f] = nw;
+    }
+    __syncthreads();
+    const double norm = s_norm;
+    const bool div = s_div != 0;
+    for (int i = threadIdx.x; i < nw; i += kBowBlock) a.values[fo + i] = div ? vals[i] / norm : vals[i];
+    __syncthreads();
+    // ---- FeatureVector: sort (node, feature) of the kept features
+    for (int t = threadIdx.x; t < n_pad; t += kBowBlock)
+        keys[t] = (t < n && a.f_w[fo + t] > 0)
+                      ? ((unsigned long long)(unsigned)a.f_node[fo + t] << 32) | (unsigned)t
+                      : ~0ull;
+    __syncthreads();
+    bitonic_sort_u64(keys, n_pad);
+    int* noff = a.node_off + (size_t)f * (a.cap + 1);
+    base = 0;
+    int nvalid = 0;
+    for (int c = 0; c < n_pad; c += kBowBlock) {
+        const int t = c + threadIdx.x;
+        const bool valid = t < n_pad && keys[t] != ~0ull;
+        const bool head = valid && (t == 0 || (keys[t] >> 32) != (keys[t - 1] >> 32));
+        if (valid) a.feat[fo + t] = (int)(keys[t] & 0xffffffffu);
+        int total;
+        const int ex = block_exclusive_scan<kBowBlock>(head ? 1 : 0, tmp, total);
+        if (head) {
+            a.node_ids[fo + base + ex] = (int)(keys[t] >> 32);
+            noff[base + ex] = t;  // kept features are sorted first: position = CSR offset
+        }
+        base += total;
+        nvalid += block_sum<kBowBlock>(valid ? 1 : 0, tmp);
+    }
+    if (threadIdx.x == 0) {
+        noff[base] = nvalid;
+        a.nn[f] = base;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>&) (ORBmatcher.cc:159-291).
+// The merge join over the two FeatureVectors (ascending node ids) visits the keyframe features
+// of every common node in node order, and within a node in feature order: that enumeration is
+// the greedy's point order.  Point p's candidates are the frame features of the same node, in
+// order, with their Hamming distance; a frame feature taken by an earlier point blocks it
+// (vpMapPointMatches[realIdxF] != NULL, 198-199), so orbfe_greedy.hip resolves it with every
+// acceptor blocking.
+struct BowMatchArgs {
+    int kf_nn, f_nn;
+    const int* kf_node_ids;
+    const int* kf_node_off;
+    const int* kf_feat;
+    const int* f_node_ids;
+    const int* f_node_off;
+    const int* f_feat;
+    const uint8_t* kf_ok;     // map point present and not bad
+    const uint4* kf_desc;
+    const uint4* f_desc;
+    const float* kf_angle;
+    int* pair;                // per KF node: matching F node or -1
+    int* npts;                // per KF node: points it contributes
+    const int* pbase;         // scan of npts (kf_nn + 1)
+    int* cnt;                 // per point
+    const int* off;           // scan of cnt
+    int2* cand;
+    int* pt_kf;               // per point: keyframe feature index
+    float* pt_angle;          // per point: its keypoint angle
+};
+
+__global__ __launch_bounds__(256) void bow_pair_kernel(BowMatchArgs a) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.kf_nn) return;
+    const int id = a.kf_node_ids[i];
+    int lo = 0, hi = a.f_nn;  // lower_bound in the frame's node ids
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (a.f_node_ids[mid] < id) lo = mid + 1; else hi = mid;
+    }
+    const int j = (lo < a.f_nn && a.f_node_ids[lo] == id) ? lo : -1;
+    a.pair[i] = j;
+    a.npts[i] = j >= 0 ? a.kf_node_off[i + 1] - a.kf_node_off[i] : 0;
+}
+
+// One thread per point: point p lives in KF node `node` (found by a binary search over pbase).
+template <bool FILL>
+__global__ __launch_bounds__(256) void bow_cand_kernel(BowMatchArgs a, int npoints) {
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= npoints) return;
+    int lo = 0, hi = a.kf_nn - 1;  // last node with pbase[node] <= p
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.pbase[mid] <= p) lo = mid; else hi = mid - 1;
+    }
+    const int node = lo;
+    const int ikf = a.kf_feat[a.kf_node_off[node] + (p - a.pbase[node])];
+    const int j = a.pair[node];
+    int n = 0;
+    if (a.kf_ok[ikf]) {
+        const int y0 = a.f_node_off[j], y1 = a.f_node_off[j + 1];
+        n = y1 - y0;
+        if (FILL) {
+            const uint4 q0 = a.kf_desc[2 * ikf], q1 = a.kf_desc[2 * ikf + 1];
+            int2* out = a.cand + a.off[p];
+            for (int y = y0; y < y1; ++y) {
+                const int jf = a.f_feat[y];
+                out[y - y0] = make_int2(jf, hamming256(q0, q1, a.f_desc[2 * jf], a.f_desc[2 * jf + 1]));
+            }
+        }
+    }
+    if (FILL) {
+        a.pt_kf[p] = ikf;
+        a.pt_angle[p] = a.kf_angle[ikf];
+    } else {
+        a.cnt[p] = n;
+    }
+}
+
+}  // namespace orbfe
+
+using namespace orbfe;
+
+struct orbfe_vocabulary {
+    int device = 0;
+    int k = 0, L = 0, scoring = 0, weighting = 0, nodes = 0, nwords = 0;
+    DevBuf child_off, child_ids, desc, word, weight;
+    // per-call scratch / staging (host forms)
+    DevBuf s_desc, s_n, s_word, s_node, s_w, o_wid, o_val, o_nw, o_nid, o_noff, o_feat, o_nn;
+    hipStream_t stream = nullptr;
+
+    VocabDev dev() const {
+        return VocabDev{L, nodes, nwords, scoring, weighting, child_off.as<int>(),
+                        child_ids.as<int>(), desc.as<uint4>(), word.as<int>(), weight.as<double>()};
+    }
+    ~orbfe_vocabulary() {
+        for (DevBuf* b : {&child_off, &child_ids, &desc, &word, &weight, &s_desc, &s_n, &s_word,
+                          &s_node, &s_w, &o_wid, &o_val, &o_nw, &o_nid, &o_noff, &o_feat, &o_nn})
+            b->release();
+        if (stream) hipStreamDestroy(stream);
+    }
+};
+
+namespace {
+// Builds the device tree from host node arrays (node 0 = root; parent[i] < i for i >= 1).
+int vocab_upload(orbfe_vocabulary* v, const std::vector<int>& parent,
+                 const std::vector<uint8_t>& is_word, const std::vector<uint8_t>& desc,
+                 const std::vector<double>& weight) {
+    const int n = (int)parent.size();
+    std::vector<int> cnt(n + 1, 0), off(n + 1, 0), ids(std::max(n - 1, 1)), word(n, 0);
+    for (int i = 1; i < n; ++i) {
+        if (parent[i] < 0 || parent[i] >= i) return ORBFE_ERR_ARG;
+        ++cnt[parent[i]];
+    }
+    for (int i = 0; i < n; ++i) off[i + 1] = off[i] + cnt[i];
+    std::vector<int> cur(off.begin(), off.end() - 1);
+    for (int i = 1; i < n; ++i) ids[cur[parent[i]]++] = i;  // insertion (file) order
+    int nw = 0;
+    for (int i = 1; i < n; ++i)
+        if (is_word[i]) word[i] = nw++;
+    v->nodes = n;
+    v->nwords = nw;
+    int st;
+    if ((st = v->child_off.ensure((n + 1) * sizeof(int)))) return st;
+    if ((st = v->child_ids.ensure(ids.size() * sizeof(int)))) return st;
+    if ((st = v->desc.ensure((size_t)n * 32))) return st;
+    if ((st = v->word.ensure((size_t)n * sizeof(int)))) return st;
+    if ((st = v->weight.ensure((size_t)n * sizeof(double)))) return st;
+    ORBFE_HIP(hipMemcpy(v->child_off.p, off.data(), (n + 1) * sizeof(int), hipMemcpyHostToDevice));
+    ORBFE_HIP(hipMemcpy(v->child_ids.p, ids.data(), ids.size() * sizeof(int), hipMemcpyHostToDevice));
+    ORBFE_HIP(hipMemcpy(v->desc.p, desc.data(), (size_t)n * 32, hipMemcpyHostToDevice));
+    ORBFE_HIP(hipMemcpy(v->word.p, word.data(), (size_t)n * sizeof(int), hipMemcpyHostToDevice));
+    ORBFE_HIP(hipMemcpy(v->weight.p, weight.data(), (size_t)n * sizeof(double), hipMemcpyHostToDevice));
+    return ORBFE_OK;
+}
+
+// TemplatedVocabulary::loadFromTextFile (TemplatedVocabulary.h:1351-1436).  Blank lines are
+// skipped.
+int vocab_parse_text(const char* path, int& k, int& L, int& scoring, int& weighting,
+                     std::vector<int>& parent, std::vector<uint8_t>& is_word,
+                     std::vector<uint8_t>& desc, std::vector<double>& weight) {
+    FILE* fp = std::fopen(path, "rb");
+    if (!fp) return ORBFE_ERR_ARG;
+    std::vector<char> buf;
+    {
+        std::fseek(fp, 0, SEEK_END);
+        const long sz = std::ftell(fp);
+        std::fseek(fp, 0, SEEK_SET);
+        if (sz < 0) { std::fclose(fp); return ORBFE_ERR_ARG; }
+        buf.resize((size_t)sz + 1);
+        const size_t got = std::fread(buf.data(), 1, (size_t)sz, fp);
+        buf[got] = 0;
+        buf.resize(got + 1);
+    }
+    std::fclose(fp);
+    char* p = buf.data();
+    char* end = buf.data() + buf.size() - 1;
+    auto line_end = [&](char* s) { char* e = s; while (e < end && *e != '\n') ++e; return e; };
+    char* e = line_end(p);
+    *e = 0;
+    int n1 = -1, n2 = -1;
+    if (std::sscanf(p, "%d %d %d %d", &k, &L, &n1, &n2) != 4 || k < 0 || k > 20 || L < 1 ||
+        L > 10 || n1 < 0 || n1 > 5 || n2 < 0 || n2 > 3)
+        return ORBFE_ERR_ARG;
+    scoring = n1;
+    weighting = n2;
+    parent.assign(1, 0);
+    is_word.assign(1, 0);
+    desc.assign(32, 0);
+    weight.assign(1, 0.0);
+    p = e < end ? e + 1 : end;
+    while (p < end) {
+        e = line_end(p);
+        *e = 0;
+        char* q = p;
+        while (*q == ' ' || *q == '\t' || *q == '\r') ++q;
+        if (*q) {
+            char* r;
+            const int pid = (int)std::strtol(q, &r, 10); q = r;
+            const int leaf = (int)std::strtol(q, &r, 10); q = r;
+            uint8_t d[32];
+            for (int i = 0; i < 32; ++i) { d[i] = (uint8_t)std::strtol(q, &r, 10); q = r; }
+            const double w = std::strtod(q, &r);
+            if (pid < 0 || pid >= (int)parent.size()) return ORBFE_ERR_ARG;
+            parent.push_back(pid);
+            is_word.push_back(leaf > 0);
+            desc.insert(desc.end(), d, d + 32);
+            weight.push_back(w);
+        }
+        p = e + 1;
+    }
+    return ORBFE_OK;
+}
+}  // namespace
+
+extern "C" {
+
+orbfe_vocabulary* orbfe_vocabulary_load_text(const char* path, int device, int* status) {
+    int st = check_device(device);
+    orbfe_vocabulary* v = nullptr;
+    try {
+        if (st == ORBFE_OK && !path) st = ORBFE_ERR_ARG;
+        if (st == ORBFE_OK) {
+            DeviceGuard dg(device);
+            v = new orbfe_vocabulary();
+            v->device = device;
+            std::vector<int> parent;
+            std::vector<uint8_t> is_word, desc;
+            std::vector<double> weight;
+            st = vocab_parse_text(path, v->k, v->L, v->scoring, v->weighting, parent, is_word,
+                                  desc, weight);
+            if (st == ORBFE_OK) st = vocab_upload(v, parent, is_word, desc, weight);
+            if (st == ORBFE_OK && hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) != hipSuccess)
+                st = ORBFE_ERR_HIP;
+        }
+    } catch (const std::bad_alloc&) {
+        st = ORBFE_ERR_NOMEM;
+    } catch (...) {
+        st = ORBFE_ERR_HIP;
+    }
+    if (st != ORBFE_OK && v) {
+        delete v;
+        v = nullptr;
+    }
+    if (status) *status = st;
+    return v;
+}
+
+orbfe_vocabulary* orbfe_vocabulary_create(int k, int L, int scoring, int weighting, int n_nodes,
+                                          const int32_t* parent, const uint8_t* is_word,
+                                          const uint8_t* desc, const double* weight, int device,
+                                          int* status) {
+    int st = check_device(device);
+    orbfe_vocabulary* v = nullptr;
+    try {
+        if (st == ORBFE_OK && (n_nodes < 1 || !parent || !is_word || !desc || !weight || k < 0 ||
+                               L < 1 || scoring < 0 || scoring > 5 || weighting < 0 || weighting > 3))
+            st = ORBFE_ERR_ARG;
+        if (st == ORBFE_OK) {
+            DeviceGuard dg(device);
+            v = new orbfe_vocabulary();
+            v->device = device;
+            v->k = k;
+            v->L = L;
+            v->scoring = scoring;
+            v->weighting = weighting;
+            st = vocab_upload(v, std::vector<int>(parent, parent + n_nodes),
+                              std::vector<uint8_t>(is_word, is_word + n_nodes),
+                              std::vector<uint8_t>(desc, desc + (size_t)n_nodes * 32),
+                              std::vector<double>(weight, weight + n_nodes));
+            if (st == ORBFE_OK && hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) != hipSuccess)
+                st = ORBFE_ERR_HIP;
+        }
+    } catch (const std::bad_alloc&) {
+        st = ORBFE_ERR_NOMEM;
+    } catch (...) {
+        st = ORBFE_ERR_HIP;
+    }
+    if (st != ORBFE_OK && v) {
+        delete v;
+        v = nullptr;
+    }
+    if (status) *status = st;
+    return v;
+}
+
+void orbfe_vocabulary_destroy(orbfe_vocabulary* v) {
+    if (!v) return;
+    DeviceGuard dg(v->device);
+    if (v->stream) hipStreamSynchronize(v->stream);
+    delete v;
+}
+
+int orbfe_vocabulary_info(const orbfe_vocabulary* v, int32_t* info) {
+    if (!v || !info) return ORBFE_ERR_ARG;
+    info[0] = v->k;
+    info[1] = v->L;
+    info[2] = v->scoring;
+    info[3] = v->weighting;
+    info[4] = v->nodes;
+    info[5] = v->nwords;
+    return ORBFE_OK;
+}
+
+int orbfe_vocabulary_set_stream(orbfe_vocabulary* v, void* hip_stream) {
+    if (!v) return ORBFE_ERR_ARG;
+    if (hip_stream) {
+        v->stream = static_cast<hipStream_t>(hip_stream);  // caller-owned from now on
+    }
+    return ORBFE_OK;
+}
+
+static int bow_launch(orbfe_vocabulary* v, int nframes, int cap, const uint8_t* d_desc,
+                      const int32_t* d_n, int levelsup, int32_t* d_word_ids, double* d_values,
+                      int32_t* d_nw, int32_t* d_node_ids, int32_t* d_node_off, int32_t* d_feat,
+                      int32_t* d_nn) {
+    int st;
+    const size_t tot = (size_t)nframes * cap;
+    if ((st = v->s_word.ensure(std::max<size_t>(tot, 1) * sizeof(int)))) return st;
+    if ((st = v->s_node.ensure(std::max<size_t>(tot, 1) * sizeof(int)))) return st;
+    if ((st = v->s_w.ensure(std::max<size_t>(tot, 1) * sizeof(double)))) return st;
+    BowArgs a;
+    a.v = v->dev();
+    a.levelsup = levelsup;
+    a.cap = cap;
+    a.desc = reinterpret_cast<const uint4*>(d_desc);
+    a.n = d_n;
+    a.f_word = v->s_word.as<int>();
+    a.f_node = v->s_node.as<int>();
+    a.f_w = v->s_w.as<double>();
+    a.word_ids = d_word_ids;
+    a.values = d_values;
+    a.nw = d_nw;
+    a.node_ids = d_node_ids;
+    a.node_off = d_node_off;
+    a.feat = d_feat;
+    a.nn = d_nn;
+    if (v->nwords > 0) {
+        hipLaunchKernelGGL(bow_descend_kernel, dim3((cap + 255) / 256, nframes), dim3(256), 0,
+                           v->stream, a);
+    } else {  // empty() vocabulary: transform returns empty vectors
+        ORBFE_HIP(hipMemsetAsync(v->s_w.p, 0, tot * sizeof(double), v->stream));
+    }
+    hipLaunchKernelGGL(bow_assemble_kernel, dim3(nframes), dim3(kBowBlock), 0, v->stream, a);
+    ORBFE_HIP(hipGetLastError());
+    return ORBFE_OK;
+}
+
+int orbfe_search_by_bow(orbfe_matcher* m, float nnratio, int check_ori, int n_kf,
+                        const uint8_t* kf_desc, const float* kf_angle, const uint8_t* kf_mp_ok,
+                        int kf_nn, const int32_t* kf_node_ids, const int32_t* kf_node_off,
+                        const int32_t* kf_feat, int n_f, const uint8_t* f_desc,
+                        const float* f_angle, int f_nn, const int32_t* f_node_ids,
+                        const int32_t* f_node_off, const int32_t* f_feat, int32_t* matches,
+                        int32_t* nmatches) {
+    if (n_kf < 0 || n_f < 0 || kf_nn < 0 || f_nn < 0 || !nmatches || (n_f && !matches) ||
+        (n_kf && (!kf_desc || !kf_angle || !kf_mp_ok)) || (n_f && (!f_desc || !f_angle)) ||
+        (kf_nn && (!kf_node_ids || !kf_node_off || !kf_feat)) ||
+        (f_nn && (!f_node_ids || !f_node_off || !f_feat)))
+        return ORBFE_ERR_ARG;
+    const int kf_tot = kf_nn ? kf_node_off[kf_nn] : 0, f_tot = f_nn ? f_node_off[f_nn] : 0;
+    for (int i = 0; i < kf_tot; ++i)
+        if (kf_feat[i] < 0 || kf_feat[i] >= n_kf) return ORBFE_ERR_ARG;
+    for (int i = 0; i < f_tot; ++i)
+        if (f_feat[i] < 0 || f_feat[i] >= n_f) return ORBFE_ERR_ARG;
+    return guarded(m, [&]() {
+        int st;
+        for (int i = 0; i < n_f; ++i) matches[i] = -1;  // vpMapPointMatches = NULL (164)
+        *nmatches = 0;
+        if (!kf_nn || !f_nn || !n_f) return ORBFE_OK;
+        BowMatchArgs a;
+        if ((st = m->up(m->fa_d, kf_desc, (size_t)n_kf * 32))) return st;
+        if ((st = m->up(m->fb_d, f_desc, (size_t)n_f * 32))) return st;
+        if ((st = m->up(m->m_f0, kf_angle, (size_t)n_kf * 4))) return st;
+        if ((st = m->up(m->m_u0, kf_mp_ok, n_kf))) return st;
+        if ((st = m->up(m->m_i0, kf_node_ids, (size_t)kf_nn * 4))) return st;
+        if ((st = m->up(m->m_i1, kf_node_off, (size_t)(kf_nn + 1) * 4))) return st;
+        if ((st = m->up(m->o_i, kf_feat, (size_t)kf_tot * 4))) return st;
+        if ((st = m->up(m->fb_cs, f_node_ids, (size_t)f_nn * 4))) return st;
+        if ((st = m->up(m->fb_ci, f_node_off, (size_t)(f_nn + 1) * 4))) return st;
+        if ((st = m->up(m->fb_co, f_feat, (size_t)f_tot * 4))) return st;
+        if ((st = m->s1.ensure((size_t)kf_nn * 4 + 16))) return st;  // pair
+        if ((st = m->s2.ensure((size_t)kf_nn * 4 + 16))) return st;  // npts
+        if ((st = m->s3.ensure((size_t)(kf_nn + 1) * 4 + 16))) return st;  // pbase
+        a.kf_nn = kf_nn;
+        a.f_nn = f_nn;
+        a.kf_node_ids = m->m_i0.as<int>();
+        a.kf_node_off = m->m_i1.as<int>();
+        a.kf_feat = m->o_i.as<int>();
+        a.f_node_ids = m->fb_cs.as<int>();
+        a.f_node_off = m->fb_ci.as<int>();
+        a.f_feat = m->fb_co.as<int>();
+        a.kf_ok = m->m_u0.as<uint8_t>();
+        a.kf_desc = m->fa_d.as<uint4>();
+        a.f_desc = m->fb_d.as<uint4>();
+        a.kf_angle = m->m_f0.as<float>();
+        a.pair = m->s1.as<int>();
+        a.npts = m->s2.as<int>();
+        a.pbase = m->s3.as<int>();
+        hipLaunchKernelGGL(bow_pair_kernel, dim3((kf_nn + 255) / 256), dim3(256), 0, m->stream, a);
+        hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, m->stream, a.npts, kf_nn, m->s3.as<int>());
+        int P = 0;
+        ORBFE_HIP(hipMemcpyAsync(&P, m->s3.as<int>() + kf_nn, sizeof(int), hipMemcpyDeviceToHost, m->stream));
+        ORBFE_HIP(hipStreamSynchronize(m->stream));
+        if (P == 0) return ORBFE_OK;
+        if ((st = m->s4.ensure((size_t)P * 4 + 16))) return st;       // pt_kf
+        if ((st = m->s5.ensure((size_t)P * 4 + 16))) return st;       // pt_angle
+        a.pt_kf = m->s4.as<int>();
+        a.pt_angle = m->s5.as<float>();
+        if ((st = m->cnt.ensure((size_t)P * 4))) return st;
+        if ((st = m->off.ensure((size_t)(P + 1) * 4))) return st;
+        a.cnt = m->cnt.as<int>();
+        a.off = m->off.as<int>();
+        const int pb = (P + 255) / 256;
+        hipLaunchKernelGGL(bow_cand_kernel<false>, dim3(pb), dim3(256), 0, m->stream, a, P);
+        hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, m->stream, a.cnt, P, m->off.as<int>());
+        int total = 0;
+        ORBFE_HIP(hipMemcpyAsync(&total, m->off.as<int>() + P, sizeof(int), hipMemcpyDeviceToHost, m->stream));
+        ORBFE_HIP(hipStreamSynchronize(m->stream));
+        if ((st = m->cand.ensure(std::max(total, 1) * sizeof(int2)))) return st;
+        a.cand = m->cand.as<int2>();
+        hipLaunchKernelGGL(bow_cand_kernel<true>, dim3(pb), dim3(256), 0, m->stream, a, P);
+        // frame slots start empty; every acceptor blocks its slot for later points
+        std::vector<int32_t> empty(n_f, -1);
+        if ((st = m->up(m->fa_k, empty.data(), (size_t)n_f * 4))) return st;
+        // greedy_accept reads the slot keypoint's angle through k[s].angle: stage the frame
+        // angles as keypoints
+        std::vector<orbfe_keypoint> fk(n_f);
+        for (int i = 0; i < n_f; ++i) fk[i] = orbfe_keypoint{0.f, 0.f, 0.f, f_angle[i], 0.f, 0, -1};
+        if ((st = m->up(m->fb_k, fk.data(), (size_t)n_f * sizeof(orbfe_keypoint)))) return st;
+        GreedyArgs g{};
+        g.m = P;
+        g.nkp = n_f;
+        g.mode = kGreedyBow;
+        g.nnratio = nnratio;
+        g.off = m->off.as<int>();
+        g.cand = m->cand.as<int2>();
+        g.nobs = nullptr;
+        g.fmp0 = g.fmp = m->fa_k.as<int>();
+        g.fobs0 = g.fobs = nullptr;
+        g.check_ori = check_ori;
+        g.q_angle = a.pt_angle;
+        g.k = m->fb_k.as<orbfe_keypoint>();
+        g.ids = a.pt_kf;
+        if ((st = m->greedy(g))) return st;
+        if ((st = m->down(matches, m->fa_k, (size_t)n_f * 4))) return st;
+        if ((st = m->down(nmatches, m->scal, sizeof(int)))) return st;
+        ORBFE_HIP(hipStreamSynchronize(m->stream));
+        return ORBFE_OK;
+    });
+}
+
+int orbfe_bow_transform(orbfe_vocabulary* v, const uint8_t* desc, int n, int levelsup,
+                        int32_t* word_ids, double* values, int32_t* nw, int32_t* node_ids,
+                        int32_t* node_off, int32_t* feat, int32_t* nn) {
+    if (!v || n < 0 || (n && !desc) || !nw || !nn || !word_ids || !values || !node_ids ||
+        !node_off || !feat)
+        return ORBFE_ERR_ARG;
+    if (n > kBowMaxFeatures) return ORBFE_ERR_UNSUPPORTED;
+    try {
+        DeviceGuard dg(v->device);
+        int st;
+        const int cap = std::max(n, 1);
+        if ((st = v->s_desc.ensure((size_t)cap * 32))) return st;
+        if ((st = v->s_n.ensure(16))) return st;
+        if ((st = v->o_wid.ensure((size_t)cap * 4))) return st;
+        if ((st = v->o_val.ensure((size_t)cap * 8))) return st;
+        if ((st = v->o_nid.ensure((size_t)cap * 4))) return st;
+        if ((st = v->o_noff.ensure((size_t)(cap + 1) * 4))) return st;
+        if ((st = v->o_feat.ensure((size_t)cap * 4))) return st;
+        if ((st = v->o_nw.ensure(16))) return st;
+        if ((st = v->o_nn.ensure(16))) return st;
+        if (n) ORBFE_HIP(hipMemcpyAsync(v->s_desc.p, desc, (size_t)n * 32, hipMemcpyHostToDevice, v->stream));
+        ORBFE_HIP(hipMemcpyAsync(v->s_n.p, &n, sizeof(int), hipMemcpyHostToDevice, v->stream));
+        if ((st = bow_launch(v, 1, cap, v->s_desc.as<uint8_t>(), v->s_n.as<int32_t>(), levelsup,
+                             v->o_wid.as<int32_t>(), v->o_val.as<double>(), v->o_nw.as<int32_t>(),
+                             v->o_nid.as<int32_t>(), v->o_noff.as<int32_t>(),
+                             v->o_feat.as<int32_t>(), v->o_nn.as<int32_t>())))
+            return st;
+        int cnt[2] = {0, 0};
+        ORBFE_HIP(hipMemcpyAsync(&cnt[0], v->o_nw.p, sizeof(int), hipMemcpyDeviceToHost, v->stream));
+        ORBFE_HIP(hipMemcpyAsync(&cnt[1], v->o_nn.p, sizeof(int), hipMemcpyDeviceToHost, v->stream));
+        ORBFE_HIP(hipStreamSynchronize(v->stream));
+        *nw = cnt[0];
+        *nn = cnt[1];
+        int nfeat = 0;
+        ORBFE_HIP(hipMemcpy(word_ids, v->o_wid.p, (size_t)cnt[0] * 4, hipMemcpyDeviceToHost));
+        ORBFE_HIP(hipMemcpy(values, v->o_val.p, (size_t)cnt[0] * 8, hipMemcpyDeviceToHost));
+        ORBFE_HIP(hipMemcpy(node_ids, v->o_nid.p, (size_t)cnt[1] * 4, hipMemcpyDeviceToHost));
+        ORBFE_HIP(hipMemcpy(node_off, v->o_noff.p, (size_t)(cnt[1] + 1) * 4, hipMemcpyDeviceToHost));
+        nfeat = cnt[1] ? node_off[cnt[1]] : 0;
+        if (!cnt[1]) node_off[0] = 0;
+        ORBFE_HIP(hipMemcpy(feat, v->o_feat.p, (size_t)nfeat * 4, hipMemcpyDeviceToHost));
+        return ORBFE_OK;
+    } catch (const std::bad_alloc&) {
+        return ORBFE_ERR_NOMEM;
+    } catch (...) {
+        return ORBFE_ERR_HIP;
+    }
+}
+
+int orbfe_bow_transform_batch_device(orbfe_vocabulary* v, int nframes, const uint8_t* d_desc,
+                                     const int32_t* d_n, int cap, int levelsup,
+                                     int32_t* d_word_ids, double* d_values, int32_t* d_nw,
+                                     int32_t* d_node_ids, int32_t* d_node_off, int32_t* d_feat,
+                                     int32_t* d_nn) {
+    if (!v || nframes < 0 || cap < 1 || !d_desc || !d_n || !d_word_ids || !d_values || !d_nw ||
+        !d_node_ids || !d_node_off || !d_feat || !d_nn)
+        return ORBFE_ERR_ARG;
+    if (cap > kBowMaxFeatures) return ORBFE_ERR_UNSUPPORTED;
+    if (nframes == 0) return ORBFE_OK;
+    try {
+        DeviceGuard dg(v->device);
+        return bow_launch(v, nframes, cap, d_desc, d_n, levelsup, d_word_ids, d_values, d_nw,
+                          d_node_ids, d_node_off, d_feat, d_nn);
+    } catch (...) {
+        return ORBFE_ERR_HIP;
+    }
+}
+
+}  // extern "C"

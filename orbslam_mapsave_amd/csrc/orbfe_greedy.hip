@@ -29,6 +29,7 @@ namespace orbfe {
 constexpr int kGreedyBlock = 256;
 constexpr int kGreedyLocal = 0;  // SBP local map: TH_HIGH + same-level ratio test (110-119)
 constexpr int kGreedyMaxD = 1;   // best <= max_dist (last frame 1411, keyframe 1545)
+constexpr int kGreedyBow = 2;    // SearchByBoW: best <= TH_LOW && best < nnratio * second (236-238)
 
 struct GreedyArgs {
     int m, nkp, mode, max_dist;
@@ -85,6 +86,18 @@ __device__ __forceinline__ int greedy_decide(const GreedyArgs& a, const int* Tc,
         if (best > 100) return -1;  // TH_HIGH
         if (bl == sl && best > a.nnratio * second) return -1;
         return bi;
+    }
+    if (a.mode == kGreedyBow) {
+        int best = 256, second = 256, bi = -1;
+        for (int e = e0; e < e1; ++e) {
+            const int2 c = a.cand[e];
+            if (Tc[c.x] < i) continue;
+            const int d = c.y & 0xffff;
+            if (d < best) { second = best; best = d; bi = c.x; }
+            else if (d < second) { second = d; }
+        }
+        if (best > 50) return -1;  // TH_LOW
+        return (float)best < a.nnratio * (float)second ? bi : -1;
     }
     int best = 256, bi = -1;
     for (int e = e0; e < e1; ++e) {

@@ -6,3 +6,4 @@
 #include "orbfe_match.hip"
 #include "orbfe_greedy.hip"
 #include "orbfe_match_api.hip"
+#include "orbfe_bow.hip"

@@ -38,7 +38,10 @@ EXPORTED = [
     "orbfe_search_by_projection_local", "orbfe_search_by_projection_last",
     "orbfe_search_by_projection_keyframe", "orbfe_distinctive_descriptors",
     "orbfe_distinctive_descriptors_device", "orbfe_search_local_points_device",
-    "orbfe_matcher_last_rounds", "orbfe_is_in_frustum",
+    "orbfe_matcher_last_rounds", "orbfe_is_in_frustum", "orbfe_vocabulary_load_text",
+    "orbfe_vocabulary_create", "orbfe_vocabulary_destroy", "orbfe_vocabulary_info",
+    "orbfe_vocabulary_set_stream", "orbfe_bow_transform", "orbfe_bow_transform_batch_device",
+    "orbfe_search_by_bow",
 ]
 
 
@@ -61,6 +64,11 @@ def lib() -> C.CDLL:
             L.orbfe_matcher_create.restype = C.c_void_p
             L.orbfe_matcher_create.argtypes = [C.c_int, C.c_void_p]
             L.orbfe_matcher_destroy.argtypes = [C.c_void_p]
+        if hasattr(L, "orbfe_vocabulary_load_text"):
+            L.orbfe_vocabulary_load_text.restype = C.c_void_p
+            L.orbfe_vocabulary_load_text.argtypes = [C.c_char_p, C.c_int, C.c_void_p]
+            L.orbfe_vocabulary_create.restype = C.c_void_p
+            L.orbfe_vocabulary_destroy.argtypes = [C.c_void_p]
         _lib = L
     return _lib
 
@@ -305,6 +313,61 @@ class ORBextractor:
             return out[:n.value].copy()
 
 
+class Vocabulary:
+    """ORBVocabulary (DBoW2 TemplatedVocabulary<FORB>) held in HBM: loadFromTextFile and
+    transform (Frame::ComputeBoW)."""
+
+    def __init__(self, path: str, device: int = 0):
+        st = C.c_int(0)
+        h = lib().orbfe_vocabulary_load_text(path.encode(), device, C.byref(st))
+        if not h:
+            raise OrbfeError("orbfe_vocabulary_load_text", st.value)
+        self._h = C.c_void_p(h)
+        info = np.zeros(6, np.int32)
+        _check("orbfe_vocabulary_info", lib().orbfe_vocabulary_info(self._h, ptr(info)))
+        self.k, self.L, self.scoring, self.weighting, self.nodes, self.words = map(int, info)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().orbfe_vocabulary_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def transform(self, desc: np.ndarray, levelsup: int = 4):
+        """-> (word_ids, values, node_ids, node_off, feat) = BowVector + FeatureVector."""
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = len(d)
+        cap = max(n, 1)
+        wid = np.zeros(cap, np.int32)
+        val = np.zeros(cap, np.float64)
+        nid = np.zeros(cap, np.int32)
+        off = np.zeros(cap + 1, np.int32)
+        feat = np.zeros(cap, np.int32)
+        nw, nn = C.c_int32(0), C.c_int32(0)
+        _check("orbfe_bow_transform", lib().orbfe_bow_transform(
+            self._h, ptr(d), n, levelsup, ptr(wid), ptr(val), C.byref(nw), ptr(nid), ptr(off),
+            ptr(feat), C.byref(nn)))
+        return (wid[:nw.value].copy(), val[:nw.value].copy(), nid[:nn.value].copy(),
+                off[:nn.value + 1].copy(), feat[:off[nn.value]].copy())
+
+    def transform_batch_device(self, nframes: int, d_desc: int, d_n: int, cap: int,
+                               levelsup: int, d_wid: int, d_val: int, d_nw: int, d_nid: int,
+                               d_noff: int, d_feat: int, d_nn: int) -> None:
+        _check("orbfe_bow_transform_batch_device", lib().orbfe_bow_transform_batch_device(
+            self._h, nframes, C.c_void_p(d_desc), C.c_void_p(d_n), cap, levelsup,
+            C.c_void_p(d_wid), C.c_void_p(d_val), C.c_void_p(d_nw), C.c_void_p(d_nid),
+            C.c_void_p(d_noff), C.c_void_p(d_feat), C.c_void_p(d_nn)))
+
+    def set_stream(self, stream_handle: int | None) -> None:
+        _check("orbfe_vocabulary_set_stream", lib().orbfe_vocabulary_set_stream(
+            self._h, C.c_void_p(stream_handle) if stream_handle else None))
+
+
 class ORBmatcher:
     """``ORBmatcher(nnratio=0.6, checkOri=true)`` (ORBmatcher.cc:41-43), GPU-backed."""
 
@@ -487,6 +550,24 @@ class ORBmatcher:
 
     def last_rounds(self) -> int:
         return lib().orbfe_matcher_last_rounds(self._h)
+
+    def SearchByBoW(self, kf_desc, kf_angle, kf_mp_ok, kf_fv, f_desc, f_angle, f_fv):
+        """SearchByBoW(KeyFrame*, Frame&, vpMapPointMatches) (ORBmatcher.cc:159-291); *_fv are
+        (node_ids, node_off, feat) FeatureVectors.  Returns (matches per frame feature, n)."""
+        kd = np.ascontiguousarray(kf_desc, np.uint8).reshape(-1, 32)
+        fd = np.ascontiguousarray(f_desc, np.uint8).reshape(-1, 32)
+        ka = np.ascontiguousarray(kf_angle, np.float32)
+        fa = np.ascontiguousarray(f_angle, np.float32)
+        ok = np.ascontiguousarray(kf_mp_ok, np.uint8)
+        kn, ko, kfe = (np.ascontiguousarray(x, np.int32) for x in kf_fv)
+        fn, fo, ffe = (np.ascontiguousarray(x, np.int32) for x in f_fv)
+        out = np.zeros(len(fd), np.int32)
+        nm = C.c_int32(0)
+        _check("orbfe_search_by_bow", lib().orbfe_search_by_bow(
+            self._h, C.c_float(self.mfNNratio), int(self.mbCheckOrientation), len(kd), ptr(kd),
+            ptr(ka), ptr(ok), len(kn), ptr(kn), ptr(ko), ptr(kfe), len(fd), ptr(fd), ptr(fa),
+            len(fn), ptr(fn), ptr(fo), ptr(ffe), ptr(out), C.byref(nm)))
+        return out, nm.value
 
     def is_in_frustum(self, xyz, normal, min_dist, max_dist, tcw, cam: Camera, bounds,
                       log_scale: float, cos_limit: float = 0.5):

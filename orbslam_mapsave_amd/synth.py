@@ -191,3 +191,40 @@ def synthetic_local_map(keys: np.ndarray, desc: np.ndarray, m: int = 50_000, see
                 frame_mp=fmp.astype(np.int32),
                 frame_mp_obs=np.where(fmp >= 0, rng.integers(0, 3, n), 0).astype(np.int32),
                 tcw=np.hstack([np.eye(3), np.zeros((3, 1))]).astype(np.float32))
+
+
+def synthetic_vocabulary_text(path: str, k: int = 10, L: int = 4, seed: int = 0,
+                              scoring: int = 0, weighting: int = 0,
+                              anchors: np.ndarray | None = None) -> None:
+    """Writes a DBoW2 TemplatedVocabulary<FORB> text file (the ORBvoc.txt format,
+    TemplatedVocabulary.h:1351-1436 / saveToTextFile): header "k L scoring weighting", then one
+    line per node in id order "parent isLeaf d0 .. d31 weight" with weights printed like
+    iostream's default (6 significant digits).  A complete k-ary tree of depth L: level-1
+    centroids are `anchors` rows (e.g. real ORB descriptors) or random bytes, every child is its
+    parent with ~12% of the bits flipped; leaf weights are idf-like, 3% stopped (0).  The file
+    ends with a newline, as saveToTextFile writes it."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    lines = [f"{k} {L}  {scoring} {weighting}"]
+    parents = [0]           # node ids of the previous level
+    descs = {0: None}
+    nid = 1
+    for level in range(1, L + 1):
+        nxt = []
+        leaf = level == L
+        for p in parents:
+            for c in range(k):
+                if level == 1:
+                    d = (anchors[c % len(anchors)] if anchors is not None
+                         else rng.integers(0, 256, 32, dtype=np.uint8))
+                else:
+                    bits = np.unpackbits(descs[p])
+                    bits ^= (rng.uniform(size=256) < 0.12).astype(np.uint8)
+                    d = np.packbits(bits)
+                descs[nid] = d
+                w = 0.0 if (leaf and rng.uniform() < 0.03) else (rng.uniform(0.5, 8.0) if leaf else 0.0)
+                lines.append(f"{p} {int(leaf)} " + " ".join(str(int(x)) for x in d) + f" {w:.6g}")
+                nxt.append(nid)
+                nid += 1
+        parents = nxt
+    with open(path, "w") as fh:
+        fh.write("\n".join(lines) + "\n")
