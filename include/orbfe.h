@@ -422,7 +422,8 @@ int orbfe_bow_transform_batch_device(orbfe_vocabulary* v, int nframes, const uin
  * 0.75, checkOri true).  Keyframe: n_kf descriptors, keypoint angles (mvKeysUn), kf_mp_ok[i] =
  * GetMapPointMatches()[i] != NULL && !isBad(), its FeatureVector (kf_nn nodes, CSR).  Frame: n_f
  * descriptors, angles (mvKeys) and FeatureVector.  matches[f] = the keyframe feature whose map
- * point lands in vpMapPointMatches[f], or -1; *nmatches as returned. */
+ * point lands in vpMapPointMatches[f], or -1; *nmatches as returned.  A common node holding more
+ * than 256 frame features returns ORBFE_ERR_UNSUPPORTED (ORBvoc level-2 nodes hold ~10). */
 int orbfe_search_by_bow(orbfe_matcher* m, float nnratio, int check_ori, int n_kf,
                         const uint8_t* kf_desc, const float* kf_angle, const uint8_t* kf_mp_ok,
                         int kf_nn, const int32_t* kf_node_ids, const int32_t* kf_node_off,

@@ -215,12 +215,6 @@ __global__ __launch_bounds__(kBowBlock) void bow_assemble_kernel(BowArgs a) {
 
 // ---------------------------------------------------------------------------------------------
 // ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>&) (ORBmatcher.cc:159-291).
-// The merge join over the two FeatureVectors (ascending node ids) visits the keyframe features
-// of every common node in node order, and within a node in feature order: that enumeration is
-// the greedy's point order.  Point p's candidates are the frame features of the same node, in
-// order, with their Hamming distance; a frame feature taken by an earlier point blocks it
-// (vpMapPointMatches[realIdxF] != NULL, 198-199), so orbfe_greedy.hip resolves it with every
-// acceptor blocking.
 struct BowMatchArgs {
     int kf_nn, f_nn;
     const int* kf_node_ids;
@@ -232,63 +226,136 @@ struct BowMatchArgs {
     const uint8_t* kf_ok;     // map point present and not bad
     const uint4* kf_desc;
     const uint4* f_desc;
-    const float* kf_angle;
-    int* pair;                // per KF node: matching F node or -1
-    int* npts;                // per KF node: points it contributes
-    const int* pbase;         // scan of npts (kf_nn + 1)
-    int* cnt;                 // per point
-    const int* off;           // scan of cnt
-    int2* cand;
-    int* pt_kf;               // per point: keyframe feature index
-    float* pt_angle;          // per point: its keypoint angle
+    const float* kf_angle;    // pKF->mvKeysUn[i].angle
+    const float* f_angle;     // F.mvKeys[i].angle
 };
 
-__global__ __launch_bounds__(256) void bow_pair_kernel(BowMatchArgs a) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= a.kf_nn) return;
-    const int id = a.kf_node_ids[i];
-    int lo = 0, hi = a.f_nn;  // lower_bound in the frame's node ids
+// SearchByBoW.  A frame feature belongs to exactly one vocabulary node, so the
+// blocking (vpMapPointMatches[realIdxF] != NULL) only couples keyframe features of the same
+// common node: each node's loop (198-245) is run by one wave, in the reference's order, and
+// the nodes run in parallel.  Lanes hold the node's frame features (candidate rank r = lane +
+// 64 j, i.e. vIndicesF order); for each keyframe feature the wave computes every unmatched
+// candidate's distance, best = min (distance << 16 | rank) -- the first minimum in order --
+// and second = the smallest distance of the other candidates, which is exactly what the
+// sequential best/second update yields.  The rotation histogram is accumulated in global
+// atomics; bow_ori_kernel then applies ComputeThreeMaxima (259-281) and clears the slots of
+// the non-top bins.
+constexpr int kBowSearchBlock = 256;   // 4 waves = 4 nodes per workgroup
+constexpr int kBowNodeMax = 256;  // frame features per node handled in registers (4 per lane)
+__device__ __forceinline__ int bow_pair_of(const BowMatchArgs& a, int na) {
+    const int id = a.kf_node_ids[na];
+    int lo = 0, hi = a.f_nn;  // FeatureVector::lower_bound in the frame's nodes
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
         if (a.f_node_ids[mid] < id) lo = mid + 1; else hi = mid;
     }
-    const int j = (lo < a.f_nn && a.f_node_ids[lo] == id) ? lo : -1;
-    a.pair[i] = j;
-    a.npts[i] = j >= 0 ? a.kf_node_off[i + 1] - a.kf_node_off[i] : 0;
+    return (lo < a.f_nn && a.f_node_ids[lo] == id) ? lo : -1;
 }
 
-// One thread per point: point p lives in KF node `node` (found by a binary search over pbase).
-template <bool FILL>
-__global__ __launch_bounds__(256) void bow_cand_kernel(BowMatchArgs a, int npoints) {
-    const int p = blockIdx.x * 256 + threadIdx.x;
-    if (p >= npoints) return;
-    int lo = 0, hi = a.kf_nn - 1;  // last node with pbase[node] <= p
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (a.pbase[mid] <= p) lo = mid; else hi = mid - 1;
-    }
-    const int node = lo;
-    const int ikf = a.kf_feat[a.kf_node_off[node] + (p - a.pbase[node])];
-    const int j = a.pair[node];
-    int n = 0;
-    if (a.kf_ok[ikf]) {
-        const int y0 = a.f_node_off[j], y1 = a.f_node_off[j + 1];
-        n = y1 - y0;
-        if (FILL) {
-            const uint4 q0 = a.kf_desc[2 * ikf], q1 = a.kf_desc[2 * ikf + 1];
-            int2* out = a.cand + a.off[p];
-            for (int y = y0; y < y1; ++y) {
-                const int jf = a.f_feat[y];
-                out[y - y0] = make_int2(jf, hamming256(q0, q1, a.f_desc[2 * jf], a.f_desc[2 * jf + 1]));
+// hist (30 bins), nm and status live in global memory, zeroed before the launch; one wave per
+// keyframe node over as many workgroups as needed.
+__global__ __launch_bounds__(kBowSearchBlock) void bow_search_kernel(BowMatchArgs a, float nnratio,
+                                                                     int check_ori, int* matches,
+                                                                     int* bins, int* hist, int* nm,
+                                                                     int* status) {
+    const int lane = threadIdx.x & 63;
+    const int na = blockIdx.x * (kBowSearchBlock / 64) + (threadIdx.x >> 6);
+    if (na < a.kf_nn) {
+        const int fb = bow_pair_of(a, na);
+        if (fb < 0) return;
+        const int y0 = a.f_node_off[fb], ny = a.f_node_off[fb + 1] - y0;
+        if (ny > kBowNodeMax) {
+            if (lane == 0) atomicExch(status, ORBFE_ERR_UNSUPPORTED);
+            return;
+        }
+        int jf[4];
+        uint4 d0[4], d1[4];
+        bool free_[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int r = lane + 64 * j;
+            free_[j] = r < ny;
+            jf[j] = free_[j] ? a.f_feat[y0 + r] : 0;
+            d0[j] = free_[j] ? a.f_desc[2 * jf[j]] : make_uint4(0, 0, 0, 0);
+            d1[j] = free_[j] ? a.f_desc[2 * jf[j] + 1] : make_uint4(0, 0, 0, 0);
+        }
+        // the node's keyframe features are fetched by the lanes in parallel (64 at a time) and
+        // broadcast in order, so the sequential loop carries no memory latency
+        const int x0 = a.kf_node_off[na], nx = a.kf_node_off[na + 1] - x0;
+        for (int xb = 0; xb < nx; xb += 64) {
+            const int xl = xb + lane;
+            int my_ikf = -1;
+            uint4 my0 = make_uint4(0, 0, 0, 0), my1 = my0;
+            if (xl < nx) {
+                my_ikf = a.kf_feat[x0 + xl];
+                if (!a.kf_ok[my_ikf]) {
+                    my_ikf = -1;
+                } else {
+                    my0 = a.kf_desc[2 * my_ikf];
+                    my1 = a.kf_desc[2 * my_ikf + 1];
+                }
+            }
+            const int cnt = min(64, nx - xb);
+            for (int t = 0; t < cnt; ++t) {
+                const int ikf = __shfl(my_ikf, t, 64);
+                if (ikf < 0) continue;
+                const uint4 q0 = make_uint4(__shfl(my0.x, t, 64), __shfl(my0.y, t, 64),
+                                            __shfl(my0.z, t, 64), __shfl(my0.w, t, 64));
+                const uint4 q1 = make_uint4(__shfl(my1.x, t, 64), __shfl(my1.y, t, 64),
+                                            __shfl(my1.z, t, 64), __shfl(my1.w, t, 64));
+                uint32_t key = 0xffffffffu;
+                int dist[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    dist[j] = free_[j] ? hamming256(q0, q1, d0[j], d1[j]) : 256;
+                    if (free_[j]) key = min(key, ((uint32_t)dist[j] << 16) | (uint32_t)(lane + 64 * j));
+                }
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) key = min(key, (uint32_t)__shfl_xor((int)key, o, 64));
+                const int b1 = key == 0xffffffffu ? 256 : (int)(key >> 16);
+                const int brank = (int)(key & 0xffff);
+                int sec = 256;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (free_[j] && lane + 64 * j != brank) sec = min(sec, dist[j]);
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) sec = min(sec, __shfl_xor(sec, o, 64));
+                if (b1 <= 50 && (float)b1 < nnratio * (float)sec) {  // TH_LOW, ratio (233-237)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        if (lane + 64 * j == brank) {
+                            free_[j] = false;
+                            matches[jf[j]] = ikf;
+                            if (check_ori) {
+                                const int bin = rot_bin(a.kf_angle[ikf], a.f_angle[jf[j]]);
+                                bins[jf[j]] = bin;
+                                atomicAdd(&hist[bin], 1);
+                            }
+                            atomicAdd(nm, 1);
+                        }
+                    }
+                }
             }
         }
     }
-    if (FILL) {
-        a.pt_kf[p] = ikf;
-        a.pt_angle[p] = a.kf_angle[ikf];
-    } else {
-        a.cnt[p] = n;
+}
+
+// The orientation filter (259-281) over every matched frame feature; one workgroup.
+__global__ __launch_bounds__(1024) void bow_ori_kernel(int n_f, int* matches, const int* bins,
+                                                       const int* hist, int* nm) {
+    __shared__ int top[3];
+    if (threadIdx.x == 0) three_maxima(hist, top[0], top[1], top[2]);
+    __syncthreads();
+    int removed = 0;
+    for (int j = threadIdx.x; j < n_f; j += 1024) {
+        if (matches[j] < 0) continue;
+        const int bin = bins[j];
+        if (bin != top[0] && bin != top[1] && bin != top[2]) {
+            matches[j] = -1;
+            ++removed;
+        }
     }
+    if (removed) atomicSub(nm, removed);
 }
 
 }  // namespace orbfe
@@ -301,7 +368,7 @@ struct orbfe_vocabulary {
     DevBuf child_off, child_ids, desc, word, weight;
     // per-call scratch / staging (host forms)
     DevBuf s_desc, s_n, s_word, s_node, s_w, o_wid, o_val, o_nw, o_nid, o_noff, o_feat, o_nn;
-    hipStream_t stream = nullptr;
+    hipStream_t own = nullptr, stream = nullptr;
 
     VocabDev dev() const {
         return VocabDev{L, nodes, nwords, scoring, weighting, child_off.as<int>(),
@@ -311,7 +378,7 @@ struct orbfe_vocabulary {
         for (DevBuf* b : {&child_off, &child_ids, &desc, &word, &weight, &s_desc, &s_n, &s_word,
                           &s_node, &s_w, &o_wid, &o_val, &o_nw, &o_nid, &o_noff, &o_feat, &o_nn})
             b->release();
-        if (stream) hipStreamDestroy(stream);
+        if (own) hipStreamDestroy(own);
     }
 };
 
@@ -424,8 +491,9 @@ orbfe_vocabulary* orbfe_vocabulary_load_text(const char* path, int device, int* 
             st = vocab_parse_text(path, v->k, v->L, v->scoring, v->weighting, parent, is_word,
                                   desc, weight);
             if (st == ORBFE_OK) st = vocab_upload(v, parent, is_word, desc, weight);
-            if (st == ORBFE_OK && hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) != hipSuccess)
+            if (st == ORBFE_OK && hipStreamCreateWithFlags(&v->own, hipStreamNonBlocking) != hipSuccess)
                 st = ORBFE_ERR_HIP;
+            v->stream = v->own;
         }
     } catch (const std::bad_alloc&) {
         st = ORBFE_ERR_NOMEM;
@@ -462,8 +530,9 @@ orbfe_vocabulary* orbfe_vocabulary_create(int k, int L, int scoring, int weighti
                               std::vector<uint8_t>(is_word, is_word + n_nodes),
                               std::vector<uint8_t>(desc, desc + (size_t)n_nodes * 32),
                               std::vector<double>(weight, weight + n_nodes));
-            if (st == ORBFE_OK && hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) != hipSuccess)
+            if (st == ORBFE_OK && hipStreamCreateWithFlags(&v->own, hipStreamNonBlocking) != hipSuccess)
                 st = ORBFE_ERR_HIP;
+            v->stream = v->own;
         }
     } catch (const std::bad_alloc&) {
         st = ORBFE_ERR_NOMEM;
@@ -498,9 +567,7 @@ int orbfe_vocabulary_info(const orbfe_vocabulary* v, int32_t* info) {
 
 int orbfe_vocabulary_set_stream(orbfe_vocabulary* v, void* hip_stream) {
     if (!v) return ORBFE_ERR_ARG;
-    if (hip_stream) {
-        v->stream = static_cast<hipStream_t>(hip_stream);  // caller-owned from now on
-    }
+    v->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : v->own;
     return ORBFE_OK;
 }
 
@@ -562,10 +629,11 @@ int orbfe_search_by_bow(orbfe_matcher* m, float nnratio, int check_ori, int n_kf
         for (int i = 0; i < n_f; ++i) matches[i] = -1;  // vpMapPointMatches = NULL (164)
         *nmatches = 0;
         if (!kf_nn || !f_nn || !n_f) return ORBFE_OK;
-        BowMatchArgs a;
+        BowMatchArgs a{};
         if ((st = m->up(m->fa_d, kf_desc, (size_t)n_kf * 32))) return st;
         if ((st = m->up(m->fb_d, f_desc, (size_t)n_f * 32))) return st;
         if ((st = m->up(m->m_f0, kf_angle, (size_t)n_kf * 4))) return st;
+        if ((st = m->up(m->m_f1, f_angle, (size_t)n_f * 4))) return st;
         if ((st = m->up(m->m_u0, kf_mp_ok, n_kf))) return st;
         if ((st = m->up(m->m_i0, kf_node_ids, (size_t)kf_nn * 4))) return st;
         if ((st = m->up(m->m_i1, kf_node_off, (size_t)(kf_nn + 1) * 4))) return st;
@@ -573,9 +641,13 @@ int orbfe_search_by_bow(orbfe_matcher* m, float nnratio, int check_ori, int n_kf
         if ((st = m->up(m->fb_cs, f_node_ids, (size_t)f_nn * 4))) return st;
         if ((st = m->up(m->fb_ci, f_node_off, (size_t)(f_nn + 1) * 4))) return st;
         if ((st = m->up(m->fb_co, f_feat, (size_t)f_tot * 4))) return st;
-        if ((st = m->s1.ensure((size_t)kf_nn * 4 + 16))) return st;  // pair
-        if ((st = m->s2.ensure((size_t)kf_nn * 4 + 16))) return st;  // npts
-        if ((st = m->s3.ensure((size_t)(kf_nn + 1) * 4 + 16))) return st;  // pbase
+        std::vector<int32_t> empty(n_f, -1);  // vpMapPointMatches = NULL (164)
+        if ((st = m->up(m->fa_k, empty.data(), (size_t)n_f * 4))) return st;
+        if ((st = m->s1.ensure((size_t)n_f * 4 + 16))) return st;  // bins per frame feature
+        if ((st = m->scal.ensure(16))) return st;
+        if ((st = m->g_hist.ensure(32 * sizeof(int)))) return st;
+        ORBFE_HIP(hipMemsetAsync(m->scal.p, 0, 16, m->stream));
+        ORBFE_HIP(hipMemsetAsync(m->g_hist.p, 0, 32 * sizeof(int), m->stream));
         a.kf_nn = kf_nn;
         a.f_nn = f_nn;
         a.kf_node_ids = m->m_i0.as<int>();
@@ -588,59 +660,22 @@ int orbfe_search_by_bow(orbfe_matcher* m, float nnratio, int check_ori, int n_kf
         a.kf_desc = m->fa_d.as<uint4>();
         a.f_desc = m->fb_d.as<uint4>();
         a.kf_angle = m->m_f0.as<float>();
-        a.pair = m->s1.as<int>();
-        a.npts = m->s2.as<int>();
-        a.pbase = m->s3.as<int>();
-        hipLaunchKernelGGL(bow_pair_kernel, dim3((kf_nn + 255) / 256), dim3(256), 0, m->stream, a);
-        hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, m->stream, a.npts, kf_nn, m->s3.as<int>());
-        int P = 0;
-        ORBFE_HIP(hipMemcpyAsync(&P, m->s3.as<int>() + kf_nn, sizeof(int), hipMemcpyDeviceToHost, m->stream));
-        ORBFE_HIP(hipStreamSynchronize(m->stream));
-        if (P == 0) return ORBFE_OK;
-        if ((st = m->s4.ensure((size_t)P * 4 + 16))) return st;       // pt_kf
-        if ((st = m->s5.ensure((size_t)P * 4 + 16))) return st;       // pt_angle
-        a.pt_kf = m->s4.as<int>();
-        a.pt_angle = m->s5.as<float>();
-        if ((st = m->cnt.ensure((size_t)P * 4))) return st;
-        if ((st = m->off.ensure((size_t)(P + 1) * 4))) return st;
-        a.cnt = m->cnt.as<int>();
-        a.off = m->off.as<int>();
-        const int pb = (P + 255) / 256;
-        hipLaunchKernelGGL(bow_cand_kernel<false>, dim3(pb), dim3(256), 0, m->stream, a, P);
-        hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, m->stream, a.cnt, P, m->off.as<int>());
-        int total = 0;
-        ORBFE_HIP(hipMemcpyAsync(&total, m->off.as<int>() + P, sizeof(int), hipMemcpyDeviceToHost, m->stream));
-        ORBFE_HIP(hipStreamSynchronize(m->stream));
-        if ((st = m->cand.ensure(std::max(total, 1) * sizeof(int2)))) return st;
-        a.cand = m->cand.as<int2>();
-        hipLaunchKernelGGL(bow_cand_kernel<true>, dim3(pb), dim3(256), 0, m->stream, a, P);
-        // frame slots start empty; every acceptor blocks its slot for later points
-        std::vector<int32_t> empty(n_f, -1);
-        if ((st = m->up(m->fa_k, empty.data(), (size_t)n_f * 4))) return st;
-        // greedy_accept reads the slot keypoint's angle through k[s].angle: stage the frame
-        // angles as keypoints
-        std::vector<orbfe_keypoint> fk(n_f);
-        for (int i = 0; i < n_f; ++i) fk[i] = orbfe_keypoint{0.f, 0.f, 0.f, f_angle[i], 0.f, 0, -1};
-        if ((st = m->up(m->fb_k, fk.data(), (size_t)n_f * sizeof(orbfe_keypoint)))) return st;
-        GreedyArgs g{};
-        g.m = P;
-        g.nkp = n_f;
-        g.mode = kGreedyBow;
-        g.nnratio = nnratio;
-        g.off = m->off.as<int>();
-        g.cand = m->cand.as<int2>();
-        g.nobs = nullptr;
-        g.fmp0 = g.fmp = m->fa_k.as<int>();
-        g.fobs0 = g.fobs = nullptr;
-        g.check_ori = check_ori;
-        g.q_angle = a.pt_angle;
-        g.k = m->fb_k.as<orbfe_keypoint>();
-        g.ids = a.pt_kf;
-        if ((st = m->greedy(g))) return st;
+        a.f_angle = m->m_f1.as<float>();
+        if ((st = m->flush())) return st;
+        hipLaunchKernelGGL(bow_search_kernel, dim3((kf_nn + 3) / 4), dim3(kBowSearchBlock), 0,
+                           m->stream, a, nnratio, check_ori, m->fa_k.as<int>(), m->s1.as<int>(),
+                           m->g_hist.as<int>(), m->scal.as<int>(), m->scal.as<int>() + 1);
+        if (check_ori)
+            hipLaunchKernelGGL(bow_ori_kernel, dim3(1), dim3(1024), 0, m->stream, n_f,
+                               m->fa_k.as<int>(), m->s1.as<int>(), m->g_hist.as<int>(),
+                               m->scal.as<int>());
+        ORBFE_HIP(hipGetLastError());
         if ((st = m->down(matches, m->fa_k, (size_t)n_f * 4))) return st;
-        if ((st = m->down(nmatches, m->scal, sizeof(int)))) return st;
-        ORBFE_HIP(hipStreamSynchronize(m->stream));
-        return ORBFE_OK;
+        int cnt[2] = {0, 0};
+        if ((st = m->down(cnt, m->scal, sizeof(cnt)))) return st;
+        if ((st = m->sync())) return st;
+        *nmatches = cnt[0];
+        return cnt[1];  // ORBFE_ERR_UNSUPPORTED: a node held more than 256 frame features
     });
 }
 

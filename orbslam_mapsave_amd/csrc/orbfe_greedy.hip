@@ -29,7 +29,6 @@ namespace orbfe {
 constexpr int kGreedyBlock = 256;
 constexpr int kGreedyLocal = 0;  // SBP local map: TH_HIGH + same-level ratio test (110-119)
 constexpr int kGreedyMaxD = 1;   // best <= max_dist (last frame 1411, keyframe 1545)
-constexpr int kGreedyBow = 2;    // SearchByBoW: best <= TH_LOW && best < nnratio * second (236-238)
 
 struct GreedyArgs {
     int m, nkp, mode, max_dist;
@@ -86,18 +85,6 @@ __device__ __forceinline__ int greedy_decide(const GreedyArgs& a, const int* Tc,
         if (best > 100) return -1;  // TH_HIGH
         if (bl == sl && best > a.nnratio * second) return -1;
         return bi;
-    }
-    if (a.mode == kGreedyBow) {
-        int best = 256, second = 256, bi = -1;
-        for (int e = e0; e < e1; ++e) {
-            const int2 c = a.cand[e];
-            if (Tc[c.x] < i) continue;
-            const int d = c.y & 0xffff;
-            if (d < best) { second = best; best = d; bi = c.x; }
-            else if (d < second) { second = d; }
-        }
-        if (best > 50) return -1;  // TH_LOW
-        return (float)best < a.nnratio * (float)second ? bi : -1;
     }
     int best = 256, bi = -1;
     for (int e = e0; e < e1; ++e) {
@@ -181,6 +168,100 @@ __global__ __launch_bounds__(kGreedyBlock) void greedy_ori_kernel(GreedyArgs a) 
     }
     const unsigned long long b = __ballot(removed);
     if ((threadIdx.x & 63) == 0 && b) atomicSub(a.nm, __popcll(b));
+}
+
+// Small problems (tracking one frame: ~1-2k points) in ONE workgroup: the same rounds, separated
+// by barriers instead of launches, then G2-G4; no host round trip.  T ping-pongs between
+// T[0] and T[1]: a round reads one and writes the other (pre-filled with the blocked-before
+// state), then the buffer it read is reset for the next round.  The converged round count is
+// left in chg[0].  T and the last-acceptor table live in LDS (3 x nkp ints), so every
+// cross-thread exchange is an LDS atomic or an LDS read after a barrier.
+constexpr int kGreedySmallBlock = 1024;
+constexpr int kGreedySmallMax = 16384;     // points handled by the single-workgroup form
+constexpr int kGreedySmallSlots = 5000;    // slots (keypoints): 3 x 4 B each within 64 KB of LDS
+__global__ __launch_bounds__(kGreedySmallBlock) void greedy_small_kernel(GreedyArgs a) {
+    extern __shared__ int lds[];
+    __shared__ int changed, nm;
+    __shared__ int h[30];
+    __shared__ int top[3];
+    const int tid = threadIdx.x;
+    int* T[2] = {lds, lds + a.nkp};
+    int* last = lds + 2 * a.nkp;
+    for (int s = tid; s < a.nkp; s += kGreedySmallBlock) {
+        const int v = greedy_preblocked(a, s) ? -1 : INT_MAX;
+        T[0][s] = v;
+        T[1][s] = v;
+        last[s] = -1;
+    }
+    for (int i = tid; i < a.m; i += kGreedySmallBlock) a.dec[i] = -2;
+    if (tid < 30) h[tid] = 0;
+    if (tid == 0) nm = 0;
+    __syncthreads();
+    int cur = 0, r = 0;
+    while (true) {
+        if (tid == 0) changed = 0;
+        __syncthreads();
+        const int* Tc = T[cur];
+        int* Tn = T[cur ^ 1];
+        bool ch = false;
+        for (int i = tid; i < a.m; i += kGreedySmallBlock) {
+            const int d = greedy_decide(a, Tc, i);
+            if (d >= 0 && (!a.nobs || a.nobs[i] > 0)) atomicMin(&Tn[d], i);
+            if (d != a.dec[i]) {
+                a.dec[i] = d;
+                ch = true;
+            }
+        }
+        if (ch) changed = 1;
+        __syncthreads();
+        ++r;
+        if (!changed) break;
+        for (int s = tid; s < a.nkp; s += kGreedySmallBlock)
+            T[cur][s] = greedy_preblocked(a, s) ? -1 : INT_MAX;
+        cur ^= 1;
+        __syncthreads();
+    }
+    // G2: last acceptor per slot, nmatches, rotation bins
+    for (int i = tid; i < a.m; i += kGreedySmallBlock) {
+        const int s = a.dec[i];
+        if (s < 0) continue;
+        atomicMax(&last[s], i);
+        atomicAdd(&nm, 1);
+        if (a.check_ori) {
+            const int bin = rot_bin(a.q_angle[i], a.k[s].angle);
+            a.bins[i] = bin;
+            atomicAdd(&h[bin], 1);
+        }
+    }
+    __syncthreads();
+    // G3: slot contents
+    for (int s = tid; s < a.nkp; s += kGreedySmallBlock) {
+        const int i = last[s];
+        if (i < 0) continue;
+        a.fmp[s] = a.ids ? a.ids[i] : i;
+        if (a.fobs) a.fobs[s] = a.nobs ? a.nobs[i] : 1;
+    }
+    __syncthreads();
+    // G4: orientation filter
+    if (a.check_ori) {
+        if (tid == 0) three_maxima(h, top[0], top[1], top[2]);
+        __syncthreads();
+        for (int i = tid; i < a.m; i += kGreedySmallBlock) {
+            const int s = a.dec[i];
+            if (s < 0) continue;
+            const int bin = a.bins[i];
+            if (bin != top[0] && bin != top[1] && bin != top[2]) {
+                a.fmp[s] = -1;
+                if (a.fobs) a.fobs[s] = 0;
+                atomicSub(&nm, 1);
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        *a.nm = nm;
+        a.chg[0] = r;
+    }
 }
 
 }  // namespace orbfe

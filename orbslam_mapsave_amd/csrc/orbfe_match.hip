@@ -206,6 +206,56 @@ __device__ __forceinline__ void features_in_area(const DevFrame& F, float x, flo
         }
 }
 
+// Wave-cooperative GetFeaturesInArea for one query per wave (every lane passes the same query):
+// lane t takes cell t of the window in the reference's ix-major, iy order (64 cells per
+// step), counts its passing items, and an exclusive wave scan of the counts places every
+// candidate at its reference rank; emit(idx, rank) runs on the lane owning the candidate.
+// Returns the candidate count (wave-uniform).  keep(idx) is an extra per-candidate filter.
+template <class Keep, class Emit>
+__device__ __forceinline__ int features_in_area_wave(const DevFrame& F, float x, float y, float r,
+                                                     int min_level, int max_level, Keep keep,
+                                                     Emit emit) {
+    const int lane = threadIdx.x & 63;
+    const int cx0 = max(0, (int)floorf((x - F.minx - r) * F.gwi));
+    if (cx0 >= kGridCols) return 0;
+    const int cx1 = min(kGridCols - 1, (int)ceilf((x - F.minx + r) * F.gwi));
+    if (cx1 < 0) return 0;
+    const int cy0 = max(0, (int)floorf((y - F.miny - r) * F.ghi));
+    if (cy0 >= kGridRows) return 0;
+    const int cy1 = min(kGridRows - 1, (int)ceilf((y - F.miny + r) * F.ghi));
+    if (cy1 < 0) return 0;
+    const bool check = min_level > 0 || max_level >= 0;
+    const int ny = cy1 - cy0 + 1, ncell = (cx1 - cx0 + 1) * ny;
+    auto pass = [&](int idx) {
+        const orbfe_keypoint kp = F.k[idx];
+        if (check) {
+            if (kp.octave < min_level) return false;
+            if (max_level >= 0 && kp.octave > max_level) return false;
+        }
+        return fabsf(kp.x - x) < r && fabsf(kp.y - y) < r && keep(idx);
+    };
+    int total = 0;
+    for (int c0 = 0; c0 < ncell; c0 += 64) {
+        const int t = c0 + lane;
+        int e0 = 0, e1 = 0, n = 0;
+        if (t < ncell) {
+            const int c = (cx0 + t / ny) * kGridRows + cy0 + t % ny;
+            e0 = F.cstart[c];
+            e1 = F.cstart[c + 1];
+            for (int e = e0; e < e1; ++e) n += pass(F.citems[e]);
+        }
+        const int inc = wave_inclusive_sum(n);
+        int rank = total + inc - n;
+        if (n)
+            for (int e = e0; e < e1; ++e) {
+                const int idx = F.citems[e];
+                if (pass(idx)) emit(idx, rank++);
+            }
+        total += __shfl(inc, 63, 64);
+    }
+    return total;
+}
+
 // Exclusive scan of counts[0..n) into off[0..n], single workgroup.
 __global__ __launch_bounds__(1024) void scan_kernel(const int* counts, int n, int* off) {
     __shared__ int tmp[1024 / 64 + 1];
@@ -227,6 +277,7 @@ struct SfiArgs {
     DevFrame f1, f2;
     const float* prev;  // 2 per F1 keypoint
     float window;
+    long long cand_cap;  // fill writes only lists that end within the capacity
     int* cnt;           // per F1 keypoint
     const int* off;     // n1 + 1
     int2* cand;         // (i2, dist)
@@ -234,26 +285,27 @@ struct SfiArgs {
 
 template <bool FILL>
 __global__ __launch_bounds__(256) void sfi_cand_kernel(SfiArgs a) {
-    const int i1 = blockIdx.x * 256 + threadIdx.x;
+    const int i1 = blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per F1 keypoint
     if (i1 >= a.f1.n) return;
+    if (FILL && a.off[i1 + 1] > a.cand_cap) return;
     const orbfe_keypoint k1 = a.f1.k[i1];
     if (k1.octave > 0) {
-        if (!FILL) a.cnt[i1] = 0;
+        if (!FILL && (threadIdx.x & 63) == 0) a.cnt[i1] = 0;
         return;
     }
     const uint4* d1 = a.f1.desc + 2 * i1;
     const uint4 q0 = d1[0], q1 = d1[1];
-    int n = 0;
     int2* out = FILL ? a.cand + a.off[i1] : nullptr;
-    features_in_area(a.f2, a.prev[2 * i1], a.prev[2 * i1 + 1], a.window, k1.octave, k1.octave,
-                     [&](int i2) {
-                         if (FILL) {
-                             const uint4* d2 = a.f2.desc + 2 * i2;
-                             out[n] = make_int2(i2, hamming256(q0, q1, d2[0], d2[1]));
-                         }
-                         ++n;
-                     });
-    if (!FILL) a.cnt[i1] = n;
+    const int n = features_in_area_wave(
+        a.f2, a.prev[2 * i1], a.prev[2 * i1 + 1], a.window, k1.octave, k1.octave,
+        [](int) { return true; },
+        [&](int i2, int rank) {
+            if (FILL) {
+                const uint4* d2 = a.f2.desc + 2 * i2;
+                out[rank] = make_int2(i2, hamming256(q0, q1, d2[0], d2[1]));
+            }
+        });
+    if (!FILL && (threadIdx.x & 63) == 0) a.cnt[i1] = n;
 }
 
 __device__ __forceinline__ int rot_bin(float a1, float a2) {  // ORBmatcher.cc:478-483
@@ -453,6 +505,7 @@ struct SbpLastArgs {
     const float* scale;
     float th;
     int mode;              // 0: [o-1, o+1], 1: forward [o, -], 2: backward [0, o]
+    long long cand_cap;
     int* cnt;
     const int* off;
     int2* cand;
@@ -460,8 +513,9 @@ struct SbpLastArgs {
 
 template <bool FILL>
 __global__ __launch_bounds__(256) void sbp_last_cand_kernel(SbpLastArgs a) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per last-frame point
     if (i >= a.n_last) return;
+    if (FILL && a.off[i + 1] > a.cand_cap) return;
     int n = 0;
     if (a.valid[i] && !a.outlier[i]) {
         const float* P = a.xyz + 3 * i;
@@ -479,20 +533,19 @@ __global__ __launch_bounds__(256) void sbp_last_cand_kernel(SbpLastArgs a) {
             const int hi = a.mode == 0 ? o + 1 : a.mode == 1 ? -1 : o;
             const uint4 q0 = a.desc[2 * i], q1 = a.desc[2 * i + 1];
             int2* out = FILL ? a.cand + a.off[i] : nullptr;
-            features_in_area(a.cur, u, v, radius, lo, hi, [&](int i2) {
-                if (a.cur.ur && a.cur.ur[i2] > 0) {
-                    const float ur = u - a.bf * invz;
-                    if (fabsf(ur - a.cur.ur[i2]) > radius) return;
-                }
-                if (FILL) {
-                    const uint4* d = a.cur.desc + 2 * i2;
-                    out[n] = make_int2(i2, hamming256(q0, q1, d[0], d[1]));
-                }
-                ++n;
-            });
+            const float ur = u - a.bf * invz;
+            n = features_in_area_wave(
+                a.cur, u, v, radius, lo, hi,
+                [&](int i2) { return !(a.cur.ur && a.cur.ur[i2] > 0 && fabsf(ur - a.cur.ur[i2]) > radius); },
+                [&](int i2, int rank) {
+                    if (FILL) {
+                        const uint4* d = a.cur.desc + 2 * i2;
+                        out[rank] = make_int2(i2, hamming256(q0, q1, d[0], d[1]));
+                    }
+                });
         }
     }
-    if (!FILL) a.cnt[i] = n;
+    if (!FILL && (threadIdx.x & 63) == 0) a.cnt[i] = n;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -518,6 +571,7 @@ struct SbpKfArgs {
     int nlevels;
     float log_scale, th;
     int* status;
+    long long cand_cap;
     int* cnt;
     const int* off;
     int2* cand;
@@ -525,8 +579,9 @@ struct SbpKfArgs {
 
 template <bool FILL>
 __global__ __launch_bounds__(256) void sbp_kf_cand_kernel(SbpKfArgs a) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per keyframe map point
     if (i >= a.n) return;
+    if (FILL && a.off[i + 1] > a.cand_cap) return;
     int n = 0;
     if (a.valid[i] && !a.bad[i] && !a.found[i]) {
         const float* P = a.xyz + 3 * i;
@@ -549,22 +604,23 @@ __global__ __launch_bounds__(256) void sbp_kf_cand_kernel(SbpKfArgs a) {
             const float ratio = a.maxd[i] / dist;
             const int lvl = (int)ceilf((float)log((double)ratio) / a.log_scale);
             if (lvl < 0 || lvl >= a.nlevels) {
-                atomicExch(a.status, ORBFE_ERR_UNSUPPORTED);  // mvScaleFactors[lvl] out of range
+                if ((threadIdx.x & 63) == 0) atomicExch(a.status, ORBFE_ERR_UNSUPPORTED);  // mvScaleFactors[lvl]
             } else {
                 const float radius = a.th * a.scale[lvl];
                 const uint4 q0 = a.desc[2 * i], q1 = a.desc[2 * i + 1];
                 int2* out = FILL ? a.cand + a.off[i] : nullptr;
-                features_in_area(a.cur, u, v, radius, lvl - 1, lvl + 1, [&](int i2) {
-                    if (FILL) {
-                        const uint4* d = a.cur.desc + 2 * i2;
-                        out[n] = make_int2(i2, hamming256(q0, q1, d[0], d[1]));
-                    }
-                    ++n;
-                });
+                n = features_in_area_wave(
+                    a.cur, u, v, radius, lvl - 1, lvl + 1, [](int) { return true; },
+                    [&](int i2, int rank) {
+                        if (FILL) {
+                            const uint4* d = a.cur.desc + 2 * i2;
+                            out[rank] = make_int2(i2, hamming256(q0, q1, d[0], d[1]));
+                        }
+                    });
             }
         }
     }
-    if (!FILL) a.cnt[i] = n;
+    if (!FILL && (threadIdx.x & 63) == 0) a.cnt[i] = n;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -12,6 +12,28 @@
 
 #include "../../include/orbfe.h"
 
+namespace orbfe {
+// Uploads of one host call: a single H2D copy of the pinned staging range into a device
+// staging buffer, then this kernel scatters the segments to their buffers (one launch instead
+// of one blit per array).  Segments are 256-byte aligned on both sides.
+constexpr int kMaxUpSeg = 24;
+struct UpScatter {
+    int n;
+    uint8_t* dst[kMaxUpSeg];
+    const uint8_t* src[kMaxUpSeg];
+    uint32_t bytes[kMaxUpSeg];
+};
+__global__ __launch_bounds__(256) void upload_scatter_kernel(UpScatter a) {
+    const int s = blockIdx.y;
+    if (s >= a.n) return;
+    const uint32_t nb = a.bytes[s], n16 = nb >> 4;
+    const uint4* src = reinterpret_cast<const uint4*>(a.src[s]);
+    uint4* dst = reinterpret_cast<uint4*>(a.dst[s]);
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256) dst[i] = src[i];
+    if (blockIdx.x == 0 && threadIdx.x < (nb & 15)) a.dst[s][16 * n16 + threadIdx.x] = a.src[s][16 * n16 + threadIdx.x];
+}
+}  // namespace orbfe
+
 using namespace orbfe;
 
 struct orbfe_matcher {
@@ -28,6 +50,7 @@ struct orbfe_matcher {
     DevBuf g_t0, g_t1, g_t2, g_dec, g_chg, g_last, g_bins, g_hist;  // greedy resolver
     Profiler prof;
     int last_rounds = 0;  // rounds the most recent greedy resolution took (diagnostics)
+    bool rounds_on_device = false;  // single-workgroup form: the count sits in g_chg[0]
 
     ~orbfe_matcher() {
         for (DevBuf* b : {&fa_k, &fa_d, &fa_ur, &fa_cs, &fa_ci, &fa_co, &fb_k, &fb_d, &fb_ur,
@@ -40,14 +63,105 @@ struct orbfe_matcher {
         if (own) hipStreamDestroy(own);
     }
 
+    // Host transfers go through a pinned staging buffer: the copy into it is a CPU memcpy and
+    // the DMA is asynchronous (pageable hipMemcpyAsync stages and blocks per call).  Every
+    // host-form entry point starts with begin() and ends with sync(), which completes the
+    // deferred downloads; the staging memory is reused from call to call.
+    uint8_t* pin = nullptr;
+    size_t pin_cap = 0, pin_used = 0;
+    std::vector<uint8_t*> pin_retired;  // outgrown buffers, freed once the stream is idle
+    struct Pending { void* dst; const uint8_t* src; size_t bytes; };
+    std::vector<Pending> pend;
+
+    struct UpSeg { uint8_t* dst; size_t off; size_t bytes; };
+    std::vector<UpSeg> upq;  // staged uploads not yet copied
+    DevBuf d_stage;
+
+    void begin() {
+        for (uint8_t* q : pin_retired) hipHostFree(q);
+        pin_retired.clear();
+        pin_used = 0;
+        pend.clear();
+        upq.clear();
+        cand_check = false;
+    }
+    // Copies the staged uploads to their device buffers (call before any kernel reads them).
+    int flush() {
+        if (upq.empty()) return ORBFE_OK;
+        size_t lo = upq[0].off, hi = 0;
+        for (const UpSeg& u : upq) { lo = std::min(lo, u.off); hi = std::max(hi, u.off + u.bytes); }
+        int st;
+        if ((st = d_stage.ensure(pin_cap))) return st;
+        ORBFE_HIP(hipMemcpyAsync(d_stage.as<uint8_t>() + lo, pin + lo, hi - lo, hipMemcpyHostToDevice, stream));
+        for (size_t b = 0; b < upq.size(); b += kMaxUpSeg) {
+            UpScatter a;
+            a.n = (int)std::min<size_t>(kMaxUpSeg, upq.size() - b);
+            size_t mx = 0;
+            for (int i = 0; i < a.n; ++i) {
+                const UpSeg& u = upq[b + i];
+                a.dst[i] = u.dst;
+                a.src[i] = d_stage.as<uint8_t>() + u.off;
+                a.bytes[i] = (uint32_t)u.bytes;
+                mx = std::max(mx, u.bytes);
+            }
+            const int gx = (int)std::min<size_t>(64, std::max<size_t>(1, (mx / 16 + 255) / 256));
+            hipLaunchKernelGGL(upload_scatter_kernel, dim3(gx, a.n), dim3(256), 0, stream, a);
+        }
+        upq.clear();
+        ORBFE_HIP(hipGetLastError());
+        return ORBFE_OK;
+    }
+    uint8_t* stage(size_t bytes) {
+        const size_t off = (pin_used + 255) & ~(size_t)255;
+        if (off + bytes > pin_cap) {
+            const size_t cap = std::max<size_t>((off + bytes) * 2, (size_t)1 << 20);
+            void* q = nullptr;
+            if (hipHostMalloc(&q, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+            if (flush() != ORBFE_OK) return nullptr;  // staged uploads reference the old buffer
+            if (pin) pin_retired.push_back(pin);  // in-flight copies may still read it
+            pin = static_cast<uint8_t*>(q);
+            pin_cap = cap;
+            pin_used = 0;
+            return stage(bytes);
+        }
+        pin_used = off + bytes;
+        return pin + off;
+    }
     int up(DevBuf& b, const void* src, size_t bytes) {
         int st = b.ensure(std::max<size_t>(bytes, 16));
         if (st) return st;
-        if (bytes) ORBFE_HIP(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, stream));
+        if (!bytes) return ORBFE_OK;
+        uint8_t* q = stage(bytes);
+        if (!q) return ORBFE_ERR_NOMEM;
+        std::memcpy(q, src, bytes);
+        upq.push_back(UpSeg{b.as<uint8_t>(), (size_t)(q - pin), bytes});
         return ORBFE_OK;
     }
     int down(void* dst, const DevBuf& b, size_t bytes) {
-        if (bytes) ORBFE_HIP(hipMemcpyAsync(dst, b.p, bytes, hipMemcpyDeviceToHost, stream));
+        if (!bytes) return ORBFE_OK;
+        uint8_t* q = stage(bytes);
+        if (!q) return ORBFE_ERR_NOMEM;
+        ORBFE_HIP(hipMemcpyAsync(q, b.p, bytes, hipMemcpyDeviceToHost, stream));
+        pend.push_back(Pending{dst, q, bytes});
+        return ORBFE_OK;
+    }
+    int sync() {
+        int st;
+        if ((st = flush())) return st;
+        ORBFE_HIP(hipStreamSynchronize(stream));
+        if (cand_check) {  // csr_async: the candidates must have fit before results count
+            int total = 0;
+            for (const Pending& d : pend)
+                if (d.dst == &cand_total) std::memcpy(&total, d.src, sizeof(int));
+            cand_check = false;
+            if ((size_t)total > cand_cap_used) {
+                pend.clear();
+                cand_need = (size_t)total;
+                return ORBFE_ERR_CAPACITY;
+            }
+        }
+        for (const Pending& d : pend) std::memcpy(d.dst, d.src, d.bytes);
+        pend.clear();
         return ORBFE_OK;
     }
 
@@ -67,6 +181,7 @@ struct orbfe_matcher {
         if ((st = cs.ensure((kGridCells + 1) * sizeof(int)))) return st;
         if ((st = ci.ensure(std::max(n, 1) * sizeof(int)))) return st;
         if ((st = co.ensure(std::max(n, 1) * sizeof(int)))) return st;
+        if ((st = flush())) return st;
         hipLaunchKernelGGL(grid_kernel, dim3(1), dim3(kGridBlock), 0, stream, k.as<orbfe_keypoint>(),
                            n, v->min_x, v->min_y, v->grid_w_inv, v->grid_h_inv, co.as<int>(),
                            cs.as<int>(), ci.as<int>());
@@ -111,14 +226,48 @@ struct orbfe_matcher {
     }
 
     // count -> scan -> fill for a candidate kernel family; returns the candidate total.
+    // per_block: queries per 256-thread block (256: thread per query, 4: wave per query).
+    // Without a host round trip: the fill is bounded by a grow-only capacity and the true total
+    // is checked by sync() (ORBFE_ERR_CAPACITY: the caller grows to cand_need and runs again).
+    int cand_total = 0;          // written by the deferred download of off[nq]
+    size_t cand_cap_used = 0;
+    bool cand_check = false;
+    size_t cand_need = 0;
     template <class Args, class CountK, class FillK>
-    int csr(Args& a, int nq, CountK ck, FillK fk, int& total) {
+    int csr_async(Args& a, int nq, CountK ck, FillK fk, int per_block) {
+        int st;
+        if ((st = cnt.ensure(std::max(nq, 1) * sizeof(int)))) return st;
+        if ((st = off.ensure((nq + 1) * sizeof(int)))) return st;
+        const size_t cap = std::max(std::max(cand.bytes / sizeof(int2), (size_t)nq * 64), cand_need);
+        if ((st = cand.ensure(std::max<size_t>(cap, 1) * sizeof(int2)))) return st;
+        a.cnt = cnt.as<int>();
+        a.off = off.as<int>();
+        a.cand = cand.as<int2>();
+        a.cand_cap = (long long)cap;
+        if ((st = flush())) return st;
+        const int blocks = std::max(1, (nq + per_block - 1) / per_block);
+        hipLaunchKernelGGL(ck, dim3(blocks), dim3(256), 0, stream, a);
+        hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, stream, cnt.as<int>(), nq, off.as<int>());
+        hipLaunchKernelGGL(fk, dim3(blocks), dim3(256), 0, stream, a);
+        ORBFE_HIP(hipGetLastError());
+        uint8_t* q = stage(sizeof(int));
+        if (!q) return ORBFE_ERR_NOMEM;
+        ORBFE_HIP(hipMemcpyAsync(q, off.as<int>() + nq, sizeof(int), hipMemcpyDeviceToHost, stream));
+        pend.push_back(Pending{&cand_total, q, sizeof(int)});
+        cand_cap_used = cap;
+        cand_check = true;
+        return ORBFE_OK;
+    }
+
+    template <class Args, class CountK, class FillK>
+    int csr(Args& a, int nq, CountK ck, FillK fk, int& total, int per_block = 256) {
         int st;
         if ((st = cnt.ensure(std::max(nq, 1) * sizeof(int)))) return st;
         if ((st = off.ensure((nq + 1) * sizeof(int)))) return st;
         a.cnt = cnt.as<int>();
         a.off = off.as<int>();
-        const int blocks = std::max(1, (nq + 255) / 256);
+        if ((st = flush())) return st;
+        const int blocks = std::max(1, (nq + per_block - 1) / per_block);
         hipLaunchKernelGGL(ck, dim3(blocks), dim3(256), 0, stream, a);
         hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, stream, cnt.as<int>(), nq, off.as<int>());
         ORBFE_HIP(hipMemcpyAsync(&total, off.as<int>() + nq, sizeof(int), hipMemcpyDeviceToHost, stream));
@@ -147,6 +296,7 @@ struct orbfe_matcher {
         if ((st = g_chg.ensure((size_t)(M + 2) * sizeof(int)))) return st;
         if ((st = g_hist.ensure(32 * sizeof(int)))) return st;
         if ((st = scal.ensure(16))) return st;
+        if ((st = flush())) return st;
         g.T[0] = g_t0.as<int>();
         g.T[1] = g_t1.as<int>();
         g.T[2] = g_t2.as<int>();
@@ -156,6 +306,14 @@ struct orbfe_matcher {
         g.bins = g_bins.as<int>();
         g.hist = g_hist.as<int>();
         g.nm = scal.as<int>();
+        if (M <= kGreedySmallMax && N <= kGreedySmallSlots && !total) {  // one workgroup
+            hipLaunchKernelGGL(greedy_small_kernel, dim3(1), dim3(kGreedySmallBlock),
+                               (size_t)3 * std::max(N, 1) * sizeof(int), stream, g);
+            ORBFE_HIP(hipGetLastError());
+            rounds_on_device = true;
+            return ORBFE_OK;
+        }
+        rounds_on_device = false;
         const int blocks = std::max(1, (std::max(std::max(M, N), 32) + kGreedyBlock - 1) / kGreedyBlock);
         const int mblocks = std::max(1, (M + kGreedyBlock - 1) / kGreedyBlock);
         const int nblocks = std::max(1, (N + kGreedyBlock - 1) / kGreedyBlock);
@@ -210,7 +368,14 @@ int guarded(orbfe_matcher* m, F&& f) {
     if (!m) return ORBFE_ERR_ARG;
     try {
         DeviceGuard dg(m->device);
-        return f();
+        m->begin();
+        const size_t need0 = m->cand_need;
+        int st = f();
+        if (st == ORBFE_ERR_CAPACITY && m->cand_need > need0) {  // candidates outgrew the bound
+            m->begin();
+            st = f();
+        }
+        return st;
     } catch (const std::bad_alloc&) {
         return ORBFE_ERR_NOMEM;
     } catch (...) {
@@ -264,11 +429,11 @@ int orbfe_hamming(orbfe_matcher* m, const uint8_t* a, const uint8_t* b, int n, i
         if ((st = m->up(m->q, a, (size_t)n * 32))) return st;
         if ((st = m->up(m->r, b, (size_t)n * 32))) return st;
         if ((st = m->out.ensure((size_t)n * sizeof(int)))) return st;
+        if ((st = m->flush())) return st;
         hipLaunchKernelGGL(hamming_kernel, dim3((n + 255) / 256), dim3(256), 0, m->stream,
                            m->q.as<uint4>(), m->r.as<uint4>(), n, m->out.as<int>());
         if ((st = m->down(dist, m->out, (size_t)n * sizeof(int)))) return st;
-        ORBFE_HIP(hipStreamSynchronize(m->stream));
-        return ORBFE_OK;
+        return m->sync();
     });
 }
 
@@ -285,12 +450,13 @@ int orbfe_bf_match(orbfe_matcher* m, const uint8_t* q, int nq, const uint8_t* r,
         if ((st = m->up(m->nq, counts, sizeof(counts)))) return st;
         if ((st = m->out.ensure((size_t)nq * 3 * sizeof(int)))) return st;
         if (nr >= 65536) return ORBFE_ERR_UNSUPPORTED;
+        if ((st = m->flush())) return st;
         hipLaunchKernelGGL(bf_match_kernel, dim3((nq + 63) / 64, 1), dim3(kBfBlock),
                            0, m->stream, m->q.as<uint8_t>(), 0ll, m->nq.as<int>(), nq,
                            m->r.as<uint8_t>(), 0ll, m->nq.as<int>() + 1, m->out.as<int>());
         std::vector<int> tri((size_t)nq * 3);
         if ((st = m->down(tri.data(), m->out, tri.size() * sizeof(int)))) return st;
-        ORBFE_HIP(hipStreamSynchronize(m->stream));
+        if ((st = m->sync())) return st;
         for (int i = 0; i < nq; ++i) {
             best_idx[i] = tri[3 * i];
             best_dist[i] = tri[3 * i + 1];
@@ -353,8 +519,7 @@ int orbfe_search_for_initialization(orbfe_matcher* m, float nnratio, int check_o
         if ((st = m->up(m->s5, prev_matched, (size_t)f1->n * 2 * sizeof(float)))) return st;
         a.prev = m->s5.as<float>();
         a.window = (float)window;
-        int total = 0;
-        if ((st = m->csr(a, f1->n, sfi_cand_kernel<false>, sfi_cand_kernel<true>, total))) return st;
+        if ((st = m->csr_async(a, f1->n, sfi_cand_kernel<false>, sfi_cand_kernel<true>, 4))) return st;
         const int n1 = f1->n, n2 = f2->n;
         if ((st = m->s1.ensure(std::max(n2, 1) * 3 * sizeof(int)))) return st;
         if ((st = m->s2.ensure(std::max(n1, 1) * 2 * sizeof(int)))) return st;
@@ -375,13 +540,13 @@ int orbfe_search_for_initialization(orbfe_matcher* m, float nnratio, int check_o
         r.rotbin = r.m12 + std::max(n1, 1);
         r.prev = m->s5.as<float>();
         r.nmatches = m->scal.as<int>();
+        if ((st = m->flush())) return st;
         hipLaunchKernelGGL(sfi_resolve_kernel, dim3(1), dim3(64), 0, m->stream, r);
         ORBFE_HIP(hipGetLastError());
         if ((st = m->down(matches12, m->s2, (size_t)n1 * sizeof(int)))) return st;
         if ((st = m->down(prev_matched, m->s5, (size_t)n1 * 2 * sizeof(float)))) return st;
         if ((st = m->down(nmatches, m->scal, sizeof(int)))) return st;
-        ORBFE_HIP(hipStreamSynchronize(m->stream));
-        return ORBFE_OK;
+        return m->sync();
     });
 }
 
@@ -445,8 +610,7 @@ int orbfe_search_by_projection_local(orbfe_matcher* m, float nnratio,
         if ((st = m->down(frame_mp, m->s1, (size_t)N * 4))) return st;
         if ((st = m->down(frame_mp_obs, m->s2, (size_t)N * 4))) return st;
         if ((st = m->down(nmatches, m->scal, sizeof(int)))) return st;
-        ORBFE_HIP(hipStreamSynchronize(m->stream));
-        return ORBFE_OK;
+        return m->sync();
     });
 }
 
@@ -504,8 +668,7 @@ int orbfe_search_by_projection_last(orbfe_matcher* m, int check_ori,
         const bool fwd = tlc[2] > cam->b && !mono;
         const bool bwd = -tlc[2] > cam->b && !mono;
         a.mode = fwd ? 1 : bwd ? 2 : 0;
-        int total = 0;
-        if ((st = m->csr(a, n_last, sbp_last_cand_kernel<false>, sbp_last_cand_kernel<true>, total)))
+        if ((st = m->csr_async(a, n_last, sbp_last_cand_kernel<false>, sbp_last_cand_kernel<true>, 4)))
             return st;
         const int N = cur->n;
         if ((st = m->up(m->s1, frame_mp, (size_t)N * 4))) return st;
@@ -535,8 +698,7 @@ int orbfe_search_by_projection_last(orbfe_matcher* m, int check_ori,
         if ((st = m->down(frame_mp, m->s1, (size_t)N * 4))) return st;
         if ((st = m->down(frame_mp_obs, m->s2, (size_t)N * 4))) return st;
         if ((st = m->down(nmatches, m->scal, sizeof(int)))) return st;
-        ORBFE_HIP(hipStreamSynchronize(m->stream));
-        return ORBFE_OK;
+        return m->sync();
     });
 }
 
@@ -592,12 +754,8 @@ int orbfe_search_by_projection_keyframe(orbfe_matcher* m, int check_ori,
         a.log_scale = log_scale_factor;
         a.th = th;
         a.status = m->scal.as<int>() + 1;
-        int total = 0;
-        if ((st = m->csr(a, n_kf, sbp_kf_cand_kernel<false>, sbp_kf_cand_kernel<true>, total)))
+        if ((st = m->csr_async(a, n_kf, sbp_kf_cand_kernel<false>, sbp_kf_cand_kernel<true>, 4)))
             return st;
-        int status = 0;  // csr() synchronized the stream after the count pass
-        ORBFE_HIP(hipMemcpy(&status, m->scal.as<int>() + 1, sizeof(int), hipMemcpyDeviceToHost));
-        if (status) return status;
         // a slot already holding a map point blocks (1529-1530), whatever its observations
         const int N = cur->n;
         if ((st = m->up(m->s1, frame_mp, (size_t)N * 4))) return st;
@@ -618,8 +776,13 @@ int orbfe_search_by_projection_keyframe(orbfe_matcher* m, int check_ori,
         if ((st = m->greedy(g))) return st;
         if ((st = m->down(frame_mp, m->s1, (size_t)N * 4))) return st;
         if ((st = m->down(nmatches, m->scal, sizeof(int)))) return st;
-        ORBFE_HIP(hipStreamSynchronize(m->stream));
-        return ORBFE_OK;
+        int status = 0;  // a predicted level outside the pyramid (outputs then unspecified)
+        uint8_t* q = m->stage(sizeof(int));
+        if (!q) return ORBFE_ERR_NOMEM;
+        ORBFE_HIP(hipMemcpyAsync(q, m->scal.as<int>() + 1, sizeof(int), hipMemcpyDeviceToHost, m->stream));
+        m->pend.push_back(orbfe_matcher::Pending{&status, q, sizeof(int)});
+        if ((st = m->sync())) return st;
+        return status;
     });
 }
 
@@ -652,14 +815,14 @@ int orbfe_distinctive_descriptors(orbfe_matcher* m, int n_mp, const int32_t* obs
         if ((st = m->up(m->m_d, obs_desc, nobs * 32))) return st;
         if ((st = m->s1.ensure((size_t)n_mp * 4))) return st;
         if ((st = m->q.ensure((size_t)n_mp * 32))) return st;
+        if ((st = m->flush())) return st;
         hipLaunchKernelGGL(distinctive_kernel, dim3((n_mp + 3) / 4), dim3(kDdBlock), 0, m->stream,
                            n_mp, m->o_i.as<int>(), m->m_d.as<uint4>(), m->s1.as<int>(),
                            desc_out ? m->q.as<uint4>() : nullptr);
         ORBFE_HIP(hipGetLastError());
         if ((st = m->down(best, m->s1, (size_t)n_mp * 4))) return st;
         if (desc_out && (st = m->down(desc_out, m->q, (size_t)n_mp * 32))) return st;
-        ORBFE_HIP(hipStreamSynchronize(m->stream));
-        return ORBFE_OK;
+        return m->sync();
     });
 }
 
@@ -779,7 +942,16 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
     });
 }
 
-int orbfe_matcher_last_rounds(const orbfe_matcher* m) { return m ? m->last_rounds : ORBFE_ERR_ARG; }
+int orbfe_matcher_last_rounds(const orbfe_matcher* m) {
+    if (!m) return ORBFE_ERR_ARG;
+    if (!m->rounds_on_device) return m->last_rounds;
+    int r = 0;
+    DeviceGuard dg(m->device);
+    if (hipStreamSynchronize(m->stream) != hipSuccess ||
+        hipMemcpy(&r, m->g_chg.p, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+        return ORBFE_ERR_HIP;
+    return r;
+}
 
 int orbfe_is_in_frustum(orbfe_matcher* m, int n, const float* xyz, const float* normal,
                         const float* min_dist, const float* max_dist, const float* tcw,
@@ -834,6 +1006,7 @@ int orbfe_is_in_frustum(orbfe_matcher* m, int n, const float* xyz, const float* 
         a.vcos = m->o_f3.as<float>();
         a.skip = a.bad = nullptr;
         a.n_in_view = nullptr;
+        if ((st = m->flush())) return st;
         hipLaunchKernelGGL(frustum_kernel, dim3((n + 255) / 256), dim3(256), 0, m->stream, a);
         ORBFE_HIP(hipGetLastError());
         if ((st = m->down(in_view, m->o_u, n))) return st;
@@ -842,8 +1015,7 @@ int orbfe_is_in_frustum(orbfe_matcher* m, int n, const float* xyz, const float* 
         if ((st = m->down(proj_xr, m->o_f2, (size_t)n * 4))) return st;
         if ((st = m->down(pred_level, m->o_i, (size_t)n * 4))) return st;
         if ((st = m->down(view_cos, m->o_f3, (size_t)n * 4))) return st;
-        ORBFE_HIP(hipStreamSynchronize(m->stream));
-        return ORBFE_OK;
+        return m->sync();
     });
 }
 
