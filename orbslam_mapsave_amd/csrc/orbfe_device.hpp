@@ -65,16 +65,11 @@ __device__ __forceinline__ int hamming256(const uint4 a0, const uint4 a1, const 
     return d;
 }
 
-// Inclusive sum over a 64-lane wave.
-__device__ __forceinline__ int wave_inclusive_sum(int x) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    return x;
-}
+// Inclusive sum over a 64-lane wave: the OCKL wavefront scan, six DPP adds (row_shr 1/2/4/8,
+// row_bcast 15/31) instead of six ds_bpermute shuffles.  Every lane of the wave must be active.
+extern "C" __device__ int __ockl_wfscan_add_i32(int, bool);
+extern "C" __device__ int __ockl_wfred_add_i32(int);
+__device__ __forceinline__ int wave_inclusive_sum(int x) { return __ockl_wfscan_add_i32(x, true); }
 
 // Slot of this lane's item in a block-shared list: one LDS atomic per wave (called by every
 // lane of the wave); -1 for lanes without an item.  Order among waves is unspecified.
@@ -89,11 +84,8 @@ __device__ __forceinline__ int wave_append(bool pred, int* counter) {
     return pred ? base + __popcll(m & ((1ull << lane) - 1)) : -1;
 }
 
-__device__ __forceinline__ int wave_sum(int x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-    return x;
-}
+// Sum over a 64-lane wave (DPP reduction, result in every lane); every lane must be active.
+__device__ __forceinline__ int wave_sum(int x) { return __ockl_wfred_add_i32(x); }
 
 // Block-wide exclusive scan of one int per thread.  `tmp` holds >= BLOCK/64 ints of LDS.
 // Returns the exclusive prefix; `total` receives the block sum.  Contains barriers: every

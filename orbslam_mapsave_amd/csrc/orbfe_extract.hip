@@ -40,6 +40,18 @@ __constant__ int c_umax[16];
 constexpr int kEdge = 19;       // EDGE_THRESHOLD (ORBextractor.cc:73)
 constexpr int kMinBorder = 16;  // EDGE_THRESHOLD - 3 (772)
 constexpr int kCellW = 30;      // W (768)
+// 16-byte global loads from addresses aligned to 4 bytes (FAST ROI rows) or to 1 byte (the
+// describe kernel's disc rows); memcpy lets the compiler pick dwordx4 with that alignment.
+__device__ __forceinline__ uint4 load16_a4(const uint8_t* p) {
+    uint4 v;
+    __builtin_memcpy(&v, __builtin_assume_aligned(p, 4), 16);
+    return v;
+}
+__device__ __forceinline__ uint4 load16_a1(const uint8_t* p) {
+    uint4 v;
+    __builtin_memcpy(&v, p, 16);
+    return v;
+}
 
 // ---------------------------------------------------------------------------------------------
 // K0 — pyramid level 0 from the caller's frame: cvtColor(CV_{RGB,BGR,RGBA,BGRA}2GRAY) of
@@ -321,30 +333,24 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
     uint8_t* roi_base = fast_lds;
     uint8_t* S = fast_lds + a.roi_rows * P;
     uint16_t* list = reinterpret_cast<uint16_t*>(S + (((a.roi_rows - 4) * P + 15) & ~15));
-    // dword loads: rows are 4-byte aligned (pitch % 4 == 0, enforced by the host)
+    // Each lane copies whole ROI rows with 16-byte loads from the dword-aligned x0a (global
+    // dwordx4 needs only 4-byte alignment; LDS rows are 16-byte aligned, P % 16 == 0).  A row
+    // spans <= 5 chunks; the bytes past x1 (< 16) stay inside the level row or the next one,
+    // and ROI rows never reach the level's last row.
     const int x0a = cell.x0 & ~3, shift = cell.x0 - x0a;
-    const int wpr = (shift + cols + 3) >> 2;
+    const int nq = (shift + cols + 15) >> 4;
     const uint8_t* img = lp.base + f * lp.fpitch + (long long)cell.y0 * lp.pitch + x0a;
-    {   // all dword loads of the ROI in flight before the LDS stores (<= 72 rows x 19 dwords)
-        const int nw = rows * wpr;
-        const DivNc dw(wpr);
-        uint32_t buf[8];
+    for (int r0 = 0; r0 < rows; r0 += 64) {
+        const int r = r0 + lane;
+        if (r < rows) {
+            const uint8_t* src = img + (long long)r * lp.pitch;
+            uint4 v[5];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int i = lane + 64 * k;
-            const int r = dw.row(i), w = i - r * wpr;
-            buf[k] = i < nw ? *reinterpret_cast<const uint32_t*>(img + (long long)r * lp.pitch + 4 * w) : 0u;
-        }
+            for (int q = 0; q < 5; ++q)
+                if (q < nq) v[q] = load16_a4(src + 16 * q);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int i = lane + 64 * k;
-            const int r = dw.row(i), w = i - r * wpr;
-            if (i < nw) *reinterpret_cast<uint32_t*>(roi_base + r * P + 4 * w) = buf[k];
-        }
-        for (int i = lane + 512; i < nw; i += 64) {  // very large cells (tiny levels) only
-            const int r = i / wpr, w = i - r * wpr;
-            *reinterpret_cast<uint32_t*>(roi_base + r * P + 4 * w) =
-                *reinterpret_cast<const uint32_t*>(img + (long long)r * lp.pitch + 4 * w);
+            for (int q = 0; q < 5; ++q)
+                if (q < nq) *reinterpret_cast<uint4*>(roi_base + r * P + 16 * q) = v[q];
         }
     }
     const uint8_t* roi = roi_base + shift;
@@ -1013,7 +1019,6 @@ constexpr int kDescWinR = 18;                        // rotated pattern radius b
 constexpr int kDescWinRows = 2 * kDescWinR + 1;      // 37
 constexpr int kDescWinP = 48;                        // bytes per window row (3 x 16)
 constexpr int kDescWinBytes = kDescWinRows * kDescWinP;
-typedef uint4 __attribute__((aligned(1))) uint4_u;  // unaligned 16-byte global load
 typedef float float2v __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
     int bx, f;
@@ -1080,7 +1085,7 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
             const LevelPtr pp = a.pyr[kl];
             const uint8_t* row = pp.base + f * pp.fpitch + (long long)(key_y(kk) + v) * pp.pitch +
                                  key_x(kk) - 15 + 16 * hh;
-            px[j] = *reinterpret_cast<const uint4_u*>(row);
+            px[j] = load16_a1(row);
         }
     }
     int M10 = 0, M01 = 0;
@@ -1393,7 +1398,7 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
         cmax = std::max(cmax, c.x1 - c.x0);
     }
     g.roi_rows = rmax;
-    g.roi_pitch = (cmax + 3 + 3) & ~3;  // + alignment shift, rounded to dwords
+    g.roi_pitch = (cmax + 3 + 15) & ~15;  // + alignment shift, 16-byte rows for b128 LDS writes
     g.cand_max = (rmax - 6) * (cmax - 6);
     // ROI + zero-bordered score plane at the ROI pitch + candidate list of u16 ROI offsets
     if ((long long)rmax * g.roi_pitch >= 65536) return ORBFE_ERR_UNSUPPORTED;
