@@ -878,8 +878,17 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
 // tile per workgroup of 32 x 8 threads; each thread makes 4 x 4 pixels from dword LDS reads.
 constexpr int kBlurTW = kBlurTileW, kBlurTH = kBlurTileH;
 constexpr int kBlurRPT = kBlurTH / 8;  // output rows per thread (256 threads = 8 x 32)
-constexpr int kBlurIP = kBlurTW + 8;   // input row: image cols [ox-4, ox+TW+4)
+// cv::borderInterpolate(p, len, BORDER_REFLECT_101) (App. A.2), any distance from the edge.
+__device__ __forceinline__ int reflect101(int p, int len) {
+    if (len == 1) return 0;
+    while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - p - 2;
+    return p;
+}
+constexpr int kBlurIW = kBlurTW + 8;   // input row: image cols [ox-4, ox+TW+4)
+constexpr int kBlurIQ = (kBlurIW + 15) / 16;  // 16-byte chunks per input row (9)
+constexpr int kBlurIP = 16 * kBlurIQ;  // LDS row pitch (144, 16-byte aligned)
 constexpr int kBlurIR = kBlurTH + 6;   // input rows [oy-3, oy+TH+3)
+constexpr int kBlurRPW = 64 / kBlurIQ;  // input rows per wave per step (7)
 __global__ __launch_bounds__(256) void blur_kernel(BlurArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t in[kBlurIR * kBlurIP];
     __shared__ __attribute__((aligned(16))) uint16_t rowp[kBlurIR * kBlurTW];  // row pairs, u16x2
@@ -893,36 +902,31 @@ __global__ __launch_bounds__(256) void blur_kernel(BlurArgs a) {
     const LevelPtr sp = a.src[l];
     const uint8_t* src = sp.base + f * sp.fpitch;
     const int tid = threadIdx.x;
-    // input rows are reflected by picking the row pointer; only dwords that straddle the left
-    // or right edge are assembled byte by byte (reflect-101, level sizes >= 4)
-    constexpr int WPR = kBlurIP / 4;
-    constexpr int NLD = (kBlurIR * WPR + 255) / 256;  // dwords per thread
-    uint32_t buf[NLD];
+    // Staging: lane (row rr = lane / 9, chunk q = lane % 9) of every wave copies 16 bytes; the
+    // four waves walk the 38 input rows 7 at a time.  Rows are reflected (REFLECT_101) by the
+    // row pointer; a chunk that leaves [0, w) is assembled byte by byte with reflected columns
+    // (tiles at the left / right edge only).  Level sizes are >= 4.
+    {
+        const int lane = tid & 63, wid = tid >> 6;
+        const int rr = lane / kBlurIQ, q = lane - rr * kBlurIQ;
+        const int x = ox - 4 + 16 * q;
+        const bool inside = x >= 0 && x + 16 <= w;
+        for (int r = wid * kBlurRPW + rr; rr < kBlurRPW && r < kBlurIR; r += 4 * kBlurRPW) {
+            const int yy = reflect101(oy - 3 + r, h);
+            const uint8_t* row = src + (long long)yy * sp.pitch;
+            uint4 v;
+            if (inside) {
+                v = load16_a4(row + x);  // pitch % 4 == 0, x % 4 == 0
+            } else {
+                uint32_t b[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int k = 0; k < NLD; ++k) {  // issue every load before the first LDS store
-        const int i = tid + 256 * k;
-        const int r = min(i / WPR, kBlurIR - 1), c = i - (i / WPR) * WPR;
-        int yy = oy - 3 + r;
-        while (yy < 0 || yy >= h) yy = yy < 0 ? -yy : 2 * h - yy - 2;
-        const uint8_t* row = src + (long long)yy * sp.pitch;
-        const int x = ox - 4 + 4 * c;
-        uint32_t v = 0;
-        if (x >= 0 && x + 4 <= w) {
-            v = *reinterpret_cast<const uint32_t*>(row + x);  // pitch % 4 == 0, x % 4 == 0
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                int xx = x + q;
-                while (xx < 0 || xx >= w) xx = xx < 0 ? -xx : 2 * w - xx - 2;
-                v |= (uint32_t)row[xx] << (8 * q);
+                for (int k = 0; k < 16; ++k) {
+                    b[k >> 2] |= (uint32_t)row[reflect101(x + k, w)] << (8 * (k & 3));
+                }
+                v = make_uint4(b[0], b[1], b[2], b[3]);
             }
+            *reinterpret_cast<uint4*>(in + r * kBlurIP + 16 * q) = v;
         }
-        buf[k] = v;
-    }
-#pragma unroll
-    for (int k = 0; k < NLD; ++k) {
-        const int i = tid + 256 * k;
-        if (i < kBlurIR * WPR) *reinterpret_cast<uint32_t*>(in + (i / WPR) * kBlurIP + 4 * (i % WPR)) = buf[k];
     }
     __syncthreads();
     // Row pass on bytes: output col c = dot4(bytes c+1..c+4, k0 k1 k2 k3) + dot4(bytes c+5..c+8,
