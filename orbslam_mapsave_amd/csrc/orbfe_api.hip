@@ -240,18 +240,7 @@ struct orbfe_extractor {
         oa.ncap_max = g.ncap_max;
         oa.sort_cap = g.sort_cap;
         ORBFE_LAUNCH(prof, ORBFE_STAGE_OCTREE, octree_kernel, dim3(L, n), dim3(kOctBlockSize), g.oct_lds, stream, oa);
-        // K4 blur
-        BlurArgs ba;
-        ba.nlevels = L;
-        for (int l = 0; l < L; ++l) {
-            ba.tile_begin[l] = g.tile_begin[l];
-            ba.w[l] = g.geo.lv[l].w;
-            ba.h[l] = g.geo.lv[l].h;
-            ba.src[l] = lp[l];
-            ba.dst[l] = bp[l];
-        }
-        for (int i = 0; i < 4; ++i) ba.taps[i] = tab.taps[i];
-        ORBFE_LAUNCH(prof, ORBFE_STAGE_BLUR, blur_kernel, dim3(g.tiles_total, n), dim3(256), 0, stream, ba);
+        // K4 (the blur) is fused into K5: each keypoint's window is blurred in LDS
         // K5 describe
         DescArgs da;
         da.nlevels = L;
@@ -262,8 +251,10 @@ struct orbfe_extractor {
             da.scale[l] = g.geo.lv[l].scale;
             da.size[l] = g.geo.lv[l].size;
             da.pyr[l] = lp[l];
-            da.blur[l] = bp[l];
+            da.w[l] = g.geo.lv[l].w;
+            da.h[l] = g.geo.lv[l].h;
         }
+        for (int i = 0; i < 4; ++i) da.taps[i] = tab.taps[i];
         da.oct_out = oct_out.as<uint32_t>();
         da.oct_cnt = oct_cnt.as<int>();
         da.kps = d_kps;
@@ -835,8 +826,24 @@ int orbfe_get_blurred_level(orbfe_extractor* h, int frame, int level, uint8_t* o
     if (!h || !h->planned || frame < 0 || frame >= h->last_n || level < 0 ||
         level >= h->tab.p.nlevels)
         return ORBFE_ERR_ARG;
-    const LevelGeo& lv = h->plan.geo.lv[level];
-    LevelPtr bp{h->blur.as<uint8_t>() + lv.off, h->plan.slab, lv.pitch};
+    const Plan& g = h->plan;
+    const LevelGeo& lv = g.geo.lv[level];
+    LevelPtr bp{h->blur.as<uint8_t>() + lv.off, g.slab, lv.pitch};
+    if (out) {  // K4 on demand: the extraction path blurs keypoint windows inside K5
+        DeviceGuard dg(h->device);
+        BlurArgs ba;
+        ba.nlevels = g.geo.nlevels;
+        for (int l = 0; l < ba.nlevels; ++l) {
+            ba.tile_begin[l] = g.tile_begin[l];
+            ba.w[l] = g.geo.lv[l].w;
+            ba.h[l] = g.geo.lv[l].h;
+            ba.src[l] = h->last_pyr[l];
+            ba.dst[l] = LevelPtr{h->blur.as<uint8_t>() + g.geo.lv[l].off, g.slab, g.geo.lv[l].pitch};
+        }
+        for (int i = 0; i < 4; ++i) ba.taps[i] = h->tab.taps[i];
+        hipLaunchKernelGGL(blur_kernel, dim3(g.tiles_total, h->last_n), dim3(256), 0, h->stream, ba);
+        ORBFE_HIP(hipGetLastError());
+    }
     return copy_level(h, bp, frame, level, out, w, hgt);
 }
 

@@ -1129,48 +1129,136 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
     // magic-number add (|v| < 2^22, round-to-nearest-even): bits(v + 1.5 * 2^23) =
     // 0x4b400000 + rne(v); v_mul_u32_u24 takes its low 24 bits, 0x400000 + rne(v), so one
     // per-keypoint constant turns the pair into the window index (18 + ry) * 48 + cx + rx.
-    uint32_t my_blo = 0, my_bhi = 0, my_kc = 0;
+    //
+    // The window is blurred here (GaussianBlur 7x7 sigma 2 REFLECT_101, ORBextractor.cc:1088-1089;
+    // K4 does not run on the extraction path): window rows y-18..y+18 x cols x0..x0+47 need raw
+    // rows y-21..y+21 and cols x0-3..x0+42 (samples reach window cols 0..39).  The wave copies 43
+    // raw rows x 3 chunks of 16 bytes from x0-4 into LDS (loads of the next keypoint in flight
+    // during the current one) and blurs window cols 0..39 of all 37 rows; when a
+    // sampled pixel's 7x7 support leaves the level, or a chunk would leave the row, the raw
+    // window is assembled byte by byte with reflect101 indices instead.  Then blur_kernel's
+    // integer passes: rows by v_dot4 into u16 row pairs, columns by v_dot2 + 2^15 >> 16.
+    uint32_t my_kc = 0;
     if (valid) {
-        const LevelPtr bp = a.blur[my_l];
-        const int x = key_x((uint32_t)my_key), y = key_y((uint32_t)my_key);
+        const int x = key_x((uint32_t)my_key);
         const int x0 = (x - kDescWinR) & ~3;
-        const uint64_t base = (uint64_t)(bp.base + f * bp.fpitch + (long long)(y - kDescWinR) * bp.pitch + x0);
-        my_blo = (uint32_t)base;
-        my_bhi = (uint32_t)(base >> 32);
         my_kc = (uint32_t)(kDescWinR * kDescWinP + (x - x0)) - 0x400000u * kDescWinP - 0x4b400000u;
     }
-    int my_st = valid ? a.blur[my_l].pitch : 0;
     float pat[16];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int c = 0; c < 4; ++c) pat[4 * q + c] = (float)c_pattern[4 * (lane + 64 * q) + c];
     const float2v MG = float2v{12582912.f, 12582912.f};
-    __shared__ __attribute__((aligned(16))) uint8_t win_all[kDescBlock / 64][2][kDescWinBytes];
-    uint8_t(*win)[kDescWinBytes] = win_all[threadIdx.x >> 6];
-    // chunk c = lane (+ 64): row c / 3, 16-byte part c % 3
-    const int ca_row = lane / 3, ca_part = lane - 3 * (lane / 3);
-    const int cb = lane + 64, cb_row = cb / 3, cb_part = cb - 3 * (cb / 3);
-    const bool cb_on = cb < kDescWinRows * 3;
-    uint4 ra = make_uint4(0u, 0u, 0u, 0u), rb = ra;
-    auto load_win = [&](int j) {
-        const uint64_t base = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)my_blo, j) |
-                              ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)my_bhi, j) << 32);
-        const long long st = __builtin_amdgcn_readlane(my_st, j);
-        const uint8_t* w0 = reinterpret_cast<const uint8_t*>(base);
-        ra = *reinterpret_cast<const uint4*>(w0 + ca_row * st + 16 * ca_part);
-        if (cb_on) rb = *reinterpret_cast<const uint4*>(w0 + cb_row * st + 16 * cb_part);
+    constexpr int kRawRows = 2 * (kDescWinR + 3) + 2;  // 44 (43 used, one pad row for pairs)
+    constexpr int kRawP = 48;                          // raw row: image cols [x0-4, x0+44)
+    constexpr int kRawQ = kRawP / 16;                  // 16-byte chunks per raw row
+    constexpr int kPairs = kRawRows / 2;               // 22 u16 row pairs
+    // samples reach window cols (x - x0) +- 18 with x - x0 in [18, 21]: cols 0..39, 10 quads
+    constexpr int kBlurQ = 10;
+    __shared__ __attribute__((aligned(16))) uint8_t raw_all[kDescBlock / 64][kRawRows * kRawP];
+    __shared__ __attribute__((aligned(16))) uint32_t rowp_all[kDescBlock / 64][kPairs * kDescWinP];
+    __shared__ __attribute__((aligned(16))) uint8_t win_all[kDescBlock / 64][kDescWinBytes];
+    uint8_t* raw = raw_all[threadIdx.x >> 6];
+    uint32_t* rowp = rowp_all[threadIdx.x >> 6];
+    uint8_t* wb = win_all[threadIdx.x >> 6];
+    const uint32_t KLO = (uint32_t)(a.taps[0] | (a.taps[1] << 8) | (a.taps[2] << 16) | (a.taps[3] << 24));
+    const uint32_t KHI = (uint32_t)(a.taps[2] | (a.taps[1] << 8) | (a.taps[0] << 16));
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    const unsigned short k0 = (unsigned short)a.taps[0], k1 = (unsigned short)a.taps[1],
+                         k2 = (unsigned short)a.taps[2], k3 = (unsigned short)a.taps[3];
+    const us2 T01 = us2{k0, k1}, T23 = us2{k2, k3}, T21 = us2{k2, k1}, T0L = us2{k0, 0},
+              T0H = us2{0, k0}, T12 = us2{k1, k2}, T32 = us2{k3, k2}, T10 = us2{k1, k0};
+    // raw chunk c = lane + 64 i (i < 3, c < 43 * 3): row c / 3, 16-byte part c % 3
+    uint4 rv[3];
+    auto load_raw = [&](int j) {
+        const int kl = __builtin_amdgcn_readlane(my_l, j);
+        const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane(my_key, j);
+        const int x = key_x(kk), y = key_y(kk), x0 = (x - kDescWinR) & ~3;
+        const LevelPtr pp = a.pyr[kl];
+        const int lw = a.w[kl], lh = a.h[kl];
+        const uint8_t* fb = pp.base + f * pp.fpitch;
+        const bool fast = x0 - 4 >= 0 && x0 + 44 <= pp.pitch && x - 21 >= 0 && x + 21 < lw &&
+                          y - 21 >= 0 && y + 21 < lh;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int c = lane + 64 * i, r = c / kRawQ, part = c - kRawQ * r;
+            rv[i] = make_uint4(0u, 0u, 0u, 0u);
+            if (r >= kRawRows - 1) continue;
+            if (fast) {
+                rv[i] = load16_a4(fb + (long long)(y - 21 + r) * pp.pitch + x0 - 4 + 16 * part);
+            } else {
+                const uint8_t* row = fb + (long long)reflect101(y - 21 + r, lh) * pp.pitch;
+                uint32_t bb[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    bb[k >> 2] |= (uint32_t)row[reflect101(x0 - 4 + 16 * part + k, lw)] << (8 * (k & 3));
+                rv[i] = make_uint4(bb[0], bb[1], bb[2], bb[3]);
+            }
+        }
     };
-    load_win(__ffsll((long long)vmask) - 1);
-    int buf = 0;
-    for (unsigned long long m = vmask; m; m &= m - 1, buf ^= 1) {
+    load_raw(__ffsll((long long)vmask) - 1);
+    for (unsigned long long m = vmask; m; m &= m - 1) {
         const int j = __ffsll((long long)m) - 1;
-        uint8_t* wb = win[buf];
-        *reinterpret_cast<uint4*>(wb + ca_row * kDescWinP + 16 * ca_part) = ra;
-        if (cb_on) *reinterpret_cast<uint4*>(wb + cb_row * kDescWinP + 16 * cb_part) = rb;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int c = lane + 64 * i;
+            if (c / kRawQ < kRawRows - 1) *reinterpret_cast<uint4*>(raw + 16 * c) = rv[i];
+        }
         __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         const unsigned long long rest = m & (m - 1);
-        if (rest) load_win(__ffsll((long long)rest) - 1);  // next keypoint's window in flight
+        if (rest) load_raw(__ffsll((long long)rest) - 1);  // next keypoint's raw window in flight
+        // row pass: item (pair pr, quad q) -> window cols 4q..4q+3 of raw rows 2pr, 2pr+1
+        for (int it = lane; it < kPairs * kBlurQ; it += 64) {
+            const int pr = it / kBlurQ, q = it - pr * kBlurQ;
+            uint32_t hh[2][4];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const uint32_t* row = reinterpret_cast<const uint32_t*>(raw + (2 * pr + e) * kRawP) + q;
+                const uint32_t w0 = row[0], w1 = row[1], w2 = row[2];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const uint32_t lo = jj < 3 ? __builtin_amdgcn_alignbyte(w1, w0, jj + 1) : w1;
+                    const uint32_t hi = jj < 3 ? __builtin_amdgcn_alignbyte(w2, w1, jj + 1) : w2;
+                    hh[e][jj] = __builtin_amdgcn_udot4(hi, KHI, __builtin_amdgcn_udot4(lo, KLO, 0u, false), false);
+                }
+            }
+            *reinterpret_cast<uint4*>(rowp + pr * kDescWinP + 4 * q) =
+                make_uint4(hh[0][0] | (hh[1][0] << 16), hh[0][1] | (hh[1][1] << 16),
+                           hh[0][2] | (hh[1][2] << 16), hh[0][3] | (hh[1][3] << 16));
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        // column pass: item (output rows 2jp, 2jp+1; quad q) from pairs jp..jp+3
+        for (int it = lane; it < ((kDescWinRows + 1) / 2) * kBlurQ; it += 64) {
+            const int jp = it / kBlurQ, q = it - jp * kBlurQ;
+            uint4 P4[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) P4[i] = *reinterpret_cast<const uint4*>(rowp + (jp + i) * kDescWinP + 4 * q);
+            uint32_t ev[4], od[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const uint32_t p0 = (&P4[0].x)[c], p1 = (&P4[1].x)[c], p2 = (&P4[2].x)[c], p3 = (&P4[3].x)[c];
+                uint32_t v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T01, 1u << 15, false);
+                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), T23, v, false);
+                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), T21, v, false);
+                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), T0L, v, false);
+                ev[c] = min(v, 0xffffffu);  // byte 2 = min(acc >> 16, 255)
+                uint32_t u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T0H, 1u << 15, false);
+                u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), T12, u, false);
+                u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), T32, u, false);
+                u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), T10, u, false);
+                od[c] = min(u, 0xffffffu);
+            }
+            *reinterpret_cast<uint32_t*>(wb + (2 * jp) * kDescWinP + 4 * q) =
+                __builtin_amdgcn_perm(ev[1], ev[0], 0x0c0c0602u) | __builtin_amdgcn_perm(ev[3], ev[2], 0x06020c0cu);
+            if (2 * jp + 1 < kDescWinRows)
+                *reinterpret_cast<uint32_t*>(wb + (2 * jp + 1) * kDescWinP + 4 * q) =
+                    __builtin_amdgcn_perm(od[1], od[0], 0x0c0c0602u) | __builtin_amdgcn_perm(od[3], od[2], 0x06020c0cu);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         const float cj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ca), j));
         const float sj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, sa), j));
         const uint32_t kc = (uint32_t)__builtin_amdgcn_readlane((int)my_kc, j);
@@ -1194,6 +1282,8 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
             const unsigned long long wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
             reinterpret_cast<unsigned long long*>(a.desc + outi * 32)[lane] = wv;
         }
+        __builtin_amdgcn_wave_barrier();  // the window is rewritten for the next keypoint
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
     if (valid) {
         const uint32_t kk = (uint32_t)my_key;

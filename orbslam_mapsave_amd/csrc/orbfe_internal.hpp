@@ -115,8 +115,9 @@ struct DescArgs {
     int nlevels, out_total, kps_cap;
     int out_off[kMaxLevels];
     float scale[kMaxLevels], size[kMaxLevels];
+    int w[kMaxLevels], h[kMaxLevels];
+    int taps[4];
     LevelPtr pyr[kMaxLevels];
-    LevelPtr blur[kMaxLevels];
     const uint32_t* oct_out;
     const int* oct_cnt;
     orbfe_keypoint* kps;
