@@ -51,18 +51,24 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
 }
 
 // ORBmatcher::DescriptorDistance (ORBmatcher.cc:1650-1666): popcount of XOR over 8 words.
-// v_bcnt_u32_b32 accumulates, so a 256-bit distance is 8 XORs + 8 bit-counts.
+// v_bcnt_u32_b32 adds its second operand, so the 8 counts chain into one accumulator: a
+// 256-bit distance is 8 v_xor + 8 v_bcnt (the compiler otherwise sums the counts with add3).
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+    return r;
+}
 __device__ __forceinline__ int hamming256(const uint4 a0, const uint4 a1, const uint4 b0,
                                           const uint4 b1) {
-    int d = __builtin_popcount(a0.x ^ b0.x);
-    d += __builtin_popcount(a0.y ^ b0.y);
-    d += __builtin_popcount(a0.z ^ b0.z);
-    d += __builtin_popcount(a0.w ^ b0.w);
-    d += __builtin_popcount(a1.x ^ b1.x);
-    d += __builtin_popcount(a1.y ^ b1.y);
-    d += __builtin_popcount(a1.z ^ b1.z);
-    d += __builtin_popcount(a1.w ^ b1.w);
-    return d;
+    uint32_t d = bcnt_acc(a0.x ^ b0.x, 0u);
+    d = bcnt_acc(a0.y ^ b0.y, d);
+    d = bcnt_acc(a0.z ^ b0.z, d);
+    d = bcnt_acc(a0.w ^ b0.w, d);
+    d = bcnt_acc(a1.x ^ b1.x, d);
+    d = bcnt_acc(a1.y ^ b1.y, d);
+    d = bcnt_acc(a1.z ^ b1.z, d);
+    d = bcnt_acc(a1.w ^ b1.w, d);
+    return (int)d;
 }
 
 // Inclusive sum over a 64-lane wave: the OCKL wavefront scan, six DPP adds (row_shr 1/2/4/8,

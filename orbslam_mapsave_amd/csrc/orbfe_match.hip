@@ -88,13 +88,18 @@ __global__ __launch_bounds__(kBfBlock) void bf_match_kernel(const uint8_t* q, lo
             tile[w][2 * lane + 1] = R[2 * (base + lane) + 1];
         }
         __syncthreads();
-#pragma unroll 4
-        for (int j = 0; j < cnt; ++j) {
+        auto step = [&](int j) {
             const unsigned d = (unsigned)hamming256(a0, a1, tile[w][2 * j], tile[w][2 * j + 1]);
             const unsigned key = (d << 16) | (unsigned)(base + j);
             const unsigned hi = max(best, key);
             best = min(best, key);
             second = min(second, hi);
+        };
+        if (cnt == kBfTile) {  // full tile: constant trip count, unrolled so the broadcast
+#pragma unroll 8          // LDS reads of the next references overlap the current counts
+            for (int j = 0; j < kBfTile; ++j) step(j);
+        } else {
+            for (int j = 0; j < cnt; ++j) step(j);
         }
         __syncthreads();
     }
