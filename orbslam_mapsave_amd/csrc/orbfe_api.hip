@@ -192,8 +192,10 @@ struct orbfe_extractor {
             bp[l] = LevelPtr{blur.as<uint8_t>() + lv.off, g.slab, lv.pitch};
         }
         lp[0] = l0;
-        // K1 cascaded pyramid: one launch per level, 128 x 32 tiles of every frame
-        for (int l = 1; l < L; ++l) {
+        // K1 cascaded pyramid: one launch per level, 128 x 32 tiles of every frame; the small
+        // top levels (tail_start ..) in one K1b launch, a workgroup per frame
+        const int ts = std::min(g.tail_start, L);
+        for (int l = 1; l < ts; ++l) {
             ResizeArgs ra;
             ra.src = lp[l - 1];
             ra.dst = lp[l];
@@ -207,6 +209,25 @@ struct orbfe_extractor {
             ra.yt = ytab.as<int>() + g.yoff[l];
             ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resize_kernel, dim3(g.rs_tiles[l], n), dim3(256),
                          g.rs_lds[l], stream, ra);
+        }
+        if (ts < L) {
+            ResizeTailArgs ta;
+            ta.src = lp[ts - 1];
+            ta.sh = g.geo.lv[ts - 1].h;
+            ta.nt = L - ts;
+            ta.lp[0] = (g.geo.lv[ts - 1].w + 3) & ~3;
+            ta.buf_b = ta.lp[0] * ta.sh;
+            for (int k = 0; k < ta.nt; ++k) {
+                const int l = ts + k;
+                ta.lp[k + 1] = (g.geo.lv[l].w + 3) & ~3;
+                ta.dw[k] = g.geo.lv[l].w;
+                ta.dh[k] = g.geo.lv[l].h;
+                ta.xt[k] = xtab.as<int>() + g.xoff[l];
+                ta.yt[k] = ytab.as<int>() + g.yoff[l];
+                ta.dst[k] = lp[l];
+            }
+            ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resize_tail_kernel, dim3(n), dim3(kTailBlock), 0,
+                         stream, ta);
         }
         // K2 FAST per cell
         const int ncells = (int)g.cells.size();

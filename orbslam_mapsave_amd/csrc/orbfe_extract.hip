@@ -211,6 +211,80 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
     }
 }
 
+// K1b — the small top levels in one launch: one 1024-thread workgroup per frame copies level
+// ts-1 into LDS, then makes levels ts .. L-1 one after the other, each from the previous one
+// held in LDS (two buffers, ping-pong), writing every level to the pyramid as well.  Same
+// host tables and integer arithmetic as resize_kernel.  Used when the two largest levels of
+// the tail fit the workgroup's LDS (levels 5-7 at 640 x 480).
+constexpr int kTailBlock = 1024;
+constexpr int kTailLds = 144 * 1024;
+__global__ __launch_bounds__(kTailBlock) void resize_tail_kernel(ResizeTailArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kTailLds];
+    const int f = blockIdx.x;
+    const int tid = threadIdx.x;
+    uint8_t* buf[2] = {lds, lds + a.buf_b};
+    {   // level ts-1 from the pyramid, dword rows (pitches % 4 == 0)
+        const LevelPtr sp = a.src;
+        const uint8_t* src = sp.base + f * sp.fpitch;
+        const int wpr = a.lp[0] >> 2;
+        for (int i = tid; i < a.sh * wpr; i += kTailBlock) {
+            const int r = i / wpr, c = i - r * wpr;
+            *reinterpret_cast<uint32_t*>(buf[0] + r * a.lp[0] + 4 * c) =
+                *reinterpret_cast<const uint32_t*>(src + (long long)r * sp.pitch + 4 * c);
+        }
+    }
+    __syncthreads();
+    for (int k = 0; k < a.nt; ++k) {
+        const uint8_t* s = buf[k & 1];
+        uint8_t* d = buf[(k + 1) & 1];
+        const int sp_l = a.lp[k], dp_l = a.lp[k + 1];
+        const int dw = a.dw[k], dh = a.dh[k];
+        const int* xt = a.xt[k];
+        const int* yt = a.yt[k];
+        const int gpr = (dw + 3) >> 2;           // 4-pixel groups per row
+        const int rps = kTailBlock / gpr;        // rows per sweep
+        const int gx = tid % gpr, ry = tid / gpr;
+        const LevelPtr dp = a.dst[k];
+        uint8_t* dst = const_cast<uint8_t*>(dp.base) + f * dp.fpitch;
+        if (ry < rps) {
+            const int x = 4 * gx;
+            const int n = min(4, dw - x);
+            int x0[4], x1[4], a0[4], a1[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int dx = min(x + q, dw - 1);
+                x0[q] = xt[3 * dx];
+                x1[q] = xt[3 * dx + 1];
+                const int aa = xt[3 * dx + 2];
+                a0[q] = aa & 0xffff;
+                a1[q] = (int)((unsigned)aa >> 16);
+            }
+            for (int y = ry; y < dh; y += rps) {
+                const int bb = yt[3 * y + 2];
+                const int b0 = bb & 0xffff, b1 = (int)((unsigned)bb >> 16);
+                const uint8_t* s0 = s + yt[3 * y] * sp_l;
+                const uint8_t* s1 = s + yt[3 * y + 1] * sp_l;
+                uint32_t packed = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int t0 = s0[x0[q]] * a0[q] + s0[x1[q]] * a1[q];
+                    const int t1 = s1[x0[q]] * a0[q] + s1[x1[q]] * a1[q];
+                    const int v = min(max((t0 * b0 + t1 * b1 + (1 << 21)) >> 22, 0), 255);
+                    packed |= (uint32_t)v << (8 * q);
+                }
+                *reinterpret_cast<uint32_t*>(d + y * dp_l + x) = packed;  // LDS pitch % 4 == 0
+                uint8_t* o = dst + (long long)y * dp.pitch + x;
+                if (n == 4) {
+                    *reinterpret_cast<uint32_t*>(o) = packed;
+                } else {
+                    for (int q = 0; q < n; ++q) o[q] = (uint8_t)(packed >> (8 * q));
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // K2 — FAST per cell.  S(p) = max(q0, -q1) - 1 where q0 (q1) is the max (min) over the 16
 // nine-pixel arcs of the min (max) of d = v - circle: p is a cv::FAST corner at threshold t iff
@@ -1486,6 +1560,17 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
         }
     }
     if (w > 4096 || h > 4096) return ORBFE_ERR_UNSUPPORTED;
+    {   // K1b: the longest run of top levels ts..L-1 (ts >= 2) whose two largest LDS images,
+        // levels ts-1 and ts (rows padded to dwords), fit the tail kernel's LDS
+        const int L = g.geo.nlevels;
+        auto bytes = [&](int l) { return (size_t)g.geo.lv[l].h * (((size_t)g.geo.lv[l].w + 3) & ~(size_t)3); };
+        g.tail_start = L;
+        for (int ts = L - 1; ts >= 2; --ts) {
+            if (bytes(ts - 1) + bytes(ts) > (size_t)kTailLds) break;
+            g.tail_start = ts;
+        }
+        if (L - g.tail_start < 2) g.tail_start = L;  // a single level gains nothing
+    }
     int rmax = 7, cmax = 7;
     for (const CellDesc& c : g.cells) {
         rmax = std::max(rmax, c.y1 - c.y0);

@@ -77,6 +77,18 @@ struct ResizeArgs {
     const int* yt;
 };
 
+struct ResizeTailArgs {
+    LevelPtr src;                 // level ts-1
+    int sh;                       // its rows
+    int nt;                       // tail levels ts .. ts+nt-1
+    int buf_b;                    // LDS offset of the second buffer
+    int lp[kMaxLevels + 1];       // LDS row pitch of level ts-1+k (k = 0 .. nt)
+    int dw[kMaxLevels], dh[kMaxLevels];
+    const int* xt[kMaxLevels];
+    const int* yt[kMaxLevels];
+    LevelPtr dst[kMaxLevels];
+};
+
 struct FastArgs {
     const CellDesc* cells;
     int ncells;
@@ -150,6 +162,7 @@ struct Plan {
     size_t fast_lds = 0;
     int rs_tiles_x[kMaxLevels] = {}, rs_tiles[kMaxLevels] = {}, rs_pitch[kMaxLevels] = {};
     size_t rs_lds[kMaxLevels] = {};
+    int tail_start = kMaxLevels;  // levels >= tail_start come from resize_tail_kernel
 };
 
 int make_tables(const orbfe_params& p, HostTables& t);
@@ -158,6 +171,7 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g);
 // kernels (orbfe_extract.hip)
 __global__ void level0_kernel(Level0Args);
 __global__ void resize_kernel(ResizeArgs);
+__global__ void resize_tail_kernel(ResizeTailArgs);
 __global__ void fast_kernel(FastArgs);
 __global__ void octree_kernel(OctArgs);
 __global__ void blur_kernel(BlurArgs);
