@@ -2,8 +2,8 @@
 // (skaegy/ORBSLAM_MapSave src/ORBmatcher.cc) and the Frame grid it queries (src/Frame.cc).
 //
 //   hamming_kernel       DescriptorDistance (1650-1666), one row pair per lane
-//   bf_match_kernel      brute-force best/second (config 3): queries in lanes, references
-//                        streamed through LDS and read as wave-wide broadcasts
+//   bf_match_kernel      brute-force best/second (config 3) on the i8 matrix cores: Hamming
+//                        as popc(r) - 2 r.q + popc(q), references streamed through LDS
 //   grid_kernel          Frame::AssignFeaturesToGrid (Frame.cc:341-356) as a CSR
 //   *_cand_kernel        GetFeaturesInArea (Frame.cc:445-498) + distances for every query in
 //                        parallel (counts, scan, fill)
@@ -48,75 +48,161 @@ __global__ __launch_bounds__(256) void hamming_kernel(const uint4* a, const uint
     if (i < n) dist[i] = hamming_rows(a + 2 * i, b + 2 * i);
 }
 
-// Brute force: problem b = blockIdx.y; a block serves 64 queries (one per lane) and its 4 waves
-// split the references into contiguous quarters.  Keys pack (distance << 16 | reference index):
-// with the first-wins rule of ORBmatcher.cc:102-114 (strict <, start at 256) the best key is
-// min(keys) and the second distance is the second-smallest key's, so each reference costs
-// 8 XOR + 8 bit-counts + one shift-or + min/max/min -- no compare chain.  An initial key of
-// 256 << 16 keeps distance-256 references out, as the strict compare does.  Partitions merge
-// with second = min(second_a, second_b, max(best_a, best_b)).  nr < 65536.
-constexpr int kBfBlock = 256;
-constexpr int kBfTile = 64;  // references per wave per tile
+// Brute force on the matrix cores.  Over the 256 descriptor bits,
+//   hamming(r, q) = popc(r) + popc(q) - 2 r.q = X + popc(q),   X = sum_k r_k (1 - 2 q_k),
+// so with references as 0/1 bytes (A operand, rows) and queries as +-1 bytes (B operand,
+// columns), one chain of 8 v_mfma_i32_32x32x32_i8 (one per 32-bit chunk) gives X exactly, and
+// popc(q) is a per-query -- per-lane, the C/D column is the lane -- constant, so the running
+// best / second of each lane run on X alone.  Keys (X << 16) + reference index, signed: the
+// first-wins rule of ORBmatcher.cc:102-114 (strict <, start at 256) makes the best key the
+// minimum and the second distance the second-smallest key's; a start key of
+// (256 - popc(q)) << 16 keeps distance-256 references out as the strict compare does.
+//
+// A block = 4 waves x 64 queries (two 32-column N-tiles per wave, their +-1 fragments resident
+// in VGPRs); references stream through LDS in tiles of 64 (two 32-row M-tiles), expanded once
+// per block from packed bits into fragment order [chunk][lane half][row] (16 B per entry, so a
+// wave's fragment read is two contiguous 512-B runs), double-buffered with one barrier per tile.
+// Lane half h holds rows 4h.. of each C/D row group; its keys carry the index without the +4,
+// added when the halves merge.  nr < 65536.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+constexpr int kBfBlock = 256;  // 4 waves x 64 queries
+constexpr int kBfRefs = 64;    // references per LDS tile
+
+// bits s .. s+3 of w as four 0/1 bytes (the multiplier spreads bit i to bit 8i, collision-free)
+__device__ __forceinline__ uint32_t nibble01(uint32_t w, int s) {
+    return ((w >> s) & 15u) * 0x204081u & 0x01010101u;
+}
+__device__ __forceinline__ i32x4 half01(uint32_t w, int h) {  // bits 16h .. 16h+15 of a chunk
+    return i32x4{(int)nibble01(w, 16 * h), (int)nibble01(w, 16 * h + 4),
+                 (int)nibble01(w, 16 * h + 8), (int)nibble01(w, 16 * h + 12)};
+}
+__device__ __forceinline__ int kmin(int a, int b) { return a < b ? a : b; }
+__device__ __forceinline__ int kmax(int a, int b) { return a > b ? a : b; }
+// (b, s) := the two smallest of {b, s, k1, k2}, b <= s
+__device__ __forceinline__ void best2(int& b, int& s, int k1, int k2) {
+    const int lo = kmin(k1, k2), hi = kmax(k1, k2);
+    s = kmin(kmin(s, hi), kmax(b, lo));
+    b = kmin(b, lo);
+}
+
 __global__ __launch_bounds__(kBfBlock) void bf_match_kernel(const uint8_t* q, long long q_pitch,
                                                             const int* nq_arr, int nq_cap,
                                                             const uint8_t* r, long long r_pitch,
                                                             const int* nr_arr, int* out) {
-    __shared__ uint4 tile[4][kBfTile * 2];
-    __shared__ unsigned part[4][64][2];
+    __shared__ i32x4 tile[2][16][kBfRefs];  // [buffer][2 * chunk + half][row]
     const int b = blockIdx.y;
     const int nq = nq_arr[b], nr = nr_arr[b];
-    if ((int)blockIdx.x * 64 >= nq) return;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int qi = blockIdx.x * 64 + lane;
-    const uint4* Q = reinterpret_cast<const uint4*>(q + b * q_pitch);
-    const uint4* R = reinterpret_cast<const uint4*>(r + b * r_pitch);
-    uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
-    if (qi < nq) {
-        a0 = Q[2 * qi];
-        a1 = Q[2 * qi + 1];
-    }
-    const int quarter = (((nr + 3) / 4) + kBfTile - 1) / kBfTile * kBfTile;
-    const int j0 = w * quarter, j1 = min(nr, j0 + quarter);
-    const unsigned kInit = 256u << 16;
-    unsigned best = kInit, second = kInit;
-    const int ntiles = (quarter + kBfTile - 1) / kBfTile;  // same count in every wave
-    for (int t = 0; t < ntiles; ++t) {
-        const int base = j0 + t * kBfTile;
-        const int cnt = max(0, min(kBfTile, j1 - base));
-        if (lane < cnt) {
-            tile[w][2 * lane] = R[2 * (base + lane)];
-            tile[w][2 * lane + 1] = R[2 * (base + lane) + 1];
-        }
-        __syncthreads();
-        auto step = [&](int j) {
-            const unsigned d = (unsigned)hamming256(a0, a1, tile[w][2 * j], tile[w][2 * j + 1]);
-            const unsigned key = (d << 16) | (unsigned)(base + j);
-            const unsigned hi = max(best, key);
-            best = min(best, key);
-            second = min(second, hi);
-        };
-        if (cnt == kBfTile) {  // full tile: constant trip count, unrolled so the broadcast
-#pragma unroll 8          // LDS reads of the next references overlap the current counts
-            for (int j = 0; j < kBfTile; ++j) step(j);
-        } else {
-            for (int j = 0; j < cnt; ++j) step(j);
-        }
-        __syncthreads();
-    }
-    part[w][lane][0] = best;
-    part[w][lane][1] = second;
-    __syncthreads();
-    if (w == 0 && qi < nq) {
+    if ((int)blockIdx.x * kBfBlock >= nq) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int col = lane & 31, h = lane >> 5;
+    const int q0 = blockIdx.x * kBfBlock + w * 64;
+    const uint8_t* R = r + b * r_pitch;
+
+    // query fragments: N-tile nt holds queries q0 + 32 nt + col
+    i32x4 bq[2][8];
+    int popc[2], best[2], second[2];
 #pragma unroll
-        for (int o = 1; o < 4; ++o) {
-            const unsigned ob = part[o][lane][0], os = part[o][lane][1];
-            second = min(min(second, os), max(best, ob));
-            best = min(best, ob);
+    for (int nt = 0; nt < 2; ++nt) {
+        const int qi = q0 + 32 * nt + col;
+        uint4 d0 = make_uint4(0, 0, 0, 0), d1 = d0;
+        if (qi < nq) {
+            const uint4* Q = reinterpret_cast<const uint4*>(q + b * q_pitch) + 2 * qi;
+            d0 = Q[0];
+            d1 = Q[1];
         }
+        const uint32_t dw[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+        int pc = 0;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            pc += __popc(dw[c]);
+            const i32x4 v = half01(dw[c], h);  // 1 - 2 bit as bytes: 0 -> 0x01, 1 -> 0xfe ^ 0x01
+            bq[nt][c] = i32x4{(int)((uint32_t)v.x * 254u ^ 0x01010101u),
+                              (int)((uint32_t)v.y * 254u ^ 0x01010101u),
+                              (int)((uint32_t)v.z * 254u ^ 0x01010101u),
+                              (int)((uint32_t)v.w * 254u ^ 0x01010101u)};
+        }
+        popc[nt] = pc;
+        best[nt] = second[nt] = (256 - pc) << 16;
+    }
+
+    // tile loader: thread -> (row tid & 63, chunks 2 (tid >> 6), +1)
+    const int lrow = tid & 63, lcp = tid >> 6;
+    auto fetch = [&](int t) {
+        const int j = t * kBfRefs + lrow;
+        return j < nr ? *reinterpret_cast<const uint2*>(R + (long long)j * 32 + 8 * lcp)
+                      : make_uint2(0, 0);
+    };
+    auto expand = [&](int buf, uint2 v) {
+        tile[buf][4 * lcp + 0][lrow] = half01(v.x, 0);
+        tile[buf][4 * lcp + 1][lrow] = half01(v.x, 1);
+        tile[buf][4 * lcp + 2][lrow] = half01(v.y, 0);
+        tile[buf][4 * lcp + 3][lrow] = half01(v.y, 1);
+    };
+    const int ntiles = (nr + kBfRefs - 1) / kBfRefs;
+    if (ntiles) expand(0, fetch(0));
+    __syncthreads();
+    for (int t = 0; t < ntiles; ++t) {
+        const int cur = t & 1;
+        const uint2 nxt = t + 1 < ntiles ? fetch(t + 1) : make_uint2(0, 0);
+        i32x16 acc[2][2];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const i32x4 a0 = tile[cur][2 * c + h][col], a1 = tile[cur][2 * c + h][32 + col];
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                acc[0][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(
+                    a0, bq[nt][c], c ? acc[0][nt] : i32x16{}, 0, 0, 0);
+                acc[1][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(
+                    a1, bq[nt][c], c ? acc[1][nt] : i32x16{}, 0, 0, 0);
+            }
+        }
+        const int base = t * kBfRefs;
+        if (base + kBfRefs <= nr) {
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+                    for (int e = 0; e < 16; e += 2) {
+                        const int i0 = base + 32 * mt + (e & 3) + 8 * (e >> 2);
+                        best2(best[nt], second[nt], (acc[mt][nt][e] << 16) + i0,
+                              (acc[mt][nt][e + 1] << 16) + i0 + 1);
+                    }
+        } else {  // last, partial tile: rows past nr never win
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+                    for (int e = 0; e < 16; e += 2) {
+                        const int i0 = base + 32 * mt + (e & 3) + 8 * (e >> 2);
+                        const int k0 = i0 + 4 * h < nr ? (acc[mt][nt][e] << 16) + i0 : INT_MAX;
+                        const int k1 = i0 + 1 + 4 * h < nr ? (acc[mt][nt][e + 1] << 16) + i0 + 1
+                                                           : INT_MAX;
+                        best2(best[nt], second[nt], k0, k1);
+                    }
+        }
+        if (t + 1 < ntiles) expand(cur ^ 1, nxt);
+        __syncthreads();
+    }
+    // merge the lane halves (the same queries, rows 4h..), then half h reports N-tile h
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+        const int kb = best[nt] + 4 * h, ks = second[nt] + 4 * h;
+        const int ob = __shfl_xor(kb, 32), os = __shfl_xor(ks, 32);
+        second[nt] = kmin(kmin(ks, os), kmax(kb, ob));
+        best[nt] = kmin(kb, ob);
+    }
+    const int qi = q0 + 32 * h + col;
+    if (qi < nq) {
+        const int kb = h ? best[1] : best[0], ks = h ? second[1] : second[0];
+        const int pc = h ? popc[1] : popc[0];
+        const int db = (kb >> 16) + pc;
         int* o = out + ((long long)b * nq_cap + qi) * 3;
-        o[0] = (best >> 16) >= 256 ? -1 : (int)(best & 0xffff);
-        o[1] = (int)(best >> 16);
-        o[2] = (int)(second >> 16);
+        o[0] = db >= 256 ? -1 : (kb & 0xffff);
+        o[1] = db;
+        o[2] = (ks >> 16) + pc;
     }
 }
 

@@ -49,6 +49,25 @@ def test_bf_match_ties(mt):
         assert np.array_equal(g, e)
 
 
+@pytest.mark.parametrize("nq,nr", [(257, 64), (64, 65), (31, 63), (2, 128), (700, 129)])
+def test_bf_match_extremes(mt, nq, nr):
+    """Partial tiles and blocks, all-zero / all-one / complementary descriptors (distances 0 and
+    256: a distance-256 reference never wins), duplicates (first-wins)."""
+    rng = np.random.Generator(np.random.PCG64(7 * nq + nr))
+    q, r = S.random_desc(rng, nq), S.random_desc(rng, nr)
+    q[0], q[-1] = 0, 255
+    r[:] = np.where(rng.random((nr, 1)) < 0.2, ~q[rng.integers(0, nq, nr)], r)
+    r[nr // 2], r[-1] = 0, 255
+    r[nr // 3] = q[1]
+    got = mt.bf_match(q, r)
+    exp = oracle.bf_match(q, r)
+    for g, e in zip(got, exp):
+        assert np.array_equal(g, e)
+    assert got[1][0] == 0 and got[1][-1] == 0                # zero / all-one references exist
+    z = mt.bf_match(np.zeros((3, 32), np.uint8), np.full((5, 32), 255, np.uint8))
+    assert (z[0] == -1).all() and (z[1] == 256).all() and (z[2] == 256).all()
+
+
 def test_bf_match_extracted(mt):
     f1, f2 = S.extract_frame(0, 1000), S.extract_frame(1, 2000)
     for g, e in zip(mt.bf_match(f1.desc, f2.desc), oracle.bf_match(f1.desc, f2.desc)):
