@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <type_traits>
 
 #include "../../include/orbfe.h"
 #include "orbfe_device.hpp"
@@ -50,24 +51,33 @@ __global__ __launch_bounds__(256) void hamming_kernel(const uint4* a, const uint
 
 // Brute force on the matrix cores.  Over the 256 descriptor bits,
 //   hamming(r, q) = popc(r) + popc(q) - 2 r.q = X + popc(q),   X = sum_k r_k (1 - 2 q_k),
-// so with references as 0/1 bytes (A operand, rows) and queries as +-1 bytes (B operand,
-// columns), one chain of 8 v_mfma_i32_32x32x32_i8 (one per 32-bit chunk) gives X exactly, and
-// popc(q) is a per-query -- per-lane, the C/D column is the lane -- constant, so the running
-// best / second of each lane run on X alone.  Keys (X << 16) + reference index, signed: the
-// first-wins rule of ORBmatcher.cc:102-114 (strict <, start at 256) makes the best key the
-// minimum and the second distance the second-smallest key's; a start key of
+// so with references as 0/1 bytes (A operand, rows) and queries as -+64 bytes (B operand,
+// columns), one chain of 8 v_mfma_i32_32x32x32_i8 (one per 32-bit chunk) gives 64 X exactly,
+// and popc(q) is a per-query -- per-lane, the C/D column is the lane -- constant, so each lane
+// ranks its references by X alone.  The chain's C input is the row's position p in the 64-row
+// reference tile, so every accumulator is already a tile-local key 64 X + p: the lane's two
+// smallest keys of a tile take one v_min_i32 + one v_med3_i32 per accumulator
+// (s' = med3(b, s, k), b' = min(b, k) for b <= s).  Per tile and query they become 32-bit keys
+// (X << 16) + index and merge into the lane's running pair: the first-wins rule of
+// ORBmatcher.cc:102-114 (strict <, start at 256) makes the best key the minimum (lowest index
+// among equal distances) and the second distance the second-smallest key's; a start key of
 // (256 - popc(q)) << 16 keeps distance-256 references out as the strict compare does.
 //
-// A block = 4 waves x 64 queries (two 32-column N-tiles per wave, their +-1 fragments resident
-// in VGPRs); references stream through LDS in tiles of 64 (two 32-row M-tiles), expanded once
-// per block from packed bits into fragment order [chunk][lane half][row] (16 B per entry, so a
-// wave's fragment read is two contiguous 512-B runs), double-buffered with one barrier per tile.
-// Lane half h holds rows 4h.. of each C/D row group; its keys carry the index without the +4,
-// added when the halves merge.  nr < 65536.
+// A block = 4 waves x 64 queries (two 32-column N-tiles per wave, their fragments resident in
+// VGPRs); references stream through LDS in tiles of 64 (two 32-row M-tiles), expanded once per
+// block from packed bits into fragment order [chunk][lane half][row] (16 B per entry, so a
+// wave's fragment read is two contiguous 512-B runs), double-buffered, one barrier per tile.
+// A tile is 4 chains (m-tile, n-tile); the ranking of each chain's 16 accumulators runs in the
+// MFMA gaps of the next chain, beside a slice of the next tile's expansion (about 5 single-issue
+// instructions per gap, pinned with sched_group_barrier).  Lane half h holds rows 4h.. of each
+// C/D row group; its keys carry the position without the +4, added when the halves merge.
+// nr < 65536.
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
-constexpr int kBfBlock = 256;  // 4 waves x 64 queries
-constexpr int kBfRefs = 64;    // references per LDS tile
+constexpr int kBfBlock = 256;               // 4 waves x 64 queries
+constexpr int kBfWords = 512 / kBfBlock;    // raw 32-bit words a thread expands per tile
+constexpr int kBfRefs = 64;                    // references per LDS tile
+constexpr int kBfNone = 0x7fff;                // tile key that never wins (> 64 * 256 + 63)
 
 // bits s .. s+3 of w as four 0/1 bytes (the multiplier spreads bit i to bit 8i, collision-free)
 __device__ __forceinline__ uint32_t nibble01(uint32_t w, int s) {
@@ -79,17 +89,33 @@ __device__ __forceinline__ i32x4 half01(uint32_t w, int h) {  // bits 16h .. 16h
 }
 __device__ __forceinline__ int kmin(int a, int b) { return a < b ? a : b; }
 __device__ __forceinline__ int kmax(int a, int b) { return a > b ? a : b; }
-// (b, s) := the two smallest of {b, s, k1, k2}, b <= s
-__device__ __forceinline__ void best2(int& b, int& s, int k1, int k2) {
-    const int lo = kmin(k1, k2), hi = kmax(k1, k2);
-    s = kmin(kmin(s, hi), kmax(b, lo));
-    b = kmin(b, lo);
+__device__ __forceinline__ int med3(int a, int b, int c) {
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ constexpr int bf_pos(int mt, int e) {  // C/D row of register e
+    return 32 * mt + (e & 3) + 8 * (e >> 2);
 }
 
-__global__ __launch_bounds__(kBfBlock) void bf_match_kernel(const uint8_t* q, long long q_pitch,
-                                                            const int* nq_arr, int nq_cap,
-                                                            const uint8_t* r, long long r_pitch,
-                                                            const int* nr_arr, int* out) {
+struct BfLane {  // one N-tile's ranking state in a lane
+    int tb, ts;       // the tile's two smallest tile-local keys
+    int best, second; // running 32-bit keys
+    __device__ __forceinline__ void push(int k) {
+        ts = med3(tb, ts, k);
+        tb = kmin(tb, k);
+    }
+    __device__ __forceinline__ void close(int base) {  // the tile's pair into the running pair
+        const int kb = ((tb >> 6) << 16) + base + (tb & 63), ks = (ts >> 6) << 16;
+        second = kmin(kmin(second, ks), kmax(best, kb));
+        best = kmin(best, kb);
+        tb = ts = kBfNone;
+    }
+};
+
+__global__ __launch_bounds__(kBfBlock) void bf_match_kernel(
+    const uint8_t* q, long long q_pitch, const int* nq_arr, int nq_cap, const uint8_t* r,
+    long long r_pitch, const int* nr_arr, int* out) {
     __shared__ i32x4 tile[2][16][kBfRefs];  // [buffer][2 * chunk + half][row]
     const int b = blockIdx.y;
     const int nq = nq_arr[b], nr = nr_arr[b];
@@ -101,7 +127,8 @@ __global__ __launch_bounds__(kBfBlock) void bf_match_kernel(const uint8_t* q, lo
 
     // query fragments: N-tile nt holds queries q0 + 32 nt + col
     i32x4 bq[2][8];
-    int popc[2], best[2], second[2];
+    int popc[2];
+    BfLane st[2];
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
         const int qi = q0 + 32 * nt + col;
@@ -116,80 +143,122 @@ __global__ __launch_bounds__(kBfBlock) void bf_match_kernel(const uint8_t* q, lo
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             pc += __popc(dw[c]);
-            const i32x4 v = half01(dw[c], h);  // 1 - 2 bit as bytes: 0 -> 0x01, 1 -> 0xfe ^ 0x01
-            bq[nt][c] = i32x4{(int)((uint32_t)v.x * 254u ^ 0x01010101u),
-                              (int)((uint32_t)v.y * 254u ^ 0x01010101u),
-                              (int)((uint32_t)v.z * 254u ^ 0x01010101u),
-                              (int)((uint32_t)v.w * 254u ^ 0x01010101u)};
+            const i32x4 v = half01(dw[c], h);  // 64 (1 - 2 bit) as bytes: 0 -> 0x40, 1 -> 0xc0
+            bq[nt][c] = i32x4{(int)((uint32_t)v.x << 7 ^ 0x40404040u),
+                              (int)((uint32_t)v.y << 7 ^ 0x40404040u),
+                              (int)((uint32_t)v.z << 7 ^ 0x40404040u),
+                              (int)((uint32_t)v.w << 7 ^ 0x40404040u)};
         }
         popc[nt] = pc;
-        best[nt] = second[nt] = (256 - pc) << 16;
+        st[nt].best = st[nt].second = (256 - pc) << 16;
+        st[nt].tb = st[nt].ts = kBfNone;
+    }
+    i32x16 pos[2];  // C input: the row's position in the tile, without the 4h
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        pos[0][e] = bf_pos(0, e);
+        pos[1][e] = bf_pos(1, e);
     }
 
-    // tile loader: thread -> (row tid & 63, chunks 2 (tid >> 6), +1)
+    // tile loader: thread -> row lrow, raw words kBfWords lcp .. (+kBfWords); rows past nr load
+    // zeros, branch-free so that the loop body stays one basic block for the scheduler
     const int lrow = tid & 63, lcp = tid >> 6;
+    struct Raw { uint32_t w[kBfWords]; };
     auto fetch = [&](int t) {
         const int j = t * kBfRefs + lrow;
-        return j < nr ? *reinterpret_cast<const uint2*>(R + (long long)j * 32 + 8 * lcp)
-                      : make_uint2(0, 0);
-    };
-    auto expand = [&](int buf, uint2 v) {
-        tile[buf][4 * lcp + 0][lrow] = half01(v.x, 0);
-        tile[buf][4 * lcp + 1][lrow] = half01(v.x, 1);
-        tile[buf][4 * lcp + 2][lrow] = half01(v.y, 0);
-        tile[buf][4 * lcp + 3][lrow] = half01(v.y, 1);
-    };
-    const int ntiles = (nr + kBfRefs - 1) / kBfRefs;
-    if (ntiles) expand(0, fetch(0));
-    __syncthreads();
-    for (int t = 0; t < ntiles; ++t) {
-        const int cur = t & 1;
-        const uint2 nxt = t + 1 < ntiles ? fetch(t + 1) : make_uint2(0, 0);
-        i32x16 acc[2][2];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const i32x4 a0 = tile[cur][2 * c + h][col], a1 = tile[cur][2 * c + h][32 + col];
-#pragma unroll
-            for (int nt = 0; nt < 2; ++nt) {
-                acc[0][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(
-                    a0, bq[nt][c], c ? acc[0][nt] : i32x16{}, 0, 0, 0);
-                acc[1][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(
-                    a1, bq[nt][c], c ? acc[1][nt] : i32x16{}, 0, 0, 0);
-            }
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(
+            R + (long long)min(j, max(nr - 1, 0)) * 32 + 4 * kBfWords * lcp);
+        Raw v;
+        if constexpr (kBfWords == 2) {
+            const uint2 u = *reinterpret_cast<const uint2*>(src);
+            v.w[0] = j < nr ? u.x : 0u;
+            v.w[1] = j < nr ? u.y : 0u;
+        } else {
+            v.w[0] = j < nr ? src[0] : 0u;
         }
-        const int base = t * kBfRefs;
-        if (base + kBfRefs <= nr) {
+        return v;
+    };
+    const int nfull = nr / kBfRefs, ntiles = (nr + kBfRefs - 1) / kBfRefs;
+    if (nr) {
+        const Raw v = fetch(0);
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-                    for (int e = 0; e < 16; e += 2) {
-                        const int i0 = base + 32 * mt + (e & 3) + 8 * (e >> 2);
-                        best2(best[nt], second[nt], (acc[mt][nt][e] << 16) + i0,
-                              (acc[mt][nt][e + 1] << 16) + i0 + 1);
-                    }
-        } else {  // last, partial tile: rows past nr never win
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-                    for (int e = 0; e < 16; e += 2) {
-                        const int i0 = base + 32 * mt + (e & 3) + 8 * (e >> 2);
-                        const int k0 = i0 + 4 * h < nr ? (acc[mt][nt][e] << 16) + i0 : INT_MAX;
-                        const int k1 = i0 + 1 + 4 * h < nr ? (acc[mt][nt][e + 1] << 16) + i0 + 1
-                                                           : INT_MAX;
-                        best2(best[nt], second[nt], k0, k1);
-                    }
+        for (int j = 0; j < kBfWords; ++j) {
+            tile[0][2 * (kBfWords * lcp + j) + 0][lrow] = half01(v.w[j], 0);
+            tile[0][2 * (kBfWords * lcp + j) + 1][lrow] = half01(v.w[j], 1);
         }
-        if (t + 1 < ntiles) expand(cur ^ 1, nxt);
-        __syncthreads();
     }
+    __syncthreads();
+
+    // One tile = chains p = 0..3 (m-tile p & 1, n-tile p >> 1), each 8 MFMAs.  In the gaps of
+    // chain p: the ranking of chain p - 1 (chain 3 of the previous tile for p = 0) and 1/32 of
+    // the next tile's expansion per MFMA.  Raw bits run two tiles ahead.
+    Raw raw = fetch(1);
+    i32x16 accp;  // the previous chain's keys
+#pragma unroll
+    for (int e = 0; e < 16; ++e) accp[e] = kBfNone;
+    auto step = [&](int t, auto partial_tag) {
+        constexpr bool partial = decltype(partial_tag)::value;
+        const int cur = t & 1;
+        const Raw raw2 = fetch(t + 2);
+        const int valid = nr - t * kBfRefs - 4 * h;  // positions >= valid lie past nr
+        uint32_t ex[4];
+        // fragment ring, two reads ahead: fragment f = 8 p + c is chunk c of m-tile p & 1
+        auto frag = [&](int f) { return tile[cur][2 * (f & 7) + h][32 * ((f >> 3) & 1) + col]; };
+        i32x4 a = frag(0), a1 = frag(1);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int mt = p & 1, nt = p >> 1;
+            const int pmt = (p + 3) & 1, pnt = ((p + 3) & 3) >> 1;  // previous chain
+            i32x16 acc;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const int f = 8 * p + c;
+                i32x4 a2 = a1;
+                if (f + 2 < 32) a2 = frag(f + 2);
+                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[nt][c], c ? acc : pos[mt], 0, 0, 0);
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int e = 2 * c + u;
+                    int k = accp[e];
+                    // chain p - 1 of this tile may be partial; chain 3 of the previous tile not
+                    if (partial && p > 0 && bf_pos(pmt, e) >= valid) k = kBfNone;
+                    st[pnt].push(k);
+                }
+                const int n = f * kBfWords / 4;  // nibble slot of this MFMA
+                if ((f * kBfWords) % 4 == 0 && n < 8 * kBfWords) {
+                    ex[n & 3] = nibble01(raw.w[n >> 3], 16 * ((n >> 2) & 1) + 4 * (n & 3));
+                    if ((n & 3) == 3)
+                        tile[cur ^ 1][2 * kBfWords * lcp + (n >> 2)][lrow] =
+                            i32x4{(int)ex[0], (int)ex[1], (int)ex[2], (int)ex[3]};
+                }
+                a = a1;
+                a1 = a2;
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // fragment read, 2 ahead
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // fillers
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            // tile t - 1's n-tile 1 (for t = 0 a no-op merge of "never wins" keys)
+            if (p == 0) st[1].close((t - 1) * kBfRefs);
+            if (p == 2) st[0].close(t * kBfRefs);  // this tile, n-tile 0
+            accp = acc;
+        }
+        raw = raw2;
+        __syncthreads();
+    };
+    for (int t = 0; t < nfull; ++t) step(t, std::false_type{});
+    if (nfull < ntiles) step(nfull, std::true_type{});
+    if (ntiles) {  // chain 3 of the last tile
+        const int valid = nr - (ntiles - 1) * kBfRefs - 4 * h;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) st[1].push(bf_pos(1, e) < valid ? accp[e] : kBfNone);
+        st[1].close((ntiles - 1) * kBfRefs);
+    }
+    int best[2] = {st[0].best, st[1].best}, second[2] = {st[0].second, st[1].second};
     // merge the lane halves (the same queries, rows 4h..), then half h reports N-tile h
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
-        const int kb = best[nt] + 4 * h, ks = second[nt] + 4 * h;
+        const int kb = best[nt] + 4 * h, ks = second[nt];
         const int ob = __shfl_xor(kb, 32), os = __shfl_xor(ks, 32);
         second[nt] = kmin(kmin(ks, os), kmax(kb, ob));
         best[nt] = kmin(kb, ob);
