@@ -260,7 +260,7 @@ struct orbfe_extractor {
         oa.oct_cnt = oct_cnt.as<int>();
         oa.ncap_max = g.ncap_max;
         oa.sort_cap = g.sort_cap;
-        ORBFE_LAUNCH(prof, ORBFE_STAGE_OCTREE, octree_kernel, dim3(L, n), dim3(kOctBlockSize), g.oct_lds, stream, oa);
+        ORBFE_LAUNCH(prof, ORBFE_STAGE_OCTREE, octree_kernel, dim3(n, L), dim3(kOctBlockSize), g.oct_lds, stream, oa);
         // K4 (the blur) is fused into K5: each keypoint's window is blurred in LDS
         // K5 describe
         DescArgs da;

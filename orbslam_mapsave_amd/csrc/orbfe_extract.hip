@@ -572,7 +572,9 @@ __device__ __forceinline__ void oct_sweep_append(const int4* list, int4* next, i
 
 __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    const int level = blockIdx.x, f = blockIdx.y;
+    // level-major block order: every frame's level-0 tree (the longest) is dispatched first,
+    // the small levels fill the remaining slots
+    const int level = blockIdx.y, f = blockIdx.x;
     const LevelGeo& L = a.geo.lv[level];
     const int NC = a.ncap_max;
     const int tid = threadIdx.x;
