@@ -432,6 +432,29 @@ int orbfe_search_by_bow(orbfe_matcher* m, float nnratio, int check_ori, int n_kf
                         const int32_t* f_node_off, const int32_t* f_feat, int32_t* matches,
                         int32_t* nmatches);
 
+/* Batched device form of SearchByBoW for Tracking::Relocalization's candidate loop, which
+ * matches the current frame against every relocalisation candidate keyframe with
+ * ORBmatcher(0.75, true) (Tracking.cc:1621, 1636-1656): n_pairs (keyframe, frame) problems in
+ * one call (n_pairs <= 65535).  Keyframes and frames are slots in the layout
+ * orbfe_bow_transform_batch_device writes, with per-slot capacity kf_cap / f_cap: slot s holds
+ * descriptors at d_*_desc + s*cap*32, angles (and the keyframe's map-point flags) at s*cap,
+ * its FeatureVector's node ids and feature indices at s*cap, node offsets at s*(cap + 1) and
+ * node count d_*_nn[s].  Pair p matches keyframe slot d_pair_kf[p] against frame slot
+ * d_pair_f[p]; d_matches[p*f_cap + j] = the keyframe feature matched to frame feature j or -1
+ * (all f_cap entries written), d_nmatches[p] = the returned count.  *d_status = 0, or
+ * ORBFE_ERR_UNSUPPORTED (a common node over 256 frame features) / ORBFE_ERR_ARG (an offset or
+ * index outside its slot; that node is skipped).  Asynchronous on the matcher's stream. */
+int orbfe_search_by_bow_batch_device(orbfe_matcher* m, float nnratio, int check_ori, int n_pairs,
+                                     const int32_t* d_pair_kf, const int32_t* d_pair_f,
+                                     int kf_cap, const uint8_t* d_kf_desc,
+                                     const float* d_kf_angle, const uint8_t* d_kf_mp_ok,
+                                     const int32_t* d_kf_nn, const int32_t* d_kf_node_ids,
+                                     const int32_t* d_kf_node_off, const int32_t* d_kf_feat,
+                                     int f_cap, const uint8_t* d_f_desc, const float* d_f_angle,
+                                     const int32_t* d_f_nn, const int32_t* d_f_node_ids,
+                                     const int32_t* d_f_node_off, const int32_t* d_f_feat,
+                                     int32_t* d_matches, int32_t* d_nmatches, int32_t* d_status);
+
 #ifdef __cplusplus
 }
 #endif

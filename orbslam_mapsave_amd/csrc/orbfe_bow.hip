@@ -214,59 +214,128 @@ __global__ __launch_bounds__(kBowBlock) void bow_assemble_kernel(BowArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>&) (ORBmatcher.cc:159-291).
+// ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>&) (ORBmatcher.cc:159-291),
+// over P (keyframe, frame) pairs at once: Tracking::Relocalization matches the current frame
+// against every candidate keyframe (Tracking.cc:1636-1656), and the host form is P = 1.
+// Keyframes and frames are "slots" in the layout orbfe_bow_transform_batch_device writes:
+// per slot s, features at s*cap (descriptors 32 B each, angles, map-point flags, FeatureVector
+// node ids and feature indices), node offsets at s*(cap + 1), node counts nn[s].
 struct BowMatchArgs {
-    int kf_nn, f_nn;
+    int kf_cap, f_cap;
+    const int* pair_kf;       // [P] keyframe slot per pair (NULL: slot 0)
+    const int* pair_f;        // [P] frame slot per pair (NULL: slot 0)
+    const int* kf_nn;         // [slot] FeatureVector nodes
     const int* kf_node_ids;
     const int* kf_node_off;
     const int* kf_feat;
+    const uint8_t* kf_ok;     // map point present and not bad
+    const uint4* kf_desc;
+    const float* kf_angle;    // pKF->mvKeysUn[i].angle
+    const int* f_nn;
     const int* f_node_ids;
     const int* f_node_off;
     const int* f_feat;
-    const uint8_t* kf_ok;     // map point present and not bad
-    const uint4* kf_desc;
     const uint4* f_desc;
-    const float* kf_angle;    // pKF->mvKeysUn[i].angle
     const float* f_angle;     // F.mvKeys[i].angle
+    int* matches;             // [P][f_cap] keyframe feature per frame feature, -1 = NULL
+    int* bins;                // [P][f_cap] scratch: rotation bin of each match
+    int* hist;                // [P][32] rotation histogram
+    int* nm;                  // [P] nmatches
+    int* done;                // [P] workgroups of the pair that finished the node loop
+    int* status;              // ORBFE_ERR_UNSUPPORTED / ORBFE_ERR_ARG on bad input
 };
 
-// SearchByBoW.  A frame feature belongs to exactly one vocabulary node, so the
-// blocking (vpMapPointMatches[realIdxF] != NULL) only couples keyframe features of the same
-// common node: each node's loop (198-245) is run by one wave, in the reference's order, and
-// the nodes run in parallel.  Lanes hold the node's frame features (candidate rank r = lane +
-// 64 j, i.e. vIndicesF order); for each keyframe feature the wave computes every unmatched
-// candidate's distance, best = min (distance << 16 | rank) -- the first minimum in order --
-// and second = the smallest distance of the other candidates, which is exactly what the
-// sequential best/second update yields.  The rotation histogram is accumulated in global
-// atomics; bow_ori_kernel then applies ComputeThreeMaxima (259-281) and clears the slots of
-// the non-top bins.
-constexpr int kBowSearchBlock = 256;   // 4 waves = 4 nodes per workgroup
-constexpr int kBowNodeMax = 256;  // frame features per node handled in registers (4 per lane)
-__device__ __forceinline__ int bow_pair_of(const BowMatchArgs& a, int na) {
-    const int id = a.kf_node_ids[na];
-    int lo = 0, hi = a.f_nn;  // FeatureVector::lower_bound in the frame's nodes
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (a.f_node_ids[mid] < id) lo = mid + 1; else hi = mid;
+// One workgroup per pair: vpMapPointMatches = NULL (164), empty histogram, nmatches = 0, the
+// pair's finished-workgroup counter; workgroup 0 clears the status.
+__global__ __launch_bounds__(256) void bow_init_kernel(BowMatchArgs a) {
+    const int p = blockIdx.x;
+    int* mt = a.matches + (size_t)p * a.f_cap;
+    for (int j = threadIdx.x; j < a.f_cap; j += 256) mt[j] = -1;
+    if (threadIdx.x < 32) a.hist[p * 32 + threadIdx.x] = 0;
+    if (threadIdx.x == 0) {
+        a.nm[p] = 0;
+        a.done[p] = 0;
+        if (p == 0) *a.status = 0;
     }
-    return (lo < a.f_nn && a.f_node_ids[lo] == id) ? lo : -1;
 }
 
-// hist (30 bins), nm and status live in global memory, zeroed before the launch; one wave per
-// keyframe node over as many workgroups as needed.
+// The orientation filter (259-281) of pair p over its matched frame features, by one workgroup.
+__device__ void bow_ori_filter(const BowMatchArgs& a, int p) {
+    __shared__ int top[3];
+    if (threadIdx.x == 0) three_maxima(a.hist + p * 32, top[0], top[1], top[2]);
+    __syncthreads();
+    int* matches = a.matches + (size_t)p * a.f_cap;
+    const int* bins = a.bins + (size_t)p * a.f_cap;
+    int removed = 0;
+    for (int j = threadIdx.x; j < a.f_cap; j += blockDim.x) {
+        if (matches[j] < 0) continue;
+        const int bin = bins[j];
+        if (bin != top[0] && bin != top[1] && bin != top[2]) {
+            matches[j] = -1;
+            ++removed;
+        }
+    }
+    if (removed) atomicSub(&a.nm[p], removed);
+}
+
+// A frame feature belongs to exactly one vocabulary node, so the blocking
+// (vpMapPointMatches[realIdxF] != NULL) only couples keyframe features of the same common node:
+// each node's loop (198-245) is run by one wave, in the reference's order, and the nodes run in
+// parallel (waves stride over the keyframe's nodes; grid.y = pairs).  Lanes hold the node's
+// frame features (candidate rank r = lane + 64 j, i.e. vIndicesF order); for each keyframe
+// feature the wave computes every unmatched candidate's distance, best = min (distance << 16 |
+// rank) -- the first minimum in order -- and second = the smallest distance of the other
+// candidates, which is exactly what the sequential best/second update yields.  The rotation
+// histogram is accumulated with atomics; bow_ori_kernel then applies ComputeThreeMaxima
+// (259-281) and clears the slots of the non-top bins.
+constexpr int kBowSearchBlock = 256;   // 4 waves
+constexpr int kBowNodeMax = 256;  // frame features per node handled in registers (4 per lane)
+__device__ __forceinline__ int bow_pair_of(const int* f_node_ids, int f_nn, int id) {
+    int lo = 0, hi = f_nn;  // FeatureVector::lower_bound in the frame's nodes
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (f_node_ids[mid] < id) lo = mid + 1; else hi = mid;
+    }
+    return (lo < f_nn && f_node_ids[lo] == id) ? lo : -1;
+}
+
 __global__ __launch_bounds__(kBowSearchBlock) void bow_search_kernel(BowMatchArgs a, float nnratio,
-                                                                     int check_ori, int* matches,
-                                                                     int* bins, int* hist, int* nm,
-                                                                     int* status) {
+                                                                     int check_ori) {
     const int lane = threadIdx.x & 63;
-    const int na = blockIdx.x * (kBowSearchBlock / 64) + (threadIdx.x >> 6);
-    if (na < a.kf_nn) {
-        const int fb = bow_pair_of(a, na);
-        if (fb < 0) return;
-        const int y0 = a.f_node_off[fb], ny = a.f_node_off[fb + 1] - y0;
+    const int p = blockIdx.y;
+    const int ks = a.pair_kf ? a.pair_kf[p] : 0, fs = a.pair_f ? a.pair_f[p] : 0;
+    const int kf_nn = a.kf_nn[ks], f_nn = a.f_nn[fs];
+    const size_t kb = (size_t)ks * a.kf_cap, fbase = (size_t)fs * a.f_cap;
+    const int* kf_node_ids = a.kf_node_ids + kb;
+    const int* kf_node_off = a.kf_node_off + (size_t)ks * (a.kf_cap + 1);
+    const int* kf_feat = a.kf_feat + kb;
+    const uint8_t* kf_ok = a.kf_ok + kb;
+    const uint4* kf_desc = a.kf_desc + 2 * kb;
+    const float* kf_angle = a.kf_angle + kb;
+    const int* f_node_ids = a.f_node_ids + fbase;
+    const int* f_node_off = a.f_node_off + (size_t)fs * (a.f_cap + 1);
+    const int* f_feat = a.f_feat + fbase;
+    const uint4* f_desc = a.f_desc + 2 * fbase;
+    const float* f_angle = a.f_angle + fbase;
+    int* matches = a.matches + (size_t)p * a.f_cap;
+    int* bins = a.bins + (size_t)p * a.f_cap;
+    int* hist = a.hist + p * 32;
+    const bool bad = kf_nn < 0 || kf_nn > a.kf_cap || f_nn < 0 || f_nn > a.f_cap;
+    if (bad && threadIdx.x == 0) atomicExch(a.status, ORBFE_ERR_ARG);
+    const int nwaves = gridDim.x * (kBowSearchBlock / 64);
+    const int n_nodes = bad ? 0 : kf_nn;
+    for (int na = blockIdx.x * (kBowSearchBlock / 64) + (threadIdx.x >> 6); na < n_nodes; na += nwaves) {
+        const int fb = bow_pair_of(f_node_ids, f_nn, kf_node_ids[na]);
+        if (fb < 0) continue;
+        const int y0 = f_node_off[fb], ny = f_node_off[fb + 1] - y0;
+        const int x0 = kf_node_off[na], nx = kf_node_off[na + 1] - x0;
+        if (y0 < 0 || ny < 0 || y0 + ny > a.f_cap || x0 < 0 || nx < 0 || x0 + nx > a.kf_cap) {
+            if (lane == 0) atomicExch(a.status, ORBFE_ERR_ARG);
+            continue;
+        }
         if (ny > kBowNodeMax) {
-            if (lane == 0) atomicExch(status, ORBFE_ERR_UNSUPPORTED);
-            return;
+            if (lane == 0) atomicExch(a.status, ORBFE_ERR_UNSUPPORTED);
+            continue;
         }
         int jf[4];
         uint4 d0[4], d1[4];
@@ -274,25 +343,24 @@ __global__ __launch_bounds__(kBowSearchBlock) void bow_search_kernel(BowMatchArg
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int r = lane + 64 * j;
-            free_[j] = r < ny;
-            jf[j] = free_[j] ? a.f_feat[y0 + r] : 0;
-            d0[j] = free_[j] ? a.f_desc[2 * jf[j]] : make_uint4(0, 0, 0, 0);
-            d1[j] = free_[j] ? a.f_desc[2 * jf[j] + 1] : make_uint4(0, 0, 0, 0);
+            jf[j] = r < ny ? f_feat[y0 + r] : -1;
+            free_[j] = jf[j] >= 0 && jf[j] < a.f_cap;
+            d0[j] = free_[j] ? f_desc[2 * jf[j]] : make_uint4(0, 0, 0, 0);
+            d1[j] = free_[j] ? f_desc[2 * jf[j] + 1] : make_uint4(0, 0, 0, 0);
         }
         // the node's keyframe features are fetched by the lanes in parallel (64 at a time) and
         // broadcast in order, so the sequential loop carries no memory latency
-        const int x0 = a.kf_node_off[na], nx = a.kf_node_off[na + 1] - x0;
         for (int xb = 0; xb < nx; xb += 64) {
             const int xl = xb + lane;
             int my_ikf = -1;
             uint4 my0 = make_uint4(0, 0, 0, 0), my1 = my0;
             if (xl < nx) {
-                my_ikf = a.kf_feat[x0 + xl];
-                if (!a.kf_ok[my_ikf]) {
+                my_ikf = kf_feat[x0 + xl];
+                if (my_ikf < 0 || my_ikf >= a.kf_cap || !kf_ok[my_ikf]) {
                     my_ikf = -1;
                 } else {
-                    my0 = a.kf_desc[2 * my_ikf];
-                    my1 = a.kf_desc[2 * my_ikf + 1];
+                    my0 = kf_desc[2 * my_ikf];
+                    my1 = kf_desc[2 * my_ikf + 1];
                 }
             }
             const int cnt = min(64, nx - xb);
@@ -327,35 +395,30 @@ __global__ __launch_bounds__(kBowSearchBlock) void bow_search_kernel(BowMatchArg
                             free_[j] = false;
                             matches[jf[j]] = ikf;
                             if (check_ori) {
-                                const int bin = rot_bin(a.kf_angle[ikf], a.f_angle[jf[j]]);
+                                const int bin = rot_bin(kf_angle[ikf], f_angle[jf[j]]);
                                 bins[jf[j]] = bin;
                                 atomicAdd(&hist[bin], 1);
                             }
-                            atomicAdd(nm, 1);
+                            atomicAdd(&a.nm[p], 1);
                         }
                     }
                 }
             }
         }
     }
-}
-
-// The orientation filter (259-281) over every matched frame feature; one workgroup.
-__global__ __launch_bounds__(1024) void bow_ori_kernel(int n_f, int* matches, const int* bins,
-                                                       const int* hist, int* nm) {
-    __shared__ int top[3];
-    if (threadIdx.x == 0) three_maxima(hist, top[0], top[1], top[2]);
+    if (!check_ori) return;
+    // the pair's last workgroup to finish runs the orientation filter: release this
+    // workgroup's matches / bins, count it, and the last one acquires everyone's
+    __shared__ int last;
     __syncthreads();
-    int removed = 0;
-    for (int j = threadIdx.x; j < n_f; j += 1024) {
-        if (matches[j] < 0) continue;
-        const int bin = bins[j];
-        if (bin != top[0] && bin != top[1] && bin != top[2]) {
-            matches[j] = -1;
-            ++removed;
-        }
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd(&a.done[p], 1) == (int)gridDim.x - 1;
     }
-    if (removed) atomicSub(nm, removed);
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    bow_ori_filter(a, p);
 }
 
 }  // namespace orbfe
@@ -607,6 +670,25 @@ static int bow_launch(orbfe_vocabulary* v, int nframes, int cap, const uint8_t* 
     return ORBFE_OK;
 }
 
+static int bow_search_launch(orbfe_matcher* m, const BowMatchArgs& a, int n_pairs, int gx,
+                             float nnratio, int check_ori) {
+    hipLaunchKernelGGL(bow_init_kernel, dim3(n_pairs), dim3(256), 0, m->stream, a);
+    hipLaunchKernelGGL(bow_search_kernel, dim3(gx, n_pairs), dim3(kBowSearchBlock), 0, m->stream,
+                       a, nnratio, check_ori);
+    ORBFE_HIP(hipGetLastError());
+    return ORBFE_OK;
+}
+
+static bool fv_ok(int nn, const int32_t* off, const int32_t* feat, int n) {
+    if (!nn) return true;
+    if (off[0] != 0) return false;
+    for (int i = 0; i < nn; ++i)
+        if (off[i + 1] < off[i]) return false;
+    for (int i = 0; i < off[nn]; ++i)
+        if (feat[i] < 0 || feat[i] >= n) return false;
+    return true;
+}
+
 int orbfe_search_by_bow(orbfe_matcher* m, float nnratio, int check_ori, int n_kf,
                         const uint8_t* kf_desc, const float* kf_angle, const uint8_t* kf_mp_ok,
                         int kf_nn, const int32_t* kf_node_ids, const int32_t* kf_node_off,
@@ -619,17 +701,17 @@ int orbfe_search_by_bow(orbfe_matcher* m, float nnratio, int check_ori, int n_kf
         (kf_nn && (!kf_node_ids || !kf_node_off || !kf_feat)) ||
         (f_nn && (!f_node_ids || !f_node_off || !f_feat)))
         return ORBFE_ERR_ARG;
+    if (!fv_ok(kf_nn, kf_node_off, kf_feat, n_kf) || !fv_ok(f_nn, f_node_off, f_feat, n_f))
+        return ORBFE_ERR_ARG;
     const int kf_tot = kf_nn ? kf_node_off[kf_nn] : 0, f_tot = f_nn ? f_node_off[f_nn] : 0;
-    for (int i = 0; i < kf_tot; ++i)
-        if (kf_feat[i] < 0 || kf_feat[i] >= n_kf) return ORBFE_ERR_ARG;
-    for (int i = 0; i < f_tot; ++i)
-        if (f_feat[i] < 0 || f_feat[i] >= n_f) return ORBFE_ERR_ARG;
     return guarded(m, [&]() {
         int st;
         for (int i = 0; i < n_f; ++i) matches[i] = -1;  // vpMapPointMatches = NULL (164)
         *nmatches = 0;
         if (!kf_nn || !f_nn || !n_f) return ORBFE_OK;
-        BowMatchArgs a{};
+        // slot 0 of each set; the caps bound every offset and index (validated above)
+        const int kf_cap = std::max({n_kf, kf_tot, kf_nn}), f_cap = std::max({n_f, f_tot, f_nn});
+        const int nn[2] = {kf_nn, f_nn};
         if ((st = m->up(m->fa_d, kf_desc, (size_t)n_kf * 32))) return st;
         if ((st = m->up(m->fb_d, f_desc, (size_t)n_f * 32))) return st;
         if ((st = m->up(m->m_f0, kf_angle, (size_t)n_kf * 4))) return st;
@@ -641,41 +723,95 @@ int orbfe_search_by_bow(orbfe_matcher* m, float nnratio, int check_ori, int n_kf
         if ((st = m->up(m->fb_cs, f_node_ids, (size_t)f_nn * 4))) return st;
         if ((st = m->up(m->fb_ci, f_node_off, (size_t)(f_nn + 1) * 4))) return st;
         if ((st = m->up(m->fb_co, f_feat, (size_t)f_tot * 4))) return st;
-        std::vector<int32_t> empty(n_f, -1);  // vpMapPointMatches = NULL (164)
-        if ((st = m->up(m->fa_k, empty.data(), (size_t)n_f * 4))) return st;
-        if ((st = m->s1.ensure((size_t)n_f * 4 + 16))) return st;  // bins per frame feature
+        if ((st = m->up(m->nq, nn, sizeof(nn)))) return st;
+        if ((st = m->fa_k.ensure((size_t)f_cap * 4))) return st;
+        if ((st = m->s1.ensure((size_t)f_cap * 4))) return st;  // bins per frame feature
         if ((st = m->scal.ensure(16))) return st;
-        if ((st = m->g_hist.ensure(32 * sizeof(int)))) return st;
-        ORBFE_HIP(hipMemsetAsync(m->scal.p, 0, 16, m->stream));
-        ORBFE_HIP(hipMemsetAsync(m->g_hist.p, 0, 32 * sizeof(int), m->stream));
-        a.kf_nn = kf_nn;
-        a.f_nn = f_nn;
+        if ((st = m->g_hist.ensure(64 * sizeof(int)))) return st;
+        BowMatchArgs a{};
+        a.kf_cap = kf_cap;
+        a.f_cap = f_cap;
+        a.kf_nn = m->nq.as<int>();
+        a.f_nn = m->nq.as<int>() + 1;
         a.kf_node_ids = m->m_i0.as<int>();
         a.kf_node_off = m->m_i1.as<int>();
         a.kf_feat = m->o_i.as<int>();
+        a.kf_ok = m->m_u0.as<uint8_t>();
+        a.kf_desc = m->fa_d.as<uint4>();
+        a.kf_angle = m->m_f0.as<float>();
         a.f_node_ids = m->fb_cs.as<int>();
         a.f_node_off = m->fb_ci.as<int>();
         a.f_feat = m->fb_co.as<int>();
-        a.kf_ok = m->m_u0.as<uint8_t>();
-        a.kf_desc = m->fa_d.as<uint4>();
         a.f_desc = m->fb_d.as<uint4>();
-        a.kf_angle = m->m_f0.as<float>();
         a.f_angle = m->m_f1.as<float>();
+        a.matches = m->fa_k.as<int>();
+        a.bins = m->s1.as<int>();
+        a.hist = m->g_hist.as<int>();
+        a.nm = m->scal.as<int>();
+        a.status = m->scal.as<int>() + 1;
+        a.done = m->g_hist.as<int>() + 32;
         if ((st = m->flush())) return st;
-        hipLaunchKernelGGL(bow_search_kernel, dim3((kf_nn + 3) / 4), dim3(kBowSearchBlock), 0,
-                           m->stream, a, nnratio, check_ori, m->fa_k.as<int>(), m->s1.as<int>(),
-                           m->g_hist.as<int>(), m->scal.as<int>(), m->scal.as<int>() + 1);
-        if (check_ori)
-            hipLaunchKernelGGL(bow_ori_kernel, dim3(1), dim3(1024), 0, m->stream, n_f,
-                               m->fa_k.as<int>(), m->s1.as<int>(), m->g_hist.as<int>(),
-                               m->scal.as<int>());
-        ORBFE_HIP(hipGetLastError());
+        if ((st = bow_search_launch(m, a, 1, (kf_nn + 3) / 4, nnratio, check_ori))) return st;
         if ((st = m->down(matches, m->fa_k, (size_t)n_f * 4))) return st;
         int cnt[2] = {0, 0};
         if ((st = m->down(cnt, m->scal, sizeof(cnt)))) return st;
         if ((st = m->sync())) return st;
         *nmatches = cnt[0];
         return cnt[1];  // ORBFE_ERR_UNSUPPORTED: a node held more than 256 frame features
+    });
+}
+
+int orbfe_search_by_bow_batch_device(orbfe_matcher* m, float nnratio, int check_ori, int n_pairs,
+                                     const int32_t* d_pair_kf, const int32_t* d_pair_f,
+                                     int kf_cap, const uint8_t* d_kf_desc,
+                                     const float* d_kf_angle, const uint8_t* d_kf_mp_ok,
+                                     const int32_t* d_kf_nn, const int32_t* d_kf_node_ids,
+                                     const int32_t* d_kf_node_off, const int32_t* d_kf_feat,
+                                     int f_cap, const uint8_t* d_f_desc, const float* d_f_angle,
+                                     const int32_t* d_f_nn, const int32_t* d_f_node_ids,
+                                     const int32_t* d_f_node_off, const int32_t* d_f_feat,
+                                     int32_t* d_matches, int32_t* d_nmatches, int32_t* d_status) {
+    if (n_pairs < 0 || n_pairs > 65535 || kf_cap < 1 || f_cap < 1 || !d_pair_kf || !d_pair_f ||
+        !d_kf_desc || !d_kf_angle || !d_kf_mp_ok || !d_kf_nn || !d_kf_node_ids ||
+        !d_kf_node_off || !d_kf_feat || !d_f_desc || !d_f_angle || !d_f_nn || !d_f_node_ids ||
+        !d_f_node_off || !d_f_feat || !d_matches || !d_nmatches || !d_status)
+        return ORBFE_ERR_ARG;
+    return guarded(m, [&]() {
+        int st;
+        if (n_pairs == 0) {
+            ORBFE_HIP(hipMemsetAsync(d_status, 0, sizeof(int32_t), m->stream));
+            return ORBFE_OK;
+        }
+        if ((st = m->s1.ensure((size_t)n_pairs * f_cap * 4))) return st;
+        if ((st = m->g_hist.ensure((size_t)n_pairs * 33 * sizeof(int)))) return st;
+        BowMatchArgs a{};
+        a.kf_cap = kf_cap;
+        a.f_cap = f_cap;
+        a.pair_kf = d_pair_kf;
+        a.pair_f = d_pair_f;
+        a.kf_nn = d_kf_nn;
+        a.kf_node_ids = d_kf_node_ids;
+        a.kf_node_off = d_kf_node_off;
+        a.kf_feat = d_kf_feat;
+        a.kf_ok = d_kf_mp_ok;
+        a.kf_desc = reinterpret_cast<const uint4*>(d_kf_desc);
+        a.kf_angle = d_kf_angle;
+        a.f_nn = d_f_nn;
+        a.f_node_ids = d_f_node_ids;
+        a.f_node_off = d_f_node_off;
+        a.f_feat = d_f_feat;
+        a.f_desc = reinterpret_cast<const uint4*>(d_f_desc);
+        a.f_angle = d_f_angle;
+        a.matches = d_matches;
+        a.bins = m->s1.as<int>();
+        a.hist = m->g_hist.as<int>();
+        a.nm = d_nmatches;
+        a.done = m->g_hist.as<int>() + (size_t)n_pairs * 32;
+        a.status = d_status;
+        // waves stride over a keyframe's nodes (ORBvoc level 2: ~100 common nodes of ~10
+        // features); enough workgroups per pair to fill the chip for a handful of candidates
+        const int gx = std::max(1, std::min((kf_cap + 3) / 4, (1024 + n_pairs - 1) / n_pairs));
+        return bow_search_launch(m, a, n_pairs, std::min(gx, 32), nnratio, check_ori);
     });
 }
 

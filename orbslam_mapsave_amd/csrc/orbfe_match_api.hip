@@ -718,7 +718,12 @@ int orbfe_search_by_projection_keyframe(orbfe_matcher* m, int check_ori,
     return guarded(m, [&]() {
         int st;
         SbpKfArgs a;
-        if ((st = m->frame(cur, false, a.cur))) return st;
+        // every upload is staged before the frame's flush: one H2D copy + one scatter launch;
+        // the status word is cleared by the same copy
+        const int32_t zero[4] = {0, 0, 0, 0};
+        if ((st = m->up(m->scal, zero, sizeof(zero)))) return st;
+        // a slot already holding a map point blocks (1529-1530), whatever its observations
+        if ((st = m->up(m->s1, frame_mp, (size_t)cur->n * 4))) return st;
         if ((st = m->up(m->m_u0, kf_mp_valid, n_kf))) return st;
         if ((st = m->up(m->m_u1, kf_mp_bad, n_kf))) return st;
         if ((st = m->up(m->o_u, already_found, n_kf))) return st;
@@ -729,8 +734,7 @@ int orbfe_search_by_projection_keyframe(orbfe_matcher* m, int check_ori,
         if ((st = m->up(m->m_d, kf_mp_desc, (size_t)n_kf * 32))) return st;
         if ((st = m->up(m->m_f4, cur->scale_factors, (size_t)cur->nlevels * 4))) return st;
         if (kf_mp_ids && (st = m->up(m->o_i, kf_mp_ids, (size_t)n_kf * 4))) return st;
-        if ((st = m->scal.ensure(16))) return st;
-        ORBFE_HIP(hipMemsetAsync(m->scal.p, 0, 16, m->stream));
+        if ((st = m->frame(cur, false, a.cur))) return st;
         a.n = n_kf;
         a.valid = m->m_u0.as<uint8_t>();
         a.bad = m->m_u1.as<uint8_t>();
@@ -756,9 +760,7 @@ int orbfe_search_by_projection_keyframe(orbfe_matcher* m, int check_ori,
         a.status = m->scal.as<int>() + 1;
         if ((st = m->csr_async(a, n_kf, sbp_kf_cand_kernel<false>, sbp_kf_cand_kernel<true>, 4)))
             return st;
-        // a slot already holding a map point blocks (1529-1530), whatever its observations
         const int N = cur->n;
-        if ((st = m->up(m->s1, frame_mp, (size_t)N * 4))) return st;
         GreedyArgs g{};
         g.m = n_kf;
         g.nkp = N;
@@ -775,14 +777,13 @@ int orbfe_search_by_projection_keyframe(orbfe_matcher* m, int check_ori,
         g.ids = kf_mp_ids ? m->o_i.as<int>() : nullptr;
         if ((st = m->greedy(g))) return st;
         if ((st = m->down(frame_mp, m->s1, (size_t)N * 4))) return st;
-        if ((st = m->down(nmatches, m->scal, sizeof(int)))) return st;
-        int status = 0;  // a predicted level outside the pyramid (outputs then unspecified)
-        uint8_t* q = m->stage(sizeof(int));
-        if (!q) return ORBFE_ERR_NOMEM;
-        ORBFE_HIP(hipMemcpyAsync(q, m->scal.as<int>() + 1, sizeof(int), hipMemcpyDeviceToHost, m->stream));
-        m->pend.push_back(orbfe_matcher::Pending{&status, q, sizeof(int)});
+        // {nmatches, status}: status != 0 is a predicted level outside the pyramid (outputs
+        // then unspecified)
+        int res[2] = {0, 0};
+        if ((st = m->down(res, m->scal, sizeof(res)))) return st;
         if ((st = m->sync())) return st;
-        return status;
+        *nmatches = res[0];
+        return res[1];
     });
 }
 

@@ -41,7 +41,7 @@ EXPORTED = [
     "orbfe_matcher_last_rounds", "orbfe_is_in_frustum", "orbfe_vocabulary_load_text",
     "orbfe_vocabulary_create", "orbfe_vocabulary_destroy", "orbfe_vocabulary_info",
     "orbfe_vocabulary_set_stream", "orbfe_bow_transform", "orbfe_bow_transform_batch_device",
-    "orbfe_search_by_bow",
+    "orbfe_search_by_bow", "orbfe_search_by_bow_batch_device",
 ]
 
 
@@ -568,6 +568,24 @@ class ORBmatcher:
             ptr(ka), ptr(ok), len(kn), ptr(kn), ptr(ko), ptr(kfe), len(fd), ptr(fd), ptr(fa),
             len(fn), ptr(fn), ptr(fo), ptr(ffe), ptr(out), C.byref(nm)))
         return out, nm.value
+
+    def search_by_bow_batch_device(self, n_pairs: int, d_pair_kf: int, d_pair_f: int,
+                                   kf_cap: int, d_kf_desc: int, d_kf_angle: int, d_kf_mp_ok: int,
+                                   d_kf_nn: int, d_kf_node_ids: int, d_kf_node_off: int,
+                                   d_kf_feat: int, f_cap: int, d_f_desc: int, d_f_angle: int,
+                                   d_f_nn: int, d_f_node_ids: int, d_f_node_off: int,
+                                   d_f_feat: int, d_matches: int, d_nmatches: int,
+                                   d_status: int) -> None:
+        """SearchByBoW over n_pairs (keyframe slot, frame slot) pairs (Tracking::Relocalization's
+        candidate loop, Tracking.cc:1636-1656); device pointers in the layout of
+        Vocabulary.transform_batch_device.  Asynchronous on the matcher's stream."""
+        v = C.c_void_p
+        _check("orbfe_search_by_bow_batch_device", lib().orbfe_search_by_bow_batch_device(
+            self._h, C.c_float(self.mfNNratio), int(self.mbCheckOrientation), n_pairs,
+            v(d_pair_kf), v(d_pair_f), kf_cap, v(d_kf_desc), v(d_kf_angle), v(d_kf_mp_ok),
+            v(d_kf_nn), v(d_kf_node_ids), v(d_kf_node_off), v(d_kf_feat), f_cap, v(d_f_desc),
+            v(d_f_angle), v(d_f_nn), v(d_f_node_ids), v(d_f_node_off), v(d_f_feat),
+            v(d_matches), v(d_nmatches), v(d_status)))
 
     def is_in_frustum(self, xyz, normal, min_dist, max_dist, tcw, cam: Camera, bounds,
                       log_scale: float, cos_limit: float = 0.5):

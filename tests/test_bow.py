@@ -283,3 +283,78 @@ def test_gpu_search_by_bow(ori, ratio, vocab_paths, frames):
                                    f.keys["angle"], f_fv, ratio, ori)
     assert nm == onm and np.array_equal(m, om)
     mt.close()
+
+
+def pack_slots(items, cap):
+    """(desc, angle, ok, fv) per slot -> arrays in orbfe_bow_transform_batch_device's layout."""
+    S_ = len(items)
+    desc = np.zeros((S_, cap, 32), np.uint8)
+    ang = np.zeros((S_, cap), np.float32)
+    ok = np.zeros((S_, cap), np.uint8)
+    nn = np.zeros(S_, np.int32)
+    nid = np.zeros((S_, cap), np.int32)
+    off = np.zeros((S_, cap + 1), np.int32)
+    feat = np.zeros((S_, cap), np.int32)
+    for s, (d, a, o, (ids, noff, fe)) in enumerate(items):
+        desc[s, :len(d)] = d
+        ang[s, :len(a)] = a
+        ok[s, :len(o)] = o
+        nn[s] = len(ids)
+        nid[s, :len(ids)] = ids
+        off[s, :len(noff)] = noff
+        feat[s, :len(fe)] = fe
+    return desc, ang, ok, nn, nid, off, feat
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ori,ratio", [(True, 0.75), (False, 0.7)])
+def test_gpu_search_by_bow_batch(ori, ratio, vocab_paths):
+    """Relocalisation's candidate loop (Tracking.cc:1636-1656) as one device call: the current
+    frame against 6 candidate keyframes (one empty, one with every map point bad), plus a
+    second frame, each pair bit-exact against the oracle's SearchByBoW."""
+    import torch
+    from orbslam_mapsave_amd.native import ORBmatcher
+    path = vocab_paths["k10L4_l1_tfidf"]
+    ov = oracle.Vocabulary(path)
+    rng = np.random.Generator(np.random.PCG64(5))
+    kfs = [S.extract_frame(s, 1000, ini=20) for s in (0, 1, 2)]
+    kfs += [S.extract_frame(0, 1000, shift=(-4, 5), ini=20), S.extract_frame(3, 400, ini=20)]
+    kf_items = []
+    for i, k in enumerate(kfs):
+        ok = (rng.uniform(size=k.n) < 0.8).astype(np.uint8) if i != 4 else np.zeros(k.n, np.uint8)
+        kf_items.append((k.desc, k.keys["angle"], ok, ov.transform(k.desc, 2)[2:]))
+    empty_fv = (np.zeros(0, np.int32), np.zeros(1, np.int32), np.zeros(0, np.int32))
+    kf_items.append((np.zeros((0, 32), np.uint8), np.zeros(0, np.float32),
+                     np.zeros(0, np.uint8), empty_fv))
+    frs = [S.extract_frame(0, 1000, shift=(2, -3), ini=20), S.extract_frame(1, 1000, shift=(1, 1), ini=20)]
+    f_items = [(f.desc, f.keys["angle"], np.ones(f.n, np.uint8), ov.transform(f.desc, 2)[2:]) for f in frs]
+    kcap, fcap = 1100, 1050
+    dev = torch.device("cuda", 0)
+    K = [torch.from_numpy(x).to(dev) for x in pack_slots(kf_items, kcap)]
+    F = [torch.from_numpy(x).to(dev) for x in pack_slots(f_items, fcap)]
+    pairs = [(k, 0) for k in range(len(kf_items))] + [(1, 1), (3, 1), (0, 0)]
+    pk = torch.tensor([p[0] for p in pairs], dtype=torch.int32, device=dev)
+    pf = torch.tensor([p[1] for p in pairs], dtype=torch.int32, device=dev)
+    P = len(pairs)
+    out = torch.full((P, fcap), 7, dtype=torch.int32, device=dev)
+    nm = torch.zeros(P, dtype=torch.int32, device=dev)
+    st = torch.full((1,), 9, dtype=torch.int32, device=dev)
+    mt = ORBmatcher(ratio, ori, device=0)
+    mt.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    mt.search_by_bow_batch_device(
+        P, pk.data_ptr(), pf.data_ptr(), kcap, K[0].data_ptr(), K[1].data_ptr(), K[2].data_ptr(),
+        K[3].data_ptr(), K[4].data_ptr(), K[5].data_ptr(), K[6].data_ptr(), fcap, F[0].data_ptr(),
+        F[1].data_ptr(), F[3].data_ptr(), F[4].data_ptr(), F[5].data_ptr(), F[6].data_ptr(),
+        out.data_ptr(), nm.data_ptr(), st.data_ptr())
+    torch.cuda.synchronize()
+    assert int(st[0]) == 0
+    got, gnm = out.cpu().numpy(), nm.cpu().numpy()
+    for p, (ki, fi) in enumerate(pairs):
+        kd, ka, kok, kfv = kf_items[ki]
+        fd, fa, _, ffv = f_items[fi]
+        om, onm = oracle.search_by_bow(kd, ka, kok, kfv, fd, fa, ffv, ratio, ori)
+        assert gnm[p] == onm, (p, gnm[p], onm)
+        assert np.array_equal(got[p, :len(fd)], om), p
+        assert (got[p, len(fd):] == -1).all()
+    assert gnm[0] > 50 and gnm[4] == 0 and gnm[5] == 0
+    mt.close()

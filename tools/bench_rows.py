@@ -273,6 +273,41 @@ def row_bow(tmpdir):
                                                 f.keys["angle"], f_fv, 0.75, True))
     emit("(f)4 SearchByBoW(KeyFrame*, Frame&) (1000 x 1000 features, level-2 nodes)", "calls/s",
          1, t, tc, (kf.n + f.n) * (32 + 8), "host ABI (uploads included), latency-bound")
+    # Tracking::Relocalization's candidate loop (Tracking.cc:1636-1656) as one device call:
+    # the current frame against P candidate keyframes, everything resident in HBM
+    from test_bow import pack_slots
+    P, kcap = 64, 1100
+    kfr = [S.extract_frame(s, 1000, shift=(s % 5, -(s % 3)), ini=20) for s in range(8)]
+    rng = np.random.Generator(np.random.PCG64(1))
+    items = [(x.desc, x.keys["angle"], (rng.uniform(size=x.n) < 0.8).astype(np.uint8),
+              ov.transform(x.desc, 4)[2:]) for x in kfr]
+    K = [torch.from_numpy(x).to(DEV) for x in pack_slots(items, kcap)]
+    F = [torch.from_numpy(x).to(DEV) for x in pack_slots([(f.desc, f.keys["angle"],
+                                                           np.ones(f.n, np.uint8), f_fv)], kcap)]
+    pk = torch.arange(P, dtype=torch.int32, device=DEV) % len(items)
+    pf = torch.zeros(P, dtype=torch.int32, device=DEV)
+    out = torch.empty((P, kcap), dtype=torch.int32, device=DEV)
+    nmv = torch.empty(P, dtype=torch.int32, device=DEV)
+    stv = torch.empty(1, dtype=torch.int32, device=DEV)
+    m = native.ORBmatcher(0.75, True, device=0)
+    m.set_stream(torch.cuda.current_stream(DEV).cuda_stream)
+
+    def gob():
+        m.search_by_bow_batch_device(P, pk.data_ptr(), pf.data_ptr(), kcap, K[0].data_ptr(),
+                                     K[1].data_ptr(), K[2].data_ptr(), K[3].data_ptr(),
+                                     K[4].data_ptr(), K[5].data_ptr(), K[6].data_ptr(), kcap,
+                                     F[0].data_ptr(), F[1].data_ptr(), F[3].data_ptr(),
+                                     F[4].data_ptr(), F[5].data_ptr(), F[6].data_ptr(),
+                                     out.data_ptr(), nmv.data_ptr(), stv.data_ptr())
+    t = timed(gob, 50)
+    assert int(stv[0]) == 0
+    x = items[1]
+    tc = cpu_timed(lambda: oracle.search_by_bow(x[0], x[1], x[2], x[3], f.desc, f.keys["angle"],
+                                                f_fv, 0.75, True))
+    emit(f"(f)4 SearchByBoW, relocalisation candidate loop (frame vs {P} keyframes, 1000 features)",
+         "pairs/s", P, t, tc, P * (kf.n + f.n) * (32 + 8),
+         "device batch: one call per relocalisation attempt (Tracking.cc:1636-1656), FeatureVectors "
+         "resident; 2 launches (init; search with the orientation filter in each pair's last workgroup)", cpu_units=1)
     m.close()
 
 
