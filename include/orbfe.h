@@ -455,6 +455,44 @@ int orbfe_search_by_bow_batch_device(orbfe_matcher* m, float nnratio, int check_
                                      const int32_t* d_f_node_off, const int32_t* d_f_feat,
                                      int32_t* d_matches, int32_t* d_nmatches, int32_t* d_status);
 
+/* ---- map-archive records of the extractor outputs (device side) ---------------------------
+ * The bodies the reference's Boost map archive stores for the extractor's outputs, written
+ * from / read into HBM (MapPoint.h:196-247; KeyFrame::serialize KeyFrame.cc:133-134 / 354-355
+ * stores mvKeys, mvKeysUn and mDescriptors, MapPoint::serialize MapPoint.cc:121 / 194 stores
+ * mDescriptor).  Keypoint record (serialize(Archive&, cv::KeyPoint&), MapPoint.h:196-209):
+ * angle, class_id, octave, response, response, pt.x, pt.y — 28 bytes, size not stored (a
+ * loaded keypoint has size 0).  cv::Mat record (save / load, MapPoint.h:215-247): cols i32,
+ * rows i32, elemSize u64, type u64, raw bytes; descriptors are rows x 32 CV_8UC1.  Boost's
+ * own framing (class-info preamble, collection counts) is the archive writer's.  All entry
+ * points are asynchronous on hip_stream (NULL = the null stream) of the current device and take
+ * at most 65535 frames / Mats per call. */
+
+/* Bytes of one cv::Mat record: 24 + rows * cols * elem_size (-1 on negative arguments). */
+int64_t orbfe_archive_mat_bytes(int rows, int cols, int elem_size);
+/* Frame f's min(d_n[f], cap) keypoints (d_keys + f*keys_pitch, orbfe_keypoint units) as
+ * consecutive 28-byte records at d_out + f*out_pitch (bytes; a multiple of 4, >= 28*cap). */
+int orbfe_archive_write_keypoints_device(int n_frames, const orbfe_keypoint* d_keys,
+                                         size_t keys_pitch, const int32_t* d_n, int cap,
+                                         uint8_t* d_out, size_t out_pitch, void* hip_stream);
+/* The inverse: min(d_n[f], cap) records -> keypoints (size 0, response = the second value). */
+int orbfe_archive_read_keypoints_device(int n_frames, const uint8_t* d_in, size_t in_pitch,
+                                        const int32_t* d_n, int cap, orbfe_keypoint* d_keys,
+                                        size_t keys_pitch, void* hip_stream);
+/* Mat k's descriptors (d_desc + k*desc_pitch, rows = d_rows[k], or rows_fixed when d_rows is
+ * NULL — 1 for MapPoint::mDescriptor — clipped to cap) as one rows x 32 CV_8UC1 record at
+ * d_out + k*out_pitch; d_len[k] (may be NULL) = its bytes.  Pitches are multiples of 8,
+ * out_pitch >= orbfe_archive_mat_bytes(cap, 32, 1). */
+int orbfe_archive_write_descriptors_device(int n_mats, const uint8_t* d_desc, size_t desc_pitch,
+                                           const int32_t* d_rows, int rows_fixed, int cap,
+                                           uint8_t* d_out, size_t out_pitch, int64_t* d_len,
+                                           void* hip_stream);
+/* Reads n_mats descriptor records (d_in + k*in_pitch) into d_desc + k*desc_pitch; d_rows[k]
+ * (may be NULL) = rows, or -1 for a record whose header is not (32, rows <= cap, 1, CV_8UC1),
+ * which sets *d_status = ORBFE_ERR_ARG (0 otherwise). */
+int orbfe_archive_read_descriptors_device(int n_mats, const uint8_t* d_in, size_t in_pitch,
+                                          int cap, uint8_t* d_desc, size_t desc_pitch,
+                                          int32_t* d_rows, int32_t* d_status, void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

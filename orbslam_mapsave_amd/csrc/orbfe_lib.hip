@@ -7,3 +7,4 @@
 #include "orbfe_greedy.hip"
 #include "orbfe_match_api.hip"
 #include "orbfe_bow.hip"
+#include "orbfe_archive.hip"

@@ -41,7 +41,9 @@ EXPORTED = [
     "orbfe_matcher_last_rounds", "orbfe_is_in_frustum", "orbfe_vocabulary_load_text",
     "orbfe_vocabulary_create", "orbfe_vocabulary_destroy", "orbfe_vocabulary_info",
     "orbfe_vocabulary_set_stream", "orbfe_bow_transform", "orbfe_bow_transform_batch_device",
-    "orbfe_search_by_bow", "orbfe_search_by_bow_batch_device",
+    "orbfe_search_by_bow", "orbfe_search_by_bow_batch_device", "orbfe_archive_mat_bytes",
+    "orbfe_archive_write_keypoints_device", "orbfe_archive_read_keypoints_device",
+    "orbfe_archive_write_descriptors_device", "orbfe_archive_read_descriptors_device",
 ]
 
 
@@ -69,6 +71,13 @@ def lib() -> C.CDLL:
             L.orbfe_vocabulary_load_text.argtypes = [C.c_char_p, C.c_int, C.c_void_p]
             L.orbfe_vocabulary_create.restype = C.c_void_p
             L.orbfe_vocabulary_destroy.argtypes = [C.c_void_p]
+        if hasattr(L, "orbfe_archive_mat_bytes"):
+            L.orbfe_archive_mat_bytes.restype = C.c_int64
+            sz, vp, i = C.c_size_t, C.c_void_p, C.c_int
+            L.orbfe_archive_write_keypoints_device.argtypes = [i, vp, sz, vp, i, vp, sz, vp]
+            L.orbfe_archive_read_keypoints_device.argtypes = [i, vp, sz, vp, i, vp, sz, vp]
+            L.orbfe_archive_write_descriptors_device.argtypes = [i, vp, sz, vp, i, i, vp, sz, vp, vp]
+            L.orbfe_archive_read_descriptors_device.argtypes = [i, vp, sz, i, vp, sz, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -311,6 +320,39 @@ class ORBextractor:
                 continue
             _check("orbfe_get_fast_keys", st)
             return out[:n.value].copy()
+
+
+def archive_mat_bytes(rows: int, cols: int = 32, elem_size: int = 1) -> int:
+    """Bytes of one cv::Mat archive record (MapPoint.h:215-247)."""
+    return int(lib().orbfe_archive_mat_bytes(rows, cols, elem_size))
+
+
+def archive_write_keypoints_device(n_frames: int, d_keys: int, keys_pitch: int, d_n: int,
+                                   cap: int, d_out: int, out_pitch: int, stream=None) -> None:
+    """Keypoint records (serialize(Archive&, cv::KeyPoint&), MapPoint.h:196-209) from HBM."""
+    _check("orbfe_archive_write_keypoints_device", lib().orbfe_archive_write_keypoints_device(
+        n_frames, d_keys, keys_pitch, d_n, cap, d_out, out_pitch, stream))
+
+
+def archive_read_keypoints_device(n_frames: int, d_in: int, in_pitch: int, d_n: int, cap: int,
+                                  d_keys: int, keys_pitch: int, stream=None) -> None:
+    _check("orbfe_archive_read_keypoints_device", lib().orbfe_archive_read_keypoints_device(
+        n_frames, d_in, in_pitch, d_n, cap, d_keys, keys_pitch, stream))
+
+
+def archive_write_descriptors_device(n_mats: int, d_desc: int, desc_pitch: int, d_rows,
+                                     rows_fixed: int, cap: int, d_out: int, out_pitch: int,
+                                     d_len=None, stream=None) -> None:
+    """rows x 32 CV_8UC1 cv::Mat records (MapPoint.h:215-229) from HBM descriptors."""
+    _check("orbfe_archive_write_descriptors_device", lib().orbfe_archive_write_descriptors_device(
+        n_mats, d_desc, desc_pitch, d_rows, rows_fixed, cap, d_out, out_pitch, d_len, stream))
+
+
+def archive_read_descriptors_device(n_mats: int, d_in: int, in_pitch: int, cap: int,
+                                    d_desc: int, desc_pitch: int, d_rows, d_status: int,
+                                    stream=None) -> None:
+    _check("orbfe_archive_read_descriptors_device", lib().orbfe_archive_read_descriptors_device(
+        n_mats, d_in, in_pitch, cap, d_desc, desc_pitch, d_rows, d_status, stream))
 
 
 class Vocabulary:
