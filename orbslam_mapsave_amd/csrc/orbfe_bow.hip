@@ -364,30 +364,37 @@ __global__ __launch_bounds__(kBowSearchBlock) void bow_search_kernel(BowMatchArg
                 }
             }
             const int cnt = min(64, nx - xb);
+            const int nj = (ny + 63) >> 6;  // candidate registers in use (wave-uniform)
             for (int t = 0; t < cnt; ++t) {
-                const int ikf = __shfl(my_ikf, t, 64);
+                // t is wave-uniform: v_readlane into scalar registers, no LDS round trip
+                const int ikf = __builtin_amdgcn_readlane(my_ikf, t);
                 if (ikf < 0) continue;
-                const uint4 q0 = make_uint4(__shfl(my0.x, t, 64), __shfl(my0.y, t, 64),
-                                            __shfl(my0.z, t, 64), __shfl(my0.w, t, 64));
-                const uint4 q1 = make_uint4(__shfl(my1.x, t, 64), __shfl(my1.y, t, 64),
-                                            __shfl(my1.z, t, 64), __shfl(my1.w, t, 64));
+                const uint4 q0 = make_uint4(__builtin_amdgcn_readlane(my0.x, t),
+                                            __builtin_amdgcn_readlane(my0.y, t),
+                                            __builtin_amdgcn_readlane(my0.z, t),
+                                            __builtin_amdgcn_readlane(my0.w, t));
+                const uint4 q1 = make_uint4(__builtin_amdgcn_readlane(my1.x, t),
+                                            __builtin_amdgcn_readlane(my1.y, t),
+                                            __builtin_amdgcn_readlane(my1.z, t),
+                                            __builtin_amdgcn_readlane(my1.w, t));
                 uint32_t key = 0xffffffffu;
                 int dist[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    dist[j] = free_[j] ? hamming256(q0, q1, d0[j], d1[j]) : 256;
-                    if (free_[j]) key = min(key, ((uint32_t)dist[j] << 16) | (uint32_t)(lane + 64 * j));
+                    dist[j] = 256;
+                    if (j < nj && free_[j]) {
+                        dist[j] = hamming256(q0, q1, d0[j], d1[j]);
+                        key = min(key, ((uint32_t)dist[j] << 16) | (uint32_t)(lane + 64 * j));
+                    }
                 }
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) key = min(key, (uint32_t)__shfl_xor((int)key, o, 64));
+                key = __ockl_wfred_min_u32(key);  // DPP wave reduction
                 const int b1 = key == 0xffffffffu ? 256 : (int)(key >> 16);
                 const int brank = (int)(key & 0xffff);
                 int sec = 256;
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    if (free_[j] && lane + 64 * j != brank) sec = min(sec, dist[j]);
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) sec = min(sec, __shfl_xor(sec, o, 64));
+                    if (j < nj && free_[j] && lane + 64 * j != brank) sec = min(sec, dist[j]);
+                sec = __ockl_wfred_min_i32(sec);
                 if (b1 <= 50 && (float)b1 < nnratio * (float)sec) {  // TH_LOW, ratio (233-237)
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {

@@ -75,6 +75,8 @@ __device__ __forceinline__ int hamming256(const uint4 a0, const uint4 a1, const 
 // row_bcast 15/31) instead of six ds_bpermute shuffles.  Every lane of the wave must be active.
 extern "C" __device__ int __ockl_wfscan_add_i32(int, bool);
 extern "C" __device__ int __ockl_wfred_add_i32(int);
+extern "C" __device__ uint32_t __ockl_wfred_min_u32(uint32_t);
+extern "C" __device__ int __ockl_wfred_min_i32(int);
 __device__ __forceinline__ int wave_inclusive_sum(int x) { return __ockl_wfscan_add_i32(x, true); }
 
 // Slot of this lane's item in a block-shared list: one LDS atomic per wave (called by every

@@ -314,5 +314,7 @@ def row_bow(tmpdir):
 if __name__ == "__main__":
     import tempfile
     with tempfile.TemporaryDirectory() as td:
-        for fn in (row_color, row_stereo, row_reloc, row_distinctive, lambda: row_bow(td)):
-            fn()
+        rows = {"color": row_color, "stereo": row_stereo, "reloc": row_reloc,
+                "distinctive": row_distinctive, "bow": lambda: row_bow(td)}
+        for name in (sys.argv[1:] or list(rows)):
+            rows[name]()
