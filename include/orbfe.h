@@ -333,7 +333,8 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
                                      const int32_t* d_mp_ids, float nnratio, float th,
                                      int32_t* d_frame_mp, int32_t* d_frame_mp_obs,
                                      uint8_t* d_in_view, int32_t* counts);
-/* Jacobi rounds the most recent SearchByProjection resolution took (diagnostics). */
+/* Jacobi rounds the most recent SearchByProjection / SearchForInitialization resolution took
+ * (diagnostics). */
 int orbfe_matcher_last_rounds(const orbfe_matcher* m);
 
 /* Relocalisation ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF,

@@ -7,10 +7,10 @@
 //   grid_kernel          Frame::AssignFeaturesToGrid (Frame.cc:341-356) as a CSR
 //   *_cand_kernel        GetFeaturesInArea (Frame.cc:445-498) + distances for every query in
 //                        parallel (counts, scan, fill)
-//   sfi_resolve_kernel   SearchForInitialization's sequential greedy semantics (H7): one wave
-//                        decides 64 consecutive queries against the committed state, commits
-//                        the prefix no earlier lane of the chunk can have influenced, and
-//                        resumes at the first conflicting lane.  Bit-identical to the loop.
+//   sfi_round_kernel     SearchForInitialization's sequential greedy-with-steals semantics (H7)
+//                        as Jacobi rounds to the unique fixed point of the in-order loop (a
+//                        wave per query, lanes over candidates); sfi_final_kernel applies the
+//                        steals, the rotation filter and the vbPrevMatched update
 //   (the SearchByProjection overloads resolve in orbfe_greedy.hip: parallel Jacobi rounds
 //    to the unique fixed point of the in-order loop)
 //   frustum_kernel       Frame::isInFrustum (387-443) + MapPoint::PredictScale (MapPoint.cc:633)
@@ -498,91 +498,135 @@ __device__ __forceinline__ int first_lane(bool pred) {
     return b ? __builtin_ctzll(b) : 64;
 }
 
-struct SfiResolveArgs {
-    int n1, n2;
-    const orbfe_keypoint* k1;
-    const orbfe_keypoint* k2;
+// SearchForInitialization's greedy loop as a fixed point.  Query i (an F1 keypoint, in index
+// order) skips candidate s when vMatchedDistance[s] <= dist (447-448); vMatchedDistance only
+// decreases, and at query i it is min{d_j : j < i accepted s with distance d_j}.  So query i's
+// decision depends only on the decisions of j < i: the system D = decide(D) has one fixed point,
+// the in-order loop's result, and Jacobi rounds reach it (after a round the lowest wrong
+// decision depends only on correct ones, so the correct prefix grows).  A round is one launch:
+// a wave per query, lanes over its candidates, best = min (dist << 16 | rank) (the first minimum
+// in GetFeaturesInArea order) and second = the minimum of the other distances, as the
+// sequential best / second update yields.  Each accepting query appends (i, dist) to its slot's
+// list for the next round (k entries per slot: 64 first, and if a round overflows that, the
+// rounds are rerun with room for every query).  Three list buffers rotate (read / write /
+// cleared), two decision buffers ping-pong.  After convergence a slot belongs to its last acceptor (steals, 466-470) and the
+// rotation histogram counts every acceptance, stolen or not (rotHist is filled at accept time).
+constexpr int kSfiSlotK = 64;
+struct SfiRoundArgs {
+    int n1, n2, k;          // k: list entries per slot
     const int* off;
-    const int2* cand;
+    const int2* cand;       // (i2, dist) in GetFeaturesInArea order
     float nnratio;
-    int check_ori;
-    int* md;        // n2 scratch: vMatchedDistance
-    int* m21;       // n2 scratch: vnMatches21
-    int* claim;     // n2 scratch: lowest claiming lane, 64 = none
-    int* m12;       // n1 out: vnMatches12
-    int* rotbin;    // n1 scratch
-    float* prev;    // 2 n1 inout
-    int* nmatches;
+    int* dec[2];            // round r reads dec[r & 1] (-2 before round 0), writes dec[~r & 1]
+    int2* list[3];          // per slot kSfiSlotK acceptors (query, dist)
+    int* lcnt[3];           // per slot acceptor count
+    int* chg;               // per round: 1 if a decision changed
+    int* overflow;          // a slot had more than k acceptors in a round
+    int* status;            // a query with 65536+ candidates (ranks do not fit the key)
 };
 
-__global__ __launch_bounds__(64) void sfi_resolve_kernel(SfiResolveArgs a) {
+__global__ __launch_bounds__(256) void sfi_round_kernel(SfiRoundArgs a, int r) {
+    const int gid = blockIdx.x * 256 + threadIdx.x;
+    if (gid < a.n2) a.lcnt[(r + 2) % 3][gid] = 0;  // the list round r + 1 fills
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= a.n1) return;
+    const int lane = threadIdx.x & 63;
+    const int e0 = a.off[i], e1 = a.off[i + 1];
+    if (e1 - e0 >= 65536) {
+        if (lane == 0) atomicExch(a.status, ORBFE_ERR_UNSUPPORTED);
+        return;
+    }
+    const int2* Lr = a.list[r % 3];
+    const int* Cr = a.lcnt[r % 3];
+    uint32_t k1 = 0xffffffffu, k2 = 0xffffffffu;  // this lane's two smallest keys
+    for (int e = e0 + lane; e < e1; e += 64) {
+        const int2 c = a.cand[e];
+        const int n = min(Cr[c.x], a.k);
+        int md = INT_MAX;  // vMatchedDistance[i2] as query i sees it
+        for (int k = 0; k < n; ++k) {
+            const int2 q = Lr[(size_t)c.x * a.k + k];
+            if (q.x < i) md = min(md, q.y);
+        }
+        if (md <= c.y) continue;
+        const uint32_t key = ((uint32_t)c.y << 16) | (uint32_t)(e - e0);
+        if (key < k1) { k2 = k1; k1 = key; }
+        else if (key < k2) { k2 = key; }
+    }
+    const uint32_t best = __ockl_wfred_min_u32(k1);
+    const uint32_t sec = __ockl_wfred_min_u32(k1 == best ? k2 : k1);
+    const int bd = best == 0xffffffffu ? INT_MAX : (int)(best >> 16);
+    const int sd = sec == 0xffffffffu ? INT_MAX : (int)(sec >> 16);
+    const bool acc = bd <= kThLow && (float)bd < (float)sd * a.nnratio;  // 455-456
+    if (lane != 0) return;
+    const int d = acc ? a.cand[e0 + (int)(best & 0xffff)].x : -1;
+    if (d != a.dec[r & 1][i]) a.chg[r] = 1;
+    a.dec[~r & 1][i] = d;
+    if (d >= 0) {
+        const int p = atomicAdd(&a.lcnt[(r + 1) % 3][d], 1);
+        if (p < a.k) a.list[(r + 1) % 3][(size_t)d * a.k + p] = make_int2(i, bd);
+        else *a.overflow = 1;
+    }
+}
+
+// The converged state: owners (last acceptor per slot), rotation consistency (492-515),
+// nmatches and the vbPrevMatched update (518-520).  One workgroup.
+struct SfiFinalArgs {
+    int n1, k;
+    const orbfe_keypoint* k1;
+    const orbfe_keypoint* k2;
+    const int* dec;
+    const int2* list;
+    const int* lcnt;
+    int check_ori;
+    int* m12;
+    int* rotbin;
+    float* prev;
+    int* nmatches;
+};
+__global__ __launch_bounds__(1024) void sfi_final_kernel(SfiFinalArgs a) {
     __shared__ int hist[kHistLen];
-    const int lane = lane_id();
-    for (int i = lane; i < a.n2; i += 64) {
-        a.md[i] = INT_MAX;
-        a.m21[i] = -1;
-        a.claim[i] = 64;
-    }
-    for (int i = lane; i < a.n1; i += 64) {
-        a.m12[i] = -1;
-        a.rotbin[i] = -1;
-    }
-    if (lane < kHistLen) hist[lane] = 0;
+    __shared__ int top[3];
+    __shared__ int nm;
+    if (threadIdx.x < kHistLen) hist[threadIdx.x] = 0;
+    if (threadIdx.x == 0) nm = 0;
     __syncthreads();
-    for (int base = 0; base < a.n1;) {
-        const int i1 = base + lane;
-        const bool valid = i1 < a.n1;
-        int best = INT_MAX, second = INT_MAX, bi = -1;
-        const int e0 = valid ? a.off[i1] : 0, e1 = valid ? a.off[i1 + 1] : 0;
-        for (int e = e0; e < e1; ++e) {
-            const int2 c = a.cand[e];
-            if (a.md[c.x] <= c.y) continue;  // ORBmatcher.cc:447-448
-            if (c.y < best) { second = best; best = c.y; bi = c.x; }
-            else if (c.y < second) { second = c.y; }
+    for (int i = threadIdx.x; i < a.n1; i += 1024) {
+        const int d = a.dec[i];
+        int own = -1, bin = -1;
+        if (d >= 0) {
+            int last = -1;
+            const int n = min(a.lcnt[d], a.k);
+            for (int k = 0; k < n; ++k) last = max(last, a.list[(size_t)d * a.k + k].x);
+            if (last == i) own = d;
+            if (a.check_ori) {
+                bin = rot_bin(a.k1[i].angle, a.k2[d].angle);
+                atomicAdd(&hist[bin], 1);
+            }
         }
-        const bool acc = valid && best <= kThLow && best < (float)second * a.nnratio;
-        if (acc) atomicMin(&a.claim[bi], lane);
-        __syncthreads();
-        bool conf = false;
-        for (int e = e0; e < e1 && !conf; ++e) conf = a.claim[a.cand[e].x] < lane;
-        const int stop = first_lane(conf);  // lanes below `stop` saw the committed state
-        if (acc && lane < stop) {
-            const int old = a.m21[bi];
-            if (old >= 0) a.m12[old] = -1;  // steal (466-470)
-            a.m12[i1] = bi;
-            a.m21[bi] = i1;
-            a.md[bi] = best;
-            if (a.check_ori) a.rotbin[i1] = rot_bin(a.k1[i1].angle, a.k2[bi].angle);
-        }
-        __syncthreads();
-        if (acc) a.claim[bi] = 64;
-        __syncthreads();
-        base += stop;
+        a.m12[i] = own;
+        a.rotbin[i] = bin;
     }
-    // rotation consistency (492-515) and vbPrevMatched update (518-520)
-    if (a.check_ori) {
-        for (int i = lane; i < a.n1; i += 64)
-            if (a.rotbin[i] >= 0) atomicAdd(&hist[a.rotbin[i]], 1);
-        __syncthreads();
-        int t1, t2, t3;
-        three_maxima(hist, t1, t2, t3);
-        for (int i = lane; i < a.n1; i += 64) {
-            const int b = a.rotbin[i];
-            if (b >= 0 && b != t1 && b != t2 && b != t3) a.m12[i] = -1;
+    __syncthreads();
+    if (a.check_ori && threadIdx.x == 0) three_maxima(hist, top[0], top[1], top[2]);
+    __syncthreads();
+    int cnt = 0;
+    for (int i = threadIdx.x; i < a.n1; i += 1024) {
+        int j = a.m12[i];
+        const int b = a.rotbin[i];
+        if (j >= 0 && a.check_ori && b != top[0] && b != top[1] && b != top[2]) {
+            j = -1;
+            a.m12[i] = -1;
         }
-        __syncthreads();
-    }
-    int nm = 0;
-    for (int i = lane; i < a.n1; i += 64) {
-        const int j = a.m12[i];
         if (j >= 0) {
-            ++nm;
+            ++cnt;
             a.prev[2 * i] = a.k2[j].x;
             a.prev[2 * i + 1] = a.k2[j].y;
         }
     }
-    nm = wave_sum(nm);
-    if (lane == 0) *a.nmatches = nm;
+    cnt = wave_sum(cnt);
+    if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&nm, cnt);
+    __syncthreads();
+    if (threadIdx.x == 0) *a.nmatches = nm;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -511,42 +511,122 @@ int orbfe_search_for_initialization(orbfe_matcher* m, float nnratio, int check_o
                                     int32_t* nmatches) {
     if (!frame_ok(f1) || !frame_ok(f2) || !nmatches || (f1->n && (!prev_matched || !matches12)))
         return ORBFE_ERR_ARG;
+    bool retried = false;
     return guarded(m, [&]() {
+        std::function<int()> attempt = [&]() -> int {
         int st;
         SfiArgs a;
+        if ((st = m->up(m->s5, prev_matched, (size_t)f1->n * 2 * sizeof(float)))) return st;
+        const int32_t zero[4] = {0, 0, 0, 0};
+        if ((st = m->up(m->scal, zero, sizeof(zero)))) return st;
         if ((st = m->frame(f1, false, a.f1))) return st;
         if ((st = m->frame(f2, true, a.f2))) return st;
-        if ((st = m->up(m->s5, prev_matched, (size_t)f1->n * 2 * sizeof(float)))) return st;
         a.prev = m->s5.as<float>();
         a.window = (float)window;
-        if ((st = m->csr_async(a, f1->n, sfi_cand_kernel<false>, sfi_cand_kernel<true>, 4))) return st;
         const int n1 = f1->n, n2 = f2->n;
-        if ((st = m->s1.ensure(std::max(n2, 1) * 3 * sizeof(int)))) return st;
+        // candidates without a host round trip: the fill is bounded by the current capacity,
+        // checked at the first synchronisation of the rounds (one retry with the exact total)
+        const size_t cap = std::max(m->cand.bytes / sizeof(int2), (size_t)64 * std::max(n1, 1));
+        if ((st = m->cand.ensure(cap * sizeof(int2)))) return st;
+        if ((st = m->cnt.ensure(std::max(n1, 1) * sizeof(int)))) return st;
+        if ((st = m->off.ensure((n1 + 1) * sizeof(int)))) return st;
+        a.cnt = m->cnt.as<int>();
+        a.off = m->off.as<int>();
+        a.cand = m->cand.as<int2>();
+        a.cand_cap = (long long)cap;
+        const int qb = std::max(1, (n1 + 3) / 4);
+        hipLaunchKernelGGL(sfi_cand_kernel<false>, dim3(qb), dim3(256), 0, m->stream, a);
+        hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, m->stream, m->cnt.as<int>(), n1, m->off.as<int>());
+        hipLaunchKernelGGL(sfi_cand_kernel<true>, dim3(qb), dim3(256), 0, m->stream, a);
+        // fixed-point rounds (sfi_round_kernel): decisions, slot lists, change flags
+        const int L2 = std::max(n2, 1);
+        if ((st = m->g_dec.ensure((size_t)2 * std::max(n1, 1) * sizeof(int)))) return st;
+        if ((st = m->g_t1.ensure((size_t)3 * L2 * sizeof(int)))) return st;
+        if ((st = m->g_chg.ensure((size_t)(n1 + 4) * sizeof(int)))) return st;  // overflow, -, rounds 0..n1
         if ((st = m->s2.ensure(std::max(n1, 1) * 2 * sizeof(int)))) return st;
-        if ((st = m->scal.ensure(16))) return st;
-        SfiResolveArgs r;
+        if ((st = m->flush())) return st;
+        int total = 0;
+        ORBFE_HIP(hipMemcpyAsync(&total, m->off.as<int>() + n1, sizeof(int), hipMemcpyDeviceToHost, m->stream));
+        SfiRoundArgs r{};
         r.n1 = n1;
         r.n2 = n2;
-        r.k1 = a.f1.k;
-        r.k2 = a.f2.k;
         r.off = m->off.as<int>();
         r.cand = m->cand.as<int2>();
         r.nnratio = nnratio;
-        r.check_ori = check_ori;
-        r.md = m->s1.as<int>();
-        r.m21 = r.md + std::max(n2, 1);
-        r.claim = r.m21 + std::max(n2, 1);
-        r.m12 = m->s2.as<int>();
-        r.rotbin = r.m12 + std::max(n1, 1);
-        r.prev = m->s5.as<float>();
-        r.nmatches = m->scal.as<int>();
-        if ((st = m->flush())) return st;
-        hipLaunchKernelGGL(sfi_resolve_kernel, dim3(1), dim3(64), 0, m->stream, r);
+        r.dec[0] = m->g_dec.as<int>();
+        r.dec[1] = r.dec[0] + std::max(n1, 1);
+        r.chg = m->g_chg.as<int>() + 2;
+        r.overflow = m->g_chg.as<int>();
+        r.status = m->scal.as<int>() + 1;
+        const int rb = std::max(1, (std::max(n1 * 64, n2) + 255) / 256);
+        // slot lists of 64 acceptors; a slot drawing more in some round (one query per slot is
+        // the usual case) reruns the rounds with room for every query
+        int conv = -1;
+        for (int k : {kSfiSlotK, std::max(n1, 1)}) {
+            r.k = k;
+            if ((st = m->g_t0.ensure((size_t)3 * L2 * k * sizeof(int2)))) return st;
+            for (int b = 0; b < 3; ++b) {
+                r.list[b] = m->g_t0.as<int2>() + (size_t)b * L2 * k;
+                r.lcnt[b] = m->g_t1.as<int>() + (size_t)b * L2;
+            }
+            // round 0 compares against 0xfefefefe (< -1: no decision), reads an empty list 0
+            ORBFE_HIP(hipMemsetAsync(r.dec[0], 0xfe, (size_t)std::max(n1, 1) * sizeof(int), m->stream));
+            ORBFE_HIP(hipMemsetAsync(m->g_t1.p, 0, (size_t)2 * L2 * sizeof(int), m->stream));
+            ORBFE_HIP(hipMemsetAsync(m->g_chg.p, 0, (size_t)(n1 + 4) * sizeof(int), m->stream));
+            int rr = 0, batch = 6, ovf = 0;
+            std::vector<int> chg_h;
+            while (conv < 0) {
+                const int r0 = rr;
+                for (int b = 0; b < batch && rr <= n1; ++b, ++rr)
+                    hipLaunchKernelGGL(sfi_round_kernel, dim3(rb), dim3(256), 0, m->stream, r, rr);
+                ORBFE_HIP(hipGetLastError());
+                chg_h.assign(rr - r0 + 2, 0);
+                ORBFE_HIP(hipMemcpyAsync(chg_h.data(), m->g_chg.as<int>(), sizeof(int), hipMemcpyDeviceToHost, m->stream));
+                ORBFE_HIP(hipMemcpyAsync(chg_h.data() + 2, r.chg + r0, (rr - r0) * sizeof(int), hipMemcpyDeviceToHost, m->stream));
+                ORBFE_HIP(hipStreamSynchronize(m->stream));
+                if ((size_t)total > cap) {
+                    if (retried) return ORBFE_ERR_HIP;
+                    if ((st = m->cand.ensure((size_t)total * sizeof(int2)))) return st;
+                    retried = true;
+                    m->begin();
+                    return attempt();
+                }
+                ovf = chg_h[0];
+                if (ovf) break;
+                for (int q = 0; q < rr - r0; ++q)
+                    if (!chg_h[2 + q]) { conv = r0 + q; break; }
+                if (conv < 0 && rr > n1) return ORBFE_ERR_HIP;  // cannot happen: the prefix grows
+                batch = std::min(batch * 2, 64);
+            }
+            if (conv >= 0) break;
+        }
+        if (conv < 0) return ORBFE_ERR_HIP;  // lists sized for every query cannot overflow
+        m->rounds_on_device = false;
+        m->last_rounds = conv + 1;
+        SfiFinalArgs fa;
+        fa.n1 = n1;
+        fa.k = r.k;
+        fa.k1 = a.f1.k;
+        fa.k2 = a.f2.k;
+        fa.dec = r.dec[~conv & 1];
+        fa.list = r.list[(conv + 1) % 3];
+        fa.lcnt = r.lcnt[(conv + 1) % 3];
+        fa.check_ori = check_ori;
+        fa.m12 = m->s2.as<int>();
+        fa.rotbin = fa.m12 + std::max(n1, 1);
+        fa.prev = m->s5.as<float>();
+        fa.nmatches = m->scal.as<int>();
+        hipLaunchKernelGGL(sfi_final_kernel, dim3(1), dim3(1024), 0, m->stream, fa);
         ORBFE_HIP(hipGetLastError());
         if ((st = m->down(matches12, m->s2, (size_t)n1 * sizeof(int)))) return st;
         if ((st = m->down(prev_matched, m->s5, (size_t)n1 * 2 * sizeof(float)))) return st;
-        if ((st = m->down(nmatches, m->scal, sizeof(int)))) return st;
-        return m->sync();
+        int res[2] = {0, 0};
+        if ((st = m->down(res, m->scal, sizeof(res)))) return st;
+        if ((st = m->sync())) return st;
+        *nmatches = res[0];
+        return res[1];
+        };
+        return attempt();
     });
 }
 

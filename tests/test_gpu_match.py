@@ -124,3 +124,51 @@ def test_is_in_frustum(mt):
     sel = e[0] == 1
     for a, b in zip(g[1:], e[1:]):
         assert np.array_equal(a[sel], b[sel])
+
+
+@pytest.mark.parametrize("n_contend,check_ori", [(5, True), (24, False), (70, True), (90, False)])
+def test_search_for_initialization_contended(mt, n_contend, check_ori):
+    """Many F1 queries competing for the same F2 keypoints: steals (466-470) in every order of
+    distances; with n_contend > 64 more acceptors of one slot in a round than the first slot
+    lists hold, so the rounds rerun with lists sized for every query."""
+    from orbslam_mapsave_amd.abi import KEYPOINT_DTYPE, Frame
+    from orbslam_mapsave_amd.native import ORBmatcher
+    rng = np.random.Generator(np.random.PCG64(n_contend))
+    scale = (np.float32(1.2) ** np.arange(8)).astype(np.float32)
+    n2 = 300
+    k2 = np.zeros(n2, KEYPOINT_DTYPE)
+    k2["x"], k2["y"] = rng.uniform(20, 620, n2), rng.uniform(20, 460, n2)
+    k2["angle"] = rng.uniform(0, 360, n2)
+    k2["octave"] = rng.integers(0, 2, n2)
+    k2["class_id"] = -1
+    d2 = S.random_desc(rng, n2)
+    hubs = rng.choice(np.flatnonzero(k2["octave"] == 0), 4, replace=False)
+    q_keys, q_desc = [], []
+    for h in hubs:  # n_contend near-copies of each hub, distances in random order
+        for _ in range(n_contend):
+            k = np.zeros(1, KEYPOINT_DTYPE)[0]
+            k["x"], k["y"] = k2["x"][h] + rng.uniform(-5, 5), k2["y"][h] + rng.uniform(-5, 5)
+            k["angle"] = (k2["angle"][h] + rng.choice([0.0, 1.0, 180.0])) % 360
+            k["class_id"] = -1
+            q_keys.append(k)
+            q_desc.append(S.flip_bits(d2[h][None], rng, rng.uniform(0.0, 0.15))[0])
+    n_rand = 200
+    kr = np.zeros(n_rand, KEYPOINT_DTYPE)
+    kr["x"], kr["y"] = rng.uniform(20, 620, n_rand), rng.uniform(20, 460, n_rand)
+    kr["angle"] = rng.uniform(0, 360, n_rand)
+    kr["octave"] = rng.integers(0, 3, n_rand)
+    kr["class_id"] = -1
+    perm = rng.permutation(len(q_keys) + n_rand)
+    k1 = np.concatenate([np.array(q_keys, KEYPOINT_DTYPE), kr])[perm]
+    d1 = np.concatenate([np.array(q_desc, np.uint8), S.random_desc(rng, n_rand)])[perm]
+    f1, f2 = Frame(k1, d1, 640, 480, scale), Frame(k2, d2, 640, 480, scale)
+    prev = np.stack([k1["x"], k1["y"]], 1).astype(np.float32)
+    m = ORBmatcher(0.9, check_ori, device=0)
+    g12, gn, gprev = m.SearchForInitialization(f1, f2, prev, 100)
+    e12, en, eprev = oracle.search_for_initialization(f1, f2, prev, 100, 0.9, check_ori)
+    assert en > 0
+    assert gn == en
+    assert np.array_equal(g12, e12)
+    assert np.array_equal(gprev, eprev)
+    assert m.last_rounds() > 0  # the fixed-point rounds resolved it
+    m.close()

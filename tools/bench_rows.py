@@ -161,6 +161,34 @@ def row_reloc():
     m.close()
 
 
+def row_track():
+    """The per-frame tracking-loop matchers through the host ABI (uploads included):
+    TrackWithMotionModel's SearchByProjection(CurrentFrame, LastFrame, th, mono)
+    (Tracking.cc:1132, ORBmatcher.cc:1331-1473) and MonocularInitialization's
+    SearchForInitialization (Tracking.cc:844, ORBmatcher.cc:408-523)."""
+    import scenarios as S
+    c = S.sbp_last_case(0)
+    args = (c["cur"], c["tcw_cur"], c["cam"], c["last_keys"], c["last_valid"], c["last_outlier"],
+            c["last_xyz"], c["last_desc"], c["last_nobs"], c["tcw_last"])
+    m = native.ORBmatcher(0.9, True, device=0)
+    t = timed(lambda: m.SearchByProjectionLast(*args, 15.0, True, last_ids=c["last_ids"]), 50)
+    tc = cpu_timed(lambda: oracle.search_by_projection_last(*args, 15.0, True, True,
+                                                            last_ids=c["last_ids"]))
+    n = len(c["last_valid"])
+    emit("tracking SearchByProjection(CurrentFrame, LastFrame) (1000 kp each, mono th 15)",
+         "calls/s", 1, t, tc, n * (12 + 32 + 28 + 8) + c["cur"].n * 60,
+         "host ABI (uploads included): one call per tracked frame, latency-bound")
+    m.close()
+    f1, f2, prev = S.sfi_case(0)
+    m = native.ORBmatcher(0.9, True, device=0)
+    t = timed(lambda: m.SearchForInitialization(f1, f2, prev, 100), 20)
+    tc = cpu_timed(lambda: oracle.search_for_initialization(f1, f2, prev, 100, 0.9, True))
+    emit("initialization SearchForInitialization(F1, F2, window 100) (2000 kp each)", "calls/s",
+         1, t, tc, (f1.n + f2.n) * 60,
+         "host ABI (uploads included): sequential greedy with steals, one wave resolves it")
+    m.close()
+
+
 def row_distinctive():
     from test_distinctive import make_case
     off, desc = make_case(3, n_mp=50_000, max_obs=20)
@@ -314,7 +342,7 @@ def row_bow(tmpdir):
 if __name__ == "__main__":
     import tempfile
     with tempfile.TemporaryDirectory() as td:
-        rows = {"color": row_color, "stereo": row_stereo, "reloc": row_reloc,
+        rows = {"color": row_color, "stereo": row_stereo, "reloc": row_reloc, "track": row_track,
                 "distinctive": row_distinctive, "bow": lambda: row_bow(td)}
         for name in (sys.argv[1:] or list(rows)):
             rows[name]()
