@@ -71,29 +71,58 @@ __global__ __launch_bounds__(kGreedyBlock) void greedy_init_kernel(GreedyArgs a)
     if (t == 0) *a.nm = 0;
 }
 
-__device__ __forceinline__ int greedy_decide(const GreedyArgs& a, const int* Tc, int i) {
-    const int e0 = a.off[i], e1 = a.off[i + 1];
-    if (a.mode == kGreedyLocal) {
-        int best = 256, bl = -1, second = 256, sl = -1, bi = -1;
-        for (int e = e0; e < e1; ++e) {
-            const int2 c = a.cand[e];
-            if (Tc[c.x] < i) continue;
-            const int d = c.y & 0xffff, lv = c.y >> 16;
+// Point i's decision given T: its best candidate among the slots not blocked for it.
+struct GreedyAcc {
+    int best = 256, bl = -1, second = 256, sl = -1, bi = -1;
+    __device__ __forceinline__ void add(const GreedyArgs& a, const int* Tc, int i, int2 c) {
+        if (Tc[c.x] < i) return;
+        const int d = c.y & 0xffff;
+        if (a.mode == kGreedyLocal) {
+            const int lv = c.y >> 16;
             if (d < best) { second = best; best = d; sl = bl; bl = lv; bi = c.x; }
             else if (d < second) { sl = lv; second = d; }
+        } else if (d < best) {
+            best = d;
+            bi = c.x;
         }
-        if (best > 100) return -1;  // TH_HIGH
-        if (bl == sl && best > a.nnratio * second) return -1;
-        return bi;
     }
-    int best = 256, bi = -1;
-    for (int e = e0; e < e1; ++e) {
-        const int2 c = a.cand[e];
-        if (Tc[c.x] < i) continue;
-        const int d = c.y & 0xffff;
-        if (d < best) { best = d; bi = c.x; }
+    __device__ __forceinline__ int result(const GreedyArgs& a) const {
+        if (a.mode == kGreedyLocal) {
+            if (best > 100) return -1;  // TH_HIGH
+            if (bl == sl && best > a.nnratio * second) return -1;
+            return bi;
+        }
+        return best <= a.max_dist ? bi : -1;
     }
-    return best <= a.max_dist ? bi : -1;
+};
+
+__device__ __forceinline__ int greedy_decide(const GreedyArgs& a, const int* Tc, int i) {
+    GreedyAcc acc;
+    for (int e = a.off[i], e1 = a.off[i + 1]; e < e1; ++e) acc.add(a, Tc, i, a.cand[e]);
+    return acc.result(a);
+}
+
+// The first kCandCache candidates of a point held in registers across the rounds of the
+// single-workgroup resolver (a round then costs LDS lookups only, no global load chain).
+constexpr int kCandCache = 8;
+struct CandCache {
+    int e0, e1;
+    int2 c[kCandCache];
+};
+__device__ __forceinline__ void cand_cache_load(const GreedyArgs& a, int i, CandCache& cc) {
+    cc.e0 = a.off[i];
+    cc.e1 = a.off[i + 1];
+#pragma unroll
+    for (int k = 0; k < kCandCache; ++k) cc.c[k] = cc.e0 + k < cc.e1 ? a.cand[cc.e0 + k] : make_int2(0, 0);
+}
+__device__ __forceinline__ int greedy_decide_cached(const GreedyArgs& a, const int* Tc, int i,
+                                                    const CandCache& cc) {
+    GreedyAcc acc;
+#pragma unroll
+    for (int k = 0; k < kCandCache; ++k)
+        if (cc.e0 + k < cc.e1) acc.add(a, Tc, i, cc.c[k]);
+    for (int e = cc.e0 + kCandCache; e < cc.e1; ++e) acc.add(a, Tc, i, a.cand[e]);
+    return acc.result(a);
 }
 
 // Round r: decisions from T[r % 3], first blocking acceptors into T[(r + 1) % 3] (holding the
@@ -174,11 +203,11 @@ __global__ __launch_bounds__(kGreedyBlock) void greedy_ori_kernel(GreedyArgs a) 
 // by barriers instead of launches, then G2-G4; no host round trip.  T ping-pongs between
 // T[0] and T[1]: a round reads one and writes the other (pre-filled with the blocked-before
 // state), then the buffer it read is reset for the next round.  The converged round count is
-// left in chg[0].  T and the last-acceptor table live in LDS (3 x nkp ints), so every
+// left in chg[0].  T, the last-acceptor table and the blocked-before state live in LDS (4 x nkp ints), so every
 // cross-thread exchange is an LDS atomic or an LDS read after a barrier.
 constexpr int kGreedySmallBlock = 1024;
 constexpr int kGreedySmallMax = 16384;     // points handled by the single-workgroup form
-constexpr int kGreedySmallSlots = 5000;    // slots (keypoints): 3 x 4 B each within 64 KB of LDS
+constexpr int kGreedySmallSlots = 5000;    // slots (keypoints): 4 x 4 B each within 80 KB of LDS
 __global__ __launch_bounds__(kGreedySmallBlock) void greedy_small_kernel(GreedyArgs a) {
     extern __shared__ int lds[];
     __shared__ int changed, nm;
@@ -187,13 +216,18 @@ __global__ __launch_bounds__(kGreedySmallBlock) void greedy_small_kernel(GreedyA
     const int tid = threadIdx.x;
     int* T[2] = {lds, lds + a.nkp};
     int* last = lds + 2 * a.nkp;
+    int* pre = lds + 3 * a.nkp;  // blocked-before state per slot
     for (int s = tid; s < a.nkp; s += kGreedySmallBlock) {
         const int v = greedy_preblocked(a, s) ? -1 : INT_MAX;
+        pre[s] = v;  // the per-round reset reads LDS, not the slot arrays
         T[0][s] = v;
         T[1][s] = v;
         last[s] = -1;
     }
     for (int i = tid; i < a.m; i += kGreedySmallBlock) a.dec[i] = -2;
+    CandCache cc;  // the candidates of point tid (most calls have <= one point per thread)
+    if (tid < a.m) cand_cache_load(a, tid, cc);
+    else cc.e0 = cc.e1 = 0;
     if (tid < 30) h[tid] = 0;
     if (tid == 0) nm = 0;
     __syncthreads();
@@ -205,7 +239,7 @@ __global__ __launch_bounds__(kGreedySmallBlock) void greedy_small_kernel(GreedyA
         int* Tn = T[cur ^ 1];
         bool ch = false;
         for (int i = tid; i < a.m; i += kGreedySmallBlock) {
-            const int d = greedy_decide(a, Tc, i);
+            const int d = i == tid ? greedy_decide_cached(a, Tc, i, cc) : greedy_decide(a, Tc, i);
             if (d >= 0 && (!a.nobs || a.nobs[i] > 0)) atomicMin(&Tn[d], i);
             if (d != a.dec[i]) {
                 a.dec[i] = d;
@@ -217,7 +251,7 @@ __global__ __launch_bounds__(kGreedySmallBlock) void greedy_small_kernel(GreedyA
         ++r;
         if (!changed) break;
         for (int s = tid; s < a.nkp; s += kGreedySmallBlock)
-            T[cur][s] = greedy_preblocked(a, s) ? -1 : INT_MAX;
+            T[cur][s] = pre[s];
         cur ^= 1;
         __syncthreads();
     }

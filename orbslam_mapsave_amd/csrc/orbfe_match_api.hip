@@ -308,7 +308,7 @@ struct orbfe_matcher {
         g.nm = scal.as<int>();
         if (M <= kGreedySmallMax && N <= kGreedySmallSlots && !total) {  // one workgroup
             hipLaunchKernelGGL(greedy_small_kernel, dim3(1), dim3(kGreedySmallBlock),
-                               (size_t)3 * std::max(N, 1) * sizeof(int), stream, g);
+                               (size_t)4 * std::max(N, 1) * sizeof(int), stream, g);
             ORBFE_HIP(hipGetLastError());
             rounds_on_device = true;
             return ORBFE_OK;
