@@ -140,6 +140,7 @@ def run_c5(args) -> None:
     for _ in range(max(args.warmup, 1)):
         step()
     barrier()
+    skew_next[0] = bool(args.skew) and S > 1 and J >= S
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -218,6 +219,14 @@ def main() -> None:
     ap.add_argument("--distinct", type=int, default=32, help="distinct synthetic seeds (cycled)")
     ap.add_argument("--streams", type=int, default=2,
                     help="sub-batches per rank, each on its own HIP stream and extractor handle")
+    ap.add_argument("--chunks", type=int, default=1,
+                    help="extraction calls per stream per step (each a sub-batch / chunks)")
+    ap.add_argument("--skew", type=int, default=0,
+                    help="1: stream k starts k/streams of a step late (its first chunk waits "
+                         "for stream 0's chunk k*chunks/streams - 1), so the streams run "
+                         "different stages at the same time")
+    ap.add_argument("--profile", type=int, default=1,
+                    help="0: no per-kernel HIP events in the timed region (no roofline)")
     ap.add_argument("--cpu-budget", type=float, default=15.0,
                     help="seconds of CPU-baseline work on rank 0 (0 disables)")
     args = ap.parse_args()
@@ -289,21 +298,38 @@ def main() -> None:
         pred = torch.as_tensor(predecessor_index(rank, world, B), device=dev)
         main = torch.cuda.current_stream(dev)
 
-    def extract_chunk(k):
-        f0 = k * C
-        exs[k].extract_batch_device(frames[f0].data_ptr(), C, W, H, W, W * H,
+    J = max(1, min(args.chunks, C))
+    while C % J:
+        J -= 1
+    CJ = C // J  # frames per extraction call
+
+    def extract_chunk(k, j=None):
+        f0, n = (k * C, C) if j is None else (k * C + j * CJ, CJ)
+        exs[k].extract_batch_device(frames[f0].data_ptr(), n, W, H, W, W * H,
                                     d_kps[f0].data_ptr(), cap, d_desc[f0].data_ptr(),
                                     d_n[f0:].data_ptr())
 
+    skew_next = [False]
+
     def step():
         if args.config == "c3":  # sub-batch k: extract + match on stream k, no cross-stream deps
-            for k in range(S):
-                f0 = k * C
-                extract_chunk(k)
-                mt.set_stream(streams[k].cuda_stream)
-                mt.bf_match_batch_device(d_desc[f0].data_ptr(), cap * 32, d_n[f0:].data_ptr(),
-                                         cap, ref_desc.data_ptr(), 0, d_nr[f0:].data_ptr(), C,
-                                         d_out[f0].data_ptr())
+            ev = {}
+            for j in range(J):
+                for k in range(S):
+                    if skew_next[0] and j == 0 and k > 0:
+                        src = max(0, k * J // S - 1)
+                        if src in ev:
+                            streams[k].wait_event(ev[src])
+                    f0 = k * C + j * CJ
+                    extract_chunk(k, j)
+                    mt.set_stream(streams[k].cuda_stream)
+                    mt.bf_match_batch_device(d_desc[f0].data_ptr(), cap * 32,
+                                             d_n[f0:].data_ptr(), cap, ref_desc.data_ptr(), 0,
+                                             d_nr[f0:].data_ptr(), CJ, d_out[f0].data_ptr())
+                    if skew_next[0] and k == 0:
+                        ev[j] = torch.cuda.Event()
+                        ev[j].record(streams[0])
+            skew_next[0] = False
         else:  # extraction on the sub-streams, then exchange + match on the main stream
             for k in range(S):
                 extract_chunk(k)
@@ -329,10 +355,11 @@ def main() -> None:
         step()
     barrier()
     for e in exs:
-        e.profile(True)
+        e.profile(bool(args.profile))
         e.profile_read()
-    mt.profile(True)
+    mt.profile(bool(args.profile))
     mt.profile_read()
+    skew_next[0] = bool(args.skew) and S > 1 and J >= S
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -381,7 +408,8 @@ def main() -> None:
             "data": f"synthetic: seeded textured {W}x{H} u8 frames ({args.distinct} distinct "
                     f"seeds per rank, cycled), resident in HBM",
             "config": {"workload": workload, "frames_per_rank_per_step": B,
-                       "streams_per_rank": S,
+                       "streams_per_rank": S, "chunks_per_stream": J,
+                       "stream_skew": bool(args.skew) and S > 1 and J >= S,
                        "global_batch": B * world, "nfeatures": NF, "reference_kp": len(ref_desc_np),
                        "mean_kp_per_frame": round(nkp, 1),
                        "parallelism": (f"frame-sharded x{world}, no data-path collective"
