@@ -215,7 +215,7 @@ struct orbfe_extractor {
             ta.src = lp[ts - 1];
             ta.sh = g.geo.lv[ts - 1].h;
             ta.nt = L - ts;
-            ta.lp[0] = (g.geo.lv[ts - 1].w + 3) & ~3;
+            ta.lp[0] = (g.geo.lv[ts - 1].w + 15) & ~15;  // 16-byte chunk staging
             ta.buf_b = ta.lp[0] * ta.sh;
             for (int k = 0; k < ta.nt; ++k) {
                 const int l = ts + k;

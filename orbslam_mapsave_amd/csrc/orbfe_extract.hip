@@ -155,20 +155,45 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
     const int ex = min(ox + kRsTW, a.dw) - 1, ey = min(oy + kRsTH, a.dh) - 1;
     const int sy0 = a.yt[3 * oy], sy1 = a.yt[3 * ey + 1];
     const int sx0 = a.xt[3 * ox] & ~3, sx1 = a.xt[3 * ex + 1];
-    const int nrow = sy1 - sy0 + 1, wpr = ((sx1 - sx0) >> 2) + 1, P = a.lds_pitch;
+    const int nrow = sy1 - sy0 + 1, P = a.lds_pitch;  // P % 16 == 0
+    const int cpr = ((sx1 - sx0) >> 4) + 1;                 // 16-byte chunks per source row
     const uint8_t* src = a.src.base + f * a.src.fpitch;
-    for (int i = threadIdx.x; i < nrow * wpr; i += 256) {
-        const int r = i / wpr, c = i - r * wpr;
-        const uint8_t* row = src + (long long)(sy0 + r) * a.src.pitch;
-        const int x = sx0 + 4 * c;
-        uint32_t v;
-        if (x + 4 <= a.sw) {
-            v = *reinterpret_cast<const uint32_t*>(row + x);  // pitch % 4 == 0, x % 4 == 0
-        } else {
-            v = 0;
-            for (int q = 0; q < 4 && x + q < a.sw; ++q) v |= (uint32_t)row[x + q] << (8 * q);
+    // source rows -> LDS in 16-byte chunks (global dwordx4 needs 4-byte alignment: sx0 % 4 ==
+    // 0, pitch % 4 == 0); four chunks per thread in flight before any LDS store.  A chunk
+    // reaching past the row end is assembled from dwords / bytes (level 0 may be the caller's
+    // buffer: nothing past its last row is read).
+    const int total = nrow * cpr;
+    for (int base = 0; base < total; base += 4 * 256) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = base + 256 * u + (int)threadIdx.x;
+            if (i >= total) continue;
+            const int r = i / cpr, c = i - r * cpr;
+            const uint8_t* row = src + (long long)(sy0 + r) * a.src.pitch;
+            const int x = sx0 + 16 * c;
+            if (x + 16 <= a.sw) {
+                v[u] = load16_a4(row + x);
+            } else {
+                uint32_t w[4];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const int xd = x + 4 * d;
+                    w[d] = 0;
+                    if (xd + 4 <= a.sw) w[d] = *reinterpret_cast<const uint32_t*>(row + xd);
+                    else
+                        for (int q = 0; q < 4 && xd + q < a.sw; ++q) w[d] |= (uint32_t)row[xd + q] << (8 * q);
+                }
+                v[u] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
         }
-        *reinterpret_cast<uint32_t*>(rs_lds + r * P + 4 * c) = v;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = base + 256 * u + (int)threadIdx.x;
+            if (i >= total) continue;
+            const int r = i / cpr, c = i - r * cpr;
+            *reinterpret_cast<uint4*>(rs_lds + r * P + 16 * c) = v[u];
+        }
     }
     __syncthreads();
     const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
@@ -223,14 +248,27 @@ __global__ __launch_bounds__(kTailBlock) void resize_tail_kernel(ResizeTailArgs 
     const int f = blockIdx.x;
     const int tid = threadIdx.x;
     uint8_t* buf[2] = {lds, lds + a.buf_b};
-    {   // level ts-1 from the pyramid, dword rows (pitches % 4 == 0)
+    {   // level ts-1 from the pyramid in 16-byte chunks (LDS pitch lp[0] % 16 == 0, inside the
+        // slab's 64-byte row pitch), four per thread in flight before the LDS stores
         const LevelPtr sp = a.src;
         const uint8_t* src = sp.base + f * sp.fpitch;
-        const int wpr = a.lp[0] >> 2;
-        for (int i = tid; i < a.sh * wpr; i += kTailBlock) {
-            const int r = i / wpr, c = i - r * wpr;
-            *reinterpret_cast<uint32_t*>(buf[0] + r * a.lp[0] + 4 * c) =
-                *reinterpret_cast<const uint32_t*>(src + (long long)r * sp.pitch + 4 * c);
+        const int cpr = a.lp[0] >> 4, total = a.sh * cpr;
+        for (int base = 0; base < total; base += 4 * kTailBlock) {
+            uint4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = base + kTailBlock * u + tid;
+                if (i >= total) continue;
+                const int r = i / cpr, c = i - r * cpr;
+                v[u] = *reinterpret_cast<const uint4*>(src + (long long)r * sp.pitch + 16 * c);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = base + kTailBlock * u + tid;
+                if (i >= total) continue;
+                const int r = i / cpr, c = i - r * cpr;
+                *reinterpret_cast<uint4*>(buf[0] + r * a.lp[0] + 16 * c) = v[u];
+            }
         }
     }
     __syncthreads();
@@ -332,25 +370,8 @@ __device__ __forceinline__ int fast_S(const uint8_t* p, int st) {
     return (int)(float)__builtin_elementwise_maximum(q.x, q.y) - 1;
 }
 
-// Necessary condition for a corner at t: a 9-arc always holds two consecutive cardinal points
-// (0/4/8/12), so both must be brighter than v + t or both darker than v - t.  w points at the
-// top-left of the pixel's 7 x 7 window (row stride st).
-__device__ __forceinline__ bool fast_maybe(const uint8_t* w, int st, int t) {
-    const int v = w[3 * st + 3];
-    const int c0 = w[6 * st + 3], c4 = w[3 * st + 6], c8 = w[3], c12 = w[3 * st];
-    const int bright = max(max(min(c0, c4), min(c4, c8)), max(min(c8, c12), min(c12, c0)));
-    const int dark = min(min(max(c0, c4), max(c4, c8)), min(max(c8, c12), max(c12, c0)));
-    return bright > v + t || dark < v - t;
-}
-
-// p / nc for p < 2^13 and nc <= 66 as (p * ceil(2^20 / nc)) >> 20: the error term p / 2^20
-// stays below 1 / nc, so the quotient is exact (no per-pixel integer division).
-struct DivNc {
-    unsigned m;
-    int nc;
-    __device__ __forceinline__ explicit DivNc(int n) : m((1u << 20) / (unsigned)max(n, 1) + 1u), nc(n) {}
-    __device__ __forceinline__ int row(int p) const { return (int)(((unsigned)p * m) >> 20); }
-};
+// Necessary condition for a corner at t (the pre-test): a 9-arc always holds two consecutive
+// cardinal points (0/4/8/12), so both must be brighter than v + t or both darker than v - t.
 
 __device__ __forceinline__ int lane_prefix(unsigned long long mask) {
     return __popcll(mask & ((1ull << (threadIdx.x & 63)) - 1));
@@ -430,13 +451,25 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
     const uint8_t* roi = roi_base + shift;
     const int nr = rows - 6, nc = cols - 6;  // candidates: ROI rows/cols 3 .. n-4
     const int ncand = (nr > 0 && nc > 0) ? nr * nc : 0;
-    const DivNc div(nc);
     // score plane: ROI pitch, rows -1 .. nr of the candidates, zero border
     for (int i = lane; i < (ncand ? ((nr + 2) * P) >> 2 : 0); i += 64) reinterpret_cast<uint32_t*>(S)[i] = 0u;
     const unsigned inv_p = 0xffffffffu / (unsigned)P + 1u;  // r = umulhi(o, inv_p) for o < 2^16
-    const int rpi = nc <= 64 ? 64 / max(nc, 1) : 0;  // candidate rows per 64-lane sweep
-    const int lr = rpi ? lane / max(nc, 1) : 0, lc = lane - lr * nc;
-    const bool lane_on = lr < rpi;
+    // Pre-test lanes: (candidate row lr, 4-pixel group lg).  Group g holds ROI-row bytes
+    // [4g, 4g + 4) of roi_base (dword aligned, P % 16 == 0); candidate columns are
+    // X0 .. X0 + nc - 1 (X0 = shift + 3), so a row spans gpr <= 18 groups (nc <= 66).
+    const int X0 = shift + 3, g0 = X0 >> 2;
+    const int gpr = ncand ? ((X0 + nc - 1) >> 2) - g0 + 1 : 1;
+    const int rps = 64 / gpr;  // candidate rows per sweep
+    const int lr = lane / gpr, lg = lane - lr * gpr;
+    const int gx = 4 * (g0 + lg);  // roi_base column of the group's byte 0
+    uint32_t vmask = 0;            // 0x80 in every byte whose pixel is a candidate column
+    if (lr < rps) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (gx + k >= X0 && gx + k < X0 + nc) vmask |= 0x80u << (8 * k);
+    }
+    const uint32_t* lds32 = reinterpret_cast<const uint32_t*>(roi_base);
+    const int P4 = P >> 2;
     __syncthreads();
     // Pass at iniThFAST: only pixels passing the pre-test at that threshold can have S >= t,
     // and every other pixel counts as 0 in the NMS, so S is computed for those alone.
@@ -444,27 +477,50 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
     int total = 0;
     for (int pass = 0; pass < 2 && total == 0; ++pass) {
         const int t = pass ? a.min_th : a.ini_th;  // rerun at minThFAST when empty (811-815)
+        // Byte-parallel pre-test (4 pixels per lane): with v_lerp_u8,
+        // lerp(c, ~v, R1) = floor((c - v + 255 + (t & 1)) / 2) per byte, and the high bit of
+        // lerp(that, M, 0) with M = 128 - ceil(t / 2) is exactly c - v > t (c > v + t); with
+        // the roles swapped, v - c > t (c < v - t) — checked for every c, v, t in
+        // tests/test_oracle_cpu.py.  A 9-arc holds two consecutive cardinal points, so a
+        // corner needs (b0 | b8) & (b4 | b12) of one polarity.
+        const uint32_t R1 = (t & 1) ? 0x01010101u : 0u;
+        const uint32_t M = (uint32_t)(128 - ((t + 1) >> 1)) * 0x01010101u;
         int cnt = 0;
-        if (rpi) {  // lanes cover rpi whole candidate rows: no per-pixel index arithmetic
-            const uint8_t* w = roi + lr * P + lc;
-            for (int r0 = 0; r0 < nr; r0 += rpi, w += rpi * P) {
-                const bool ok = lane_on && r0 + lr < nr && fast_maybe(w, P, t);
-                const unsigned long long m = __ballot(ok);
-                if (ok) list[cnt + lane_prefix(m)] = (uint16_t)((r0 + lr) * P + lc);  // row-major
-                cnt += __popcll(m);
+        for (int r0 = 0; r0 < nr; r0 += rps) {
+            const int cr = r0 + lr;
+            uint32_t fl = 0;
+            if (vmask && cr < nr) {
+                const int w = (cr + 3) * P4 + (gx >> 2);  // dword of the group's centres
+                const uint32_t cur = lds32[w], prv = lds32[w - 1], nxt = lds32[w + 1];
+                const uint32_t up = lds32[w - 3 * P4], dn = lds32[w + 3 * P4];
+                const uint32_t c4 = __builtin_amdgcn_alignbyte(nxt, cur, 3);   // column + 3
+                const uint32_t c12 = __builtin_amdgcn_alignbyte(cur, prv, 1);  // column - 3
+                const uint32_t ncur = ~cur;
+                auto hb = [&](uint32_t c) {
+                    return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(c, ncur, R1), M, 0u);
+                };
+                auto hd = [&](uint32_t c) {
+                    return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(cur, ~c, R1), M, 0u);
+                };
+                const uint32_t br = (hb(dn) | hb(up)) & (hb(c4) | hb(c12));
+                const uint32_t dk = (hd(dn) | hd(up)) & (hd(c4) | hd(c12));
+                fl = (br | dk) & vmask;
             }
-        } else {
-            for (int base = 0; base < ncand; base += 64) {
-                const int p = base + lane;
-                bool ok = false;
-                if (p < ncand) {
-                    const int r = div.row(p), cc = p - r * nc;
-                    ok = fast_maybe(roi + r * P + cc, P, t);
-                }
-                const unsigned long long m = __ballot(ok);
-                if (ok) list[cnt + lane_prefix(m)] = (uint16_t)(div.row(p) * (P - nc) + p);  // r*P+c
-                cnt += __popcll(m);
+            const unsigned long long b0 = __ballot(fl & 0x80u), b1 = __ballot(fl & 0x8000u),
+                                     b2 = __ballot(fl & 0x800000u), b3 = __ballot(fl & 0x80000000u);
+            if (fl) {  // row-major: earlier lanes, then this lane's lower bytes
+                auto below = [](unsigned long long b, uint32_t acc) {  // popc(b & lanes below)
+                    return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)b, acc));
+                };
+                int pos = (int)below(b3, below(b2, below(b1, below(b0, (uint32_t)cnt))));
+                const int ob = cr * P + gx - X0;  // ROI offset of byte 0's window
+                if (fl & 0x80u) list[pos++] = (uint16_t)ob;
+                if (fl & 0x8000u) list[pos++] = (uint16_t)(ob + 1);
+                if (fl & 0x800000u) list[pos++] = (uint16_t)(ob + 2);
+                if (fl & 0x80000000u) list[pos] = (uint16_t)(ob + 3);
             }
+            cnt += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
         }
         __syncthreads();
 #pragma unroll 2
@@ -1545,8 +1601,9 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
                 }
                 g.rs_tiles_x[l] = (dw + kRsTW - 1) / kRsTW;
                 g.rs_tiles[l] = g.rs_tiles_x[l] * ((dh + kRsTH - 1) / kRsTH);
-                g.rs_pitch[l] = 4 * need_w;
-                g.rs_lds[l] = (size_t)need_rows * 4 * need_w;
+                // 16-byte chunks: the widest tile's dwords rounded up to whole chunks
+                g.rs_pitch[l] = 16 * ((need_w + 3) / 4);
+                g.rs_lds[l] = (size_t)need_rows * g.rs_pitch[l];
                 if (g.rs_lds[l] > 64 * 1024) return ORBFE_ERR_UNSUPPORTED;  // scale factors > ~3
             }
             g.yoff[l] = (int)g.ytab.size();
@@ -1565,7 +1622,7 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
     {   // K1b: the longest run of top levels ts..L-1 (ts >= 2) whose two largest LDS images,
         // levels ts-1 and ts (rows padded to dwords), fit the tail kernel's LDS
         const int L = g.geo.nlevels;
-        auto bytes = [&](int l) { return (size_t)g.geo.lv[l].h * (((size_t)g.geo.lv[l].w + 3) & ~(size_t)3); };
+        auto bytes = [&](int l) { return (size_t)g.geo.lv[l].h * (((size_t)g.geo.lv[l].w + 15) & ~(size_t)15); };
         g.tail_start = L;
         for (int ts = L - 1; ts >= 2; --ts) {
             if (bytes(ts - 1) + bytes(ts) > (size_t)kTailLds) break;

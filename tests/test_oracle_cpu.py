@@ -381,3 +381,18 @@ def test_golden_matchers():
     fr = oracle.is_in_frustum(**S.frustum_case(0))
     assert np.array_equal(fr[0], g["fr_in"])
     assert np.array_equal(np.where(fr[0] == 1, fr[4], -99), g["fr_lvl"])
+
+
+def test_fast_pretest_lerp_identity():
+    """fast_kernel's byte-parallel pre-test: with v_lerp_u8 semantics per byte,
+    lerp(a, b, r) = (a + b + (r & 1)) >> 1, the high bit of lerp(lerp(c, ~v, t & 1), M, 0) with
+    M = 128 - ceil(t / 2) equals c > v + t, and lerp(lerp(v, ~c, t & 1), M, 0) equals c < v - t,
+    for every byte c, v and threshold t."""
+    c = np.arange(256)[:, None]
+    v = np.arange(256)[None, :]
+    for t in range(256):
+        r, M = t & 1, 128 - ((t + 1) >> 1)
+        bright = ((((c + (255 - v) + r) >> 1) + M) >> 1) >= 128
+        dark = ((((v + (255 - c) + r) >> 1) + M) >> 1) >= 128
+        assert np.array_equal(bright, c > v + t), t
+        assert np.array_equal(dark, c < v - t), t
