@@ -548,7 +548,7 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
 // Keys stay in original order (cell-row-major, FAST emission order); each live key carries the
 // list position of its node.  Single-key nodes remember their key and drop out of the key set.
 // Final: per node the max response, first (lowest original index) on ties (741-759).
-constexpr int kOctBlock = 512;
+constexpr int kOctBlock = kOctBlockSize;
 constexpr int OCT_UNROLL = 4;
 
 struct OctLds {  // carve of the dynamic LDS region (sizes in elements)

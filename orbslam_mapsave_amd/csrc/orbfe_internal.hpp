@@ -179,7 +179,10 @@ __global__ void describe_kernel(DescArgs);
 extern __constant__ int c_umax[16];
 
 constexpr int kFastBlockSize = 64;
-constexpr int kOctBlockSize = 512;
+#ifndef ORBFE_OCT_BLOCK
+#define ORBFE_OCT_BLOCK 256  // 128: 248K, 256: 254K, 512: 243K, 1024: 220K frames/s (c3)
+#endif
+constexpr int kOctBlockSize = ORBFE_OCT_BLOCK;
 constexpr int kDescBlockSize = 256;
 constexpr int kDescGroupSize = 8;  // oct-tree output slots per describe wave
 constexpr int kBlurTileW = 128, kBlurTileH = 32;

@@ -21,7 +21,8 @@ from .abi import (KEYPOINT_DTYPE, ORBFE_ERR_CAPACITY, ORBFE_OK, Camera, Frame, F
                   MapPoints, OrbfeError, Params, ptr)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "liborbfe.so")
+# ORBFE_LIB selects another build of the same library (A/B runs of build variants)
+LIB_PATH = os.environ.get("ORBFE_LIB") or os.path.join(_HERE, "lib", "liborbfe.so")
 _lib: C.CDLL | None = None
 
 # every symbol include/orbfe.h declares (checked by tests/test_abi.py)
