@@ -183,8 +183,14 @@ constexpr int kFastBlockSize = 64;
 #define ORBFE_OCT_BLOCK 256  // 128: 248K, 256: 254K, 512: 243K, 1024: 220K frames/s (c3)
 #endif
 constexpr int kOctBlockSize = ORBFE_OCT_BLOCK;
-constexpr int kDescBlockSize = 256;
-constexpr int kDescGroupSize = 8;  // oct-tree output slots per describe wave
+#ifndef ORBFE_DESC_BLOCK
+#define ORBFE_DESC_BLOCK 256
+#endif
+#ifndef ORBFE_DESC_GROUP
+#define ORBFE_DESC_GROUP 8
+#endif
+constexpr int kDescBlockSize = ORBFE_DESC_BLOCK;
+constexpr int kDescGroupSize = ORBFE_DESC_GROUP;  // oct-tree output slots per describe wave
 constexpr int kBlurTileW = 128, kBlurTileH = 32;
 
 }  // namespace orbfe
