@@ -224,7 +224,11 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
         for (int k = 0; k < 4; ++k) {
             const int t0 = s0[x0[k]] * a0[k] + s0[x1[k]] * a1[k];
             const int t1 = s1[x0[k]] * a0[k] + s1[x1[k]] * a1[k];
-            const int v = min(max((t0 * b0 + t1 * b1 + (1 << 21)) >> 22, 0), 255);
+            // FixedPtCast<int, uchar, 22>: the sum is never negative (pixels and coefficients
+            // are), so only the upper clamp remains, on the unsigned value.  The signed form
+            // min(max(x >> 22, 0), 255) can be matched to gfx950's v_ashr_pk_u8_i32 for two of
+            // the four bytes, and that packing was seen to corrupt the upper two bytes.
+            const uint32_t v = min(((uint32_t)(t0 * b0 + t1 * b1) + (1u << 21)) >> 22, 255u);
             packed |= (uint32_t)v << (8 * k);
         }
         uint8_t* d = dst + (long long)y * a.dst.pitch + x;
@@ -307,7 +311,7 @@ __global__ __launch_bounds__(kTailBlock) void resize_tail_kernel(ResizeTailArgs 
                 for (int q = 0; q < 4; ++q) {
                     const int t0 = s0[x0[q]] * a0[q] + s0[x1[q]] * a1[q];
                     const int t1 = s1[x0[q]] * a0[q] + s1[x1[q]] * a1[q];
-                    const int v = min(max((t0 * b0 + t1 * b1 + (1 << 21)) >> 22, 0), 255);
+                    const uint32_t v = min(((uint32_t)(t0 * b0 + t1 * b1) + (1u << 21)) >> 22, 255u);  // as in resize_kernel
                     packed |= (uint32_t)v << (8 * q);
                 }
                 *reinterpret_cast<uint32_t*>(d + y * dp_l + x) = packed;  // LDS pitch % 4 == 0

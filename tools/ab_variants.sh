@@ -1,3 +1,5 @@
+# A/B of library build variants: bash tools/ab_variants.sh NAME... runs the extractor parity
+# tests and the c3 (1 and 2 streams) / c4 benches with ORBFE_LIB=orbslam_mapsave_amd/lib/liborbfe_NAME.so
 mkdir -p gpurun_out/ab
 set -o pipefail
 for v in "$@"; do
