@@ -34,8 +34,15 @@ for f in ("bench.json", "trace_bench.json"):
 FRAMES = int(os.environ.get("BENCH_SUBBATCH", "128"))
 trace_rows = list(csv.DictReader(open(os.path.join(SRC, "trace", "run_kernel_trace.csv"))))
 shapes = collections.defaultdict(set)
+
+
+def bench_shape(r):  # frames on grid y, or on grid x (oct-tree, resize tail: a block per frame)
+    return (int(r["Grid_Size_Y"]) == FRAMES or
+            int(r["Grid_Size_X"]) == FRAMES * int(r["Workgroup_Size_X"]))
+
+
 for r in trace_rows:
-    if int(r["Grid_Size_Y"]) == FRAMES:
+    if bench_shape(r):
         shapes[short(r["Kernel_Name"])].add(
             int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"]))
 
@@ -84,7 +91,7 @@ for n, v in summary.items():
 dur = collections.defaultdict(list)
 for r in trace_rows:
     n = short(r["Kernel_Name"])
-    if int(r["Grid_Size_Y"]) == FRAMES and n.endswith("kernel"):
+    if bench_shape(r) and n.endswith("kernel"):
         dur[n].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 launch = {n: {"launches": len(v), "grids": sorted(shapes[n]), "avg_ms": round(sum(v) / len(v) / 1e6, 5)}
           for n, v in dur.items()}
