@@ -165,18 +165,23 @@ class ORBextractor:
     def __call__(self, image: np.ndarray, mask: np.ndarray | None = None):
         """Returns (keypoints[KEYPOINT_DTYPE], descriptors uint8 (n, 32)); an empty image
         returns (None, None) like the reference, which leaves its outputs untouched."""
-        image = np.ascontiguousarray(image, np.uint8)
+        image = np.asarray(image)
         if image.size == 0:
             return None, None
+        # a row-strided u8 view (a cv::Mat ROI: step > cols) is passed as is, with its stride
+        if not (image.dtype == np.uint8 and image.ndim == 2 and image.strides[1] == 1 and
+                image.strides[0] >= image.shape[1]):
+            image = np.ascontiguousarray(image, np.uint8)
         h, w = image.shape
+        stride = image.strides[0]
         m = None if mask is None or np.size(mask) == 0 else np.ascontiguousarray(mask, np.uint8)
         cap = self.capacity()
         kps = np.zeros(cap, KEYPOINT_DTYPE)
         desc = np.zeros((cap, 32), np.uint8)
         n = C.c_int(0)
         _check("orbfe_extract", lib().orbfe_extract(
-            self._h, ptr(image), w, h, C.c_size_t(w), ptr(m), C.c_size_t(w), ptr(kps), cap,
-            ptr(desc), C.byref(n)))
+            self._h, C.c_void_p(image.ctypes.data), w, h, C.c_size_t(stride), ptr(m),
+            C.c_size_t(w), ptr(kps), cap, ptr(desc), C.byref(n)))
         return kps[:n.value].copy(), desc[:n.value].copy()
 
     def extract_color(self, image: np.ndarray, pix: int, mask: np.ndarray | None = None,
