@@ -1563,9 +1563,9 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
             lv.nini = 0;
             lv.hx = 1.f;
         }
-        // list bound: phase 1 <= max(N, 4 nIni), phase 2 <= N + 2 (DESIGN.md "oct-tree")
-        if (lv.nini > 4) return ORBFE_ERR_UNSUPPORTED;
-        lv.ncap = std::max(lv.nfeat + 4, 20);
+        // list bound: the first pass <= 4 nIni, later phase-1 passes <= N, phase 2 <= N + 2
+        // (DESIGN.md "oct-tree"); the initial nodes index arrays of the same capacity
+        lv.ncap = std::max({lv.nfeat + 4, 4 * lv.nini, 20});
         lv.out_off = out;
         out += lv.ncap;
         ncap_max = std::max(ncap_max, lv.ncap);

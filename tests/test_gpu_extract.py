@@ -104,10 +104,11 @@ def test_other_configs(cfg):
     e.close()
 
 
-@pytest.mark.parametrize("w,h", [(641, 479), (333, 257), (200, 170), (1024, 1024), (1600, 480)])
+@pytest.mark.parametrize("w,h", [(641, 479), (333, 257), (200, 170), (1024, 1024), (1600, 480),
+                                 (2048, 512), (3000, 300)])
 def test_odd_sizes(w, h):
     """Ragged sizes (odd widths / heights, levels whose rows are not multiples of 4, square and
-    wide frames: nIni = round(w / h) from 1 to 4, ORBextractor.cc:542), against the oracle."""
+    wide frames: nIni = round(w / h) from 1 to 20, ORBextractor.cc:542), against the oracle."""
     from orbslam_mapsave_amd.native import ORBextractor
     e = ORBextractor(1000, 1.2, 8, 20, 7, device=0, max_width=w, max_height=h)
     pp = oracle.params(1000, 1.2, 8, 20, 7)
@@ -131,12 +132,12 @@ def test_strided_roi(ex, p):
 
 
 def test_unsupported_inputs_are_refused():
-    """Frames above 4096 px, and frames where a level's round(w / h) exceeds 4 (the oct-tree's
-    list capacity bound), fail loudly with ORBFE_ERR_UNSUPPORTED, never silently."""
+    """Frames above 4096 px (the workspace plan) fail loudly with
+    ORBFE_ERR_UNSUPPORTED, never silently."""
     from orbslam_mapsave_amd.abi import ORBFE_ERR_UNSUPPORTED, OrbfeError
     from orbslam_mapsave_amd.native import ORBextractor
     e = ORBextractor(1000, 1.2, 8, 20, 7, device=0)
-    for shape in ((200, 4100), (512, 2048)):
+    for shape in ((200, 4100), (4100, 300)):
         with pytest.raises(OrbfeError) as ei:
             e(np.zeros(shape, np.uint8))
         assert ei.value.status == ORBFE_ERR_UNSUPPORTED
