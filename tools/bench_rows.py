@@ -99,6 +99,21 @@ def row_color():
     ex.close()
 
 
+def row_single():
+    """Tracking's per-frame call: ORBextractor::operator() on one 640x480 frame through the host
+    ABI (upload, the whole pipeline, download of keypoints and descriptors), as Frame::ExtractORB
+    issues it (Frame.cc:358-364) — the latency a drop-in replacement adds per tracked frame."""
+    img = synthetic_frame(3, 640, 480)
+    ex = native.ORBextractor(1000, 1.2, 8, 20, 7, device=0, max_width=640, max_height=480)
+    t = timed(lambda: ex(img), 200)
+    p = oracle.params(1000, 1.2, 8, 20, 7)
+    tc = cpu_timed(lambda: oracle.extract(p, img))
+    emit("single-frame ORBextractor::operator() latency (640x480, 1000 kp, host ABI)",
+         "frames/s", 1, t, tc, 640 * 480 + 1000 * 60,
+         "host ABI: one frame per call, H2D upload + pipeline + D2H, synchronous", cpu_units=1)
+    ex.close()
+
+
 def row_stereo():
     B, W, H = 128, 640, 480
     pairs = [synthetic_stereo_pair(s % 16, W, H) for s in range(B)]
@@ -342,7 +357,7 @@ def row_bow(tmpdir):
 if __name__ == "__main__":
     import tempfile
     with tempfile.TemporaryDirectory() as td:
-        rows = {"color": row_color, "stereo": row_stereo, "reloc": row_reloc, "track": row_track,
+        rows = {"single": row_single, "color": row_color, "stereo": row_stereo, "reloc": row_reloc, "track": row_track,
                 "distinctive": row_distinctive, "bow": lambda: row_bow(td)}
         for name in (sys.argv[1:] or list(rows)):
             rows[name]()
