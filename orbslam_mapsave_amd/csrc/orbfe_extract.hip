@@ -247,6 +247,7 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
 // the tail fit the workgroup's LDS (levels 5-7 at 640 x 480).
 constexpr int kTailBlock = 1024;
 constexpr int kTailLds = 144 * 1024;
+constexpr int kTailRows = 512;  // rows of a tail level whose y table is staged in LDS
 __global__ __launch_bounds__(kTailBlock) void resize_tail_kernel(ResizeTailArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kTailLds];
     const int f = blockIdx.x;
@@ -276,13 +277,18 @@ __global__ __launch_bounds__(kTailBlock) void resize_tail_kernel(ResizeTailArgs 
         }
     }
     __syncthreads();
+    // the row tables of the level being made, staged in LDS: the row loop below would
+    // otherwise wait on three dependent global loads per iteration
+    __shared__ int yts[3 * kTailRows];
     for (int k = 0; k < a.nt; ++k) {
         const uint8_t* s = buf[k & 1];
         uint8_t* d = buf[(k + 1) & 1];
         const int sp_l = a.lp[k], dp_l = a.lp[k + 1];
         const int dw = a.dw[k], dh = a.dh[k];
         const int* xt = a.xt[k];
-        const int* yt = a.yt[k];
+        const int* yt = yts;
+        for (int i = tid; i < 3 * dh; i += kTailBlock) yts[i] = a.yt[k][i];
+        __syncthreads();
         const int gpr = (dw + 3) >> 2;           // 4-pixel groups per row
         const int rps = kTailBlock / gpr;        // rows per sweep
         const int gx = tid % gpr, ry = tid / gpr;
@@ -1629,7 +1635,7 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
         auto bytes = [&](int l) { return (size_t)g.geo.lv[l].h * (((size_t)g.geo.lv[l].w + 15) & ~(size_t)15); };
         g.tail_start = L;
         for (int ts = L - 1; ts >= 2; --ts) {
-            if (bytes(ts - 1) + bytes(ts) > (size_t)kTailLds) break;
+            if (bytes(ts - 1) + bytes(ts) > (size_t)kTailLds || g.geo.lv[ts].h > kTailRows) break;
             g.tail_start = ts;
         }
         if (L - g.tail_start < 2) g.tail_start = L;  // a single level gains nothing
