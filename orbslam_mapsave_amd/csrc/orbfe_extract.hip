@@ -578,6 +578,7 @@ struct OctLds {  // carve of the dynamic LDS region (sizes in elements)
     int* aux2;
     unsigned long long* s64;  // sort keys (phase 2) / best response (final)
     int* tmp;
+    int* cellv;     // 2 x block: a chunk of cells' key offsets and slots (compaction)
     int* scal;      // scalars
 };
 
@@ -657,6 +658,7 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
         s.aux = p; p += NC;
         s.aux2 = p; p += NC;
         s.tmp = p; p += 64;
+        s.cellv = p; p += 2 * kOctBlock;
         s.scal = p;
     }
     uint32_t* out = a.oct_out + f * a.geo.out_total + L.out_off;
@@ -672,13 +674,25 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
         const int n = c < L.cell_end ? a.cell_cnt[f * a.ncells + c] : 0;
         int chunk_total;
         const int off = block_exclusive_scan<kOctBlock>(n, s.tmp, chunk_total);
-        if (n) {
-            const uint32_t* src = a.cell_keys + f * a.cell_cap_total + a.cells[c].slot;
-            for (int i = 0; i < n; ++i) K[nkeys + off + i] = src[i];
+        // cooperative copy: thread e takes key e of the chunk, found by a binary search over
+        // the cells' offsets (the last cell starting at or before e: empty cells before it
+        // share its offset), so no thread walks a cell's keys one dependent load at a time
+        s.cellv[tid] = off;
+        s.cellv[kOctBlock + tid] = c < L.cell_end ? a.cells[c].slot : 0;
+        __syncthreads();
+        const int ncell = min(kOctBlock, L.cell_end - base);
+        const uint32_t* src = a.cell_keys + f * a.cell_cap_total;
+        for (int e = tid; e < chunk_total; e += kOctBlock) {
+            int lo = 0, hi = ncell - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (s.cellv[mid] <= e) lo = mid; else hi = mid - 1;
+            }
+            K[nkeys + e] = src[s.cellv[kOctBlock + lo] + (e - s.cellv[lo])];
         }
         nkeys += chunk_total;
+        __syncthreads();  // cellv is rewritten by the next chunk
     }
-    __syncthreads();
     if (nkeys == 0 || L.nini < 1) {
         if (tid == 0) *out_cnt = 0;
         return;
@@ -1660,7 +1674,8 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
     int sort_cap = 1;
     while (sort_cap < ncap_max) sort_cap <<= 1;
     g.sort_cap = sort_cap;
-    g.oct_lds = (size_t)2 * sort_cap * 4 + (size_t)ncap_max * 4 * (10 + 8 + 2) + 64 * 4 + 64;
+    g.oct_lds = (size_t)2 * sort_cap * 4 + (size_t)ncap_max * 4 * (10 + 8 + 2) + 64 * 4 +
+                (size_t)2 * kOctBlockSize * 4 + 64;
     return ORBFE_OK;
 }
 
