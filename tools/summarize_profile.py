@@ -3,8 +3,9 @@
 profiles/<round>/ and profiles/traffic_c3.json (read by bench.py for roofline.traffic).
 
 Traffic per launch = 2 x FETCH_SIZE + WRITE_SIZE (KB -> bytes): on gfx950 FETCH_SIZE counts half
-of the bytes of a coalesced streaming read (MI355X_MICROARCH.md §HBM); our kernels read dwords
-per lane, a width the guide lists as uncalibrated, so the doubled figure is an estimate."""
+of the bytes of a coalesced streaming read (MI355X_MICROARCH.md §HBM).  The guide calibrates 16-B
+reads only; tools/probe/fetch_cal.hip measures the same 0.5 for 4-B-per-lane reads and 1.0 for
+WRITE_SIZE at 4 and 16 B per lane (profiles/r01/fetch_calibration.json)."""
 import csv
 import collections
 import json
