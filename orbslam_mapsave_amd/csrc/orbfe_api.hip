@@ -5,6 +5,7 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -140,6 +141,102 @@ struct orbfe_extractor {
     std::vector<uint8_t> h_desc;
     std::vector<int32_t> h_n;
 
+    // Single-frame host path (Frame::ExtractORB's per-frame call): pinned staging and the whole
+    // H2D copy + pipeline + D2H sequence captured once into a HIP graph per frame size and
+    // replayed, so a call costs one graph launch instead of ~15 kernel launches and pageable
+    // copies.  Rebuilt when the plan or any buffer it captured changes.
+    struct Pinned {
+        uint8_t* p = nullptr;
+        size_t bytes = 0;
+        int ensure(size_t n) {
+            if (n <= bytes) return ORBFE_OK;
+            if (p) hipHostFree(p);
+            p = nullptr;
+            bytes = 0;
+            if (hipHostMalloc(reinterpret_cast<void**>(&p), n, hipHostMallocDefault) != hipSuccess)
+                return ORBFE_ERR_NOMEM;
+            bytes = n;
+            return ORBFE_OK;
+        }
+        void release() {
+            if (p) hipHostFree(p);
+            p = nullptr;
+            bytes = 0;
+        }
+    };
+    Pinned pin_in, pin_kps, pin_desc, pin_n;
+    hipGraphExec_t g1 = nullptr;
+    const void* g1_key[8] = {};  // the buffers and plan the graph was captured with
+    bool graph_broken = std::getenv("ORBFE_NO_GRAPH") != nullptr;  // capture failed once (or
+                                 // disabled for A/B runs): keep to the launch path
+
+    void drop_graph() {
+        if (g1) hipGraphExecDestroy(g1);
+        g1 = nullptr;
+    }
+
+    // ORBFE_OK with *done = true when the graph path ran; *done = false to take the plain path.
+    int run_single_graph(const uint8_t* img, int w, int h, size_t stride, bool* done) {
+        *done = false;
+        if (graph_broken || prof.on) return ORBFE_OK;
+        int st;
+        if ((st = set_plan(w, h))) return st;
+        if ((st = ensure_frames(1))) return st;
+        const int cap = kp_capacity();
+        if ((st = out_kps.ensure((size_t)cap * sizeof(orbfe_keypoint)))) return st;
+        if ((st = out_desc.ensure((size_t)cap * 32))) return st;
+        if ((st = out_n.ensure(sizeof(int32_t)))) return st;
+        if ((st = pin_in.ensure((size_t)w * h))) return st;
+        if ((st = pin_kps.ensure((size_t)cap * sizeof(orbfe_keypoint)))) return st;
+        if ((st = pin_desc.ensure((size_t)cap * 32))) return st;
+        if ((st = pin_n.ensure(sizeof(int32_t)))) return st;
+        const void* key[8] = {pyr.p, out_kps.p, out_desc.p, out_n.p, pin_in.p, pin_kps.p,
+                              reinterpret_cast<const void*>((uintptr_t)w << 32 | (uint32_t)h),
+                              reinterpret_cast<const void*>((uintptr_t)frames_cap)};
+        if (g1 && std::memcmp(key, g1_key, sizeof(key)) != 0) drop_graph();
+        const Plan& g = plan;
+        const LevelGeo& l0 = g.geo.lv[0];
+        if (!g1) {
+            hipGraph_t graph = nullptr;
+            if (hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+                graph_broken = true;
+                return ORBFE_OK;
+            }
+            bool ok = hipMemcpy2DAsync(pyr.as<uint8_t>() + l0.off, l0.pitch, pin_in.p, w, w, h,
+                                       hipMemcpyHostToDevice, stream) == hipSuccess;
+            LevelPtr lp0{pyr.as<uint8_t>() + l0.off, g.slab, l0.pitch};
+            ok = ok && run(1, lp0, out_kps.as<orbfe_keypoint>(), cap, out_desc.as<uint8_t>(),
+                           out_n.as<int32_t>()) == ORBFE_OK;
+            ok = ok && hipMemcpyAsync(pin_n.p, out_n.p, sizeof(int32_t), hipMemcpyDeviceToHost,
+                                      stream) == hipSuccess;
+            ok = ok && hipMemcpyAsync(pin_kps.p, out_kps.p, (size_t)cap * sizeof(orbfe_keypoint),
+                                      hipMemcpyDeviceToHost, stream) == hipSuccess;
+            ok = ok && hipMemcpyAsync(pin_desc.p, out_desc.p, (size_t)cap * 32,
+                                      hipMemcpyDeviceToHost, stream) == hipSuccess;
+            const bool ended = hipStreamEndCapture(stream, &graph) == hipSuccess;
+            ok = ok && ended && graph &&
+                 hipGraphInstantiate(&g1, graph, nullptr, nullptr, 0) == hipSuccess;
+            if (graph) hipGraphDestroy(graph);
+            (void)hipGetLastError();
+            if (!ok) {
+                g1 = nullptr;
+                graph_broken = true;
+                return ORBFE_OK;
+            }
+            std::memcpy(g1_key, key, sizeof(key));
+        }
+        if (stride == (size_t)w) {
+            std::memcpy(pin_in.p, img, (size_t)w * h);
+        } else {
+            for (int r = 0; r < h; ++r) std::memcpy(pin_in.p + (size_t)r * w, img + r * stride, w);
+        }
+        ORBFE_HIP(hipGraphLaunch(g1, stream));
+        ORBFE_HIP(hipStreamSynchronize(stream));
+        last_n = 1;
+        *done = true;
+        return ORBFE_OK;
+    }
+
     int set_plan(int w, int h) {
         if (planned && plan.w == w && plan.h == h) return ORBFE_OK;
         Plan g;
@@ -194,7 +291,8 @@ struct orbfe_extractor {
         lp[0] = l0;
         // K1 cascaded pyramid: one launch per level, 128 x 32 tiles of every frame; the small
         // top levels (tail_start ..) in one K1b launch, a workgroup per frame
-        const int ts = std::min(g.tail_start, L);
+        // (a batch of a few frames would leave most CUs idle in the tail: per-level launches)
+        const int ts = n >= kTailMinFrames ? std::min(g.tail_start, L) : L;
         for (int l = 1; l < ts; ++l) {
             ResizeArgs ra;
             ra.src = lp[l - 1];
@@ -281,9 +379,19 @@ struct orbfe_extractor {
         da.kps = d_kps;
         da.desc = d_desc;
         da.n_out = d_n;
-        const int per_block = (kDescBlockSize / 64) * kDescGroupSize;  // slots per workgroup
-        ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, describe_kernel, dim3((g.geo.out_total + per_block - 1) / per_block, n),
-                           dim3(kDescBlockSize), 0, stream, da);
+        // a wave takes kDescGroupSize keypoints (the trig and pattern loads amortised over the
+        // group); small batches take kDescGroupSmall, for four times the waves in flight
+        if (n >= kDescSmallBatch) {
+            const int per_block = (kDescBlockSize / 64) * kDescGroupSize;  // slots per workgroup
+            ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, describe_kernel<kDescGroupSize>,
+                         dim3((g.geo.out_total + per_block - 1) / per_block, n),
+                         dim3(kDescBlockSize), 0, stream, da);
+        } else {
+            const int per_block = (kDescBlockSize / 64) * kDescGroupSmall;
+            ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, describe_kernel<kDescGroupSmall>,
+                         dim3((g.geo.out_total + per_block - 1) / per_block, n),
+                         dim3(kDescBlockSize), 0, stream, da);
+        }
         ORBFE_HIP(hipGetLastError());
         last_n = n;
         for (int l = 0; l < L; ++l) last_pyr[l] = lp[l];
@@ -398,6 +506,8 @@ struct orbfe_extractor {
                           &oct_out, &oct_cnt, &out_kps, &out_desc, &out_n, &stage, &rects, &st_off, &st_items,
                           &st_sad, &st_status, &st_kl, &st_dl, &st_kr, &st_dr, &st_n, &st_ur, &st_dp})
             b->release();
+        drop_graph();
+        for (Pinned* q : {&pin_in, &pin_kps, &pin_desc, &pin_n}) q->release();
         prof.release();
         if (own) hipStreamDestroy(own);
     }
@@ -495,6 +605,19 @@ static int extract_host_common(orbfe_extractor* h, const uint8_t* const* imgs, i
                                size_t mask_stride, const orbfe_rect* rects, orbfe_keypoint* kps,
                                int kps_cap, uint8_t* desc, int32_t* n_out) {
     DeviceGuard dg(h->device);
+    if (n == 1 && pix == ORBFE_PIX_GRAY && !(masks && masks[0]) && !rects) {
+        bool done = false;
+        int st = h->run_single_graph(imgs[0], w, hgt, stride, &done);
+        if (st != ORBFE_OK) return st;
+        if (done) {
+            const int cnt = *reinterpret_cast<const int32_t*>(h->pin_n.p);
+            n_out[0] = cnt;
+            if (cnt > kps_cap) return ORBFE_ERR_CAPACITY;
+            std::memcpy(kps, h->pin_kps.p, (size_t)cnt * sizeof(orbfe_keypoint));
+            if (desc) std::memcpy(desc, h->pin_desc.p, (size_t)cnt * 32);
+            return ORBFE_OK;
+        }
+    }
     int st = h->run_host(imgs, n, w, hgt, stride, pix, masks, mask_stride, rects);
     if (st != ORBFE_OK) return st;
     const int cap = h->kp_capacity();

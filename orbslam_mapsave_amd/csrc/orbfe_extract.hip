@@ -1174,12 +1174,13 @@ __global__ __launch_bounds__(256) void blur_kernel(BlurArgs a) {
 //   3. per keypoint, lane k evaluates the rotated pattern pairs k + 64 r (pattern held in
 //      registers across the group) and 4 ballots make the 256-bit descriptor.
 constexpr int kDescBlock = kDescBlockSize;
-constexpr int kDescGroup = kDescGroupSize;
+constexpr int kDescGroupSmall = 2;  // small batches (single-frame latency): 4x the waves
 constexpr int kDescWinR = 18;                        // rotated pattern radius bound (< 18.5)
 constexpr int kDescWinRows = 2 * kDescWinR + 1;      // 37
 constexpr int kDescWinP = 48;                        // bytes per window row (3 x 16)
 constexpr int kDescWinBytes = kDescWinRows * kDescWinP;
 typedef float float2v __attribute__((ext_vector_type(2)));
+template <int kDescGroup>
 __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
     int bx, f;
     xcd_block(bx, f);

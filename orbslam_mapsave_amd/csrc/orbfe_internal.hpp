@@ -175,7 +175,7 @@ __global__ void resize_tail_kernel(ResizeTailArgs);
 __global__ void fast_kernel(FastArgs);
 __global__ void octree_kernel(OctArgs);
 __global__ void blur_kernel(BlurArgs);
-__global__ void describe_kernel(DescArgs);
+template <int kDescGroup> __global__ void describe_kernel(DescArgs);
 extern __constant__ int c_umax[16];
 
 constexpr int kFastBlockSize = 64;
@@ -190,6 +190,8 @@ constexpr int kOctBlockSize = ORBFE_OCT_BLOCK;
 #define ORBFE_DESC_GROUP 8
 #endif
 constexpr int kDescBlockSize = ORBFE_DESC_BLOCK;
+constexpr int kDescSmallBatch = 8;  // batches below this use kDescGroupSmall keypoints per wave
+constexpr int kTailMinFrames = 8;   // batches below this skip the one-workgroup-per-frame tail
 constexpr int kDescGroupSize = ORBFE_DESC_GROUP;  // oct-tree output slots per describe wave
 constexpr int kBlurTileW = 128, kBlurTileH = 32;
 
