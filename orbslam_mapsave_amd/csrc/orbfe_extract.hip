@@ -879,20 +879,37 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
         const int m = flag_sh[0];
         int P = 1;
         while (P < m) P <<= 1;
-        for (int i = m + tid; i < P; i += kOctBlock) s.s64[i] = 0ull;
-        __syncthreads();
-        for (int k = 2; k <= P; k <<= 1)  // bitonic sort, descending
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int i = tid; i < P; i += kOctBlock) {
-                    const int ij = i ^ j;
-                    if (ij > i) {
-                        const unsigned long long x = s.s64[i], y = s.s64[ij];
-                        const bool desc = (i & k) == 0;
-                        if (desc ? (x < y) : (x > y)) { s.s64[i] = y; s.s64[ij] = x; }
+        if (P <= 64) {  // one wave sorts in registers: no barrier per step
+            if (tid < 64) {
+                unsigned long long v = tid < m ? s.s64[tid] : 0ull;
+                for (int k = 2; k <= P; k <<= 1)  // bitonic sort, descending
+                    for (int j = k >> 1; j > 0; j >>= 1) {
+                        const unsigned lo = __shfl_xor((unsigned)v, j, 64);
+                        const unsigned hi = __shfl_xor((unsigned)(v >> 32), j, 64);
+                        const unsigned long long y = ((unsigned long long)hi << 32) | lo;
+                        // the lower index of a pair keeps the larger key on descending runs
+                        const bool keep_max = ((tid & j) == 0) == ((tid & k) == 0);
+                        v = keep_max ? (v > y ? v : y) : (v < y ? v : y);
                     }
-                }
-                __syncthreads();
+                if (tid < P) s.s64[tid] = v;
             }
+            __syncthreads();
+        } else {
+            for (int i = m + tid; i < P; i += kOctBlock) s.s64[i] = 0ull;
+            __syncthreads();
+            for (int k = 2; k <= P; k <<= 1)  // bitonic sort, descending
+                for (int j = k >> 1; j > 0; j >>= 1) {
+                    for (int i = tid; i < P; i += kOctBlock) {
+                        const int ij = i ^ j;
+                        if (ij > i) {
+                            const unsigned long long x = s.s64[i], y = s.s64[ij];
+                            const bool desc = (i & k) == 0;
+                            if (desc ? (x < y) : (x > y)) { s.s64[i] = y; s.s64[ij] = x; }
+                        }
+                    }
+                    __syncthreads();
+                }
+        }
         {
             const int *bx = s.box(cur), *by = s.boy(cur);
             int *qc = s.qc, *qk = s.qk;
