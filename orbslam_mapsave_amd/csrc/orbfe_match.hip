@@ -337,6 +337,78 @@ __global__ __launch_bounds__(kGridBlock) void grid_kernel(const orbfe_keypoint* 
     }
 }
 
+constexpr int kGridPer = 8;                           // keypoints per thread held in registers
+constexpr int kGridLdsMax = kGridBlock * kGridPer;    // 8192: the items list fits LDS (32 KB)
+// grid_kernel for n <= kGridLdsMax: the cell of every keypoint stays in registers and the items
+// list is filled, ordered and only then copied out of LDS, so no step waits on a chain of
+// dependent global loads (grid_kernel's insertion sort walks global memory).
+__global__ __launch_bounds__(kGridBlock) void grid_lds_kernel(const orbfe_keypoint* k, int n,
+                                                              float minx, float miny, float gwi,
+                                                              float ghi, int* cstart,
+                                                              int* citems) {
+    __shared__ int cnt[kGridCells];
+    __shared__ int items[kGridLdsMax];
+    __shared__ int tmp[kGridBlock / 64 + 1];
+    for (int c = threadIdx.x; c < kGridCells; c += kGridBlock) cnt[c] = 0;
+    __syncthreads();
+    int mine[kGridPer];  // cells of keypoints threadIdx.x + j * kGridBlock
+#pragma unroll
+    for (int j = 0; j < kGridPer; ++j) {
+        const int i = threadIdx.x + j * kGridBlock;
+        mine[j] = -1;
+        if (i < n) {
+            const int gx = (int)roundf((k[i].x - minx) * gwi);
+            const int gy = (int)roundf((k[i].y - miny) * ghi);
+            if (gx >= 0 && gx < kGridCols && gy >= 0 && gy < kGridRows) {
+                mine[j] = gx * kGridRows + gy;  // mGrid[ix][iy]
+                atomicAdd(&cnt[mine[j]], 1);
+            }
+        }
+    }
+    __syncthreads();
+    constexpr int PER = (kGridCells + kGridBlock - 1) / kGridBlock;
+    int local[PER], sum = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int c = threadIdx.x * PER + j;
+        local[j] = c < kGridCells ? cnt[c] : 0;
+        sum += local[j];
+    }
+    int total;
+    int off = block_exclusive_scan<kGridBlock>(sum, tmp, total);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int c = threadIdx.x * PER + j;
+        if (c < kGridCells) {
+            cstart[c] = off;
+            cnt[c] = off;  // cursor
+        }
+        off += local[j];
+    }
+    if (threadIdx.x == 0) cstart[kGridCells] = total;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kGridPer; ++j)
+        if (mine[j] >= 0) items[atomicAdd(&cnt[mine[j]], 1)] = threadIdx.x + j * kGridBlock;
+    __syncthreads();
+    // insertion order = index order: sort each cell's items; cnt[c] is now the end of cell c
+    // and cnt[c - 1] its start
+    for (int c = threadIdx.x; c < kGridCells; c += kGridBlock) {
+        const int e = cnt[c], s0 = c ? cnt[c - 1] : 0;
+        for (int q = s0 + 1; q < e; ++q) {
+            const int v = items[q];
+            int b = q - 1;
+            while (b >= s0 && items[b] > v) {
+                items[b + 1] = items[b];
+                --b;
+            }
+            items[b + 1] = v;
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < total; i += kGridBlock) citems[i] = items[i];
+}
+
 // Frame::GetFeaturesInArea (Frame.cc:445-498): visits candidates in ix-major, iy, insertion
 // order and calls fn(idx) for each.
 template <class Fn>

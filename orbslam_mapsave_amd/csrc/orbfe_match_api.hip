@@ -165,6 +165,17 @@ struct orbfe_matcher {
         return ORBFE_OK;
     }
 
+    // Frame::AssignFeaturesToGrid: the LDS form up to kGridLdsMax keypoints.
+    void launch_grid(const orbfe_keypoint* k, int n, const orbfe_frame_view* v, int* cellof,
+                     int* cstart, int* citems) {
+        if (n <= kGridLdsMax)
+            hipLaunchKernelGGL(grid_lds_kernel, dim3(1), dim3(kGridBlock), 0, stream, k, n,
+                               v->min_x, v->min_y, v->grid_w_inv, v->grid_h_inv, cstart, citems);
+        else
+            hipLaunchKernelGGL(grid_kernel, dim3(1), dim3(kGridBlock), 0, stream, k, n, v->min_x,
+                               v->min_y, v->grid_w_inv, v->grid_h_inv, cellof, cstart, citems);
+    }
+
     // Uploads a frame view and builds its 64 x 48 grid (Frame::AssignFeaturesToGrid).
     int frame(const orbfe_frame_view* v, bool second, DevFrame& F) {
         DevBuf& k = second ? fb_k : fa_k;
@@ -182,9 +193,7 @@ struct orbfe_matcher {
         if ((st = ci.ensure(std::max(n, 1) * sizeof(int)))) return st;
         if ((st = co.ensure(std::max(n, 1) * sizeof(int)))) return st;
         if ((st = flush())) return st;
-        hipLaunchKernelGGL(grid_kernel, dim3(1), dim3(kGridBlock), 0, stream, k.as<orbfe_keypoint>(),
-                           n, v->min_x, v->min_y, v->grid_w_inv, v->grid_h_inv, co.as<int>(),
-                           cs.as<int>(), ci.as<int>());
+        launch_grid(k.as<orbfe_keypoint>(), n, v, co.as<int>(), cs.as<int>(), ci.as<int>());
         F.k = k.as<orbfe_keypoint>();
         F.desc = d.as<uint4>();
         F.ur = v->u_right ? u.as<float>() : nullptr;
@@ -207,9 +216,7 @@ struct orbfe_matcher {
         if ((st = fa_cs.ensure((kGridCells + 1) * sizeof(int)))) return st;
         if ((st = fa_ci.ensure(std::max(n, 1) * sizeof(int)))) return st;
         if ((st = fa_co.ensure(std::max(n, 1) * sizeof(int)))) return st;
-        hipLaunchKernelGGL(grid_kernel, dim3(1), dim3(kGridBlock), 0, stream, v->keys_un, n,
-                           v->min_x, v->min_y, v->grid_w_inv, v->grid_h_inv, fa_co.as<int>(),
-                           fa_cs.as<int>(), fa_ci.as<int>());
+        launch_grid(v->keys_un, n, v, fa_co.as<int>(), fa_cs.as<int>(), fa_ci.as<int>());
         F.k = v->keys_un;
         F.desc = reinterpret_cast<const uint4*>(v->desc);
         F.ur = v->u_right;

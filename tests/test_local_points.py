@@ -55,6 +55,7 @@ def test_gpu_search_local_points(seed, m, th, stereo):
     d_ur = torch.from_numpy(f.u_right).to(dev) if f.u_right is not None else None
     d_inv = torch.zeros(m, dtype=torch.uint8, device=dev)
     mt = ORBmatcher(0.8, False, device=0)
+    torch.cuda.synchronize()  # the inputs (and d_inv's fill) on torch's stream are complete
     gnm, gnto = mt.search_local_points_device(
         f.n, d_keys.data_ptr(), d_desc.data_ptr(), d_ur.data_ptr() if d_ur is not None else None,
         S.W, S.H, f.scale_factors, lm["tcw"], cam, LOG_SCALE, 0.5, m, T["xyz"].data_ptr(),
