@@ -140,7 +140,6 @@ def run_c5(args) -> None:
     for _ in range(max(args.warmup, 1)):
         step()
     barrier()
-    skew_next[0] = bool(args.skew) and S > 1 and J >= S
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
