@@ -10,6 +10,7 @@ import csv
 import collections
 import json
 import os
+import re
 import shutil
 import sys
 
@@ -20,7 +21,7 @@ DST = os.path.join(ROOT, "profiles", R)
 os.makedirs(DST, exist_ok=True)
 
 def short(name):
-    return name.split("(")[0].replace("orbfe::", "").replace("void ", "")
+    return re.sub(r"<.*>$", "", name.split("(")[0].replace("orbfe::", "").replace("void ", ""))
 
 # kernel stats (copy + a compact table)
 shutil.copy(os.path.join(SRC, "trace", "run_kernel_stats.csv"), os.path.join(DST, "kernel_stats.csv"))
