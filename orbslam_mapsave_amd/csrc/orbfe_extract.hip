@@ -1188,8 +1188,8 @@ __global__ __launch_bounds__(256) void blur_kernel(BlurArgs a) {
 //      constant byte masks: m10 = sum (u + 16) I - 16 sum I, m01 = v sum I (integers, exact);
 //   2. lane j computes keypoint j's fastAtan2 and its double-precision cos / sin once, so the
 //      trig costs one wave instruction stream per group instead of one per keypoint;
-//   3. per keypoint, lane k evaluates the rotated pattern pairs k + 64 r (pattern held in
-//      registers across the group) and 4 ballots make the 256-bit descriptor.
+//   3. per keypoint, lane k evaluates the rotated pattern pairs k + 64 r (pattern held packed
+//      in 4 registers across the group) and 4 ballots make the 256-bit descriptor.
 constexpr int kDescBlock = kDescBlockSize;
 constexpr int kDescGroupSmall = 2;  // small batches (single-frame latency): 4x the waves
 constexpr int kDescWinR = 18;                        // rotated pattern radius bound (< 18.5)
@@ -1252,32 +1252,39 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
         wu[d] = x;
         w1[d] = y;
     }
-    // every keypoint's 16-byte row load is issued before the first reduction
-    uint4 px[kDescGroup];
-#pragma unroll
-    for (int j = 0; j < kDescGroup; ++j) {
-        px[j] = make_uint4(0u, 0u, 0u, 0u);
-        if (((vmask >> j) & 1) && r < 31) {
-            const int kl = __builtin_amdgcn_readlane(my_l, j);
-            const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane(my_key, j);
-            const LevelPtr pp = a.pyr[kl];
-            const uint8_t* row = pp.base + f * pp.fpitch + (long long)(key_y(kk) + v) * pp.pitch +
-                                 key_x(kk) - 15 + 16 * hh;
-            px[j] = load16_a1(row);
-        }
-    }
+    // the 16-byte row loads of kIcBatch keypoints are issued before their first reduction
+    // (4 at a time: 16 VGPRs of loads in flight, not 32)
+    constexpr int kIcBatch = kDescGroup < 4 ? kDescGroup : 4;
     int M10 = 0, M01 = 0;
 #pragma unroll
-    for (int j = 0; j < kDescGroup; ++j) {
-        const uint4 p4 = px[j];
-        const int su = (int)__builtin_amdgcn_udot4(p4.x, wu[0], __builtin_amdgcn_udot4(p4.y, wu[1],
-                       __builtin_amdgcn_udot4(p4.z, wu[2], __builtin_amdgcn_udot4(p4.w, wu[3], 0u, false), false), false), false);
-        const int s = (int)__builtin_amdgcn_udot4(p4.x, w1[0], __builtin_amdgcn_udot4(p4.y, w1[1],
-                      __builtin_amdgcn_udot4(p4.z, w1[2], __builtin_amdgcn_udot4(p4.w, w1[3], 0u, false), false), false), false);
-        const int m10 = wave_sum(su - 16 * s), m01 = wave_sum(v * s);
-        if (lane == j) {
-            M10 = m10;
-            M01 = m01;
+    for (int j0 = 0; j0 < kDescGroup; j0 += kIcBatch) {
+        uint4 px[kIcBatch];
+#pragma unroll
+        for (int jb = 0; jb < kIcBatch; ++jb) {
+            const int j = j0 + jb;
+            px[jb] = make_uint4(0u, 0u, 0u, 0u);
+            if (((vmask >> j) & 1) && r < 31) {
+                const int kl = __builtin_amdgcn_readlane(my_l, j);
+                const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane(my_key, j);
+                const LevelPtr pp = a.pyr[kl];
+                const uint8_t* row = pp.base + f * pp.fpitch + (long long)(key_y(kk) + v) * pp.pitch +
+                                     key_x(kk) - 15 + 16 * hh;
+                px[jb] = load16_a1(row);
+            }
+        }
+#pragma unroll
+        for (int jb = 0; jb < kIcBatch; ++jb) {
+            const int j = j0 + jb;
+            const uint4 p4 = px[jb];
+            const int su = (int)__builtin_amdgcn_udot4(p4.x, wu[0], __builtin_amdgcn_udot4(p4.y, wu[1],
+                           __builtin_amdgcn_udot4(p4.z, wu[2], __builtin_amdgcn_udot4(p4.w, wu[3], 0u, false), false), false), false);
+            const int s = (int)__builtin_amdgcn_udot4(p4.x, w1[0], __builtin_amdgcn_udot4(p4.y, w1[1],
+                          __builtin_amdgcn_udot4(p4.z, w1[2], __builtin_amdgcn_udot4(p4.w, w1[3], 0u, false), false), false), false);
+            const int m10 = wave_sum(su - 16 * s), m01 = wave_sum(v * s);
+            if (lane == j) {
+                M10 = m10;
+                M01 = m01;
+            }
         }
     }
 
@@ -1318,11 +1325,12 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
         const int x0 = (x - kDescWinR) & ~3;
         my_kc = (uint32_t)(kDescWinR * kDescWinP + (x - x0)) - 0x400000u * kDescWinP - 0x4b400000u;
     }
-    float pat[16];
+    // Pattern pairs lane + 64 q as 4 packed int8 (x1, y1, x2, y2), widened to float per
+    // keypoint: 4 VGPRs held across the loop instead of 16 (and the compiler's hoisted products
+    // with them: 98 -> 70 VGPRs, 4 -> 7 waves per SIMD).
+    int patw[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) pat[4 * q + c] = (float)c_pattern[4 * (lane + 64 * q) + c];
+    for (int q = 0; q < 4; ++q) patw[q] = reinterpret_cast<const int*>(c_pattern)[lane + 64 * q];
     const float2v MG = float2v{12582912.f, 12582912.f};
     constexpr int kRawRows = 2 * (kDescWinR + 3) + 2;  // 44 (43 used, one pad row for pairs)
     constexpr int kRawP = 48;                          // raw row: image cols [x0-4, x0+44)
@@ -1330,12 +1338,15 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
     constexpr int kPairs = kRawRows / 2;               // 22 u16 row pairs
     // samples reach window cols (x - x0) +- 18 with x - x0 in [18, 21]: cols 0..39, 10 quads
     constexpr int kBlurQ = 10;
-    __shared__ __attribute__((aligned(16))) uint8_t raw_all[kDescBlock / 64][kRawRows * kRawP];
-    __shared__ __attribute__((aligned(16))) uint32_t rowp_all[kDescBlock / 64][kPairs * kDescWinP];
-    __shared__ __attribute__((aligned(16))) uint8_t win_all[kDescBlock / 64][kDescWinBytes];
+    // The raw window is dead once the row pass has read it and the blurred window is written
+    // after that (same wave, LDS ops in order), so the two share one buffer.
+    constexpr int kRawWinBytes = kRawRows * kRawP > kDescWinBytes ? kRawRows * kRawP : kDescWinBytes;
+    __shared__ __attribute__((aligned(16))) uint8_t raw_all[kDescBlock / 64][kRawWinBytes];
+    constexpr int kRowpP = 4 * kBlurQ;                 // u16 row-pair pitch: window cols 0..39
+    __shared__ __attribute__((aligned(16))) uint32_t rowp_all[kDescBlock / 64][kPairs * kRowpP];
     uint8_t* raw = raw_all[threadIdx.x >> 6];
     uint32_t* rowp = rowp_all[threadIdx.x >> 6];
-    uint8_t* wb = win_all[threadIdx.x >> 6];
+    uint8_t* wb = raw;
     const uint32_t KLO = (uint32_t)(a.taps[0] | (a.taps[1] << 8) | (a.taps[2] << 16) | (a.taps[3] << 24));
     const uint32_t KHI = (uint32_t)(a.taps[2] | (a.taps[1] << 8) | (a.taps[0] << 16));
     typedef unsigned short us2 __attribute__((ext_vector_type(2)));
@@ -1398,7 +1409,7 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
                     hh[e][jj] = __builtin_amdgcn_udot4(hi, KHI, __builtin_amdgcn_udot4(lo, KLO, 0u, false), false);
                 }
             }
-            *reinterpret_cast<uint4*>(rowp + pr * kDescWinP + 4 * q) =
+            *reinterpret_cast<uint4*>(rowp + pr * kRowpP + 4 * q) =
                 make_uint4(hh[0][0] | (hh[1][0] << 16), hh[0][1] | (hh[1][1] << 16),
                            hh[0][2] | (hh[1][2] << 16), hh[0][3] | (hh[1][3] << 16));
         }
@@ -1409,7 +1420,7 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
             const int jp = it / kBlurQ, q = it - jp * kBlurQ;
             uint4 P4[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) P4[i] = *reinterpret_cast<const uint4*>(rowp + (jp + i) * kDescWinP + 4 * q);
+            for (int i = 0; i < 4; ++i) P4[i] = *reinterpret_cast<const uint4*>(rowp + (jp + i) * kRowpP + 4 * q);
             uint32_t ev[4], od[4];
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
@@ -1440,6 +1451,11 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
         int i0[4], i1[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
+            float pat[16];
+            asm volatile("" : "+v"(patw[q]));  // keeps the widening inside the loop
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                pat[4 * q + c] = (float)(int)(int8_t)(uint8_t)((uint32_t)patw[q] >> (8 * c));
             const float2v r0 = (pat[4 * q] * SC + pat[4 * q + 1] * CSn) + MG;
             const float2v r1 = (pat[4 * q + 2] * SC + pat[4 * q + 3] * CSn) + MG;
             // (__builtin_bit_cast of an ext-vector element reads element 0 in this clang:
