@@ -164,7 +164,10 @@ int orbfe_synchronize(orbfe_extractor* h);
 /* Per-kernel timing of the extraction pipeline: when enabled, a HIP event pair is recorded on
  * the handle's stream around every kernel launch.  orbfe_profile_read synchronizes the stream
  * and returns, per stage (ORBFE_STAGE_*), the summed duration in ms and the launch count since
- * the previous read.  Used by bench.py for the roofline figure; off by default. */
+ * the previous read.  Used by bench.py for the roofline figure; off by default.
+ * enable: 0 off, 1 every stage, or ORBFE_PROFILE_STAGE(s) OR-ed together to time only those
+ * stages (the other launches carry no events). */
+#define ORBFE_PROFILE_STAGE(s) (2 << (s))
 #define ORBFE_STAGE_MASK     0   /* K0: colour conversion + mask (level 0) */
 #define ORBFE_STAGE_RESIZE   1
 #define ORBFE_STAGE_FAST     2

@@ -77,13 +77,14 @@ int check_device(int device) {
 // dispatch packet itself, so a pair brackets exactly one kernel), read by orbfe_profile_read.
 struct Profiler {
     bool on = false;
+    unsigned mask = ~0u;  // stages that get events (orbfe_profile)
     std::vector<hipEvent_t> a, b;
     std::vector<int> kind;
     size_t used = 0;
     // Returns the event pair for the next launch of stage k (nullptrs when off).
     void slot(int k, hipEvent_t* e0, hipEvent_t* e1) {
         *e0 = *e1 = nullptr;
-        if (!on) return;
+        if (!on || !((mask >> k) & 1u)) return;
         if (used == a.size()) {
             hipEvent_t x, y;
             if (hipEventCreate(&x) != hipSuccess) return;
@@ -910,7 +911,9 @@ int orbfe_human_mask_rect(const float* joints, int njoints, int w, int hgt, orbf
 
 int orbfe_profile(orbfe_extractor* h, int enable) {
     if (!h) return ORBFE_ERR_ARG;
+    if (enable < 0 || (enable > 1 && (enable & 1))) return ORBFE_ERR_ARG;
     h->prof.on = enable != 0;
+    h->prof.mask = enable > 1 ? (unsigned)enable >> 1 : ~0u;
     h->prof.used = 0;
     return ORBFE_OK;
 }

@@ -285,9 +285,15 @@ class ORBextractor:
 
     STAGES = ("mask", "resize", "fast", "octree", "blur", "describe")
 
-    def profile(self, enable: bool) -> None:
-        """Record a HIP event pair around every kernel launch (orbfe_profile)."""
-        _check("orbfe_profile", lib().orbfe_profile(self._h, int(enable)))
+    def profile(self, enable: bool, stages=None) -> None:
+        """Record a HIP event pair around every kernel launch (orbfe_profile), or only around
+        the launches of the named stages (e.g. ("fast",))."""
+        mode = int(bool(enable))
+        if enable and stages is not None:
+            mode = 0
+            for st in stages:
+                mode |= 2 << self.STAGES.index(st)
+        _check("orbfe_profile", lib().orbfe_profile(self._h, mode))
 
     def profile_read(self) -> dict:
         """{stage: (total_ms, launches)} since the previous read (orbfe_profile_read)."""

@@ -33,7 +33,9 @@ for f in ("bench.json", "trace_bench.json"):
 # trace has the grid per dimension; the PMC csv only the total, so the bench shapes found in the
 # trace (kernel, total grid) select the PMC dispatches.  Multi-launch stages (resize: one launch
 # per level) are averaged over all their bench-shape launches, as bench.py's avg_launch_ms is.
-FRAMES = int(os.environ.get("BENCH_SUBBATCH", "128"))
+_cfg = json.loads(open(os.path.join(SRC, "bench.json")).read())["config"]
+FRAMES = int(os.environ.get("BENCH_SUBBATCH", 0)) or (
+    _cfg["frames_per_rank_per_step"] // _cfg.get("streams_per_rank", 1) // _cfg.get("chunks_per_stream", 1))
 trace_rows = list(csv.DictReader(open(os.path.join(SRC, "trace", "run_kernel_trace.csv"))))
 shapes = collections.defaultdict(set)
 
@@ -100,3 +102,22 @@ launch = {n: {"launches": len(v), "grids": sorted(shapes[n]), "avg_ms": round(su
 json.dump(launch, open(os.path.join(DST, "bench_shape_launches.json"), "w"), indent=1)
 for n, v in sorted(launch.items()):
     print(n, v)
+
+# The committed bench line was measured before this round's PMC passes: give its roofline the
+# traffic just measured, and record its live launch duration beside rocprofv3's for the same
+# kernel and shape.
+bpath = os.path.join(DST, "bench.json")
+line = json.loads(open(bpath).read().strip().splitlines()[-1])
+roof = line.get("roofline") or {}
+k = roof.get("kernel")
+if k:
+    roof["traffic"] = traffic.get(k.replace("_kernel", ""), roof.get("traffic"))
+    with open(bpath, "w") as fh:
+        fh.write(json.dumps(line) + "\n")
+    check = {"kernel": k, "frames_per_launch": FRAMES,
+             "bench_avg_launch_ms (HIP events, timed steps)": roof.get("avg_launch_ms"),
+             "rocprofv3_avg_ms (bench-shape launches)": launch.get(k, {}).get("avg_ms"),
+             "traffic_bytes_per_launch (2 x FETCH_SIZE + WRITE_SIZE)": roof["traffic"],
+             "algorithmic_bytes_per_launch": roof.get("bytes_per_launch")}
+    json.dump(check, open(os.path.join(DST, "roofline_check.json"), "w"), indent=1)
+    print(check)
