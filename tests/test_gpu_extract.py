@@ -89,6 +89,28 @@ def test_batch_matches_single(ex, p):
         assert np.array_equal(desc[f, :cnt[f]], odesc)
 
 
+def test_profile_stage_mask(ex, p):
+    """orbfe_profile: events on every launch, or on the masked stages' launches only (bench.py's
+    timed steps); results stay bit-exact either way."""
+    imgs = np.stack([synthetic_frame(s, 640, 480) for s in range(2)])
+    okps, odesc = oracle.extract(p, imgs[1])
+    ex.profile(True)
+    ex.profile_read()
+    kps, desc, cnt = ex.extract_batch(imgs)
+    every = ex.profile_read()
+    ex.profile(True, stages=("fast", "describe"))
+    kps2, desc2, cnt2 = ex.extract_batch(imgs)
+    masked = ex.profile_read()
+    ex.profile(False)
+    for st in ("resize", "fast", "octree", "describe"):
+        assert every[st][1] >= 1 and every[st][0] > 0, (st, every)
+    assert masked["fast"][1] == every["fast"][1] and masked["describe"][1] == every["describe"][1]
+    assert all(masked[st][1] == 0 for st in ("mask", "resize", "octree", "blur")), masked
+    _assert_same_keys(kps[1, :cnt[1]], okps)
+    _assert_same_keys(kps2[1, :cnt2[1]], okps)
+    assert np.array_equal(desc[1, :cnt[1]], odesc) and np.array_equal(desc2[1, :cnt2[1]], odesc)
+
+
 @pytest.mark.parametrize("cfg", [(2000, 1.2, 8, 32, 7, 640, 480), (2000, 1.2, 8, 20, 7, 1920, 1080),
                                  (500, 1.5, 4, 20, 7, 1280, 720), (1000, 1.2, 8, 32, 7, 752, 480)])
 def test_other_configs(cfg):
