@@ -355,16 +355,18 @@ __device__ __forceinline__ half2v fast_h2(uint32_t b) {
 }
 __device__ __forceinline__ int fast_S(const uint8_t* p, int st) {
     const half2v V = fast_h2(p[0]);
-    const half2v Vs = half2v{V.x, -V.y};
     const uint32_t x[16] = {p[3 * st],      p[3 * st + 1],  p[2 * st + 2],  p[st + 3],
                             p[3],           p[-st + 3],     p[-2 * st + 2], p[-3 * st + 1],
                             p[-3 * st],     p[-3 * st - 1], p[-2 * st - 2], p[-st - 3],
                             p[-3],          p[st - 3],      p[2 * st - 2],  p[3 * st - 1]};
+    // The centre is subtracted once at the end: min over an arc of (x - v) = (min x) - v and of
+    // (v - x) = v - (max x), so the arcs run on e = (-X, X) (the sign is a source modifier of
+    // v_pk_minimum3_f16) and q + (V, -V) restores (q0, -q1).
     half2v e[16], m3[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const half2v X = fast_h2(x[k]);
-        e[k] = Vs + half2v{-X.x, X.y};
+        e[k] = half2v{-X.x, X.y};
     }
 #pragma unroll
     for (int k = 0; k < 16; ++k)
@@ -377,6 +379,7 @@ __device__ __forceinline__ int fast_S(const uint8_t* p, int st) {
             __builtin_elementwise_minimum(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15]);
         q = __builtin_elementwise_maximum(q, m9);
     }
+    q = q + half2v{V.x, -V.y};
     return (int)(float)__builtin_elementwise_maximum(q.x, q.y) - 1;
 }
 
