@@ -1397,33 +1397,50 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         const unsigned long long rest = m & (m - 1);
         if (rest) load_raw(__ffsll((long long)rest) - 1);  // next keypoint's raw window in flight
-        // row pass: item (pair pr, quad q) -> window cols 4q..4q+3 of raw rows 2pr, 2pr+1
-        for (int it = lane; it < kPairs * kBlurQ; it += 64) {
-            const int pr = it / kBlurQ, q = it - pr * kBlurQ;
-            uint32_t hh[2][4];
+        // row pass: item (pair pr, quad q) -> window cols 4q..4q+3 of raw rows 2pr, 2pr+1.
+        // Items it = lane + 64 i: (pr, q) advance by (6, 4) or, when q wraps, (7, -6), and the
+        // raw offset with them (no division or multiply in the loop); (pr, q) sits at dword
+        // 4 it of rowp (kRowpP = 4 kBlurQ).
+        static_assert(64 % kBlurQ == 4 && 64 / kBlurQ == 6 && kRowpP == 4 * kBlurQ,
+                      "blur stepping assumes 10 quads");
+        {
+            const int pr0 = lane / kBlurQ, q0 = lane - pr0 * kBlurQ;
+            int q = q0;
+            int ro = 2 * pr0 * kRawP + 4 * q0;  // byte offset of (row 2pr, quad q) in raw
+            for (int it = lane; it < kPairs * kBlurQ; it += 64) {
+                uint32_t hh[2][4];
 #pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const uint32_t* row = reinterpret_cast<const uint32_t*>(raw + (2 * pr + e) * kRawP) + q;
-                const uint32_t w0 = row[0], w1 = row[1], w2 = row[2];
+                for (int e = 0; e < 2; ++e) {
+                    const uint32_t* row = reinterpret_cast<const uint32_t*>(raw + ro + e * kRawP);
+                    const uint32_t w0 = row[0], w1 = row[1], w2 = row[2];
 #pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    const uint32_t lo = jj < 3 ? __builtin_amdgcn_alignbyte(w1, w0, jj + 1) : w1;
-                    const uint32_t hi = jj < 3 ? __builtin_amdgcn_alignbyte(w2, w1, jj + 1) : w2;
-                    hh[e][jj] = __builtin_amdgcn_udot4(hi, KHI, __builtin_amdgcn_udot4(lo, KLO, 0u, false), false);
+                    for (int jj = 0; jj < 4; ++jj) {
+                        const uint32_t lo = jj < 3 ? __builtin_amdgcn_alignbyte(w1, w0, jj + 1) : w1;
+                        const uint32_t hi = jj < 3 ? __builtin_amdgcn_alignbyte(w2, w1, jj + 1) : w2;
+                        hh[e][jj] = __builtin_amdgcn_udot4(hi, KHI, __builtin_amdgcn_udot4(lo, KLO, 0u, false), false);
+                    }
                 }
+                // row 2pr in the low half, 2pr+1 in the high half (both < 2^16): one v_perm each
+                *reinterpret_cast<uint4*>(rowp + 4 * it) =
+                    make_uint4(__builtin_amdgcn_perm(hh[1][0], hh[0][0], 0x05040100u),
+                               __builtin_amdgcn_perm(hh[1][1], hh[0][1], 0x05040100u),
+                               __builtin_amdgcn_perm(hh[1][2], hh[0][2], 0x05040100u),
+                               __builtin_amdgcn_perm(hh[1][3], hh[0][3], 0x05040100u));
+                const bool wrap = q >= kBlurQ - 4;
+                q += wrap ? 4 - kBlurQ : 4;
+                ro += wrap ? 7 * 2 * kRawP + 4 * (4 - kBlurQ) : 6 * 2 * kRawP + 16;
             }
-            *reinterpret_cast<uint4*>(rowp + pr * kRowpP + 4 * q) =
-                make_uint4(hh[0][0] | (hh[1][0] << 16), hh[0][1] | (hh[1][1] << 16),
-                           hh[0][2] | (hh[1][2] << 16), hh[0][3] | (hh[1][3] << 16));
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        // column pass: item (output rows 2jp, 2jp+1; quad q) from pairs jp..jp+3
+        // column pass: item (output rows 2jp, 2jp+1; quad q) from pairs jp..jp+3, stepped as
+        // the row pass
+        int cq = lane % kBlurQ;
+        int wq = 2 * (lane / kBlurQ) * kDescWinP + 4 * cq;  // byte offset of (row 2jp, quad q)
         for (int it = lane; it < ((kDescWinRows + 1) / 2) * kBlurQ; it += 64) {
-            const int jp = it / kBlurQ, q = it - jp * kBlurQ;
             uint4 P4[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) P4[i] = *reinterpret_cast<const uint4*>(rowp + (jp + i) * kRowpP + 4 * q);
+            for (int i = 0; i < 4; ++i) P4[i] = *reinterpret_cast<const uint4*>(rowp + 4 * it + i * kRowpP);
             uint32_t ev[4], od[4];
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
@@ -1439,11 +1456,14 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
                 u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), T10, u, false);
                 od[c] = min(u, 0xffffffu);
             }
-            *reinterpret_cast<uint32_t*>(wb + (2 * jp) * kDescWinP + 4 * q) =
+            *reinterpret_cast<uint32_t*>(wb + wq) =
                 __builtin_amdgcn_perm(ev[1], ev[0], 0x0c0c0602u) | __builtin_amdgcn_perm(ev[3], ev[2], 0x06020c0cu);
-            if (2 * jp + 1 < kDescWinRows)
-                *reinterpret_cast<uint32_t*>(wb + (2 * jp + 1) * kDescWinP + 4 * q) =
+            if (wq < (kDescWinRows - 1) * kDescWinP)  // row 2jp + 1 exists: jp < 18
+                *reinterpret_cast<uint32_t*>(wb + wq + kDescWinP) =
                     __builtin_amdgcn_perm(od[1], od[0], 0x0c0c0602u) | __builtin_amdgcn_perm(od[3], od[2], 0x06020c0cu);
+            const bool wrap = cq >= kBlurQ - 4;
+            cq += wrap ? 4 - kBlurQ : 4;
+            wq += wrap ? 7 * 2 * kDescWinP + 4 * (4 - kBlurQ) : 6 * 2 * kDescWinP + 16;
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
