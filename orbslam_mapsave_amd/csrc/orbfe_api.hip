@@ -343,7 +343,10 @@ struct orbfe_extractor {
             fa.cell_cnt = cell_cnt.as<int>();
             fa.cell_keys = cell_keys.as<uint32_t>();
             for (int l = 0; l < L; ++l) fa.pyr[l] = lp[l];
-            ORBFE_LAUNCH(prof, ORBFE_STAGE_FAST, fast_kernel, dim3(ncells, n), dim3(kFastBlockSize), g.fast_lds, stream, fa);
+            if (g.roi_pitch == kFastPitch)
+                ORBFE_LAUNCH(prof, ORBFE_STAGE_FAST, fast_kernel<kFastPitch>, dim3(ncells, n), dim3(kFastBlockSize), g.fast_lds, stream, fa);
+            else
+                ORBFE_LAUNCH(prof, ORBFE_STAGE_FAST, fast_kernel<0>, dim3(ncells, n), dim3(kFastBlockSize), g.fast_lds, stream, fa);
         }
         // K3 oct-tree per (frame, level)
         OctArgs oa;

@@ -429,6 +429,9 @@ __device__ __forceinline__ int fast_emit(const uint8_t* S, const uint16_t* list,
     return o;
 }
 
+// kP: the ROI pitch as a compile-time constant (48 for every cell width up to 45 px, i.e. the
+// common frame sizes), so the 16 circle offsets of fast_S become LDS immediates; 0 = runtime.
+template <int kP>
 __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char fast_lds[];
     int c, f;
@@ -437,7 +440,7 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
     const CellDesc cell = a.cells[c];
     const LevelPtr lp = a.pyr[cell.level];
     const int rows = cell.y1 - cell.y0, cols = cell.x1 - cell.x0;
-    const int P = a.roi_pitch;
+    const int P = kP ? kP : a.roi_pitch;
     uint8_t* roi_base = fast_lds;
     uint8_t* S = fast_lds + a.roi_rows * P;
     uint16_t* list = reinterpret_cast<uint16_t*>(S + (((a.roi_rows - 4) * P + 15) & ~15));
@@ -548,6 +551,9 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
     }
     if (lane == 0) a.cell_cnt[f * a.ncells + c] = min(total, cell.cap);
 }
+
+template __global__ void fast_kernel<0>(FastArgs);
+template __global__ void fast_kernel<kFastPitch>(FastArgs);
 
 // ---------------------------------------------------------------------------------------------
 // K3 — DistributeOctTree as a data-parallel emulation of the reference's std::list.

@@ -172,7 +172,8 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g);
 __global__ void level0_kernel(Level0Args);
 __global__ void resize_kernel(ResizeArgs);
 __global__ void resize_tail_kernel(ResizeTailArgs);
-__global__ void fast_kernel(FastArgs);
+template <int kP> __global__ void fast_kernel(FastArgs);
+constexpr int kFastPitch = 48;  // fast_kernel<kFastPitch>: ROI pitch known at compile time
 __global__ void octree_kernel(OctArgs);
 __global__ void blur_kernel(BlurArgs);
 template <int kDescGroup> __global__ void describe_kernel(DescArgs);
