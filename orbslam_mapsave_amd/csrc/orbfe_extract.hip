@@ -222,13 +222,15 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
         uint32_t packed = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int t0 = s0[x0[k]] * a0[k] + s0[x1[k]] * a1[k];
-            const int t1 = s1[x0[k]] * a0[k] + s1[x1[k]] * a1[k];
+            // coefficients sum to 2048 (INTER_RESIZE_COEF_SCALE): t < 2^19, t * b < 2^30, so
+            // every product is a full-rate v_mul_u32_u24 (not the quarter-rate v_mul_lo_u32)
+            const uint32_t t0 = __umul24(s0[x0[k]], a0[k]) + __umul24(s0[x1[k]], a1[k]);
+            const uint32_t t1 = __umul24(s1[x0[k]], a0[k]) + __umul24(s1[x1[k]], a1[k]);
             // FixedPtCast<int, uchar, 22>: the sum is never negative (pixels and coefficients
             // are), so only the upper clamp remains, on the unsigned value.  The signed form
             // min(max(x >> 22, 0), 255) can be matched to gfx950's v_ashr_pk_u8_i32 for two of
             // the four bytes, and that packing was seen to corrupt the upper two bytes.
-            const uint32_t v = min(((uint32_t)(t0 * b0 + t1 * b1) + (1u << 21)) >> 22, 255u);
+            const uint32_t v = min((__umul24(t0, b0) + __umul24(t1, b1) + (1u << 21)) >> 22, 255u);
             packed |= (uint32_t)v << (8 * k);
         }
         uint8_t* d = dst + (long long)y * a.dst.pitch + x;
@@ -315,9 +317,9 @@ __global__ __launch_bounds__(kTailBlock) void resize_tail_kernel(ResizeTailArgs 
                 uint32_t packed = 0;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const int t0 = s0[x0[q]] * a0[q] + s0[x1[q]] * a1[q];
-                    const int t1 = s1[x0[q]] * a0[q] + s1[x1[q]] * a1[q];
-                    const uint32_t v = min(((uint32_t)(t0 * b0 + t1 * b1) + (1u << 21)) >> 22, 255u);  // as in resize_kernel
+                    const uint32_t t0 = __umul24(s0[x0[q]], a0[q]) + __umul24(s0[x1[q]], a1[q]);
+                    const uint32_t t1 = __umul24(s1[x0[q]], a0[q]) + __umul24(s1[x1[q]], a1[q]);
+                    const uint32_t v = min((__umul24(t0, b0) + __umul24(t1, b1) + (1u << 21)) >> 22, 255u);  // as in resize_kernel
                     packed |= (uint32_t)v << (8 * q);
                 }
                 *reinterpret_cast<uint32_t*>(d + y * dp_l + x) = packed;  // LDS pitch % 4 == 0
