@@ -278,7 +278,7 @@ def main() -> None:
         e.set_stream(streams[k].cuda_stream)
         exs.append(e)
     mt = ORBmatcher(0.9, True, device=local)
-    cap = exs[0].capacity()
+    cap = exs[0].capacity(W, H)
     d_kps = torch.empty((B, cap * 28), dtype=torch.uint8, device=dev)
     d_desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
     d_n = torch.zeros(B, dtype=torch.int32, device=dev)

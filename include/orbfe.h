@@ -95,9 +95,14 @@ int   orbfe_get_scale_tables(const orbfe_extractor* h, float* scale, float* inv_
                              float* sigma2, float* inv_sigma2);
 /* mnFeaturesPerLevel (ORBextractor.cc:434-445). */
 int   orbfe_get_features_per_level(const orbfe_extractor* h, int32_t* out);
-/* Per-frame keypoint capacity that can never overflow for this handle's params
- * (sum over levels of the oct-tree bound, see DESIGN.md "capacity"). */
+/* Per-frame keypoint capacity that can never overflow for this handle's params and ANY
+ * supported input size (w, h <= 4096): the sum over levels of the oct-tree output bound
+ * max(N_l + 4, 4 nIni_l, 20) at the widest aspect ratio (DESIGN.md "capacity"). */
 int   orbfe_keypoint_capacity(const orbfe_extractor* h);
+/* The same bound for one input size (w x hgt): what DistributeOctTree (ORBextractor.cc:538-762)
+ * can return per level at that size, summed.  <= orbfe_keypoint_capacity(h); negative status
+ * for an unsupported size. */
+int   orbfe_keypoint_capacity_for(const orbfe_extractor* h, int w, int hgt);
 
 /* Replaces ORBextractor::operator()(image, mask, keypoints, descriptors)
  * (ORBextractor.h:64-66, ORBextractor.cc:1042-1108), called from Frame::ExtractORB
@@ -141,7 +146,9 @@ int orbfe_extract_batch(orbfe_extractor* h, const uint8_t* const* imgs, int n, i
 
 /* Device-resident throughput form: d_imgs holds n frames, frame f at d_imgs + f*frame_pitch,
  * rows `stride` bytes apart.  d_masks NULL or laid out like d_imgs.  Outputs are device
- * slabs laid out as in orbfe_extract_batch.  Asynchronous on the handle's stream. */
+ * slabs laid out as in orbfe_extract_batch.  Asynchronous on the handle's stream.
+ * kps_cap below orbfe_keypoint_capacity_for(h, w, hgt) returns ORBFE_ERR_CAPACITY before any
+ * device work, so no frame is ever truncated; d_n_out[f] is frame f's keypoint count. */
 int orbfe_extract_batch_device(orbfe_extractor* h, const uint8_t* d_imgs, int n, int w, int hgt,
                                size_t stride, size_t frame_pitch, const uint8_t* d_masks,
                                orbfe_keypoint* d_kps, int kps_cap, uint8_t* d_desc,
@@ -339,6 +346,24 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
 /* Jacobi rounds the most recent SearchByProjection / SearchForInitialization resolution took
  * (diagnostics). */
 int orbfe_matcher_last_rounds(const orbfe_matcher* m);
+/* Calls of this matcher rerun because their candidate lists outgrew the device buffer (the
+ * first attempt bounds every fill by the buffer and reads unfilled lists as empty; the rerun
+ * uses the exact total) — diagnostics for the capacity tests. */
+int orbfe_matcher_capacity_retries(const orbfe_matcher* m);
+
+/* Frame::GetFeaturesInArea (Frame.cc:445-498) over the 64 x 48 grid of
+ * Frame::AssignFeaturesToGrid / PosInGrid (Frame.cc:341-356, 500-510), exactly as every matcher
+ * above builds and queries it — exported for the grid's parity tests.  Query q is
+ * (x[q], y[q], r[q], min_level[q], max_level[q]); its candidates, in the reference's order (cell
+ * column ix, then row iy, then insertion order), go to items[off[q] .. off[q + 1]).  off holds
+ * nq + 1 entries (off[nq] = total).  wave != 0 runs the wave-per-query form
+ * (SearchForInitialization, last-frame and keyframe SearchByProjection), wave == 0 the
+ * thread-per-query form (local-map SearchByProjection).  total > items_cap: ORBFE_ERR_CAPACITY
+ * with off filled and items untouched.  Synchronous; host buffers. */
+int orbfe_features_in_area(orbfe_matcher* m, const orbfe_frame_view* f, int nq, const float* x,
+                           const float* y, const float* r, const int32_t* min_level,
+                           const int32_t* max_level, int wave, int32_t* off, int32_t* items,
+                           int items_cap);
 
 /* Relocalisation ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF,
  * const set<MapPoint*>& sAlreadyFound, th, ORBdist) (ORBmatcher.cc:1475-1602), called by

@@ -50,7 +50,8 @@ public:
                     size_t mask_step, std::vector<orbfe_keypoint>& keypoints,
                     std::vector<uint8_t>& descriptors) {
         if (!image || cols <= 0 || rows <= 0) return;
-        const int cap = orbfe_keypoint_capacity(h_);
+        const int cap = orbfe_keypoint_capacity_for(h_, cols, rows);
+        if (cap < 0) throw Error("orbfe_keypoint_capacity_for", cap);
         keypoints.resize(cap);
         descriptors.resize((size_t)cap * 32);
         int n = 0;

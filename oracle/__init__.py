@@ -62,7 +62,7 @@ def level_sizes(p: Params, w: int, h: int):
 
 
 def capacity(p: Params) -> int:
-    return int(p.nfeatures) + 4 * int(p.nlevels) + 64
+    return int(p.nfeatures) + 4 * int(p.nlevels) + 4096  # >= any oct-tree output (wide frames)
 
 
 def cvt_gray(img: np.ndarray, pix: int) -> np.ndarray:

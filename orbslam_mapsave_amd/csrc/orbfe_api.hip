@@ -166,6 +166,8 @@ struct orbfe_extractor {
         }
     };
     Pinned pin_in, pin_kps, pin_desc, pin_n;
+    // Every buffer the capture embeds is either in g1_key (outputs, pinned staging) or is a
+    // plan / workspace buffer: set_plan and a growing ensure_frames drop the graph.
     hipGraphExec_t g1 = nullptr;
     const void* g1_key[8] = {};  // the buffers and plan the graph was captured with
     bool graph_broken = std::getenv("ORBFE_NO_GRAPH") != nullptr;  // capture failed once (or
@@ -256,6 +258,7 @@ struct orbfe_extractor {
         plan = std::move(g);
         planned = true;
         frames_cap = 0;  // workspace sizes depend on the plan
+        drop_graph();    // the captured launches embed the old plan's tables and buffers
         return ORBFE_OK;
     }
 
@@ -275,6 +278,7 @@ struct orbfe_extractor {
         if ((st = oct_out.ensure(N * g.geo.out_total * sizeof(uint32_t)))) return st;
         if ((st = oct_cnt.ensure(N * g.geo.nlevels * sizeof(int)))) return st;
         frames_cap = n;
+        drop_graph();  // any workspace above may have moved
         return ORBFE_OK;
     }
 
@@ -598,10 +602,28 @@ int orbfe_get_features_per_level(const orbfe_extractor* h, int32_t* out) {
 
 int orbfe_keypoint_capacity(const orbfe_extractor* h) {
     if (!h) return ORBFE_ERR_ARG;
-    // per-level list bound max(N + 4, 20) (nIni <= 4 is enforced), summed over levels
+    // Sum over levels of the oct-tree list bound max(N + 4, 4 nIni, 20) (plan_geometry) at the
+    // largest nIni any supported input (w, h <= 4096) gives that level: a level with FAST
+    // cells has bh = h_l - 32 >= 30, so nIni <= round((round(4096 / s_l) - 32) / 30).
     int c = 0;
-    for (int l = 0; l < h->tab.p.nlevels; ++l) c += std::max(h->tab.nfeat[l] + 4, 20);
+    for (int l = 0; l < h->tab.p.nlevels; ++l) {
+        const int wl = (int)std::lrintf(4096.f * h->tab.inv[l]);
+        const int nini = std::max(1, (int)std::lround((double)(wl - 32) / 30.0));
+        c += std::max({h->tab.nfeat[l] + 4, 4 * nini, 20});
+    }
     return c;
+}
+
+int orbfe_keypoint_capacity_for(const orbfe_extractor* h, int w, int hgt) {
+    if (!h || w <= 0 || hgt <= 0) return ORBFE_ERR_ARG;
+    if (h->planned && h->plan.w == w && h->plan.h == hgt) return h->plan.geo.out_total;
+    try {
+        Plan g;
+        const int st = plan_geometry(h->tab, w, hgt, g);
+        return st != ORBFE_OK ? st : g.geo.out_total;
+    } catch (const std::bad_alloc&) {
+        return ORBFE_ERR_NOMEM;
+    }
 }
 
 static int extract_host_common(orbfe_extractor* h, const uint8_t* const* imgs, int n, int w,

@@ -1217,7 +1217,8 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
     if (bx == 0 && threadIdx.x == 0) {
         int n = 0;
         for (int l = 0; l < a.nlevels; ++l) n += max(cnt[l], 0);
-        a.n_out[f] = min(n, a.kps_cap);
+        a.n_out[f] = n;  // the true count: entries past kps_cap are not written (truncation
+                         // is visible to the caller as n_out > kps_cap)
     }
     const int s0 = (bx * (kDescBlock / 64) + (threadIdx.x >> 6)) * kDescGroup;
     if (s0 >= a.out_total) return;

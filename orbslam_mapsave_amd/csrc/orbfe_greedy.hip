@@ -35,6 +35,9 @@ struct GreedyArgs {
     float nnratio;
     const int* off;       // m + 1
     const int2* cand;     // (slot, dist | octave << 16)
+    long long cand_cap;   // entries the fill could write: a list ending past it was not
+                          // filled (the host then retries with the exact total), so it is
+                          // read as empty and never indexes past the buffer
     const int* nobs;      // per point; NULL: every point blocks (keyframe overload)
     const int* fmp0;      // slot contents before the call (-1 = NULL)
     const int* fobs0;     // their Observations(); NULL: any held point blocks
@@ -96,9 +99,18 @@ struct GreedyAcc {
     }
 };
 
+// [e0, e1) of point i's candidates, empty when the list was not filled (past cand_cap).
+__device__ __forceinline__ void greedy_range(const GreedyArgs& a, int i, int& e0, int& e1) {
+    e0 = a.off[i];
+    e1 = a.off[i + 1];
+    if (e1 > a.cand_cap) e1 = e0;
+}
+
 __device__ __forceinline__ int greedy_decide(const GreedyArgs& a, const int* Tc, int i) {
     GreedyAcc acc;
-    for (int e = a.off[i], e1 = a.off[i + 1]; e < e1; ++e) acc.add(a, Tc, i, a.cand[e]);
+    int e0, e1;
+    greedy_range(a, i, e0, e1);
+    for (int e = e0; e < e1; ++e) acc.add(a, Tc, i, a.cand[e]);
     return acc.result(a);
 }
 
@@ -110,8 +122,7 @@ struct CandCache {
     int2 c[kCandCache];
 };
 __device__ __forceinline__ void cand_cache_load(const GreedyArgs& a, int i, CandCache& cc) {
-    cc.e0 = a.off[i];
-    cc.e1 = a.off[i + 1];
+    greedy_range(a, i, cc.e0, cc.e1);
 #pragma unroll
     for (int k = 0; k < kCandCache; ++k) cc.c[k] = cc.e0 + k < cc.e1 ? a.cand[cc.e0 + k] : make_int2(0, 0);
 }

@@ -118,7 +118,10 @@ __global__ __launch_bounds__(kBfBlock) void bf_match_kernel(
     long long r_pitch, const int* nr_arr, int* out) {
     __shared__ i32x4 tile[2][16][kBfRefs];  // [buffer][2 * chunk + half][row]
     const int b = blockIdx.y;
-    const int nq = nq_arr[b], nr = nr_arr[b];
+    // counts above the slab capacities (an extraction reports its true count when it holds
+    // more keypoints than kps_cap) are clamped to the rows the slabs hold
+    const int nq = min(nq_arr[b], nq_cap);
+    const int nr = r_pitch >= 32 ? min((long long)nr_arr[b], r_pitch / 32) : nr_arr[b];
     if ((int)blockIdx.x * kBfBlock >= nq) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int col = lane & 31, h = lane >> 5;
@@ -504,6 +507,49 @@ __global__ __launch_bounds__(1024) void scan_kernel(const int* counts, int n, in
 }
 
 // ---------------------------------------------------------------------------------------------
+// Frame::GetFeaturesInArea (Frame.cc:445-498) as a batch of queries — the parity probe of the
+// grid (orbfe_features_in_area): both forms the matchers use, thread-per-query
+// (features_in_area, SearchByProjection local map) and wave-per-query (features_in_area_wave,
+// SearchForInitialization / last frame / keyframe), write each query's candidates in the
+// reference's order to items[off[q] ..).
+struct FiaArgs {
+    DevFrame f;
+    int nq;
+    const float* x;
+    const float* y;
+    const float* r;
+    const int* lo;
+    const int* hi;
+    int* cnt;
+    const int* off;
+    int* items;
+};
+template <bool FILL>
+__global__ __launch_bounds__(256) void fia_thread_kernel(FiaArgs a) {
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    if (q >= a.nq) return;
+    const int o = FILL ? a.off[q] : 0;
+    int n = 0;
+    features_in_area(a.f, a.x[q], a.y[q], a.r[q], a.lo[q], a.hi[q], [&](int idx) {
+        if (FILL) a.items[o + n] = idx;
+        ++n;
+    });
+    if (!FILL) a.cnt[q] = n;
+}
+template <bool FILL>
+__global__ __launch_bounds__(256) void fia_wave_kernel(FiaArgs a) {
+    const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= a.nq) return;
+    const int o = FILL ? a.off[q] : 0;
+    const int n = features_in_area_wave(
+        a.f, a.x[q], a.y[q], a.r[q], a.lo[q], a.hi[q], [](int) { return true; },
+        [&](int idx, int rank) {
+            if (FILL) a.items[o + rank] = idx;
+        });
+    if (!FILL && (threadIdx.x & 63) == 0) a.cnt[q] = n;
+}
+
+// ---------------------------------------------------------------------------------------------
 // SearchForInitialization (ORBmatcher.cc:408-523)
 struct SfiArgs {
     DevFrame f1, f2;
@@ -588,6 +634,8 @@ struct SfiRoundArgs {
     int n1, n2, k;          // k: list entries per slot
     const int* off;
     const int2* cand;       // (i2, dist) in GetFeaturesInArea order
+    long long cand_cap;     // a list ending past it was not filled: read as empty (the host
+                            // sees the total exceed the capacity and reruns the call)
     float nnratio;
     int* dec[2];            // round r reads dec[r & 1] (-2 before round 0), writes dec[~r & 1]
     int2* list[3];          // per slot kSfiSlotK acceptors (query, dist)
@@ -603,7 +651,8 @@ __global__ __launch_bounds__(256) void sfi_round_kernel(SfiRoundArgs a, int r) {
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= a.n1) return;
     const int lane = threadIdx.x & 63;
-    const int e0 = a.off[i], e1 = a.off[i + 1];
+    const int e0 = a.off[i];
+    const int e1 = a.off[i + 1] > a.cand_cap ? e0 : a.off[i + 1];
     if (e1 - e0 >= 65536) {
         if (lane == 0) atomicExch(a.status, ORBFE_ERR_UNSUPPORTED);
         return;

@@ -50,6 +50,7 @@ struct orbfe_matcher {
     DevBuf g_t0, g_t1, g_t2, g_dec, g_chg, g_last, g_bins, g_hist;  // greedy resolver
     Profiler prof;
     int last_rounds = 0;  // rounds the most recent greedy resolution took (diagnostics)
+    int capacity_retries = 0;  // calls rerun because the candidates outgrew the buffer
     bool rounds_on_device = false;  // single-workgroup form: the count sits in g_chg[0]
 
     ~orbfe_matcher() {
@@ -313,6 +314,9 @@ struct orbfe_matcher {
         g.bins = g_bins.as<int>();
         g.hist = g_hist.as<int>();
         g.nm = scal.as<int>();
+        // the fill's capacity: csr() sized it to the exact total; csr_async() and a device
+        // total (`total`) bound it, and lists past it were not filled
+        g.cand_cap = total ? (long long)cap : cand_check ? (long long)cand_cap_used : LLONG_MAX;
         if (M <= kGreedySmallMax && N <= kGreedySmallSlots && !total) {  // one workgroup
             hipLaunchKernelGGL(greedy_small_kernel, dim3(1), dim3(kGreedySmallBlock),
                                (size_t)4 * std::max(N, 1) * sizeof(int), stream, g);
@@ -379,6 +383,7 @@ int guarded(orbfe_matcher* m, F&& f) {
         const size_t need0 = m->cand_need;
         int st = f();
         if (st == ORBFE_ERR_CAPACITY && m->cand_need > need0) {  // candidates outgrew the bound
+            ++m->capacity_retries;
             m->begin();
             st = f();
         }
@@ -559,6 +564,7 @@ int orbfe_search_for_initialization(orbfe_matcher* m, float nnratio, int check_o
         r.n2 = n2;
         r.off = m->off.as<int>();
         r.cand = m->cand.as<int2>();
+        r.cand_cap = (long long)cap;
         r.nnratio = nnratio;
         r.dec[0] = m->g_dec.as<int>();
         r.dec[1] = r.dec[0] + std::max(n1, 1);
@@ -595,6 +601,7 @@ int orbfe_search_for_initialization(orbfe_matcher* m, float nnratio, int check_o
                     if (retried) return ORBFE_ERR_HIP;
                     if ((st = m->cand.ensure((size_t)total * sizeof(int2)))) return st;
                     retried = true;
+                    ++m->capacity_retries;
                     m->begin();
                     return attempt();
                 }
@@ -1016,6 +1023,7 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
         if (st == ORBFE_ERR_CAPACITY && !retried) {
             if ((st = m->cand.ensure((size_t)total * sizeof(int2)))) return st;
             retried = true;
+            ++m->capacity_retries;
             return attempt();
         }
         if (st) return st;
@@ -1028,6 +1036,57 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
         };
         return attempt();
     });
+}
+
+int orbfe_features_in_area(orbfe_matcher* m, const orbfe_frame_view* f, int nq, const float* x,
+                           const float* y, const float* r, const int32_t* min_level,
+                           const int32_t* max_level, int wave, int32_t* off, int32_t* items,
+                           int items_cap) {
+    if (!frame_ok(f) || nq < 0 || !off || items_cap < 0 || (items_cap && !items) ||
+        (nq && (!x || !y || !r || !min_level || !max_level)))
+        return ORBFE_ERR_ARG;
+    return guarded(m, [&]() {
+        int st;
+        FiaArgs a;
+        if ((st = m->up(m->m_f0, x, (size_t)nq * 4))) return st;
+        if ((st = m->up(m->m_f1, y, (size_t)nq * 4))) return st;
+        if ((st = m->up(m->m_f2, r, (size_t)nq * 4))) return st;
+        if ((st = m->up(m->m_i0, min_level, (size_t)nq * 4))) return st;
+        if ((st = m->up(m->m_i1, max_level, (size_t)nq * 4))) return st;
+        if ((st = m->frame(f, false, a.f))) return st;  // AssignFeaturesToGrid (flushes)
+        if ((st = m->cnt.ensure(std::max(nq, 1) * sizeof(int)))) return st;
+        if ((st = m->off.ensure((size_t)(nq + 1) * sizeof(int)))) return st;
+        a.nq = nq;
+        a.x = m->m_f0.as<float>();
+        a.y = m->m_f1.as<float>();
+        a.r = m->m_f2.as<float>();
+        a.lo = m->m_i0.as<int>();
+        a.hi = m->m_i1.as<int>();
+        a.cnt = m->cnt.as<int>();
+        a.off = m->off.as<int>();
+        const int blocks = std::max(1, wave ? (nq + 3) / 4 : (nq + 255) / 256);
+        if (wave) hipLaunchKernelGGL(fia_wave_kernel<false>, dim3(blocks), dim3(256), 0, m->stream, a);
+        else hipLaunchKernelGGL(fia_thread_kernel<false>, dim3(blocks), dim3(256), 0, m->stream, a);
+        hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, m->stream, m->cnt.as<int>(), nq,
+                           m->off.as<int>());
+        ORBFE_HIP(hipGetLastError());
+        if ((st = m->down(off, m->off, (size_t)(nq + 1) * 4))) return st;
+        if ((st = m->sync())) return st;
+        const int total = off[nq];
+        if (total > items_cap) return ORBFE_ERR_CAPACITY;
+        if ((st = m->s1.ensure((size_t)std::max(total, 1) * sizeof(int)))) return st;
+        a.items = m->s1.as<int>();
+        if (wave) hipLaunchKernelGGL(fia_wave_kernel<true>, dim3(blocks), dim3(256), 0, m->stream, a);
+        else hipLaunchKernelGGL(fia_thread_kernel<true>, dim3(blocks), dim3(256), 0, m->stream, a);
+        ORBFE_HIP(hipGetLastError());
+        m->begin();
+        if ((st = m->down(items, m->s1, (size_t)total * 4))) return st;
+        return m->sync();
+    });
+}
+
+int orbfe_matcher_capacity_retries(const orbfe_matcher* m) {
+    return m ? m->capacity_retries : ORBFE_ERR_ARG;
 }
 
 int orbfe_matcher_last_rounds(const orbfe_matcher* m) {

@@ -66,7 +66,7 @@ __global__ __launch_bounds__(kStereoRowsBlock) void stereo_rows_kernel(StereoArg
     __shared__ int cnt[kStereoMaxRows + 1];
     __shared__ int tmp[kStereoRowsBlock / 64];
     const int f = blockIdx.x;
-    const int nr = a.nr[f];
+    const int nr = min(a.nr[f], a.kps_cap);
     const orbfe_keypoint* kr = a.kr + (size_t)f * a.kps_cap;
     const int R = a.nrows;
     for (int y = threadIdx.x; y <= R; y += kStereoRowsBlock) cnt[y] = 0;
@@ -115,7 +115,7 @@ __global__ __launch_bounds__(kStereoBlock) void stereo_match_kernel(StereoArgs a
     const int f = blockIdx.y;
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int il = blockIdx.x * (kStereoBlock / 64) + wid;
-    const int nl = a.nl[f];
+    const int nl = min(a.nl[f], a.kps_cap);
     if (il >= nl) return;
     const size_t fo = (size_t)f * a.kps_cap;
     float* ur_out = a.u_right + fo;
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(kStereoFilterBlock) void stereo_filter_kernel(Stere
     __shared__ int hist[256];
     __shared__ int s_sel[2];
     const int f = blockIdx.x;
-    const int nl = a.nl[f];
+    const int nl = min(a.nl[f], a.kps_cap);
     const size_t fo = (size_t)f * a.kps_cap;
     const int* sad = a.sad + fo;
     if (threadIdx.x < 256) hist[threadIdx.x] = 0;

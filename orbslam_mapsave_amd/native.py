@@ -29,6 +29,7 @@ _lib: C.CDLL | None = None
 EXPORTED = [
     "orbfe_create", "orbfe_destroy", "orbfe_get_levels", "orbfe_get_scale_factor",
     "orbfe_get_scale_tables", "orbfe_get_features_per_level", "orbfe_keypoint_capacity",
+    "orbfe_keypoint_capacity_for",
     "orbfe_extract", "orbfe_extract_color", "orbfe_human_mask_rect", "orbfe_extract_batch",
     "orbfe_extract_batch_device", "orbfe_extract_color_batch_device", "orbfe_set_stream",
     "orbfe_synchronize", "orbfe_compute_stereo_matches", "orbfe_compute_stereo_matches_device",
@@ -39,7 +40,7 @@ EXPORTED = [
     "orbfe_search_by_projection_local", "orbfe_search_by_projection_last",
     "orbfe_search_by_projection_keyframe", "orbfe_distinctive_descriptors",
     "orbfe_distinctive_descriptors_device", "orbfe_search_local_points_device",
-    "orbfe_matcher_last_rounds", "orbfe_is_in_frustum", "orbfe_vocabulary_load_text",
+    "orbfe_matcher_last_rounds", "orbfe_matcher_capacity_retries", "orbfe_features_in_area", "orbfe_is_in_frustum", "orbfe_vocabulary_load_text",
     "orbfe_vocabulary_create", "orbfe_vocabulary_destroy", "orbfe_vocabulary_info",
     "orbfe_vocabulary_set_stream", "orbfe_bow_transform", "orbfe_bow_transform_batch_device",
     "orbfe_search_by_bow", "orbfe_search_by_bow_batch_device", "orbfe_archive_mat_bytes",
@@ -158,8 +159,14 @@ class ORBextractor:
         _check("orbfe_get_features_per_level", lib().orbfe_get_features_per_level(self._h, ptr(out)))
         return out
 
-    def capacity(self) -> int:
-        return lib().orbfe_keypoint_capacity(self._h)
+    def capacity(self, w: int | None = None, h: int | None = None) -> int:
+        """Keypoints per frame that can never overflow: for a w x h input when given
+        (orbfe_keypoint_capacity_for), else for every supported size."""
+        if w is None or h is None:
+            return lib().orbfe_keypoint_capacity(self._h)
+        c = lib().orbfe_keypoint_capacity_for(self._h, int(w), int(h))
+        _check("orbfe_keypoint_capacity_for", min(c, 0))
+        return c
 
     # ---- operator() (ORBextractor.cc:1042-1108)
     def __call__(self, image: np.ndarray, mask: np.ndarray | None = None):
@@ -175,7 +182,7 @@ class ORBextractor:
         h, w = image.shape
         stride = image.strides[0]
         m = None if mask is None or np.size(mask) == 0 else np.ascontiguousarray(mask, np.uint8)
-        cap = self.capacity()
+        cap = self.capacity(w, h)
         kps = np.zeros(cap, KEYPOINT_DTYPE)
         desc = np.zeros((cap, 32), np.uint8)
         n = C.c_int(0)
@@ -198,7 +205,7 @@ class ORBextractor:
             raise ValueError(f"pix {pix} needs {PIX_CHANNELS[pix]} channels, image has {cn}")
         m = None if mask is None or np.size(mask) == 0 else np.ascontiguousarray(mask, np.uint8)
         r = None if rect is None else (C.c_int32 * 4)(*rect)
-        cap = self.capacity()
+        cap = self.capacity(w, h)
         kps = np.zeros(cap, KEYPOINT_DTYPE)
         desc = np.zeros((cap, 32), np.uint8)
         n = C.c_int(0)
@@ -253,7 +260,7 @@ class ORBextractor:
         """Host batch: (n, h, w) uint8 -> (kps (n, cap), desc (n, cap, 32), counts (n,))."""
         images = np.ascontiguousarray(images, np.uint8)
         n, h, w = images.shape
-        cap = self.capacity()
+        cap = self.capacity(w, h)
         kps = np.zeros((n, cap), KEYPOINT_DTYPE)
         desc = np.zeros((n, cap, 32), np.uint8)
         cnt = np.zeros(n, np.int32)
@@ -604,6 +611,32 @@ class ORBmatcher:
 
     def last_rounds(self) -> int:
         return lib().orbfe_matcher_last_rounds(self._h)
+
+    def GetFeaturesInArea(self, F: Frame, x, y, r, min_level=-1, max_level=-1, wave=False):
+        """Frame::GetFeaturesInArea (Frame.cc:445-498) for arrays of queries on F's grid
+        (orbfe_features_in_area).  Returns one int32 array of keypoint indices per query, in
+        the reference's candidate order."""
+        x = np.ascontiguousarray(np.atleast_1d(x), np.float32)
+        nq = len(x)
+        y = np.ascontiguousarray(np.broadcast_to(np.asarray(y, np.float32), (nq,)))
+        r = np.ascontiguousarray(np.broadcast_to(np.asarray(r, np.float32), (nq,)))
+        lo = np.ascontiguousarray(np.broadcast_to(np.asarray(min_level, np.int32), (nq,)))
+        hi = np.ascontiguousarray(np.broadcast_to(np.asarray(max_level, np.int32), (nq,)))
+        off = np.zeros(nq + 1, np.int32)
+        fv = F.view()
+        st = lib().orbfe_features_in_area(self._h, C.byref(fv), nq, ptr(x), ptr(y), ptr(r),
+                                          ptr(lo), ptr(hi), int(bool(wave)), ptr(off), None, 0)
+        items = np.zeros(max(int(off[nq]), 1), np.int32)
+        if st == ORBFE_ERR_CAPACITY:
+            st = lib().orbfe_features_in_area(self._h, C.byref(fv), nq, ptr(x), ptr(y), ptr(r),
+                                              ptr(lo), ptr(hi), int(bool(wave)), ptr(off),
+                                              ptr(items), len(items))
+        _check("orbfe_features_in_area", st)
+        return [items[off[q]:off[q + 1]].copy() for q in range(nq)]
+
+    def capacity_retries(self) -> int:
+        """Calls rerun because their candidates outgrew the device buffer (diagnostics)."""
+        return lib().orbfe_matcher_capacity_retries(self._h)
 
     def SearchByBoW(self, kf_desc, kf_angle, kf_mp_ok, kf_fv, f_desc, f_angle, f_fv):
         """SearchByBoW(KeyFrame*, Frame&, vpMapPointMatches) (ORBmatcher.cc:159-291); *_fv are

@@ -52,7 +52,7 @@ def test_gpu_archive_extracted_frames():
     dev = torch.device("cuda", 0)
     W, H, B = S.W, S.H, 3
     ex = ORBextractor(1000, 1.2, 8, 20, 7, device=0)
-    cap = ex.capacity()
+    cap = ex.capacity(W, H)
     imgs = np.stack([synthetic_frame(s, W, H) for s in range(B)])
     D = torch.from_numpy(imgs).to(dev)
     kps = torch.zeros((B, cap * 28), dtype=torch.uint8, device=dev)

@@ -152,7 +152,7 @@ def test_color_batch_device_unaligned():
     d_img = torch.from_numpy(buf).to(dev)
     d_m = torch.from_numpy(masks).to(dev)
     d_r = torch.from_numpy(rects).to(dev)
-    cap = e.capacity()
+    cap = e.capacity(w, h)
     d_k = torch.zeros((n, cap * 28), dtype=torch.uint8, device=dev)
     d_d = torch.zeros((n, cap, 32), dtype=torch.uint8, device=dev)
     d_n = torch.zeros(n, dtype=torch.int32, device=dev)

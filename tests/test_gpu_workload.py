@@ -30,7 +30,7 @@ def test_bench_workload_parity():
         e = ORBextractor(NF, 1.2, 8, 32, 7, device=0, max_width=W, max_height=H, max_batch=C)
         e.set_stream(streams[k].cuda_stream)
         exs.append(e)
-    cap = exs[0].capacity()
+    cap = exs[0].capacity(W, H)
     d_kps = torch.zeros((B, cap * 28), dtype=torch.uint8, device=dev)
     d_desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
     d_n = torch.zeros(B, dtype=torch.int32, device=dev)
@@ -95,7 +95,7 @@ def test_config4_workload_parity():
         e = ORBextractor(NF4, 1.2, 8, 32, 7, device=0, max_width=W4, max_height=H4, max_batch=C)
         e.set_stream(streams[k].cuda_stream)
         exs.append(e)
-    cap = exs[0].capacity()
+    cap = exs[0].capacity(W4, H4)
     d_kps = torch.zeros((B4, cap * 28), dtype=torch.uint8, device=dev)
     d_desc = torch.zeros((B4, cap, 32), dtype=torch.uint8, device=dev)
     d_n = torch.zeros(B4, dtype=torch.int32, device=dev)

@@ -165,7 +165,7 @@ def test_gpu_stereo_batch_device():
     Rs = torch.from_numpy(np.stack([b for _, b in pairs])).to(dev)
     el = ORBextractor(1000, 1.2, 8, 20, 7, device=0, max_width=w, max_height=h, max_batch=n)
     er = ORBextractor(1000, 1.2, 8, 20, 7, device=0, max_width=w, max_height=h, max_batch=n)
-    cap = el.capacity()
+    cap = el.capacity(w, h)
     out = {}
     for side, e, X in (("l", el, Ls), ("r", er, Rs)):
         k = torch.zeros((n, cap * 28), dtype=torch.uint8, device=dev)

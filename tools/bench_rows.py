@@ -78,7 +78,7 @@ def row_color():
     d_img = torch.from_numpy(cf).to(DEV)
     ex = native.ORBextractor(1000, 1.2, 8, 32, 7, device=0, max_width=W, max_height=H, max_batch=B)
     ex.set_stream(torch.cuda.current_stream(DEV).cuda_stream)
-    cap = ex.capacity()
+    cap = ex.capacity(W, H)
     k = torch.empty((B, cap * 28), dtype=torch.uint8, device=DEV)
     d = torch.empty((B, cap, 32), dtype=torch.uint8, device=DEV)
     n = torch.empty(B, dtype=torch.int32, device=DEV)
@@ -124,7 +124,7 @@ def row_stereo():
     s = torch.cuda.current_stream(DEV).cuda_stream
     el.set_stream(s)
     er.set_stream(s)
-    cap = el.capacity()
+    cap = el.capacity(W, H)
     bufs = {}
     for side, e, X in (("l", el, L), ("r", er, R)):
         kk = torch.empty((B, cap * 28), dtype=torch.uint8, device=DEV)
