@@ -86,6 +86,21 @@ orbfe_extractor* orbfe_create(const orbfe_params* params, int device, int max_wi
                               int max_height, int max_batch, int* status);
 void orbfe_destroy(orbfe_extractor* h);
 
+/* Which build of the reference's OpenCV 3.3 primitives the pixel arithmetic reproduces
+ * (tests/golden/README.md).  ORBFE_ARITH_SCALAR (the default): OpenCV's scalar
+ * paths — resize FixedPtCast<int,uchar,22>, blur FixedPtCastEx, uncontracted rotation products.
+ * ORBFE_ARITH_X86_SIMD: what an x86-64 build of the reference computes — the SSE2 bodies of
+ * VResizeLinearVec_32s8u (ORBextractor.cc:1123; ~18 % of the pixels of levels >= 1 differ
+ * by 1 from the scalar path) and SymmColumnVec_32s8u (1089; ties rounded to even) with the
+ * scalar tails past them, and the descriptor rotation FMA-contracted as GCC -O3 on an FMA host
+ * builds computeOrbDescriptor (117-119).  The oct-tree's heap-address tie order (H2) cannot
+ * be reproduced by any build and stays the documented creation-sequence rule.  Synchronizes
+ * the handle's stream; applies to later calls. */
+#define ORBFE_ARITH_SCALAR   0
+#define ORBFE_ARITH_X86_SIMD 1
+int orbfe_set_arithmetic(orbfe_extractor* h, int mode);
+int orbfe_get_arithmetic(const orbfe_extractor* h);
+
 /* Getters — ORBextractor::GetLevels / GetScaleFactor / GetScaleFactors /
  * GetInverseScaleFactors / GetScaleSigmaSquares / GetInverseScaleSigmaSquares
  * (ORBextractor.h:68-88).  Table outputs hold nlevels floats each; any may be NULL. */

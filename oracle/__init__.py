@@ -40,6 +40,31 @@ def _check(fn: str, st: int) -> None:
         raise OrbfeError(fn, st)
 
 
+# Build-dependent readings of the reference for the residual study (orb_oracle.h,
+# oracle/residuals.py); 0 is the pinned oracle every GPU test compares against.
+VAR_H2_ADDR, VAR_H4_COSF, VAR_H4_FMA, VAR_H5_SSE2, VAR_H6_SIMD = 1, 2, 4, 8, 16
+
+
+def set_variant(flags: int) -> None:
+    _check("oracle_set_variant", lib().oracle_set_variant(int(flags)))
+
+
+class variant:
+    """with oracle.variant(flags): ... — the oracle under another reading, restored on exit."""
+
+    def __init__(self, flags: int):
+        self.flags = flags
+
+    def __enter__(self):
+        self.prev = lib().oracle_get_variant()
+        set_variant(self.flags)
+        return self
+
+    def __exit__(self, *exc):
+        set_variant(self.prev)
+        return False
+
+
 def params(nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7) -> Params:
     return Params(nfeatures, scale_factor, nlevels, ini_th, min_th)
 

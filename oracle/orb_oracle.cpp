@@ -19,6 +19,9 @@
 //   H5  resize: scalar FixedPtCast<int,uchar,22> vertical pass everywhere;
 //   H6  blur: integer 8U smooth path ((sum + 2^15) >> 16) everywhere (no IPP, no float SIMD);
 //   H8  PredictScale log: (float)log((double)ratio), i.e. correctly rounded logf.
+// oracle_set_variant switches to the other build-dependent readings (H2 heap-address order,
+// H4 glibc cosf/sinf and FMA contraction, H5 SSE2 resize rounding, H6 SIMD blur rounding) for
+// the residual study only (oracle/residuals.py); the GPU is checked against variant 0.
 #include "orb_oracle.h"
 
 #include <algorithm>
@@ -46,6 +49,34 @@ inline short sat_short(float v) {
     return (short)std::min(std::max(iv, (int)SHRT_MIN), (int)SHRT_MAX);
 }
 inline uint8_t sat_u8(int v) { return (uint8_t)std::min(std::max(v, 0), 255); }
+
+// Build-dependent readings for the residual study; 0 = the pinned oracle.
+enum {
+    kVarH2Addr = 1,   // oct-tree phase-2 ties by real heap address (ORBextractor.cc:680-683)
+    kVarH4Cosf = 2,   // rBRIEF rotation with glibc cosf / sinf (std::cos(float), 111-112)
+    kVarH4Fma = 4,    // ... and x*b + y*a contracted as GCC -O3 -march=<FMA host> does (117-119)
+    kVarH5Sse2 = 8,   // resize vertical pass: OpenCV's SSE2 VResizeLinearVec_32s8u body
+    kVarH6Simd = 16,  // blur column pass: OpenCV's SSE2 SymmColumnVec_32s8u (float) body
+};
+int g_variant = 0;
+
+// Pixels [0, n) of a row that OpenCV 3.3's SSE2 vertical kernels produce (the rest goes to
+// the scalar tail): VResizeLinearVec_32s8u runs 16-pixel steps while x <= w - 16, then 4-pixel
+// steps while x < w - 4; SymmColumnVec_32s8u runs 16-pixel steps while i <= w - 16, then
+// 4-pixel steps while i <= w - 4.
+inline int sse2_body_resize(int w) {
+    int x = 0;
+    while (x <= w - 16) x += 16;
+    while (x < w - 4) x += 4;
+    return x;
+}
+inline int sse2_body_blur(int w) {
+    int i = 0;
+    while (i <= w - 16) i += 16;
+    while (i <= w - 4) i += 4;
+    return i;
+}
+inline int sat_s16(int v) { return std::min(std::max(v, -32768), 32767); }
 
 const int kPatchSize = 31;      // PATCH_SIZE      (ORBextractor.cc:71)
 const int kHalfPatch = 15;      // HALF_PATCH_SIZE (ORBextractor.cc:72)
@@ -150,7 +181,16 @@ void resize_linear(const uint8_t* src, int sw, int sh, size_t sstride, uint8_t* 
         hpass(r0, t0);
         hpass(r1, t1);
         uint8_t* d = dst + (size_t)dy * dstride;
-        for (int dx = 0; dx < dw; ++dx)  // FixedPtCast<int, uchar, 22>
+        int dx = 0;
+        if (g_variant & kVarH5Sse2) {  // H5: ((((T0>>4)*b0)>>16) + (((T1>>4)*b1)>>16) + 2) >> 2
+            const int xb = sse2_body_resize(dw);
+            for (; dx < xb; ++dx) {
+                const int x0 = sat_s16(t0[dx] >> 4), y0 = sat_s16(t1[dx] >> 4);
+                const int m = sat_s16(((x0 * (int)(short)b0) >> 16) + ((y0 * (int)(short)b1) >> 16));
+                d[dx] = sat_u8(sat_s16(m + 2) >> 2);
+            }
+        }
+        for (; dx < dw; ++dx)  // FixedPtCast<int, uchar, 22>
             d[dx] = sat_u8((t0[dx] * b0 + t1[dx] * b1 + (1 << 21)) >> 22);
     }
 }
@@ -190,12 +230,23 @@ void gaussian_blur(const uint8_t* src, int w, int h, size_t stride, uint8_t* dst
             rows[(size_t)y * w + x] = acc;
         }
     }
+    // H6: the SSE2 body sums k_j / 2^16 * R in float (every partial sum exact below 2^24) and
+    // converts with _mm_cvtps_epi32, i.e. rounds the same value half to EVEN; the scalar
+    // FixedPtCastEx rounds half up.  They differ only when acc % 2^16 == 2^15.
+    const int xb = (g_variant & kVarH6Simd) ? sse2_body_blur(w) : 0;
     for (int y = 0; y < h; ++y) {
         uint8_t* d = dst + (size_t)y * dstride;
         for (int x = 0; x < w; ++x) {
             int acc = 0;
             for (int j = 0; j < 7; ++j) acc += k[j] * rows[(size_t)reflect101(y + j - 3, h) * w + x];
-            d[x] = sat_u8((acc + (1 << 15)) >> 16);
+            if (x < xb) {
+                int q = acc >> 16;
+                const int rem = acc & 0xffff;
+                if (rem > 0x8000 || (rem == 0x8000 && (q & 1))) ++q;
+                d[x] = acc >= (1 << 24) ? 255 : sat_u8(q);
+            } else {
+                d[x] = sat_u8((acc + (1 << 15)) >> 16);
+            }
         }
     }
 }
@@ -299,8 +350,10 @@ void fast_detect(const uint8_t* img, int rows, int cols, size_t step, int thresh
 
 // ---------------------------------------------------------------------------------------------
 // A4 — per-cell FAST with the minThFAST fallback (ComputeKeyPointsOctTree, 764-831).
-void level_fast_keys(const Tables& t, const Plane& lev, std::vector<Key>& keys) {
+void level_fast_keys(const Tables& t, const Plane& lev, std::vector<Key>& keys,
+                     std::vector<int>* cell_counts = nullptr) {
     keys.clear();
+    if (cell_counts) cell_counts->clear();
     const float kW = 30;
     const int min_bx = kEdge - 3, min_by = min_bx;
     const int max_bx = lev.w - kEdge + 3, max_by = lev.h - kEdge + 3;
@@ -328,6 +381,7 @@ void level_fast_keys(const Tables& t, const Plane& lev, std::vector<Key>& keys) 
                 k.y += (float)(i * hcell);
                 keys.push_back(k);
             }
+            if (cell_counts) cell_counts->push_back((int)cell.size());
         }
     }
 }
@@ -450,6 +504,130 @@ std::vector<Key> distribute(const std::vector<Key>& in, int min_x, int max_x, in
     return result;
 }
 
+// H2 variant — the oct-tree with the reference's own heap objects, so that phase 2's
+// sort(pair<int, ExtractorNode*>) (680-683) orders equal sizes by real glibc addresses instead
+// of creation sequence.  RefNode has ExtractorNode's layout (ORBextractor.h:37-48: a vector of
+// 28-byte cv::KeyPoints, four cv::Point2i, a list iterator, a bool: 72 bytes, list node 88),
+// and the function performs the reference's allocations in the reference's order: the initial
+// nodes' reserve + push_back copies and the vKeys growth of the assignment loop (548-568); per
+// division four children reserving the parent's size (DivideNode 486-507), the push_front copy
+// of each non-empty child (list node first, then its exact-size vector), the parent's erase,
+// then the children's destruction in reverse declaration order (605-663, 694-736); the
+// size/pointer vectors (reserve 4 x nodes, the phase-2 copy); the result reserve.
+struct KP28 {  // cv::KeyPoint
+    float x, y, size, angle, response;
+    int octave, class_id;
+};
+struct RefNode {
+    std::vector<KP28> vKeys;
+    int UL[2], UR[2], BL[2], BR[2];
+    std::list<RefNode>::iterator lit;
+    bool bNoMore = false;
+
+    void divide(RefNode& n1, RefNode& n2, RefNode& n3, RefNode& n4) const {
+        const int hx = (int)std::ceil((float)(UR[0] - UL[0]) / 2);
+        const int hy = (int)std::ceil((float)(BR[1] - UL[1]) / 2);
+        auto set = [](int* p, int x, int y) { p[0] = x; p[1] = y; };
+        set(n1.UL, UL[0], UL[1]);          set(n1.UR, UL[0] + hx, UL[1]);
+        set(n1.BL, UL[0], UL[1] + hy);     set(n1.BR, UL[0] + hx, UL[1] + hy);
+        n1.vKeys.reserve(vKeys.size());
+        set(n2.UL, n1.UR[0], n1.UR[1]);    set(n2.UR, UR[0], UR[1]);
+        set(n2.BL, n1.BR[0], n1.BR[1]);    set(n2.BR, UR[0], UL[1] + hy);
+        n2.vKeys.reserve(vKeys.size());
+        set(n3.UL, n1.BL[0], n1.BL[1]);    set(n3.UR, n1.BR[0], n1.BR[1]);
+        set(n3.BL, BL[0], BL[1]);          set(n3.BR, n1.BR[0], BL[1]);
+        n3.vKeys.reserve(vKeys.size());
+        set(n4.UL, n3.UR[0], n3.UR[1]);    set(n4.UR, n2.BR[0], n2.BR[1]);
+        set(n4.BL, n3.BR[0], n3.BR[1]);    set(n4.BR, BR[0], BR[1]);
+        n4.vKeys.reserve(vKeys.size());
+        for (const KP28& k : vKeys) {
+            if (k.x < n1.UR[0]) (k.y < n1.BR[1] ? n1 : n3).vKeys.push_back(k);
+            else (k.y < n1.BR[1] ? n2 : n4).vKeys.push_back(k);
+        }
+        for (RefNode* c : {&n1, &n2, &n3, &n4})
+            if (c->vKeys.size() == 1) c->bNoMore = true;
+    }
+};
+
+std::vector<KP28> distribute_heap(const std::vector<KP28>& in, int min_x, int max_x, int min_y,
+                                  int max_y, int n_target, int nfeatures) {
+    const int n_ini = (int)std::round((float)(max_x - min_x) / (max_y - min_y));
+    const float hx = (float)(max_x - min_x) / n_ini;
+    std::list<RefNode> nodes;
+    std::vector<RefNode*> ini;
+    ini.resize(n_ini);
+    for (int i = 0; i < n_ini; ++i) {
+        RefNode ni;
+        ni.UL[0] = (int)(hx * (float)i);        ni.UL[1] = 0;
+        ni.UR[0] = (int)(hx * (float)(i + 1));  ni.UR[1] = 0;
+        ni.BL[0] = ni.UL[0];                    ni.BL[1] = max_y - min_y;
+        ni.BR[0] = ni.UR[0];                    ni.BR[1] = max_y - min_y;
+        ni.vKeys.reserve(in.size());
+        nodes.push_back(ni);
+        ini[i] = &nodes.back();
+    }
+    for (const KP28& k : in) ini[std::min((size_t)(k.x / hx), (size_t)n_ini - 1)]->vKeys.push_back(k);
+    for (auto it = nodes.begin(); it != nodes.end();) {
+        if (it->vKeys.size() == 1) { it->bNoMore = true; ++it; }
+        else if (it->vKeys.empty()) it = nodes.erase(it);
+        else ++it;
+    }
+    bool finish = false;
+    std::vector<std::pair<int, RefNode*>> size_ptr;
+    size_ptr.reserve(nodes.size() * 4);
+    // the non-empty children of a division, pushed to the front; expandable ones recorded
+    auto push_children = [&](RefNode& n1, RefNode& n2, RefNode& n3, RefNode& n4, int* n_expand) {
+        for (RefNode* c : {&n1, &n2, &n3, &n4}) {
+            if (c->vKeys.empty()) continue;
+            nodes.push_front(*c);
+            if (c->vKeys.size() > 1) {
+                if (n_expand) ++*n_expand;
+                size_ptr.push_back(std::make_pair((int)c->vKeys.size(), &nodes.front()));
+                nodes.front().lit = nodes.begin();
+            }
+        }
+    };
+    while (!finish) {
+        int prev = (int)nodes.size();
+        int n_expand = 0;
+        size_ptr.clear();
+        for (auto it = nodes.begin(); it != nodes.end();) {
+            if (it->bNoMore) { ++it; continue; }
+            RefNode n1, n2, n3, n4;
+            it->divide(n1, n2, n3, n4);
+            push_children(n1, n2, n3, n4, &n_expand);
+            it = nodes.erase(it);
+        }
+        if ((int)nodes.size() >= n_target || (int)nodes.size() == prev) {
+            finish = true;
+        } else if ((int)nodes.size() + n_expand * 3 > n_target) {
+            while (!finish) {
+                prev = (int)nodes.size();
+                std::vector<std::pair<int, RefNode*>> order = size_ptr;
+                size_ptr.clear();
+                std::sort(order.begin(), order.end());  // equal sizes: by address
+                for (int j = (int)order.size() - 1; j >= 0; --j) {
+                    RefNode n1, n2, n3, n4;
+                    order[j].second->divide(n1, n2, n3, n4);
+                    push_children(n1, n2, n3, n4, nullptr);
+                    nodes.erase(order[j].second->lit);
+                    if ((int)nodes.size() >= n_target) break;
+                }
+                if ((int)nodes.size() >= n_target || (int)nodes.size() == prev) finish = true;
+            }
+        }
+    }
+    std::vector<KP28> result;
+    result.reserve(nfeatures);
+    for (RefNode& n : nodes) {  // max response per node, first on ties (741-759)
+        const KP28* best = &n.vKeys[0];
+        for (size_t k = 1; k < n.vKeys.size(); ++k)
+            if (n.vKeys[k].response > best->response) best = &n.vKeys[k];
+        result.push_back(*best);
+    }
+    return result;
+}
+
 // ---------------------------------------------------------------------------------------------
 // A8 — IC_Angle (76-103) with cv::fastAtan2 (App. A.4).
 const float kAtanP1 = 0.9997878412794807f * (float)(180 / M_PI);
@@ -493,12 +671,23 @@ float ic_angle(const uint8_t* img, size_t step, float px, float py, const int* u
 
 // A10 — computeOrbDescriptor (107-146): 256 intensity tests on the blurred level.
 const float kDegToRad = (float)(M_PI / 180.f);
+}  // namespace
+extern "C" void oracle_rot_fma(float, int, const int*, int, int*, int*);
+extern "C" void oracle_rot_plain(float, int, const int*, int, int*, int*);
+namespace {
+
 void orb_descriptor(const uint8_t* img, size_t step, const Key& k, uint8_t* desc) {
     const float ang = k.angle * kDegToRad;
     const float a = (float)std::cos((double)ang), b = (float)std::sin((double)ang);
     const uint8_t* c = img + (size_t)cv_round(k.y) * step + cv_round(k.x);
     const long s = (long)step;
+    int vy[512], vx[512];  // H4 variants: offsets from oracle/variant_rot.cpp
+    const bool h4 = (g_variant & (kVarH4Cosf | kVarH4Fma)) != 0;
+    if (h4)
+        ((g_variant & kVarH4Fma) ? oracle_rot_fma : oracle_rot_plain)(
+            k.angle, (g_variant & kVarH4Cosf) != 0, kPattern, 512, vy, vx);
     auto sample = [&](int idx) {
+        if (h4) return (int)c[vy[idx] * s + vx[idx]];
         const float px = (float)kPattern[2 * idx], py = (float)kPattern[2 * idx + 1];
         return (int)c[cv_round(px * b + py * a) * s + cv_round(px * a - py * b)];
     };
@@ -555,6 +744,40 @@ void level_keypoints(const Tables& t, int level, const Plane& lev, std::vector<K
     for (Key& k : out) k.angle = ic_angle(lev.px.data(), lev.w, k.x, k.y, t.umax);
 }
 
+// H2 variant of level_keypoints: ComputeKeyPointsOctTree's per-level allocations (the
+// vToDistributeKeys reserve, one growing vKeysCell per cell, 777-828; allKeypoints[level]
+// reserve + copy-assignment of the result, 830-833) around distribute_heap.
+void level_keypoints_heap(const Tables& t, int level, const Plane& lev,
+                          std::vector<KP28>& all_level, std::vector<Key>& out) {
+    std::vector<Key> cand;
+    std::vector<int> counts;
+    level_fast_keys(t, lev, cand, &counts);
+    std::vector<KP28> to_distribute;
+    to_distribute.reserve((size_t)t.nfeatures * 10);
+    size_t k0 = 0;
+    for (int c : counts) {
+        std::vector<KP28> cell;
+        for (int i = 0; i < c; ++i) {
+            const Key& k = cand[k0 + i];
+            cell.push_back(KP28{k.x, k.y, 7.f, -1.f, k.response, 0, -1});
+        }
+        for (const KP28& k : cell) to_distribute.push_back(k);
+        k0 += c;
+    }
+    all_level.reserve(t.nfeatures);
+    const int min_b = kEdge - 3;
+    if (!to_distribute.empty())
+        all_level = distribute_heap(to_distribute, min_b, lev.w - kEdge + 3, min_b,
+                                    lev.h - kEdge + 3, t.nfeat[level], t.nfeatures);
+    out.clear();
+    for (const KP28& k : all_level) {
+        Key o{k.x + min_b, k.y + min_b, k.response};
+        o.octave = level;
+        out.push_back(o);
+    }
+    for (Key& k : out) k.angle = ic_angle(lev.px.data(), lev.w, k.x, k.y, t.umax);
+}
+
 int extract(const Tables& t, const uint8_t* img, int w, int h, size_t stride,
             const uint8_t* mask, size_t mstride, orbfe_keypoint* kps, int cap, uint8_t* desc,
             int* n_out) {
@@ -562,9 +785,12 @@ int extract(const Tables& t, const uint8_t* img, int w, int h, size_t stride,
     std::vector<Plane> pyr;
     build_pyramid(t, img, w, h, stride, mask, mstride, pyr);
     std::vector<std::vector<Key>> all(t.nlevels);
+    std::vector<std::vector<KP28>> all_heap;  // H2: allKeypoints.resize(nlevels) (766)
+    if (g_variant & kVarH2Addr) all_heap.resize(t.nlevels);
     int total = 0;
     for (int l = 0; l < t.nlevels; ++l) {
-        level_keypoints(t, l, pyr[l], all[l]);
+        if (g_variant & kVarH2Addr) level_keypoints_heap(t, l, pyr[l], all_heap[l], all[l]);
+        else level_keypoints(t, l, pyr[l], all[l]);
         total += (int)all[l].size();
     }
     if (n_out) *n_out = total;
@@ -717,6 +943,13 @@ int oracle_tables(const orbfe_params* p, float* scale, float* inv, float* sigma2
         for (int v = 0; v <= kHalfPatch; ++v) umax[v] = t.umax[v];
     return ORBFE_OK;
 }
+
+int oracle_set_variant(int flags) {
+    if (flags < 0 || flags > 31) return ORBFE_ERR_ARG;
+    g_variant = flags;
+    return ORBFE_OK;
+}
+int oracle_get_variant(void) { return g_variant; }
 
 int oracle_level_sizes(const orbfe_params* p, int w, int h, int32_t* lw, int32_t* lh) {
     Tables t;

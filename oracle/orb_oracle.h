@@ -26,6 +26,13 @@ int oracle_tables(const orbfe_params* p, float* scale, float* inv_scale, float* 
 /* Level sizes of the pyramid for a w x h input (ORBextractor.cc:1114-1115). */
 int oracle_level_sizes(const orbfe_params* p, int w, int h, int32_t* lw, int32_t* lh);
 
+/* Residual study only (oracle/residuals.py): switch to other build-dependent readings of the
+ * reference.  Bits: 1 H2 oct-tree ties by real heap address, 2 H4 glibc cosf/sinf, 4 H4 FMA
+ * contraction, 8 H5 SSE2 resize rounding, 16 H6 SIMD blur rounding; 0 = the pinned oracle the
+ * GPU is checked against.  Process-global, not thread-safe. */
+int oracle_set_variant(int flags);
+int oracle_get_variant(void);
+
 /* Full operator() (ORBextractor.cc:1042-1108). */
 int oracle_extract(const orbfe_params* p, const uint8_t* img, int w, int h, size_t stride,
                    const uint8_t* mask, size_t mask_stride, orbfe_keypoint* kps, int kps_cap,

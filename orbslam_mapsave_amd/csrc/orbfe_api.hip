@@ -124,6 +124,8 @@ struct orbfe_extractor {
     int device = 0;
     hipStream_t own = nullptr, stream = nullptr;
     HostTables tab{};
+    int arith = ORBFE_ARITH_SCALAR;  // orbfe_set_arithmetic
+    bool x86() const { return arith == ORBFE_ARITH_X86_SIMD; }
     Plan plan;
     bool planned = false;
     int frames_cap = 0;
@@ -310,6 +312,7 @@ struct orbfe_extractor {
             ra.lds_pitch = g.rs_pitch[l];
             ra.xt = xtab.as<int>() + g.xoff[l];
             ra.yt = ytab.as<int>() + g.yoff[l];
+            ra.simd_xb = x86() ? sse2_body_resize(ra.dw) : 0;
             ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resize_kernel, dim3(g.rs_tiles[l], n), dim3(256),
                          g.rs_lds[l], stream, ra);
         }
@@ -328,6 +331,7 @@ struct orbfe_extractor {
                 ta.xt[k] = xtab.as<int>() + g.xoff[l];
                 ta.yt[k] = ytab.as<int>() + g.yoff[l];
                 ta.dst[k] = lp[l];
+                ta.simd_xb[k] = x86() ? sse2_body_resize(ta.dw[k]) : 0;
             }
             ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resize_tail_kernel, dim3(n), dim3(kTailBlock), 0,
                          stream, ta);
@@ -380,6 +384,7 @@ struct orbfe_extractor {
             da.pyr[l] = lp[l];
             da.w[l] = g.geo.lv[l].w;
             da.h[l] = g.geo.lv[l].h;
+            da.simd_xb[l] = x86() ? sse2_body_blur(da.w[l]) : 0;
         }
         for (int i = 0; i < 4; ++i) da.taps[i] = tab.taps[i];
         da.oct_out = oct_out.as<uint32_t>();
@@ -389,16 +394,20 @@ struct orbfe_extractor {
         da.n_out = d_n;
         // a wave takes kDescGroupSize keypoints (the trig and pattern loads amortised over the
         // group); small batches take kDescGroupSmall, for four times the waves in flight
-        if (n >= kDescSmallBatch) {
-            const int per_block = (kDescBlockSize / 64) * kDescGroupSize;  // slots per workgroup
-            ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, describe_kernel<kDescGroupSize>,
-                         dim3((g.geo.out_total + per_block - 1) / per_block, n),
-                         dim3(kDescBlockSize), 0, stream, da);
+        // (x86 arithmetic: the rotation FMA-contracted, kFma)
+        const int group = n >= kDescSmallBatch ? kDescGroupSize : kDescGroupSmall;
+        const int per_block = (kDescBlockSize / 64) * group;  // slots per workgroup
+        const dim3 dgrid((g.geo.out_total + per_block - 1) / per_block, n);
+        if (group == kDescGroupSize) {
+            if (x86())
+                ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, (describe_kernel<kDescGroupSize, true>), dgrid, dim3(kDescBlockSize), 0, stream, da);
+            else
+                ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, (describe_kernel<kDescGroupSize, false>), dgrid, dim3(kDescBlockSize), 0, stream, da);
         } else {
-            const int per_block = (kDescBlockSize / 64) * kDescGroupSmall;
-            ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, describe_kernel<kDescGroupSmall>,
-                         dim3((g.geo.out_total + per_block - 1) / per_block, n),
-                         dim3(kDescBlockSize), 0, stream, da);
+            if (x86())
+                ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, (describe_kernel<kDescGroupSmall, true>), dgrid, dim3(kDescBlockSize), 0, stream, da);
+            else
+                ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, (describe_kernel<kDescGroupSmall, false>), dgrid, dim3(kDescBlockSize), 0, stream, da);
         }
         ORBFE_HIP(hipGetLastError());
         last_n = n;
@@ -578,6 +587,17 @@ void orbfe_destroy(orbfe_extractor* h) {
     hipStreamSynchronize(h->stream);
     delete h;
 }
+
+int orbfe_set_arithmetic(orbfe_extractor* h, int mode) {
+    if (!h || (mode != ORBFE_ARITH_SCALAR && mode != ORBFE_ARITH_X86_SIMD)) return ORBFE_ERR_ARG;
+    DeviceGuard dg(h->device);
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return ORBFE_ERR_HIP;
+    if (mode != h->arith) h->drop_graph();  // the captured launches carry the old mode
+    h->arith = mode;
+    return ORBFE_OK;
+}
+
+int orbfe_get_arithmetic(const orbfe_extractor* h) { return h ? h->arith : ORBFE_ERR_ARG; }
 
 int orbfe_get_levels(const orbfe_extractor* h) { return h ? h->tab.p.nlevels : ORBFE_ERR_ARG; }
 float orbfe_get_scale_factor(const orbfe_extractor* h) { return h ? h->tab.p.scale_factor : 0.f; }
@@ -1011,6 +1031,7 @@ int orbfe_get_blurred_level(orbfe_extractor* h, int frame, int level, uint8_t* o
             ba.h[l] = g.geo.lv[l].h;
             ba.src[l] = h->last_pyr[l];
             ba.dst[l] = LevelPtr{h->blur.as<uint8_t>() + g.geo.lv[l].off, g.slab, g.geo.lv[l].pitch};
+            ba.simd_xb[l] = h->x86() ? sse2_body_blur(g.geo.lv[l].w) : 0;
         }
         for (int i = 0; i < 4; ++i) ba.taps[i] = h->tab.taps[i];
         hipLaunchKernelGGL(blur_kernel, dim3(g.tiles_total, h->last_n), dim3(256), 0, h->stream, ba);

@@ -146,6 +146,20 @@ __global__ __launch_bounds__(256) void level0_kernel(Level0Args a) {
 // source rows/cols the tile touches are staged in LDS with dword loads, then each thread makes
 // 4 x 4 pixels from host-built tables xt[3*dx] = {sx, min(sx+1,sw-1), a0 | a1<<16} and
 // yt[3*dy] = {sy0, sy1 clipped, b0 | b1<<16}.
+// One output pixel of the vertical pass from the two horizontal sums t0, t1 (< 2^19) and the
+// row coefficients b0 + b1 = 2048.  Scalar FixedPtCast<int, uchar, 22>: the sum is never
+// negative, so only the upper clamp remains (the signed min(max(x >> 22, 0), 255) form can be
+// matched to gfx950's v_ashr_pk_u8_i32 for two of four bytes, and that packing was seen to
+// corrupt the upper two).  With `sse2` the x86 body of VResizeLinearVec_32s8u (H5):
+// ((((t0 >> 4) * b0) >> 16) + (((t1 >> 4) * b1) >> 16) + 2) >> 2, every operand < 2^24 (no
+// 16-bit saturation is reachable).  All products are full-rate v_mul_u32_u24.
+__device__ __forceinline__ uint32_t resize_px(uint32_t t0, uint32_t t1, uint32_t b0, uint32_t b1,
+                                              bool sse2) {
+    const uint32_t sc = (__umul24(t0, b0) + __umul24(t1, b1) + (1u << 21)) >> 22;
+    const uint32_t sv = ((__umul24(t0 >> 4, b0) >> 16) + (__umul24(t1 >> 4, b1) >> 16) + 2) >> 2;
+    return min(sse2 ? sv : sc, 255u);
+}
+
 constexpr int kRsTW = 128, kRsTH = 32;
 __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
@@ -226,12 +240,7 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
             // every product is a full-rate v_mul_u32_u24 (not the quarter-rate v_mul_lo_u32)
             const uint32_t t0 = __umul24(s0[x0[k]], a0[k]) + __umul24(s0[x1[k]], a1[k]);
             const uint32_t t1 = __umul24(s1[x0[k]], a0[k]) + __umul24(s1[x1[k]], a1[k]);
-            // FixedPtCast<int, uchar, 22>: the sum is never negative (pixels and coefficients
-            // are), so only the upper clamp remains, on the unsigned value.  The signed form
-            // min(max(x >> 22, 0), 255) can be matched to gfx950's v_ashr_pk_u8_i32 for two of
-            // the four bytes, and that packing was seen to corrupt the upper two bytes.
-            const uint32_t v = min((__umul24(t0, b0) + __umul24(t1, b1) + (1u << 21)) >> 22, 255u);
-            packed |= (uint32_t)v << (8 * k);
+            packed |= resize_px(t0, t1, b0, b1, x + k < a.simd_xb) << (8 * k);
         }
         uint8_t* d = dst + (long long)y * a.dst.pitch + x;
         if (n == 4) {
@@ -286,7 +295,7 @@ __global__ __launch_bounds__(kTailBlock) void resize_tail_kernel(ResizeTailArgs 
         const uint8_t* s = buf[k & 1];
         uint8_t* d = buf[(k + 1) & 1];
         const int sp_l = a.lp[k], dp_l = a.lp[k + 1];
-        const int dw = a.dw[k], dh = a.dh[k];
+        const int dw = a.dw[k], dh = a.dh[k], xb = a.simd_xb[k];
         const int* xt = a.xt[k];
         const int* yt = yts;
         for (int i = tid; i < 3 * dh; i += kTailBlock) yts[i] = a.yt[k][i];
@@ -319,8 +328,7 @@ __global__ __launch_bounds__(kTailBlock) void resize_tail_kernel(ResizeTailArgs 
                 for (int q = 0; q < 4; ++q) {
                     const uint32_t t0 = __umul24(s0[x0[q]], a0[q]) + __umul24(s0[x1[q]], a1[q]);
                     const uint32_t t1 = __umul24(s1[x0[q]], a0[q]) + __umul24(s1[x1[q]], a1[q]);
-                    const uint32_t v = min((__umul24(t0, b0) + __umul24(t1, b1) + (1u << 21)) >> 22, 255u);  // as in resize_kernel
-                    packed |= (uint32_t)v << (8 * q);
+                    packed |= resize_px(t0, t1, b0, b1, x + q < xb) << (8 * q);
                 }
                 *reinterpret_cast<uint32_t*>(d + y * dp_l + x) = packed;  // LDS pitch % 4 == 0
                 uint8_t* o = dst + (long long)y * dp.pitch + x;
@@ -1057,6 +1065,13 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Column-pass rounding.  The sums carry 0x7fff; the scalar FixedPtCastEx (sum + 2^15) >> 16
+// adds one more, the x86 SIMD body (H6: float sum, exact below 2^24, _mm_cvtps_epi32) rounds
+// half to even: (sum + 0x7fff + bit 16 of sum) >> 16.  v = sum + 0x7fff.
+__device__ __forceinline__ uint32_t blur_round_bit(uint32_t v, bool even) {
+    return even ? ((v - 0x7fffu) >> 16) & 1u : 1u;
+}
+
 // K4 — GaussianBlur(7x7, sigma 2, REFLECT_101) integer path: row pass R = sum k_i I (<= 65535,
 // kept as u16), column pass (sum k_j R + 2^15) >> 16 saturated (App. A.2).  128 x 32 output
 // tile per workgroup of 32 x 8 threads; each thread makes 4 x 4 pixels from dword LDS reads.
@@ -1155,6 +1170,9 @@ __global__ __launch_bounds__(256) void blur_kernel(BlurArgs a) {
     for (int i = 0; i < kBlurRPT / 2 + 3; ++i)
         Pq[i] = *reinterpret_cast<const uint4*>(rowp + (((kBlurRPT / 2) * lty + i) * kBlurTW + 4 * ltx) * 2);
     const int x = ox + 4 * ltx;
+    // x86 arithmetic: the 4 columns lie wholly in the SIMD body or wholly in the tail (both
+    // x and simd_xb are multiples of 4)
+    const bool even = x < a.simd_xb[l];
 #pragma unroll
     for (int j = 0; j < kBlurRPT; ++j) {
         const int y = oy + kBlurRPT * lty + j;
@@ -1167,17 +1185,17 @@ __global__ __launch_bounds__(256) void blur_kernel(BlurArgs a) {
                            p3 = (&Pq[b + 3].x)[c];
             uint32_t v;
             if ((j & 1) == 0) {
-                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T01, 1u << 15, false);
+                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T01, 0x7fffu, false);
                 v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), T23, v, false);
                 v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), T21, v, false);
                 v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), T0L, v, false);
             } else {
-                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T0H, 1u << 15, false);
+                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T0H, 0x7fffu, false);
                 v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), T12, v, false);
                 v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), T32, v, false);
                 v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), T10, v, false);
             }
-            acc[c] = min(v, 0xffffffu);  // byte 2 = min(acc >> 16, 255)
+            acc[c] = min(v + blur_round_bit(v, even), 0xffffffu);  // byte 2 = min(acc >> 16, 255)
         }
         const uint32_t packed = __builtin_amdgcn_perm(acc[1], acc[0], 0x0c0c0602u) |
                                 __builtin_amdgcn_perm(acc[3], acc[2], 0x06020c0cu);
@@ -1208,7 +1226,7 @@ constexpr int kDescWinRows = 2 * kDescWinR + 1;      // 37
 constexpr int kDescWinP = 48;                        // bytes per window row (3 x 16)
 constexpr int kDescWinBytes = kDescWinRows * kDescWinP;
 typedef float float2v __attribute__((ext_vector_type(2)));
-template <int kDescGroup>
+template <int kDescGroup, bool kFma>
 __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
     int bx, f;
     xcd_block(bx, f);
@@ -1332,9 +1350,11 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
     // window is assembled byte by byte with reflect101 indices instead.  Then blur_kernel's
     // integer passes: rows by v_dot4 into u16 row pairs, columns by v_dot2 + 2^15 >> 16.
     uint32_t my_kc = 0;
+    int my_x0 = 0;
     if (valid) {
         const int x = key_x((uint32_t)my_key);
         const int x0 = (x - kDescWinR) & ~3;
+        my_x0 = x0;
         my_kc = (uint32_t)(kDescWinR * kDescWinP + (x - x0)) - 0x400000u * kDescWinP - 0x4b400000u;
     }
     // Pattern pairs lane + 64 q as 4 packed int8 (x1, y1, x2, y2), widened to float per
@@ -1446,7 +1466,11 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
         // the row pass
         int cq = lane % kBlurQ;
         int wq = 2 * (lane / kBlurQ) * kDescWinP + 4 * cq;  // byte offset of (row 2jp, quad q)
+        // x86 arithmetic: window quad cq is level columns x0 + 4 cq ..; x0 and simd_xb are
+        // multiples of 4, so a quad is wholly SIMD body or tail
+        const int xq = (int)__builtin_amdgcn_readlane(my_x0, j) - a.simd_xb[(int)__builtin_amdgcn_readlane(my_l, j)];
         for (int it = lane; it < ((kDescWinRows + 1) / 2) * kBlurQ; it += 64) {
+            const bool even = xq + 4 * cq < 0;
             uint4 P4[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) P4[i] = *reinterpret_cast<const uint4*>(rowp + 4 * it + i * kRowpP);
@@ -1454,16 +1478,16 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 const uint32_t p0 = (&P4[0].x)[c], p1 = (&P4[1].x)[c], p2 = (&P4[2].x)[c], p3 = (&P4[3].x)[c];
-                uint32_t v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T01, 1u << 15, false);
+                uint32_t v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T01, 0x7fffu, false);
                 v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), T23, v, false);
                 v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), T21, v, false);
                 v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), T0L, v, false);
-                ev[c] = min(v, 0xffffffu);  // byte 2 = min(acc >> 16, 255)
-                uint32_t u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T0H, 1u << 15, false);
+                ev[c] = min(v + blur_round_bit(v, even), 0xffffffu);  // byte 2 = min(acc >> 16, 255)
+                uint32_t u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T0H, 0x7fffu, false);
                 u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), T12, u, false);
                 u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), T32, u, false);
                 u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), T10, u, false);
-                od[c] = min(u, 0xffffffu);
+                od[c] = min(u + blur_round_bit(u, even), 0xffffffu);
             }
             *reinterpret_cast<uint32_t*>(wb + wq) =
                 __builtin_amdgcn_perm(ev[1], ev[0], 0x0c0c0602u) | __builtin_amdgcn_perm(ev[3], ev[2], 0x06020c0cu);
@@ -1488,8 +1512,16 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
 #pragma unroll
             for (int c = 0; c < 4; ++c)
                 pat[4 * q + c] = (float)(int)(int8_t)(uint8_t)((uint32_t)patw[q] >> (8 * c));
-            const float2v r0 = (pat[4 * q] * SC + pat[4 * q + 1] * CSn) + MG;
-            const float2v r1 = (pat[4 * q + 2] * SC + pat[4 * q + 3] * CSn) + MG;
+            // kFma (x86 arithmetic, H4): x*b + y*a as a GCC -O3 build on an FMA host contracts
+            // it, fma(x, b, y*a) and fma(x, a, -(y*b)) (oracle/variant_rot.cpp)
+            float2v r0, r1;
+            if constexpr (kFma) {
+                r0 = __builtin_elementwise_fma(float2v{pat[4 * q], pat[4 * q]}, SC, pat[4 * q + 1] * CSn) + MG;
+                r1 = __builtin_elementwise_fma(float2v{pat[4 * q + 2], pat[4 * q + 2]}, SC, pat[4 * q + 3] * CSn) + MG;
+            } else {
+                r0 = (pat[4 * q] * SC + pat[4 * q + 1] * CSn) + MG;
+                r1 = (pat[4 * q + 2] * SC + pat[4 * q + 3] * CSn) + MG;
+            }
             // (__builtin_bit_cast of an ext-vector element reads element 0 in this clang:
             // go through __float_as_uint on copied scalars)
             const float r0y = r0.x, r0x = r0.y, r1y = r1.x, r1x = r1.y;

@@ -75,6 +75,7 @@ struct ResizeArgs {
     int tiles_x, lds_pitch;
     const int* xt;
     const int* yt;
+    int simd_xb;           // x86 arithmetic: columns [0, simd_xb) use the SSE2 rounding (H5)
 };
 
 struct ResizeTailArgs {
@@ -87,6 +88,7 @@ struct ResizeTailArgs {
     const int* xt[kMaxLevels];
     const int* yt[kMaxLevels];
     LevelPtr dst[kMaxLevels];
+    int simd_xb[kMaxLevels];      // per tail level, as ResizeArgs::simd_xb
 };
 
 struct FastArgs {
@@ -121,6 +123,7 @@ struct BlurArgs {
     int taps[4];
     LevelPtr src[kMaxLevels];
     LevelPtr dst[kMaxLevels];
+    int simd_xb[kMaxLevels];  // x86 arithmetic: columns [0, simd_xb) round half to even (H6)
 };
 
 struct DescArgs {
@@ -135,7 +138,25 @@ struct DescArgs {
     orbfe_keypoint* kps;
     uint8_t* desc;
     int32_t* n_out;
+    int simd_xb[kMaxLevels];  // as BlurArgs::simd_xb, for the fused per-keypoint blur
 };
+
+// Pixels [0, n) of a w-pixel row that OpenCV 3.3's x86 SSE2 vertical kernels produce (the rest
+// is the scalar tail): VResizeLinearVec_32s8u steps 16 while x <= w - 16, then 4 while
+// x < w - 4; SymmColumnVec_32s8u steps 16 while i <= w - 16, then 4 while i <= w - 4.  Both
+// are multiples of 4.
+inline int sse2_body_resize(int w) {
+    int x = 0;
+    while (x <= w - 16) x += 16;
+    while (x < w - 4) x += 4;
+    return x;
+}
+inline int sse2_body_blur(int w) {
+    int i = 0;
+    while (i <= w - 16) i += 16;
+    while (i <= w - 4) i += 4;
+    return i;
+}
 
 // Host-side ctor tables (ORBextractor.cc:409-469) + blur taps.
 struct HostTables {
@@ -176,7 +197,7 @@ template <int kP> __global__ void fast_kernel(FastArgs);
 constexpr int kFastPitch = 48;  // fast_kernel<kFastPitch>: ROI pitch known at compile time
 __global__ void octree_kernel(OctArgs);
 __global__ void blur_kernel(BlurArgs);
-template <int kDescGroup> __global__ void describe_kernel(DescArgs);
+template <int kDescGroup, bool kFma> __global__ void describe_kernel(DescArgs);
 extern __constant__ int c_umax[16];
 
 constexpr int kFastBlockSize = 64;

@@ -29,7 +29,7 @@ _lib: C.CDLL | None = None
 EXPORTED = [
     "orbfe_create", "orbfe_destroy", "orbfe_get_levels", "orbfe_get_scale_factor",
     "orbfe_get_scale_tables", "orbfe_get_features_per_level", "orbfe_keypoint_capacity",
-    "orbfe_keypoint_capacity_for",
+    "orbfe_keypoint_capacity_for", "orbfe_set_arithmetic", "orbfe_get_arithmetic",
     "orbfe_extract", "orbfe_extract_color", "orbfe_human_mask_rect", "orbfe_extract_batch",
     "orbfe_extract_batch_device", "orbfe_extract_color_batch_device", "orbfe_set_stream",
     "orbfe_synchronize", "orbfe_compute_stereo_matches", "orbfe_compute_stereo_matches_device",
@@ -158,6 +158,14 @@ class ORBextractor:
         out = np.zeros(self.nlevels, np.int32)
         _check("orbfe_get_features_per_level", lib().orbfe_get_features_per_level(self._h, ptr(out)))
         return out
+
+    ARITH_SCALAR, ARITH_X86_SIMD = 0, 1
+
+    def set_arithmetic(self, mode: int) -> None:
+        """orbfe_set_arithmetic: ARITH_SCALAR (OpenCV's scalar paths, the default) or
+        ARITH_X86_SIMD (the SSE2 resize / blur bodies and FMA-contracted rotation of an x86
+        build of the reference)."""
+        _check("orbfe_set_arithmetic", lib().orbfe_set_arithmetic(self._h, int(mode)))
 
     def capacity(self, w: int | None = None, h: int | None = None) -> int:
         """Keypoints per frame that can never overflow: for a w x h input when given

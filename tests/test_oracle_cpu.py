@@ -49,6 +49,18 @@ def test_pattern_constants():
     assert v[:4].tolist() == [8, -3, 9, 5] and v[-4:].tolist() == [-1, -6, 0, -11]
 
 
+def test_pattern_matches_reference_fixture():
+    """include/orbfe_pattern.inc (compiled into the kernels and the oracle) equals the
+    reference's bit_pattern_31_ (ORBextractor.cc:149-407) value for value, as read from the
+    reference text by tests/golden/make_pattern_fixture.py."""
+    import json
+    d = os.path.dirname(__file__)
+    fx = json.load(open(os.path.join(d, "golden", "pattern_fixture.json")))
+    txt = open(os.path.join(d, "..", "include", "orbfe_pattern.inc")).read().split("*/", 1)[1]
+    v = [int(x) for x in txt.replace(",", " ").split()]
+    assert fx["count"] == 1024 and v == fx["values"]
+
+
 def test_fast_atan2_known_answers():
     y = np.array([0, 1, 0, -1, 1, -1, 3, 0], np.float32)
     x = np.array([1, 0, -1, 0, 1, -1, -4, 0], np.float32)
