@@ -313,8 +313,12 @@ struct orbfe_extractor {
             ra.xt = xtab.as<int>() + g.xoff[l];
             ra.yt = ytab.as<int>() + g.yoff[l];
             ra.simd_xb = x86() ? sse2_body_resize(ra.dw) : 0;
-            ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resize_kernel, dim3(g.rs_tiles[l], n), dim3(256),
-                         g.rs_lds[l], stream, ra);
+            if (x86())
+                ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resize_kernel<true>, dim3(g.rs_tiles[l], n),
+                             dim3(256), g.rs_lds[l], stream, ra);
+            else
+                ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resize_kernel<false>, dim3(g.rs_tiles[l], n),
+                             dim3(256), g.rs_lds[l], stream, ra);
         }
         if (ts < L) {
             ResizeTailArgs ta;
@@ -333,8 +337,12 @@ struct orbfe_extractor {
                 ta.dst[k] = lp[l];
                 ta.simd_xb[k] = x86() ? sse2_body_resize(ta.dw[k]) : 0;
             }
-            ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resize_tail_kernel, dim3(n), dim3(kTailBlock), 0,
-                         stream, ta);
+            if (x86())
+                ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resize_tail_kernel<true>, dim3(n),
+                             dim3(kTailBlock), 0, stream, ta);
+            else
+                ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resize_tail_kernel<false>, dim3(n),
+                             dim3(kTailBlock), 0, stream, ta);
         }
         // K2 FAST per cell
         const int ncells = (int)g.cells.size();

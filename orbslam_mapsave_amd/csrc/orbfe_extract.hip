@@ -153,14 +153,17 @@ __global__ __launch_bounds__(256) void level0_kernel(Level0Args a) {
 // corrupt the upper two).  With `sse2` the x86 body of VResizeLinearVec_32s8u (H5):
 // ((((t0 >> 4) * b0) >> 16) + (((t1 >> 4) * b1) >> 16) + 2) >> 2, every operand < 2^24 (no
 // 16-bit saturation is reachable).  All products are full-rate v_mul_u32_u24.
+template <bool kX86>
 __device__ __forceinline__ uint32_t resize_px(uint32_t t0, uint32_t t1, uint32_t b0, uint32_t b1,
                                               bool sse2) {
     const uint32_t sc = (__umul24(t0, b0) + __umul24(t1, b1) + (1u << 21)) >> 22;
+    if constexpr (!kX86) return min(sc, 255u);
     const uint32_t sv = ((__umul24(t0 >> 4, b0) >> 16) + (__umul24(t1 >> 4, b1) >> 16) + 2) >> 2;
     return min(sse2 ? sv : sc, 255u);
 }
 
 constexpr int kRsTW = 128, kRsTH = 32;
+template <bool kX86>
 __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
     int bx, f;
@@ -240,7 +243,7 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
             // every product is a full-rate v_mul_u32_u24 (not the quarter-rate v_mul_lo_u32)
             const uint32_t t0 = __umul24(s0[x0[k]], a0[k]) + __umul24(s0[x1[k]], a1[k]);
             const uint32_t t1 = __umul24(s1[x0[k]], a0[k]) + __umul24(s1[x1[k]], a1[k]);
-            packed |= resize_px(t0, t1, b0, b1, x + k < a.simd_xb) << (8 * k);
+            packed |= resize_px<kX86>(t0, t1, b0, b1, x + k < a.simd_xb) << (8 * k);
         }
         uint8_t* d = dst + (long long)y * a.dst.pitch + x;
         if (n == 4) {
@@ -259,6 +262,7 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
 constexpr int kTailBlock = 1024;
 constexpr int kTailLds = 144 * 1024;
 constexpr int kTailRows = 512;  // rows of a tail level whose y table is staged in LDS
+template <bool kX86>
 __global__ __launch_bounds__(kTailBlock) void resize_tail_kernel(ResizeTailArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kTailLds];
     const int f = blockIdx.x;
@@ -328,7 +332,7 @@ __global__ __launch_bounds__(kTailBlock) void resize_tail_kernel(ResizeTailArgs 
                 for (int q = 0; q < 4; ++q) {
                     const uint32_t t0 = __umul24(s0[x0[q]], a0[q]) + __umul24(s0[x1[q]], a1[q]);
                     const uint32_t t1 = __umul24(s1[x0[q]], a0[q]) + __umul24(s1[x1[q]], a1[q]);
-                    packed |= resize_px(t0, t1, b0, b1, x + q < xb) << (8 * q);
+                    packed |= resize_px<kX86>(t0, t1, b0, b1, x + q < xb) << (8 * q);
                 }
                 *reinterpret_cast<uint32_t*>(d + y * dp_l + x) = packed;  // LDS pitch % 4 == 0
                 uint8_t* o = dst + (long long)y * dp.pitch + x;
@@ -1226,7 +1230,7 @@ constexpr int kDescWinRows = 2 * kDescWinR + 1;      // 37
 constexpr int kDescWinP = 48;                        // bytes per window row (3 x 16)
 constexpr int kDescWinBytes = kDescWinRows * kDescWinP;
 typedef float float2v __attribute__((ext_vector_type(2)));
-template <int kDescGroup, bool kFma>
+template <int kDescGroup, bool kX86>
 __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
     int bx, f;
     xcd_block(bx, f);
@@ -1468,7 +1472,9 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
         int wq = 2 * (lane / kBlurQ) * kDescWinP + 4 * cq;  // byte offset of (row 2jp, quad q)
         // x86 arithmetic: window quad cq is level columns x0 + 4 cq ..; x0 and simd_xb are
         // multiples of 4, so a quad is wholly SIMD body or tail
-        const int xq = (int)__builtin_amdgcn_readlane(my_x0, j) - a.simd_xb[(int)__builtin_amdgcn_readlane(my_l, j)];
+        const int xq = kX86 ? (int)__builtin_amdgcn_readlane(my_x0, j) - a.simd_xb[(int)__builtin_amdgcn_readlane(my_l, j)] : 0;
+        // the sums carry 0x7fff (x86: + the half-to-even bit on the SIMD body) or 2^15
+        constexpr uint32_t kRnd = kX86 ? 0x7fffu : 0x8000u;
         for (int it = lane; it < ((kDescWinRows + 1) / 2) * kBlurQ; it += 64) {
             const bool even = xq + 4 * cq < 0;
             uint4 P4[4];
@@ -1478,16 +1484,18 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 const uint32_t p0 = (&P4[0].x)[c], p1 = (&P4[1].x)[c], p2 = (&P4[2].x)[c], p3 = (&P4[3].x)[c];
-                uint32_t v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T01, 0x7fffu, false);
+                uint32_t v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T01, kRnd, false);
                 v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), T23, v, false);
                 v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), T21, v, false);
                 v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), T0L, v, false);
-                ev[c] = min(v + blur_round_bit(v, even), 0xffffffu);  // byte 2 = min(acc >> 16, 255)
-                uint32_t u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T0H, 0x7fffu, false);
+                if constexpr (kX86) v += blur_round_bit(v, even);
+                ev[c] = min(v, 0xffffffu);  // byte 2 = min(acc >> 16, 255)
+                uint32_t u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T0H, kRnd, false);
                 u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), T12, u, false);
                 u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), T32, u, false);
                 u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), T10, u, false);
-                od[c] = min(u + blur_round_bit(u, even), 0xffffffu);
+                if constexpr (kX86) u += blur_round_bit(u, even);
+                od[c] = min(u, 0xffffffu);
             }
             *reinterpret_cast<uint32_t*>(wb + wq) =
                 __builtin_amdgcn_perm(ev[1], ev[0], 0x0c0c0602u) | __builtin_amdgcn_perm(ev[3], ev[2], 0x06020c0cu);
@@ -1512,10 +1520,10 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
 #pragma unroll
             for (int c = 0; c < 4; ++c)
                 pat[4 * q + c] = (float)(int)(int8_t)(uint8_t)((uint32_t)patw[q] >> (8 * c));
-            // kFma (x86 arithmetic, H4): x*b + y*a as a GCC -O3 build on an FMA host contracts
+            // x86 arithmetic (H4): x*b + y*a as a GCC -O3 build on an FMA host contracts
             // it, fma(x, b, y*a) and fma(x, a, -(y*b)) (oracle/variant_rot.cpp)
             float2v r0, r1;
-            if constexpr (kFma) {
+            if constexpr (kX86) {
                 r0 = __builtin_elementwise_fma(float2v{pat[4 * q], pat[4 * q]}, SC, pat[4 * q + 1] * CSn) + MG;
                 r1 = __builtin_elementwise_fma(float2v{pat[4 * q + 2], pat[4 * q + 2]}, SC, pat[4 * q + 3] * CSn) + MG;
             } else {

@@ -191,13 +191,13 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g);
 
 // kernels (orbfe_extract.hip)
 __global__ void level0_kernel(Level0Args);
-__global__ void resize_kernel(ResizeArgs);
-__global__ void resize_tail_kernel(ResizeTailArgs);
+template <bool kX86> __global__ void resize_kernel(ResizeArgs);
+template <bool kX86> __global__ void resize_tail_kernel(ResizeTailArgs);
 template <int kP> __global__ void fast_kernel(FastArgs);
 constexpr int kFastPitch = 48;  // fast_kernel<kFastPitch>: ROI pitch known at compile time
 __global__ void octree_kernel(OctArgs);
 __global__ void blur_kernel(BlurArgs);
-template <int kDescGroup, bool kFma> __global__ void describe_kernel(DescArgs);
+template <int kDescGroup, bool kX86> __global__ void describe_kernel(DescArgs);
 extern __constant__ int c_umax[16];
 
 constexpr int kFastBlockSize = 64;
