@@ -130,7 +130,7 @@ struct orbfe_extractor {
     bool planned = false;
     int frames_cap = 0;
     DevBuf cells, xtab, ytab;
-    DevBuf pyr, blur, cell_cnt, cell_keys, keys, act, oct_out, oct_cnt;
+    DevBuf pyr, blur, cell_cnt, cell_keys, keys, act, oct_out, oct_cnt, level_keys;
     DevBuf out_kps, out_desc, out_n;  // staging for the host-pointer entry points
     DevBuf stage, rects;              // host colour frames / rectangle masks (level-0 inputs)
     DevBuf st_off, st_items, st_sad, st_status;           // stereo workspaces (left handle)
@@ -279,6 +279,9 @@ struct orbfe_extractor {
         if ((st = act.ensure(N * 2 * std::max<long long>(1, g.geo.key_total) * sizeof(int4)))) return st;
         if ((st = oct_out.ensure(N * g.geo.out_total * sizeof(uint32_t)))) return st;
         if ((st = oct_cnt.ensure(N * g.geo.nlevels * sizeof(int)))) return st;
+        if ((st = level_keys.ensure(N * kMaxLevels * sizeof(int)))) return st;
+        // the FAST kernel adds into these, the oct-tree kernel reads and clears them
+        ORBFE_HIP(hipMemsetAsync(level_keys.p, 0, N * kMaxLevels * sizeof(int), stream));
         frames_cap = n;
         drop_graph();  // any workspace above may have moved
         return ORBFE_OK;
@@ -358,6 +361,7 @@ struct orbfe_extractor {
             fa.cand_max = g.cand_max;
             fa.cell_cnt = cell_cnt.as<int>();
             fa.cell_keys = cell_keys.as<uint32_t>();
+            fa.level_keys = level_keys.as<int>();
             for (int l = 0; l < L; ++l) fa.pyr[l] = lp[l];
             if (g.roi_pitch == kFastPitch)
                 ORBFE_LAUNCH(prof, ORBFE_STAGE_FAST, fast_kernel<kFastPitch>, dim3(ncells, n), dim3(kFastBlockSize), g.fast_lds, stream, fa);
@@ -372,12 +376,14 @@ struct orbfe_extractor {
         oa.cell_cap_total = g.cell_cap_total;
         oa.cell_cnt = cell_cnt.as<int>();
         oa.cell_keys = cell_keys.as<uint32_t>();
+        oa.level_keys = level_keys.as<int>();
         oa.keys = keys.as<uint32_t>();
         oa.act = act.as<int4>();
         oa.oct_out = oct_out.as<uint32_t>();
         oa.oct_cnt = oct_cnt.as<int>();
         oa.ncap_max = g.ncap_max;
         oa.sort_cap = g.sort_cap;
+        oa.lds_keys = g.oct_keys;
         ORBFE_LAUNCH(prof, ORBFE_STAGE_OCTREE, octree_kernel, dim3(n, L), dim3(kOctBlockSize), g.oct_lds, stream, oa);
         // K4 (the blur) is fused into K5: each keypoint's window is blurred in LDS
         // K5 describe
@@ -528,7 +534,7 @@ struct orbfe_extractor {
 
     ~orbfe_extractor() {
         for (DevBuf* b : {&cells, &xtab, &ytab, &pyr, &blur, &cell_cnt, &cell_keys, &keys, &act,
-                          &oct_out, &oct_cnt, &out_kps, &out_desc, &out_n, &stage, &rects, &st_off, &st_items,
+                          &oct_out, &oct_cnt, &level_keys, &out_kps, &out_desc, &out_n, &stage, &rects, &st_off, &st_items,
                           &st_sad, &st_status, &st_kl, &st_dl, &st_kr, &st_dr, &st_n, &st_ur, &st_dp})
             b->release();
         drop_graph();

@@ -563,7 +563,12 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
         total = fast_emit(S, list, cnt, P, inv_p, t, cell, out, cell.cap);
         __syncthreads();
     }
-    if (lane == 0) a.cell_cnt[f * a.ncells + c] = min(total, cell.cap);
+    if (lane == 0) {
+        const int n = min(total, cell.cap);
+        a.cell_cnt[f * a.ncells + c] = n;
+        // the level's key total for the oct-tree (which reads it and resets it to 0)
+        if (n) atomicAdd(&a.level_keys[f * kMaxLevels + cell.level], n);
+    }
 }
 
 template __global__ void fast_kernel<0>(FastArgs);
@@ -578,11 +583,13 @@ template __global__ void fast_kernel<kFastPitch>(FastArgs);
 //   phase-2 round: the expandable nodes sorted by (size desc, creation seq desc) [H2] are
 //                 divided in that order until size >= N: new list = reverse(children in
 //                 processing order) ++ (untouched nodes, in order)     (675-736)
-// Keys stay in original order (cell-row-major, FAST emission order); each live key carries the
-// list position of its node.  Single-key nodes remember their key and drop out of the key set.
-// Final: per node the max response, first (lowest original index) on ties (741-759).
+// Keys stay in original order (cell-row-major, FAST emission order) in K; NODE[k] is the list
+// position of key k's node, or -1 once that node holds this key alone (it then remembers the
+// key itself).  Both live in LDS (kOctLdsKeys keys: every level of the bench configs, whose
+// FAST lists stay below ~3,300 keys), so every pass is a sweep of LDS reads and LDS atomics;
+// a level with more keys runs the same code on global arrays.  Final: per node the max
+// response, first (lowest original index) on ties (741-759).
 constexpr int kOctBlock = kOctBlockSize;
-constexpr int OCT_UNROLL = 4;
 
 struct OctLds {  // carve of the dynamic LDS region (sizes in elements)
     // two node lists (b = 0 / 1), 5 arrays of NC each: box x0 | x1 << 16, boy y0 | y1 << 16,
@@ -601,8 +608,9 @@ struct OctLds {  // carve of the dynamic LDS region (sizes in elements)
     int* aux2;
     unsigned long long* s64;  // sort keys (phase 2) / best response (final)
     int* tmp;
-    int* cellv;     // 2 x block: a chunk of cells' key offsets and slots (compaction)
     int* scal;      // scalars
+    uint32_t* keys;  // kOctLdsKeys packed keys (LDS form)
+    short* node;     // kOctLdsKeys node positions (LDS form)
 };
 
 __device__ __forceinline__ int quadrant(int box, int boy, int x, int y) {
@@ -621,116 +629,48 @@ __device__ __forceinline__ void child_box(int box, int boy, int q, int& cbx, int
     cby = cy0 | (cy1 << 16);
 }
 
-// Sweeps over a live-key list: every thread loads OCT_UNROLL entries before using any.
-template <class F>
-__device__ __forceinline__ void oct_sweep(const int4* list, int nact, F&& body) {
-    for (int e0 = threadIdx.x; e0 < nact; e0 += OCT_UNROLL * kOctBlock) {
-        int4 ens[OCT_UNROLL];
+// ORBFE_OCT_TIMING builds (tools/probe/oct_timing.py) record per-phase shader-clock stamps of
+// every (frame, level) tree: [0] start, [1] counted, [2] compacted, [3] initial nodes,
+// [4 + p] phase-1 pass p, [12 + r] phase-2 round r, [30] passes | rounds << 8, [31] end.
+#ifdef ORBFE_OCT_TIMING
+__device__ long long g_oct_t[256 * 16 * 32];
+#define OCT_MARK(tm, i) do { if (threadIdx.x == 0 && (tm)) (tm)[(i)] = clock64(); } while (0)
+#else
+#define OCT_MARK(tm, i) do { } while (0)
+#endif
+
+// Sweep over the live keys (NODE >= 0): body(k, packed key, node) for each.  A thread loads
+// kOctU keys and their nodes before using any, so their LDS round trips overlap.
+constexpr int kOctU = 4;
+template <class KT, class NT, class F>
+__device__ __forceinline__ void oct_sweep(const KT* K, const NT* NODE, int nkeys, F&& body) {
+    for (int k0 = threadIdx.x; k0 < nkeys; k0 += kOctU * kOctBlock) {
+        int node[kOctU];
+        uint32_t kk[kOctU];
 #pragma unroll
-        for (int u = 0; u < OCT_UNROLL; ++u) {
-            const int e = e0 + u * kOctBlock;
-            ens[u] = e < nact ? list[e] : make_int4(0, 0, -1, 0);
+        for (int u = 0; u < kOctU; ++u) {
+            const int k = k0 + u * kOctBlock;
+            node[u] = k < nkeys ? (int)NODE[k] : -1;
+            kk[u] = k < nkeys ? K[k] : 0u;
         }
 #pragma unroll
-        for (int u = 0; u < OCT_UNROLL; ++u)
-            if (ens[u].z >= 0) body(ens[u]);
+        for (int u = 0; u < kOctU; ++u)
+            if (node[u] >= 0) body(k0 + u * kOctBlock, kk[u], node[u]);
     }
 }
 
-// As oct_sweep; body sets the entry's node in the next list, and entries whose node still
-// holds >= 2 keys are appended to it.
-template <class F>
-__device__ __forceinline__ void oct_sweep_append(const int4* list, int4* next, int nact,
-                                                 const int* next_cnt, int* next_n, F&& body) {
-    for (int e0 = threadIdx.x; e0 < nact; e0 += OCT_UNROLL * kOctBlock) {
-        int4 ens[OCT_UNROLL];
-#pragma unroll
-        for (int u = 0; u < OCT_UNROLL; ++u) {
-            const int e = e0 + u * kOctBlock;
-            ens[u] = e < nact ? list[e] : make_int4(0, 0, -1, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < OCT_UNROLL; ++u) {
-            int np = 0;
-            if (ens[u].z >= 0) body(ens[u], np);
-            const bool live = ens[u].z >= 0 && next_cnt[np] >= 2;
-            const int slot = wave_append(live, next_n);
-            if (live) next[slot] = make_int4(ens[u].x, ens[u].y, np, 0);
-        }
-    }
-}
-
-__global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    // level-major block order: every frame's level-0 tree (the longest) is dispatched first,
-    // the small levels fill the remaining slots
-    const int level = blockIdx.y, f = blockIdx.x;
-    const LevelGeo& L = a.geo.lv[level];
-    const int NC = a.ncap_max;
+// The tree of one (frame, level) after its keys are in K (nkeys, original order).
+template <class KT, class NT>
+__device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds& s, const LevelGeo& L, KT* K,
+                             NT* NODE, int nkeys, uint32_t* out, int* out_cnt,
+                                              long long* tm) {
     const int tid = threadIdx.x;
-    OctLds s;
-    {
-        int* p = reinterpret_cast<int*>(lds_raw);
-        s.s64 = reinterpret_cast<unsigned long long*>(p);
-        p += 2 * a.sort_cap;
-        s.lists = p;
-        s.nc = NC;
-        p += 10 * NC;
-        s.qc = p; p += 4 * NC;
-        s.qk = p; p += 4 * NC;
-        s.aux = p; p += NC;
-        s.aux2 = p; p += NC;
-        s.tmp = p; p += 64;
-        s.cellv = p; p += 2 * kOctBlock;
-        s.scal = p;
-    }
-    uint32_t* out = a.oct_out + f * a.geo.out_total + L.out_off;
-    int* out_cnt = a.oct_cnt + f * a.geo.nlevels + level;
     const int ncap = L.ncap;
     const int N = L.nfeat;
-
-    // ---- 1. compact this level's cell outputs into original key order
-    uint32_t* K = a.keys + f * a.geo.key_total + L.key_off;
-    int nkeys = 0;
-    for (int base = L.cell_begin; base < L.cell_end; base += kOctBlock) {
-        const int c = base + tid;
-        const int n = c < L.cell_end ? a.cell_cnt[f * a.ncells + c] : 0;
-        int chunk_total;
-        const int off = block_exclusive_scan<kOctBlock>(n, s.tmp, chunk_total);
-        // cooperative copy: thread e takes key e of the chunk, found by a binary search over
-        // the cells' offsets (the last cell starting at or before e: empty cells before it
-        // share its offset), so no thread walks a cell's keys one dependent load at a time
-        s.cellv[tid] = off;
-        s.cellv[kOctBlock + tid] = c < L.cell_end ? a.cells[c].slot : 0;
-        __syncthreads();
-        const int ncell = min(kOctBlock, L.cell_end - base);
-        const uint32_t* src = a.cell_keys + f * a.cell_cap_total;
-        for (int e = tid; e < chunk_total; e += kOctBlock) {
-            int lo = 0, hi = ncell - 1;
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (s.cellv[mid] <= e) lo = mid; else hi = mid - 1;
-            }
-            K[nkeys + e] = src[s.cellv[kOctBlock + lo] + (e - s.cellv[lo])];
-        }
-        nkeys += chunk_total;
-        __syncthreads();  // cellv is rewritten by the next chunk
-    }
-    if (nkeys == 0 || L.nini < 1) {
-        if (tid == 0) *out_cnt = 0;
-        return;
-    }
-
-    // live keys {packed key, key index, node}: the key travels with its entry, so a sweep is
-    // one 16-byte load per key with OCT_UNROLL of them in flight per thread
-    int4* const act0 = a.act + f * a.geo.key_total * 2 + L.key_off * 2;
-    int4* const act1 = act0 + L.key_cap;
-#define ACT(b) ((b) ? act1 : act0)  // runtime-indexed pointer arrays would live in scratch
-    int* nact_sh = s.scal;        // scal[0..1]: active counters
-    int* flag_sh = s.scal + 2;    // scal[2]: overflow / misc
+    int* flag_sh = s.scal + 2;    // scal[2]: counters
     int* rmin_sh = s.scal + 3;    // scal[3]: phase-2 cut index
 
-    // ---- 2. initial nodes (542-584)
+    // ---- initial nodes (542-584)
     const int nini = L.nini;
     const float hX = L.hx;
     const int H = L.bh;
@@ -738,12 +678,9 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
         s.qc[i] = 0;
         s.qk[i] = -1;
     }
-    if (tid == 0) { nact_sh[0] = 0; nact_sh[1] = 0; flag_sh[0] = 0; }
     __syncthreads();
     for (int k = tid; k < nkeys; k += kOctBlock) {
-        const uint32_t kk = K[k];
-        const int x = key_x(kk);
-        const int node = min((int)((float)x / hX), nini - 1);  // vpIniNodes[kp.pt.x/hX] (568)
+        const int node = min((int)((float)key_x(K[k]) / hX), nini - 1);  // vpIniNodes[kp.pt.x/hX] (568)
         atomicAdd(&s.qc[node], 1);
         s.qk[node] = k;
     }
@@ -771,36 +708,31 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
         size = total;
     }
     __syncthreads();
-    for (int k0 = 0; k0 < nkeys; k0 += kOctBlock) {
-        const int k = k0 + tid;
-        const uint32_t kk = k < nkeys ? K[k] : 0u;
-        const int node = k < nkeys ? s.aux[min((int)((float)key_x(kk) / hX), nini - 1)] : 0;
-        const bool live = k < nkeys && s.cnt(0)[node] >= 2;
-        const int slot = wave_append(live, &nact_sh[0]);
-        if (live) ACT(0)[slot] = make_int4((int)kk, k, node, 0);
+    for (int k = tid; k < nkeys; k += kOctBlock) {
+        const int node = s.aux[min((int)((float)key_x(K[k]) / hX), nini - 1)];
+        NODE[k] = s.cnt(0)[node] >= 2 ? node : -1;
     }
     __syncthreads();
+    OCT_MARK(tm, 3);
     int cur = 0;
-    int nact = nact_sh[0];
     int seq_base = nini;
     bool finished = false;
     bool phase2 = false;
-    __syncthreads();
+    int npass = 0, nround = 0;
 
-    // ---- 3. phase 1: split every open node per pass (593-671)
+    // ---- phase 1: split every open node per pass (593-671)
     for (int pass = 0; pass < 64 && !finished && !phase2; ++pass) {
         const int prev = size;
         const int nxt = cur ^ 1;
         for (int i = tid; i < 4 * size; i += kOctBlock) s.qc[i] = 0;
-        if (tid == 0) nact_sh[nxt] = 0;
         __syncthreads();
         {
             const int *bx = s.box(cur), *by = s.boy(cur);
             int *qc = s.qc, *qk = s.qk;
-            oct_sweep(ACT(cur), nact, [=](const int4 en) {
-                const int q = quadrant(bx[en.z], by[en.z], key_x(en.x), key_y(en.x));
-                atomicAdd(&qc[en.z * 4 + q], 1);
-                qk[en.z * 4 + q] = en.y;
+            oct_sweep(K, NODE, nkeys, [=](int k, uint32_t kk, int node) {
+                const int q = quadrant(bx[node], by[node], key_x(kk), key_y(kk));
+                atomicAdd(&qc[node * 4 + q], 1);
+                qk[node * 4 + q] = k;
             });
         }
         __syncthreads();
@@ -821,17 +753,19 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
                     keep = 1;
                 }
             }
-            int t1, t2;
-            const int o1 = block_exclusive_scan<kOctBlock>(nch, s.tmp, t1);
-            const int o2 = block_exclusive_scan<kOctBlock>(keep, s.tmp, t2);
-            const int te = block_sum<kOctBlock>(ne, s.tmp);
+            // one scan for all three: children (bits 0-10), kept (11-19), expandable (20-30);
+            // a chunk of kOctBlock <= 256 nodes sums to <= 1024 / 256 / 1024, so no field
+            // carries into the next or into the sign bit
+            static_assert(kOctBlock <= 256, "scan packing assumes <= 256 threads");
+            int t;
+            const int o = block_exclusive_scan<kOctBlock>(nch | (keep << 11) | (ne << 20), s.tmp, t);
             if (i < size) {
-                s.aux[i] = csize + o1;
-                s.aux2[i] = ksize + o2;
+                s.aux[i] = csize + (o & 0x7ff);
+                s.aux2[i] = ksize + ((o >> 11) & 0x1ff);
             }
-            csize += t1;
-            ksize += t2;
-            nexp += te;
+            csize += t & 0x7ff;
+            ksize += (t >> 11) & 0x1ff;
+            nexp += t >> 20;
         }
         const int nsize = csize + ksize;
         if (nsize > ncap) {  // cannot happen for ncap >= max(N + 3, 4 * nIni)
@@ -868,29 +802,28 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
         }
         __syncthreads();
         {
-            const int *bx = s.box(cur), *by = s.boy(cur), *qk = s.qk;
-            oct_sweep_append(ACT(cur), ACT(nxt), nact, s.cnt(nxt), &nact_sh[nxt], [=](const int4 en, int& np) {
-                const int q = quadrant(bx[en.z], by[en.z], key_x(en.x), key_y(en.x));
-                np = qk[en.z * 4 + q];
+            const int *bx = s.box(cur), *by = s.boy(cur), *qk = s.qk, *ncnt = s.cnt(nxt);
+            oct_sweep(K, NODE, nkeys, [=](int k, uint32_t kk, int node) {
+                const int np = qk[node * 4 + quadrant(bx[node], by[node], key_x(kk), key_y(kk))];
+                NODE[k] = ncnt[np] >= 2 ? np : -1;
             });
         }
         __syncthreads();
-        nact = nact_sh[nxt];
         cur = nxt;
         size = nsize;
         seq_base += csize;
         if (size >= N || size == prev) finished = true;
         else if (size + nexp * 3 > N) phase2 = true;
-        __syncthreads();
+        OCT_MARK(tm, 4 + min(pass, 7));
+        ++npass;
     }
 
-    // ---- 4. phase 2: divide the biggest nodes first until the budget is reached (675-736)
+    // ---- phase 2: divide the biggest nodes first until the budget is reached (675-736)
     for (int round = 0; round < 64 && !finished; ++round) {
         const int prev = size;
         const int nxt = cur ^ 1;
         // expandable nodes -> sort keys (size desc, seq desc); carries the list position
-        if (tid == 0) { flag_sh[0] = 0; nact_sh[nxt] = 0; *rmin_sh = 0x7fffffff; }
-        for (int i = tid; i < 4 * size; i += kOctBlock) s.qc[i] = 0;
+        if (tid == 0) { flag_sh[0] = 0; *rmin_sh = 0x7fffffff; }
         __syncthreads();
         for (int i = tid; i < size; i += kOctBlock)
             if (s.cnt(cur)[i] >= 2) {
@@ -918,28 +851,30 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
             }
             __syncthreads();
         } else {
-            for (int i = m + tid; i < P; i += kOctBlock) s.s64[i] = 0ull;
+            // rank sort (the keys are distinct: seq is unique): an entry's rank is the number of
+            // larger keys; every thread scans all m keys (LDS broadcast reads), two barriers
+            // instead of a bitonic network's log2(P)(log2(P)+1)/2.  qc (4 NC ints) holds the
+            // sorted copy until it is cleared below.
+            unsigned long long* srt = reinterpret_cast<unsigned long long*>(s.qc);
+            for (int j = tid; j < m; j += kOctBlock) {
+                const unsigned long long v = s.s64[j];
+                int rank = 0;
+                for (int i = 0; i < m; ++i) rank += s.s64[i] > v;
+                srt[rank] = v;
+            }
             __syncthreads();
-            for (int k = 2; k <= P; k <<= 1)  // bitonic sort, descending
-                for (int j = k >> 1; j > 0; j >>= 1) {
-                    for (int i = tid; i < P; i += kOctBlock) {
-                        const int ij = i ^ j;
-                        if (ij > i) {
-                            const unsigned long long x = s.s64[i], y = s.s64[ij];
-                            const bool desc = (i & k) == 0;
-                            if (desc ? (x < y) : (x > y)) { s.s64[i] = y; s.s64[ij] = x; }
-                        }
-                    }
-                    __syncthreads();
-                }
+            for (int j = tid; j < m; j += kOctBlock) s.s64[j] = srt[j];
+            __syncthreads();
         }
+        for (int i = tid; i < 4 * size; i += kOctBlock) s.qc[i] = 0;
+        __syncthreads();
         {
             const int *bx = s.box(cur), *by = s.boy(cur);
             int *qc = s.qc, *qk = s.qk;
-            oct_sweep(ACT(cur), nact, [=](const int4 en) {
-                const int q = quadrant(bx[en.z], by[en.z], key_x(en.x), key_y(en.x));
-                atomicAdd(&qc[en.z * 4 + q], 1);
-                qk[en.z * 4 + q] = en.y;
+            oct_sweep(K, NODE, nkeys, [=](int k, uint32_t kk, int node) {
+                const int q = quadrant(bx[node], by[node], key_x(kk), key_y(kk));
+                atomicAdd(&qc[node * 4 + q], 1);
+                qk[node * 4 + q] = k;
             });
         }
         __syncthreads();
@@ -1027,34 +962,31 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
         }
         __syncthreads();
         {
-            const int *bx = s.box(cur), *by = s.boy(cur), *qk = s.qk, *aux = s.aux, *aux2 = s.aux2;
-            oct_sweep_append(ACT(cur), ACT(nxt), nact, s.cnt(nxt), &nact_sh[nxt], [=](const int4 en, int& np) {
-                if (aux2[en.z] > 0) {
-                    const int q = quadrant(bx[en.z], by[en.z], key_x(en.x), key_y(en.x));
-                    np = qk[en.z * 4 + q];
-                } else {
-                    np = aux[en.z];
-                }
+            const int *bx = s.box(cur), *by = s.boy(cur), *qk = s.qk, *aux = s.aux,
+                      *aux2 = s.aux2, *ncnt = s.cnt(nxt);
+            oct_sweep(K, NODE, nkeys, [=](int k, uint32_t kk, int node) {
+                const int np = aux2[node] > 0
+                                   ? qk[node * 4 + quadrant(bx[node], by[node], key_x(kk), key_y(kk))]
+                                   : aux[node];
+                NODE[k] = ncnt[np] >= 2 ? np : -1;
             });
         }
         __syncthreads();
-        nact = nact_sh[nxt];
         cur = nxt;
         size = nsize;
         seq_base += csize;
         if (size >= N || size == prev) finished = true;
-        __syncthreads();
+        OCT_MARK(tm, 12 + min(round, 17));
+        ++nround;
     }
 
-    // ---- 5. retain the best key per node (740-759), emit in list order
+    // ---- retain the best key per node (740-759), emit in list order
     for (int i = tid; i < size; i += kOctBlock) s.s64[i] = 0ull;
     __syncthreads();
     {
         unsigned long long* best = s.s64;
-        oct_sweep(ACT(cur), nact, [=](const int4 en) {
-            const unsigned long long v =
-                ((unsigned long long)key_score(en.x) << 32) | (0xffffffffu - (unsigned)en.y);
-            atomicMax(&best[en.z], v);
+        oct_sweep(K, NODE, nkeys, [=](int k, uint32_t kk, int node) {
+            atomicMax(&best[node], ((unsigned long long)key_score(kk) << 32) | (0xffffffffu - (unsigned)k));
         });
     }
     __syncthreads();
@@ -1065,7 +997,111 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
         out[i] = pack_key(key_x(kk) + kMinBorder, key_y(kk) + kMinBorder, key_score(kk));
     }
     if (tid == 0) *out_cnt = size;
-#undef ACT
+#ifdef ORBFE_OCT_TIMING
+    if (tid == 0 && tm) tm[30] = npass | (nround << 8) | ((long long)nkeys << 16);
+#endif
+    OCT_MARK(tm, 31);
+}
+
+__global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    // level-major block order: every frame's level-0 tree (the longest) is dispatched first,
+    // the small levels fill the remaining slots
+    const int level = blockIdx.y, f = blockIdx.x;
+    const LevelGeo& L = a.geo.lv[level];
+    const int NC = a.ncap_max;
+    const int tid = threadIdx.x;
+    OctLds s;
+    {
+        int* p = reinterpret_cast<int*>(lds_raw);
+        s.s64 = reinterpret_cast<unsigned long long*>(p);
+        p += 2 * a.sort_cap;
+        s.keys = reinterpret_cast<uint32_t*>(p);
+        p += a.lds_keys;
+        s.lists = p;
+        s.nc = NC;
+        p += 10 * NC;
+        s.qc = p; p += 4 * NC;
+        s.qk = p; p += 4 * NC;
+        s.aux = p; p += NC;
+        s.aux2 = p; p += NC;
+        s.tmp = p; p += 64;
+        s.scal = p; p += 16;
+        s.node = reinterpret_cast<short*>(p);
+    }
+    uint32_t* out = a.oct_out + f * a.geo.out_total + L.out_off;
+    int* out_cnt = a.oct_cnt + f * a.geo.nlevels + level;
+    long long* tm = nullptr;
+#ifdef ORBFE_OCT_TIMING
+    if (f < 256) tm = g_oct_t + (f * 16 + level) * 32;
+#endif
+    OCT_MARK(tm, 0);
+
+    // ---- 1. this level's key count (summed by the FAST kernel; reset for the next call)
+    if (tid == 0) s.scal[0] = a.level_keys[f * kMaxLevels + level];
+    __syncthreads();
+    const int total = s.scal[0];
+    if (tid == 0) a.level_keys[f * kMaxLevels + level] = 0;
+    if (total == 0 || L.nini < 1) {
+        if (tid == 0) *out_cnt = 0;
+        OCT_MARK(tm, 31);
+        return;
+    }
+    OCT_MARK(tm, 1);
+    // ---- 2. compact the cell outputs into original key order (LDS when they fit): a thread
+    // per cell copies the cell's keys to its scanned offset, loads batched 8 at a time
+    const bool in_lds = total <= a.lds_keys;
+    uint32_t* K = in_lds ? s.keys : a.keys + f * a.geo.key_total + L.key_off;
+    const uint32_t* src = a.cell_keys + f * a.cell_cap_total;
+    int nkeys = 0;
+    // the first two chunks' counts and slots are loaded together (one global round trip for
+    // the <= 2 * kOctBlock cells of most levels)
+    int n_next = 0;
+    long long slot_next = 0;
+    {
+        const int c = L.cell_begin + kOctBlock + tid;
+        if (c < L.cell_end) {
+            n_next = a.cell_cnt[f * a.ncells + c];
+            slot_next = a.cells[c].slot;
+        }
+    }
+    for (int base = L.cell_begin; base < L.cell_end; base += kOctBlock) {
+        const int c = base + tid;
+        int n = 0;
+        long long slot = 0;
+        if (base == L.cell_begin) {
+            if (c < L.cell_end) {
+                n = a.cell_cnt[f * a.ncells + c];
+                slot = a.cells[c].slot;
+            }
+        } else if (base == L.cell_begin + kOctBlock) {
+            n = n_next;
+            slot = slot_next;
+        } else if (c < L.cell_end) {
+            n = a.cell_cnt[f * a.ncells + c];
+            slot = a.cells[c].slot;
+        }
+        int chunk_total;
+        const int off = nkeys + block_exclusive_scan<kOctBlock>(n, s.tmp, chunk_total);
+        for (int i0 = 0; i0 < n; i0 += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (i0 + i < n) v[i] = src[slot + i0 + i];
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (i0 + i < n) K[off + i0 + i] = v[i];
+        }
+        nkeys += chunk_total;
+    }
+    __syncthreads();
+    OCT_MARK(tm, 2);
+    if (in_lds) {
+        octree_level(a, s, L, s.keys, s.node, nkeys, out, out_cnt, tm);
+    } else {  // more keys than LDS holds: the same passes over global arrays
+        int* node = reinterpret_cast<int*>(a.act) + (f * a.geo.key_total + L.key_off);
+        octree_level(a, s, L, K, node, nkeys, out, out_cnt, tm);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1780,9 +1816,22 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
     int sort_cap = 1;
     while (sort_cap < ncap_max) sort_cap <<= 1;
     g.sort_cap = sort_cap;
-    g.oct_lds = (size_t)2 * sort_cap * 4 + (size_t)ncap_max * 4 * (10 + 8 + 2) + 64 * 4 +
-                (size_t)2 * kOctBlockSize * 4 + 64;
+    // LDS-resident keys per level: ~10x the largest level budget covers the FAST lists of
+    // textured frames (640x480 @1000: <= 1,900 keys per level; 1080p @2000: <= 3,300), at
+    // most kOctLdsKeys; a level with more runs on global arrays
+    int nf_max = 0;
+    for (int l = 0; l < L; ++l) nf_max = std::max(nf_max, g.geo.lv[l].nfeat);
+    g.oct_keys = std::min(kOctLdsKeys, std::max(1024, (10 * nf_max + 255) & ~255));
+    g.oct_lds = (size_t)2 * sort_cap * 4 + (size_t)g.oct_keys * 4 +
+                (size_t)ncap_max * 4 * (10 + 8 + 2) + 64 * 4 + 16 * 4 + (size_t)g.oct_keys * 2;
     return ORBFE_OK;
 }
 
 }  // namespace orbfe
+
+#ifdef ORBFE_OCT_TIMING
+extern "C" int orbfe_debug_oct_timing(long long* out, int n) {
+    n = n < 256 * 16 * 32 ? n : 256 * 16 * 32;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(orbfe::g_oct_t), (size_t)n * sizeof(long long)) == hipSuccess ? 0 : -3;
+}
+#endif

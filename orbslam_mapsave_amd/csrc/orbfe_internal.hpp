@@ -99,6 +99,7 @@ struct FastArgs {
     int roi_pitch, roi_rows, cand_max;  // dynamic-LDS carve of fast_kernel
     int* cell_cnt;         // [frame][cell]
     uint32_t* cell_keys;   // [frame][cell_cap_total]
+    int* level_keys;       // [frame][kMaxLevels] keys per level (atomic sums; 0 on entry)
     LevelPtr pyr[kMaxLevels];
 };
 
@@ -109,11 +110,14 @@ struct OctArgs {
     long long cell_cap_total;
     const int* cell_cnt;
     const uint32_t* cell_keys;
+    int* level_keys;       // [frame][kMaxLevels] from fast_kernel; reset to 0 after reading
     uint32_t* keys;        // [frame][key_total] compacted per level
-    int4* act;             // [frame][2 * key_total] live keys (packed key, key index, node, -)
+    int4* act;             // [frame][2 * key_total]: node positions of levels whose keys
+                           // exceed kOctLdsKeys (int per key)
     uint32_t* oct_out;     // [frame][out_total]
     int* oct_cnt;          // [frame][nlevels]
     int ncap_max, sort_cap;
+    int lds_keys;          // keys of a level held in LDS (Plan::oct_keys)
 };
 
 struct BlurArgs {
@@ -179,6 +183,7 @@ struct Plan {
     int ncap_max = 0, sort_cap = 0, tiles_total = 0;
     int tile_begin[kMaxLevels] = {};
     size_t oct_lds = 0;
+    int oct_keys = 0;      // LDS key capacity of the oct-tree kernel
     int roi_pitch = 0, roi_rows = 0, cand_max = 0;
     size_t fast_lds = 0;
     int rs_tiles_x[kMaxLevels] = {}, rs_tiles[kMaxLevels] = {}, rs_pitch[kMaxLevels] = {};
@@ -205,6 +210,7 @@ constexpr int kFastBlockSize = 64;
 #define ORBFE_OCT_BLOCK 256  // 128: 248K, 256: 254K, 512: 243K, 1024: 220K frames/s (c3)
 #endif
 constexpr int kOctBlockSize = ORBFE_OCT_BLOCK;
+constexpr int kOctLdsKeys = 4096;  // max oct-tree keys of one level held in LDS (else global)
 #ifndef ORBFE_DESC_BLOCK
 #define ORBFE_DESC_BLOCK 256
 #endif
