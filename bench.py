@@ -62,25 +62,87 @@ def algorithmic_bytes(stage: str, w: int, h: int, nkp: float, nref: float = 0.0)
     return 0.0
 
 
-def cpu_baseline(frames: np.ndarray, ref_desc: np.ndarray, budget_s: float) -> dict:
-    """The CPU oracle (a port of the reference CPU path, oracle/orb_oracle.cpp) on one host
-    thread: extract(1000 kp) + brute-force match vs the 2000-kp reference, frame after frame,
-    until `budget_s` of CPU work."""
+def host_cpu() -> dict:
+    """Host core count and CPU model ("report the core count and model")."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    nproc = os.cpu_count() or 1
+    try:
+        nproc = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    # the GPU box gives one GPU's job a share of the host (OMP_NUM_THREADS is set to it)
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(nproc, share) if share > 0 else nproc
+    return {"model": model, "nproc": nproc, "threads": max(1, threads)}
+
+
+def cpu_baseline(frames: np.ndarray, ref_desc: np.ndarray | None, budget_s: float,
+                 nfeatures: int = 1000, what: str = "") -> dict:
+    """The CPU oracle (a port of the reference CPU path, oracle/orb_oracle.cpp, -O3) on the
+    bench's own frames, BASELINE.md §2: (i) one thread, frames in sequence, after 50 warm-up
+    frames, until >= 1000 frames or `budget_s`; (ii) all cores of this job's host share, one
+    extractor state per thread (ctypes releases the GIL), for ~budget_s / 3.  Each frame is
+    extract(nfeatures) + brute-force match against `ref_desc` (or against the previous frame's
+    descriptors when ref_desc is None: config 4's f vs f-1)."""
+    import concurrent.futures as cf
     import oracle  # test infrastructure: the cpu_baseline leg is allowed to load it
-    p = oracle.params(1000, 1.2, 8, 32, 7)
-    done, t0 = 0, time.perf_counter()
-    while True:
-        kps, desc = oracle.extract(p, frames[done % len(frames)])
-        oracle.bf_match(desc, ref_desc)
-        done += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s and done >= 5:
-            break
-    return {"value": round(done / el, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{done} of the bench's 640x480 frames, extract(1000 kp) + BF match vs the "
-                      f"2000-kp reference, 1 thread, oracle/orb_oracle.cpp -O3, {el:.1f} s"}
+    p = oracle.params(nfeatures, 1.2, 8, 32, 7)
+    host = host_cpu()
+
+    def one(i, prev):
+        kps, desc = oracle.extract(p, frames[i % len(frames)])
+        oracle.bf_match(desc, ref_desc if ref_desc is not None else prev)
+        return desc
+
+    prev = oracle.extract(p, frames[-1])[1]
+    for i in range(min(50, len(frames) * 2)):  # warm-up
+        prev = one(i, prev)
+    times = []
+    t0 = time.perf_counter()
+    while len(times) < 1000 and (time.perf_counter() - t0 < budget_s or len(times) < 5):
+        a = time.perf_counter()
+        prev = one(len(times), prev)
+        times.append(time.perf_counter() - a)
+    el1 = time.perf_counter() - t0
+    T = host["threads"]
+    budget_all = max(budget_s / 3, 2.0)
+    stop = time.perf_counter() + budget_all
+
+    def worker(k):
+        n, pv = 0, oracle.extract(p, frames[k % len(frames)])[1]
+        while time.perf_counter() < stop or n < 2:
+            pv = one(k + n * T, pv)
+            n += 1
+        return n
+
+    ta = time.perf_counter()
+    with cf.ThreadPoolExecutor(T) as pool:
+        done_all = sum(pool.map(worker, range(T)))
+    el_all = time.perf_counter() - ta
+    ms = np.array(times) * 1e3
+    return {"value": round(len(times) / el1, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+            "threads": 1, "median_ms": round(float(np.median(ms)), 3),
+            "mean_ms": round(float(ms.mean()), 3),
+            "all_core": {"value": round(done_all / el_all, 3), "unit": "frames/s", "threads": T,
+                         "frames": done_all, "seconds": round(el_all, 2)},
+            "host": host,
+            "sample": f"{len(times)} of the bench's frames {what} after 50 warm-up frames, 1 "
+                      f"thread, {el1:.1f} s (oracle/orb_oracle.cpp -O3 -march=x86-64-v3); "
+                      f"all-core: {done_all} frames on {T} threads in {el_all:.1f} s"}
 
 
+C2_METRIC = ("frames/sec ORB extract (8-level pyramid + FAST-9 + oct-tree + rBRIEF), 640×480 "
+             "@1000 kp, 1 MI355X")
+C4_METRIC = ("frames/sec ORB extract+match, 1920×1080 @2000 kp, batch 256 sharded over 1/2/4/8 "
+             "MI355X with an RCCL descriptor all-gather; % HBM roofline")
 C5_METRIC = ("frames/sec tracking-loop SearchByProjection (isInFrustum + SearchByProjection) vs "
              "50k-MapPoint local map, 640×480, 1 MI355X")
 
@@ -208,13 +270,27 @@ def run_c5(args) -> None:
         dist.destroy_process_group()
 
 
-def main() -> None:
+def e2e_bytes(w: int, h: int, nf: int, nq: int = 0, nr: int = 0) -> int:
+    """SURVEY.md §8(d) end-to-end algorithmic bytes per frame: input + cascaded resize (read +
+    write) + FAST read + blur read/write + N (31x31 patch + 512 samples + keypoint + descriptor),
+    plus 32 (Q + R) + 12 Q for a brute-force match (6,261,674 B at 640x480 @1000; +108,000)."""
+    P = [a * b for a, b in level_sizes(w, h)]
+    b = w * h + sum(P[:-1]) + sum(P[1:]) + sum(P) + 2 * sum(P) + nf * (961 + 512) + nf * (28 + 32)
+    if nq:
+        b += 32 * (nq + nr) + 12 * nq
+    return int(b)
+
+
+def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="frames per rank per step")
-    ap.add_argument("--config", default="c3", choices=["c3", "c4", "c5"])
+    ap.add_argument("--batch", type=int, default=256, help="frames per rank per step (c3)")
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--per-rank", type=int, default=0,
+                    help="c4: frames per rank (default 256 / world; 32 rehearses the 8-GPU "
+                         "per-rank shape on one GPU)")
     ap.add_argument("--distinct", type=int, default=32, help="distinct synthetic seeds (cycled)")
     ap.add_argument("--streams", type=int, default=1,
                     help="sub-batches per rank, each on its own HIP stream and extractor handle "
@@ -233,36 +309,19 @@ def main() -> None:
                     help="0: no per-kernel HIP events in the timed region (no roofline)")
     ap.add_argument("--cpu-budget", type=float, default=15.0,
                     help="seconds of CPU-baseline work on rank 0 (0 disables)")
-    args = ap.parse_args()
+    return ap.parse_args()
 
+
+def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, warmup):
+    """One extraction benchmark: every step, every rank extracts B frames (device-resident) and,
+    by `mode`, matches nothing ("none", config 2), each frame against a 2000-kp reference
+    ("ref", config 3), or each frame against its global predecessor after the descriptor
+    all-gather ("pred", config 4).  Returns the measurement (rank 0) or None."""
     import torch
     import torch.distributed as dist
-
-    if args.config == "c5":
-        return run_c5(args)
-
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-
     from orbslam_mapsave_amd.native import ORBextractor, ORBmatcher
+    from orbslam_mapsave_amd.shard import PredecessorMatch
     from orbslam_mapsave_amd.synth import synthetic_batch, synthetic_frame
-
-    if args.config == "c3":
-        W, H, NF, NREF = 640, 480, 1000, 2000
-        B = args.batch
-        workload = ("configs[2]: 640x480 extract (8-level pyramid, FAST-9, oct-tree, rBRIEF, "
-                    "1000 kp) + brute-force Hamming match vs a 2000-kp reference frame")
-    else:
-        W, H, NF, NREF = 1920, 1080, 2000, 2000
-        B = max(1, 256 // world)
-        workload = ("configs[3]: 1920x1080 @2000 kp, global batch 256 sharded round-robin, "
-                    "RCCL all-gather of descriptor slabs, frame f vs f-1 match")
 
     frames_np = synthetic_batch(B, W, H, first_seed=1000 * rank, distinct=args.distinct)
     frames = torch.from_numpy(frames_np).to(dev)
@@ -284,23 +343,25 @@ def main() -> None:
     d_n = torch.zeros(B, dtype=torch.int32, device=dev)
     d_out = torch.empty((B, cap, 3), dtype=torch.int32, device=dev)
 
-    # reference frame (config 3): extracted once on the GPU with the 2x-feature extractor
-    ref_np = synthetic_frame(999_999, W, H)
-    ex_ref = ORBextractor(NREF, 1.2, 8, 32, 7, device=local, max_width=W, max_height=H)
-    ref_kps, ref_desc_np = ex_ref(ref_np)
-    ex_ref.close()
-    ref_desc = torch.from_numpy(np.ascontiguousarray(ref_desc_np)).to(dev)
-    d_nr = torch.full((B,), len(ref_desc_np), dtype=torch.int32, device=dev)
+    ref_desc_np = None
+    if mode == "ref":  # reference frame (config 3): the 2x-feature extractor, once on the GPU
+        ref_np = synthetic_frame(999_999, W, H)
+        ex_ref = ORBextractor(NREF, 1.2, 8, 32, 7, device=local, max_width=W, max_height=H)
+        ref_kps, ref_desc_np = ex_ref(ref_np)
+        ex_ref.close()
+        ref_desc = torch.from_numpy(np.ascontiguousarray(ref_desc_np)).to(dev)
+        d_nr = torch.full((B,), len(ref_desc_np), dtype=torch.int32, device=dev)
     torch.cuda.synchronize(dev)
 
-    if args.config == "c4":
-        g_desc = torch.zeros((world * B, cap, 32), dtype=torch.uint8, device=dev)
-        g_n = torch.zeros(world * B, dtype=torch.int32, device=dev)
-        d_prev = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
-        d_prev_n = torch.zeros(B, dtype=torch.int32, device=dev)
-        from orbslam_mapsave_amd.shard import gather_slabs, predecessor_index
-        pred = torch.as_tensor(predecessor_index(rank, world, B), device=dev)
-        main = torch.cuda.current_stream(dev)
+    if mode == "pred":
+        main_stream = torch.cuda.current_stream(dev)
+
+        def bf(q, qn, r, rn, out):
+            mt.set_stream(main_stream.cuda_stream)
+            mt.bf_match_batch_device(q.data_ptr(), cap * 32, qn.data_ptr(), cap, r.data_ptr(),
+                                     cap * 32, rn.data_ptr(), q.shape[0], out.data_ptr())
+
+        pm = PredecessorMatch(rank, world, B, cap, dev, bf)
 
     J = max(1, min(args.chunks, C))
     while C % J:
@@ -316,7 +377,7 @@ def main() -> None:
     skew_next = [False]
 
     def step():
-        if args.config == "c3":  # sub-batch k: extract + match on stream k, no cross-stream deps
+        if mode != "pred":  # sub-batch k: extract (+ match) on stream k, no cross-stream deps
             ev = {}
             for j in range(J):
                 for k in range(S):
@@ -326,10 +387,11 @@ def main() -> None:
                             streams[k].wait_event(ev[src])
                     f0 = k * C + j * CJ
                     extract_chunk(k, j)
-                    mt.set_stream(streams[k].cuda_stream)
-                    mt.bf_match_batch_device(d_desc[f0].data_ptr(), cap * 32,
-                                             d_n[f0:].data_ptr(), cap, ref_desc.data_ptr(), 0,
-                                             d_nr[f0:].data_ptr(), CJ, d_out[f0].data_ptr())
+                    if mode == "ref":
+                        mt.set_stream(streams[k].cuda_stream)
+                        mt.bf_match_batch_device(d_desc[f0].data_ptr(), cap * 32,
+                                                 d_n[f0:].data_ptr(), cap, ref_desc.data_ptr(), 0,
+                                                 d_nr[f0:].data_ptr(), CJ, d_out[f0].data_ptr())
                     if skew_next[0] and k == 0:
                         ev[j] = torch.cuda.Event()
                         ev[j].record(streams[0])
@@ -338,16 +400,10 @@ def main() -> None:
             for k in range(S):
                 extract_chunk(k)
             for k in range(S):
-                main.wait_stream(streams[k])
-            gather_slabs(d_desc, d_n, g_desc, g_n, world)
-            torch.index_select(g_desc, 0, pred, out=d_prev)
-            torch.index_select(g_n, 0, pred, out=d_prev_n)
-            mt.set_stream(main.cuda_stream)
-            mt.bf_match_batch_device(d_desc.data_ptr(), cap * 32, d_n.data_ptr(), cap,
-                                     d_prev.data_ptr(), cap * 32, d_prev_n.data_ptr(), B,
-                                     d_out.data_ptr())
+                main_stream.wait_stream(streams[k])
+            pm.step(d_desc, d_n, d_out)
             for k in range(S):
-                streams[k].wait_stream(main)
+                streams[k].wait_stream(main_stream)
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -363,7 +419,7 @@ def main() -> None:
         acc["bf_match"] = mt.profile_read()
         return acc
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     barrier()
     # Probe steps (untimed): events on every kernel give the per-stage table and pick the
@@ -387,7 +443,7 @@ def main() -> None:
     mt.profile_read()
     skew_next[0] = bool(args.skew) and S > 1 and J >= S
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     barrier()
     dt = time.perf_counter() - t0
@@ -400,56 +456,137 @@ def main() -> None:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    for e in exs:
+        e.close()
+    mt.close()
+    if rank != 0:
+        return None
+    K = steps
+    per_step = {s_: probe[s_][0] / max(probe_steps, 1) for s_ in STAGES}
+    dom_ms, dom_launches = stages[dom] if dom else (0.0, 0)
+    nref = float(len(ref_desc_np)) if mode == "ref" else nkp
+    bytes_per_step = algorithmic_bytes(dom, W, H, nkp, nref) * B if dom else 0.0
+    achieved = bytes_per_step / (dom_ms / K / 1e3) / 1e9 if dom_ms > 0 else 0.0
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+    if os.path.exists(tpath) and args.config != "c2":
+        with open(tpath) as fh:
+            traffic = json.load(fh).get(dom) if dom else None
+    roof = {"bound": "hbm", "kernel": f"{dom}_kernel" if dom else None,
+            "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "bytes_per_launch": round(bytes_per_step * K / max(dom_launches, 1)),
+            "avg_launch_ms": round(dom_ms / max(dom_launches, 1), 4)}
+    value = world * B * K / dt
+    nq = NF if mode != "none" else 0
+    e2e = e2e_bytes(W, H, NF, nq, NREF if mode == "ref" else (NF if mode == "pred" else 0))
+    return {"value": value, "dt": dt, "K": K, "B": B, "S": S, "J": J, "nkp": nkp,
+            "roofline": roof, "per_step": per_step, "probe_steps": probe_steps,
+            "ref_kp": len(ref_desc_np) if ref_desc_np is not None else None,
+            "frames_np": frames_np, "ref_desc_np": ref_desc_np,
+            "end_to_end": {"bytes_per_frame": e2e, "achieved": round(e2e * value / 1e9, 2),
+                           "unit": "GB/s", "frac": round(e2e * value / 1e9 / HBM_PEAK_GBS, 5),
+                           "model": "SURVEY.md §8(d) algorithmic bytes per frame x frames/s"}}
+
+
+def main() -> None:
+    args = parse_args()
+    import torch
+    import torch.distributed as dist
+
+    if args.config == "c5":
+        return run_c5(args)
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    sweep = None
+    if args.config == "c2":
+        W, H, NF, NREF = 640, 480, 1000, 0
+        metric = C2_METRIC
+        workload = ("configs[1]: 640x480 extract only (8-level pyramid, FAST-9, oct-tree, "
+                    "rBRIEF, 1000 kp), batch sweep B in {1, 64, 256}, >= 1000 frames after 50 "
+                    "warm-up frames per B; value at B = 256")
+        sweep = {}
+        for Bc in (1, 64, 256):
+            r = run_extract(args, dev, rank, world, local, W, H, NF, NREF, Bc, "none",
+                            max(args.steps, -(-1000 // Bc)), max(args.warmup, -(-50 // Bc)))
+            if rank == 0:
+                sweep[str(Bc)] = {"frames_per_s": round(r["value"], 1),
+                                  "ms_per_call": round(r["dt"] / r["K"] * 1e3, 4),
+                                  "frames": Bc * r["K"] * world,
+                                  "dominant": r["roofline"]["kernel"],
+                                  "dominant_frac": r["roofline"]["frac"],
+                                  "stage_ms_per_call": {k: round(v, 4) for k, v in r["per_step"].items()}}
+        B = 256
+        parallelism = f"frame-sharded x{world}, no data-path collective"
+    elif args.config == "c3":
+        W, H, NF, NREF = 640, 480, 1000, 2000
+        B = args.batch
+        metric = METRIC
+        workload = ("configs[2]: 640x480 extract (8-level pyramid, FAST-9, oct-tree, rBRIEF, "
+                    "1000 kp) + brute-force Hamming match vs a 2000-kp reference frame")
+        r = run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, "ref", args.steps,
+                        args.warmup)
+        parallelism = f"frame-sharded x{world}, no data-path collective"
+    else:
+        W, H, NF, NREF = 1920, 1080, 2000, 2000
+        B = args.per_rank if args.per_rank > 0 else max(1, 256 // world)
+        metric = C4_METRIC
+        workload = (f"configs[3]: 1920x1080 @2000 kp, global batch {B * world} sharded "
+                    "round-robin, RCCL all-gather of descriptor slabs, frame f vs f-1 match")
+        r = run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, "pred", args.steps,
+                        args.warmup)
+        parallelism = f"frame-sharded x{world} + RCCL all-gather"
 
     if rank == 0:
-        K = args.steps
-        value = world * B * K / dt
-        per_step = {s: probe[s][0] / max(probe_steps, 1) for s in STAGES}
-        dom_ms, dom_launches = stages[dom] if dom else (0.0, 0)
-        nref = float(len(ref_desc_np)) if args.config == "c3" else nkp
-        bytes_per_step = algorithmic_bytes(dom, W, H, nkp, nref) * B if dom else 0.0
-        achieved = bytes_per_step / (dom_ms / K / 1e3) / 1e9 if dom_ms > 0 else 0.0
-        traffic = None
-        tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
-        if os.path.exists(tpath):
-            with open(tpath) as fh:
-                traffic = json.load(fh).get(dom) if dom else None
-        roof = {"bound": "hbm", "kernel": f"{dom}_kernel" if dom else None, "achieved": round(achieved, 2),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": traffic,
-                "bytes_per_launch": round(bytes_per_step * K / max(dom_launches, 1)),
-                "avg_launch_ms": round(dom_ms / max(dom_launches, 1), 4)}
         cpu = None
-        if world == 1 and args.cpu_budget > 0 and args.config == "c3":
-            cpu = cpu_baseline(frames_np[:args.distinct], ref_desc_np, args.cpu_budget)
+        if world == 1 and args.cpu_budget > 0:
+            if args.config == "c4":
+                cpu = cpu_baseline(r["frames_np"][:min(args.distinct, 8)], None, args.cpu_budget,
+                                   NF, "(1920x1080, extract 2000 kp + BF match vs frame f-1)")
+            elif args.config == "c3":
+                cpu = cpu_baseline(r["frames_np"][:args.distinct], r["ref_desc_np"],
+                                   args.cpu_budget, NF,
+                                   "(640x480, extract 1000 kp + BF match vs the 2000-kp reference)")
+            else:
+                cpu = cpu_baseline(r["frames_np"][:args.distinct], None, args.cpu_budget, NF,
+                                   "(640x480, extract 1000 kp + BF match vs frame f-1)")
+                cpu["sample"] += " [the CPU leg matches f vs f-1: an upper bound on extract-only]"
+        K, S, J = r["K"], r["S"], r["J"]
         line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
-            "steps": K, "warmup": args.warmup, "ms_per_step": round(dt / K * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak" if args.config == "c3" else "strong",
+            "metric": metric, "value": round(r["value"], 2), "unit": "frames/s", "n_gpus": world,
+            "steps": K, "warmup": args.warmup, "ms_per_step": round(r["dt"] / K * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak" if args.config != "c4" else "strong",
             "vs_baseline": None, "dtype": "u8",
             "data": f"synthetic: seeded textured {W}x{H} u8 frames ({args.distinct} distinct "
                     f"seeds per rank, cycled), resident in HBM",
             "config": {"workload": workload, "frames_per_rank_per_step": B,
                        "streams_per_rank": S, "chunks_per_stream": J,
                        "stream_skew": bool(args.skew) and S > 1 and J >= S,
-                       "global_batch": B * world, "nfeatures": NF, "reference_kp": len(ref_desc_np),
-                       "mean_kp_per_frame": round(nkp, 1),
-                       "parallelism": (f"frame-sharded x{world}, no data-path collective"
-                                       if args.config == "c3" else f"frame-sharded x{world} + RCCL all-gather")},
-            "roofline": roof,
+                       "global_batch": B * world, "nfeatures": NF, "reference_kp": r["ref_kp"],
+                       "mean_kp_per_frame": round(r["nkp"], 1), "parallelism": parallelism},
+            "roofline": r["roofline"],
+            "end_to_end": r["end_to_end"],
             "cpu_baseline": cpu,
-            "stage_ms_per_step": {s: round(v, 4) for s, v in per_step.items()},
-            "stage_note": (f"summed kernel durations per step over {probe_steps} untimed probe steps "
-                           "(events on every launch); the timed steps carry events on the "
-                           "roofline kernel only" + ("; sub-batch streams overlap, so the sum "
-                           "can exceed ms_per_step" if S > 1 else "")),
+            "stage_ms_per_step": {k: round(v, 4) for k, v in r["per_step"].items()},
+            "stage_note": (f"summed kernel durations per step over {r['probe_steps']} untimed "
+                           "probe steps (events on every launch); the timed steps carry events "
+                           "on the roofline kernel only" + ("; sub-batch streams overlap, so the "
+                           "sum can exceed ms_per_step" if S > 1 else "")),
         }
+        if sweep is not None:
+            line["batch_sweep"] = sweep
         if cpu:
-            line["gpu_over_cpu"] = round(value / cpu["value"], 1)
+            line["gpu_over_cpu"] = round(r["value"] / cpu["value"], 1)
+            line["gpu_over_cpu_all_core"] = round(r["value"] / cpu["all_core"]["value"], 1)
         print(json.dumps(line), flush=True)
-    for e in exs:
-        e.close()
-    mt.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -49,3 +49,29 @@ def gather_slabs(desc: torch.Tensor, counts: torch.Tensor, g_desc: torch.Tensor,
         return
     dist.all_gather_into_tensor(g_desc, desc)
     dist.all_gather_into_tensor(g_counts, counts)
+
+
+class PredecessorMatch:
+    """Config 4's exchange + match step (BASELINE configs[3]), one instance per rank: every
+    rank holds B = per_rank frames' descriptor slabs (B x cap x 32 u8) and keypoint counts,
+    all-gathers them (gather_slabs: RCCL over xGMI on the GPU, gloo in the CPU tests), picks
+    each local frame's global predecessor (predecessor_index) and calls
+    match(desc, counts, prev_desc, prev_counts, out) — frame f's queries against frame f - 1,
+    the tracking pattern of SearchByProjection(CurrentFrame, LastFrame) (ORBmatcher.cc:1331).
+    The buffers live on `device`; bench.py passes the GPU brute-force matcher as `match`."""
+
+    def __init__(self, rank: int, world: int, per_rank: int, cap: int, device, match):
+        self.world = world
+        self.match = match
+        self.g_desc = torch.zeros((world * per_rank, cap, 32), dtype=torch.uint8, device=device)
+        self.g_n = torch.zeros(world * per_rank, dtype=torch.int32, device=device)
+        self.prev = torch.zeros((per_rank, cap, 32), dtype=torch.uint8, device=device)
+        self.prev_n = torch.zeros(per_rank, dtype=torch.int32, device=device)
+        self.pred = torch.as_tensor(predecessor_index(rank, world, per_rank), device=device)
+
+    def step(self, desc: torch.Tensor, counts: torch.Tensor, out) -> None:
+        gather_slabs(desc, counts, self.g_desc, self.g_n, self.world)
+        torch.index_select(self.g_desc, 0, self.pred, out=self.prev)
+        torch.index_select(self.g_n, 0, self.pred, out=self.prev_n)
+        self.match(desc, counts, self.prev, self.prev_n, out)
+

@@ -1,0 +1,94 @@
+"""Config 4's real step function (orbslam_mapsave_amd.shard.PredecessorMatch: all-gather of the
+descriptor slabs, predecessor selection, frame f vs f - 1 match) — the one bench.py --config c4
+runs over RCCL — executed over gloo at world sizes 1, 2 and 4 on oracle-extracted 1920x1080
+@2000-keypoint frames.  SURVEY §4: the rank-sharded results must be byte-identical to the
+single-process run, for every global frame."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from orbslam_mapsave_amd.shard import PredecessorMatch, global_frame
+
+GLOBAL = 8     # global batch (the bench's is 256; the step does not depend on it)
+CAP = 2112     # slab capacity (>= any count of these frames)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.fixture(scope="module")
+def slabs():
+    import oracle
+    from orbslam_mapsave_amd.synth import synthetic_frame
+    p = oracle.params(2000, 1.2, 8, 32, 7)
+    desc = np.zeros((GLOBAL, CAP, 32), np.uint8)
+    cnt = np.zeros(GLOBAL, np.int32)
+    for f in range(GLOBAL):
+        _, d = oracle.extract(p, synthetic_frame(500 + f, 1920, 1080))
+        assert len(d) <= CAP
+        desc[f, :len(d)] = d
+        cnt[f] = len(d)
+    return desc, cnt
+
+
+def oracle_match(desc, counts, prev, prev_n, out):
+    import oracle
+    out.fill_(-7)
+    for j in range(desc.shape[0]):
+        q = desc[j, :int(counts[j])].numpy()
+        r = prev[j, :int(prev_n[j])].numpy()
+        bi, bd, sd = oracle.bf_match(q, r)
+        out[j, :len(q)] = torch.from_numpy(np.stack([bi, bd, sd], 1).astype(np.int32))
+
+
+def _worker(rank, world, port, desc, cnt, res):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    per = GLOBAL // world
+    mine = [global_frame(rank, world, j) for j in range(per)]
+    d = torch.from_numpy(desc[mine].copy())
+    n = torch.from_numpy(cnt[mine].copy())
+    out = torch.zeros((per, CAP, 3), dtype=torch.int32)
+    PredecessorMatch(rank, world, per, CAP, "cpu", oracle_match).step(d, n, out)
+    res[rank] = {f: out[j].numpy().tobytes() for j, f in enumerate(mine)}
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_world(world, desc, cnt):
+    if world == 1:
+        res = {}
+        _worker(0, 1, 0, desc, cnt, res)
+        return res[0]
+    out = mp.Manager().dict()
+    mp.spawn(_worker, args=(world, _free_port(), desc, cnt, out), nprocs=world, join=True)
+    merged = {}
+    for r in range(world):
+        merged.update(out[r])
+    return merged
+
+
+def test_c4_step_identical_across_world_sizes(slabs):
+    desc, cnt = slabs
+    base = run_world(1, desc, cnt)
+    assert sorted(base) == list(range(GLOBAL))
+    # world 1 itself is the plain f vs f - 1 match (frame 0 against the last frame)
+    import oracle
+    for f in (0, 5):
+        p = (f - 1) % GLOBAL
+        bi, bd, sd = oracle.bf_match(desc[f, :cnt[f]], desc[p, :cnt[p]])
+        got = np.frombuffer(base[f], np.int32).reshape(CAP, 3)[:cnt[f]]
+        assert np.array_equal(got, np.stack([bi, bd, sd], 1))
+    for world in (2, 4):
+        assert run_world(world, desc, cnt) == base, f"world {world} differs from world 1"
