@@ -38,6 +38,16 @@ struct GreedyArgs {
     long long cand_cap;   // entries the fill could write: a list ending past it was not
                           // filled (the host then retries with the exact total), so it is
                           // read as empty and never indexes past the buffer
+    int kfix;             // > 0: fixed-slot layout, point i's candidates at i * kfix ..
+    const int* fcnt;      //      with fcnt[i] of them (off unused)
+    int* save_fmp;        // fused path: fmp0 / fobs0 saved here (restore point of a
+    int* save_fobs;       //   speculative call)
+    int* done;            // fused path (non-NULL): greedy_accept_kernel's finished-workgroup
+                          //   counter (0 between calls); its last workgroup finalises
+    const int* blk;       //   per-workgroup tallies of sbp_local_fused_kernel (3 each, nblk)
+    int nblk;
+    int* stats;           //   [1] nToMatch [2] status [3] overflow [4] chg[conv_round] [5] rounds
+    int conv_round;
     const int* nobs;      // per point; NULL: every point blocks (keyframe overload)
     const int* fmp0;      // slot contents before the call (-1 = NULL)
     const int* fobs0;     // their Observations(); NULL: any held point blocks
@@ -101,6 +111,11 @@ struct GreedyAcc {
 
 // [e0, e1) of point i's candidates, empty when the list was not filled (past cand_cap).
 __device__ __forceinline__ void greedy_range(const GreedyArgs& a, int i, int& e0, int& e1) {
+    if (a.kfix) {
+        e0 = i * a.kfix;
+        e1 = e0 + a.fcnt[i];
+        return;
+    }
     e0 = a.off[i];
     e1 = a.off[i + 1];
     if (e1 > a.cand_cap) e1 = e0;
@@ -175,6 +190,46 @@ __global__ __launch_bounds__(kGreedyBlock) void greedy_accept_kernel(GreedyArgs 
     }
     const unsigned long long b = __ballot(acc);
     if ((threadIdx.x & 63) == 0 && b) atomicAdd(a.nm, __popcll(b));
+    if (!a.done) return;
+    // fused path: the last workgroup to finish writes the slots (greedy_slots_kernel's work),
+    // sums the candidate kernel's per-workgroup tallies and reports convergence; it resets
+    // the counter for the next call
+    __shared__ int is_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        is_last = atomicAdd(a.done, 1) == (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!is_last) return;
+    __threadfence();
+    for (int s = threadIdx.x; s < a.nkp; s += kGreedyBlock) {
+        const int j = __hip_atomic_load(&a.last[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (j < 0) continue;
+        a.fmp[s] = a.ids ? a.ids[j] : j;
+        if (a.fobs) a.fobs[s] = a.nobs ? a.nobs[j] : 1;
+    }
+    if (threadIdx.x < 64) {
+        int in = 0, ovf = 0, bad = 0;
+        for (int k = threadIdx.x; k < a.nblk; k += 64) {
+            in += a.blk[3 * k];
+            ovf += a.blk[3 * k + 1];
+            bad += a.blk[3 * k + 2];
+        }
+        in = wave_sum(in);
+        ovf = wave_sum(ovf);
+        bad = wave_sum(bad);
+        if (threadIdx.x == 0) {
+            a.stats[1] = in;                               // nToMatch
+            a.stats[2] = bad ? ORBFE_ERR_UNSUPPORTED : 0;  // a predicted level outside the pyramid
+            a.stats[3] = ovf;                              // points past kSbpFix candidates
+            a.stats[4] = a.chg[a.conv_round];              // 0: converged
+            int r = 0;
+            while (r < a.conv_round && a.chg[r] != 0) ++r;
+            a.stats[5] = r + 1;                            // rounds to the fixed point
+            *a.done = 0;
+        }
+    }
 }
 
 // G3: slot contents = last acceptor.
@@ -307,6 +362,129 @@ __global__ __launch_bounds__(kGreedySmallBlock) void greedy_small_kernel(GreedyA
         *a.nm = nm;
         a.chg[0] = r;
     }
+}
+
+// Single-pass form of the tracking call (Tracking::SearchLocalPoints, config 5): isInFrustum and
+// the candidate search of SearchByProjection in ONE kernel, which also does greedy_init_kernel's
+// work.  Every workgroup stages the frame's grid (cstart, citems) and its keypoints' x, y,
+// octave in LDS, so the per-point GetFeaturesInArea walk reads LDS instead of chains of
+// dependent global loads; each point writes its candidates straight to kSbpFix fixed slots
+// (i * kSbpFix ..) with the count in cnt[i] (no count / scan / fill passes).  Per-workgroup
+// tallies (points in view, points with more than kSbpFix candidates, predicted levels outside
+// the pyramid) go to blk[3 * block ..] and greedy_accept_kernel's last workgroup sums them, so
+// nothing needs clearing before the launch.  Frames of up to kSbpFixKp keypoints; an overflow
+// makes the host rerun the call through the CSR path.
+constexpr int kSbpFix = 16;
+constexpr int kSbpFixKp = 2048;
+struct SbpFusedArgs {
+    FrustumArgs fr;        // in_view is written; px / py / pxr / lvl / vcos are not
+    SbpLocalArgs s;        // f, mp.m, mp.desc, th, nlevels, cnt, cand
+    float scalev[kMaxLevels];  // mvScaleFactors
+    int* blk;              // 3 per workgroup: in view, overflow, bad level
+    GreedyArgs g;          // initialised here (greedy_init_kernel's work)
+    int rounds;            // g.chg[0 .. rounds] cleared
+};
+__global__ __launch_bounds__(256) void sbp_local_fused_kernel(SbpFusedArgs fa) {
+    const SbpLocalArgs& a = fa.s;
+    __shared__ int cs[kGridCells + 1];
+    __shared__ int ci[kSbpFixKp];
+    __shared__ float2 kxy[kSbpFixKp];
+    __shared__ int8_t koct[kSbpFixKp];
+    __shared__ int tally[3];
+    const DevFrame& F = a.f;
+    const int tid = threadIdx.x;
+    const int i = blockIdx.x * 256 + tid;
+    {   // greedy_init_kernel's work, spread over the grid (which covers max(m, nkp) threads)
+        const GreedyArgs& g = fa.g;
+        if (i < g.nkp) {
+            const int v = greedy_preblocked(g, i) ? -1 : INT_MAX;
+            g.T[0][i] = v;
+            g.T[1][i] = v;
+            g.last[i] = -1;
+            g.save_fmp[i] = g.fmp0[i];
+            g.save_fobs[i] = g.fobs0[i];
+        }
+        if (i < g.m) g.dec[i] = -2;
+        if (i <= fa.rounds) g.chg[i] = 0;
+        if (i == 0) *g.nm = 0;
+    }
+    if (tid < 3) tally[tid] = 0;
+    for (int c = tid; c <= kGridCells; c += 256) cs[c] = F.cstart[c];
+    for (int k = tid; k < F.n; k += 256) {
+        const orbfe_keypoint kp = F.k[k];
+        kxy[k] = make_float2(kp.x, kp.y);
+        koct[k] = (int8_t)min(max(kp.octave, -128), 127);
+    }
+    __syncthreads();
+    const int total = cs[kGridCells];
+    for (int e = tid; e < total; e += 256) ci[e] = F.citems[e];
+    __syncthreads();
+    int in = 0, ovf = 0, bad_level = 0;
+    if (i < a.mp.m) {
+        fa.fr.in_view[i] = 0;  // isInFrustum starts with mbTrackInView = false (Frame.cc:389)
+        FrustumOut o;
+        int n = 0;
+        if (frustum_eval(fa.fr, i, o)) {
+            fa.fr.in_view[i] = 1;
+            in = 1;
+            const int pl = o.lvl;
+            if (pl < 0 || pl >= a.nlevels) {  // F.mvScaleFactors[nPredictedLevel] out of range
+                bad_level = 1;
+            } else {
+                float r = o.vc > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos (131-137)
+                if (a.th != 1.0) r *= a.th;
+                const float rs = r * fa.scalev[pl];
+                const float x = o.u, y = o.v;
+                int2* out = a.cand + (size_t)i * kSbpFix;
+                // GetFeaturesInArea(x, y, rs, pl - 1, pl) (Frame.cc:445-498) on the LDS copy, in
+                // features_in_area's order (ix-major, iy, insertion); the level check is on
+                // (maxLevel = pl >= 0)
+                const int cx0 = max(0, (int)floorf((x - F.minx - rs) * F.gwi));
+                const int cx1 = min(kGridCols - 1, (int)ceilf((x - F.minx + rs) * F.gwi));
+                const int cy0 = max(0, (int)floorf((y - F.miny - rs) * F.ghi));
+                const int cy1 = min(kGridRows - 1, (int)ceilf((y - F.miny + rs) * F.ghi));
+                if (cx0 < kGridCols && cx1 >= 0 && cy0 < kGridRows && cy1 >= 0) {
+                    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
+                    bool qd = false;
+                    for (int ix = cx0; ix <= cx1; ++ix)
+                        for (int iy = cy0; iy <= cy1; ++iy) {
+                            const int c = ix * kGridRows + iy;
+                            for (int e = cs[c], e1 = cs[c + 1]; e < e1; ++e) {
+                                const int idx = ci[e];
+                                const int oct = koct[idx];
+                                if (oct < pl - 1 || oct > pl) continue;
+                                const float2 kp = kxy[idx];
+                                if (!(fabsf(kp.x - x) < rs && fabsf(kp.y - y) < rs)) continue;
+                                if (F.ur && F.ur[idx] > 0) {  // stereo consistency (91-96)
+                                    const float er = fabsf(o.ur - F.ur[idx]);
+                                    if (er > r * fa.scalev[pl]) continue;
+                                }
+                                if (n < kSbpFix) {
+                                    if (!qd) {
+                                        q0 = a.mp.desc[2 * i];
+                                        q1 = a.mp.desc[2 * i + 1];
+                                        qd = true;
+                                    }
+                                    const uint4* d = F.desc + 2 * idx;
+                                    out[n] = make_int2(idx, hamming256(q0, q1, d[0], d[1]) | (oct << 16));
+                                }
+                                ++n;
+                            }
+                        }
+                }
+                ovf = n > kSbpFix;
+            }
+        }
+        a.cnt[i] = min(n, kSbpFix);
+    }
+    const int w_in = wave_sum(in), w_ovf = wave_sum(ovf), w_bad = wave_sum(bad_level);
+    if ((tid & 63) == 0) {
+        if (w_in) atomicAdd(&tally[0], w_in);
+        if (w_ovf) atomicAdd(&tally[1], w_ovf);
+        if (w_bad) atomicAdd(&tally[2], w_bad);
+    }
+    __syncthreads();
+    if (tid < 3) fa.blk[3 * blockIdx.x + tid] = tally[tid];
 }
 
 }  // namespace orbfe

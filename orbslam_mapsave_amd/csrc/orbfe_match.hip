@@ -1023,6 +1023,42 @@ struct FrustumArgs {
     int* n_in_view;
 };
 
+struct FrustumOut {
+    float u, ur, v, vc;
+    int lvl;
+};
+// Frame::isInFrustum (Frame.cc:387-443) + MapPoint::PredictScale (MapPoint.cc:633-642) of point
+// i into registers; false when not in view.  Writes nothing.
+__device__ __forceinline__ bool frustum_eval(const FrustumArgs& a, int i, FrustumOut& o) {
+    if ((a.skip && a.skip[i]) || (a.bad && a.bad[i])) return false;
+    const float* P = a.xyz + 3 * i;
+    float pc[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+        pc[r] = ((a.T[4 * r] * P[0] + a.T[4 * r + 1] * P[1]) + a.T[4 * r + 2] * P[2]) + a.T[4 * r + 3];
+    if (pc[2] < 0.0f) return false;
+    const float invz = 1.0f / pc[2];
+    const float u = a.fx * pc[0] * invz + a.cx;
+    const float v = a.fy * pc[1] * invz + a.cy;
+    if (u < a.minx || u > a.maxx) return false;
+    if (v < a.miny || v > a.maxy) return false;
+    const float dmax = 1.2f * a.maxd[i], dmin = 0.8f * a.mind[i];
+    const float po0 = P[0] - a.ow[0], po1 = P[1] - a.ow[1], po2 = P[2] - a.ow[2];
+    const float dist = (float)sqrt((double)po0 * po0 + (double)po1 * po1 + (double)po2 * po2);
+    if (dist < dmin || dist > dmax) return false;
+    const float* nv = a.normal + 3 * i;
+    const double dot = (double)po0 * nv[0] + (double)po1 * nv[1] + (double)po2 * nv[2];
+    const float vc = (float)(dot / dist);
+    if (vc < a.cos_limit) return false;
+    const float ratio = a.maxd[i] / dist;
+    o.lvl = (int)ceilf((float)log((double)ratio) / a.log_scale);
+    o.u = u;
+    o.ur = u - a.bf * invz;
+    o.v = v;
+    o.vc = vc;
+    return true;
+}
+
 __device__ __forceinline__ bool frustum_point(const FrustumArgs& a, int i) {
     a.in_view[i] = 0;  // isInFrustum starts with mbTrackInView = false (Frame.cc:389)
     if ((a.skip && a.skip[i]) || (a.bad && a.bad[i])) return false;

@@ -46,7 +46,7 @@ struct orbfe_matcher {
     DevBuf s1, s2, s3, s4, s5;                      // resolve scratch / outputs
     DevBuf m_f0, m_f1, m_f2, m_f3, m_f4, m_u0, m_u1, m_i0, m_i1, m_d;  // per-map-point inputs
     DevBuf o_u, o_f0, o_f1, o_f2, o_f3, o_i;        // frustum outputs
-    DevBuf scal;
+    DevBuf scal, done_ctr;
     DevBuf g_t0, g_t1, g_t2, g_dec, g_chg, g_last, g_bins, g_hist;  // greedy resolver
     Profiler prof;
     int last_rounds = 0;  // rounds the most recent greedy resolution took (diagnostics)
@@ -58,7 +58,7 @@ struct orbfe_matcher {
                           &fb_cs, &fb_ci, &fb_co, &q, &r, &nq, &nr, &out, &cnt, &off, &cand, &s1,
                           &s2, &s3, &s4, &s5, &m_f0, &m_f1, &m_f2, &m_f3, &m_f4, &m_u0, &m_u1,
                           &m_i0, &m_i1, &m_d, &o_u, &o_f0, &o_f1, &o_f2, &o_f3, &o_i, &scal,
-                          &g_t0, &g_t1, &g_t2, &g_dec, &g_chg, &g_last, &g_bins, &g_hist})
+                          &g_t0, &g_t1, &g_t2, &g_dec, &g_chg, &g_last, &g_bins, &g_hist, &done_ctr})
             b->release();
         prof.release();
         if (own) hipStreamDestroy(own);
@@ -939,7 +939,7 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
     return guarded(m, [&]() {
         int st;
         const int M = n_mp, N = frame->n;
-        if ((st = m->scal.ensure(16))) return st;
+        if ((st = m->scal.ensure(64))) return st;
         if ((st = m->m_f4.ensure(std::max<size_t>(16, (size_t)frame->nlevels * 4)))) return st;
         ORBFE_HIP(hipMemcpyAsync(m->m_f4.p, frame->scale_factors, (size_t)frame->nlevels * 4,
                                  hipMemcpyHostToDevice, m->stream));
@@ -947,6 +947,114 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
             if ((st = b->ensure(std::max<size_t>(16, (size_t)M * 4)))) return st;
         int* d_cnt = m->scal.as<int>() + 1;     // nToMatch
         int* d_status = m->scal.as<int>() + 2;  // UB level
+        // Fast path (frames of <= kSbpFixKp keypoints): the grid, ONE kernel for isInFrustum +
+        // candidates (fixed per-point slots) + the greedy initialisation, kBlindRounds rounds
+        // launched without looking (a round after a change-free one is a no-op), the
+        // acceptances whose last workgroup writes the slots and the tallies, and ONE
+        // synchronisation reading {nmatches, nToMatch, status, overflow, last round's
+        // changes, rounds}.  A point with more than kSbpFix candidates or a map that needs more
+        // rounds (rare) restores the slots saved by the fused kernel and takes the CSR path.
+        if (N <= kSbpFixKp && frame->nlevels <= kMaxLevels && M > 0) {
+            constexpr int kBlindRounds = 6;
+            const int fblocks = (std::max(std::max(M, N), kBlindRounds + 1) + 255) / 256;
+            if ((st = m->cand.ensure((size_t)M * kSbpFix * sizeof(int2)))) return st;
+            if ((st = m->cnt.ensure((size_t)M * sizeof(int)))) return st;
+            if ((st = m->s1.ensure(std::max(N, 1) * sizeof(int)))) return st;
+            if ((st = m->s2.ensure(std::max(N, 1) * sizeof(int)))) return st;
+            if ((st = m->s3.ensure((size_t)3 * fblocks * sizeof(int)))) return st;
+            if ((st = m->g_t0.ensure(std::max(N, 1) * sizeof(int)))) return st;
+            if ((st = m->g_t1.ensure(std::max(N, 1) * sizeof(int)))) return st;
+            if ((st = m->g_t2.ensure(std::max(N, 1) * sizeof(int)))) return st;
+            if ((st = m->g_last.ensure(std::max(N, 1) * sizeof(int)))) return st;
+            if ((st = m->g_dec.ensure((size_t)M * sizeof(int)))) return st;
+            if ((st = m->g_chg.ensure((size_t)(M + 2) * sizeof(int)))) return st;
+            if (!m->done_ctr.p) {  // the accept kernel's counter: zero once, reset by its user
+                if ((st = m->done_ctr.ensure(64))) return st;
+                ORBFE_HIP(hipMemsetAsync(m->done_ctr.p, 0, 64, m->stream));
+            }
+            SbpFusedArgs fu{};
+            FrustumArgs& fa = fu.fr;
+            fa.n = M;
+            fa.xyz = d_xyz;
+            fa.normal = d_normal;
+            fa.mind = d_min_dist;
+            fa.maxd = d_max_dist;
+            std::memcpy(fa.T, tcw, sizeof(fa.T));
+            camera_center(tcw, fa.ow);
+            fa.fx = cam->fx;
+            fa.fy = cam->fy;
+            fa.cx = cam->cx;
+            fa.cy = cam->cy;
+            fa.bf = cam->bf;
+            fa.minx = frame->min_x;
+            fa.maxx = frame->max_x;
+            fa.miny = frame->min_y;
+            fa.maxy = frame->max_y;
+            fa.log_scale = log_scale_factor;
+            fa.cos_limit = viewing_cos_limit;
+            fa.in_view = d_in_view;
+            fa.skip = d_skip;
+            fa.bad = d_bad;
+            SbpLocalArgs& a = fu.s;
+            if ((st = m->frame_device(frame, a.f))) return st;  // AssignFeaturesToGrid
+            a.mp.m = M;
+            a.mp.desc = reinterpret_cast<const uint4*>(d_desc);
+            a.th = th;
+            a.nlevels = frame->nlevels;
+            a.cnt = m->cnt.as<int>();
+            a.cand = m->cand.as<int2>();
+            for (int l = 0; l < frame->nlevels; ++l) fu.scalev[l] = frame->scale_factors[l];
+            fu.blk = m->s3.as<int>();
+            fu.rounds = kBlindRounds;
+            GreedyArgs& g = fu.g;
+            g.m = M;
+            g.nkp = N;
+            g.mode = kGreedyLocal;
+            g.nnratio = nnratio;
+            g.kfix = kSbpFix;
+            g.fcnt = m->cnt.as<int>();
+            g.cand = m->cand.as<int2>();
+            g.cand_cap = LLONG_MAX;
+            g.nobs = d_nobs;
+            g.fmp0 = g.fmp = d_frame_mp;
+            g.fobs0 = g.fobs = d_frame_mp_obs;
+            g.ids = d_mp_ids;
+            g.T[0] = m->g_t0.as<int>();
+            g.T[1] = m->g_t1.as<int>();
+            g.T[2] = m->g_t2.as<int>();
+            g.dec = m->g_dec.as<int>();
+            g.chg = m->g_chg.as<int>();
+            g.last = m->g_last.as<int>();
+            g.nm = m->scal.as<int>();
+            g.save_fmp = m->s1.as<int>();
+            g.save_fobs = m->s2.as<int>();
+            g.done = m->done_ctr.as<int>();
+            g.blk = m->s3.as<int>();
+            g.nblk = fblocks;
+            g.stats = m->scal.as<int>();
+            g.conv_round = kBlindRounds - 1;
+            hipLaunchKernelGGL(sbp_local_fused_kernel, dim3(fblocks), dim3(256), 0, m->stream, fu);
+            const int rblocks = std::max(1, (std::max(std::max(M, N), 32) + kGreedyBlock - 1) / kGreedyBlock);
+            for (int r = 0; r < kBlindRounds; ++r)
+                hipLaunchKernelGGL(greedy_round_kernel, dim3(rblocks), dim3(kGreedyBlock), 0, m->stream, g, r);
+            hipLaunchKernelGGL(greedy_accept_kernel, dim3((M + kGreedyBlock - 1) / kGreedyBlock),
+                               dim3(kGreedyBlock), 0, m->stream, g);
+            ORBFE_HIP(hipGetLastError());
+            m->rounds_on_device = false;
+            int host[6] = {0, 0, 0, 0, 0, 0};
+            ORBFE_HIP(hipMemcpyAsync(host, m->scal.p, sizeof(host), hipMemcpyDeviceToHost, m->stream));
+            ORBFE_HIP(hipStreamSynchronize(m->stream));
+            if (!host[3] && host[4] == 0) {  // no overflow, converged
+                m->last_rounds = host[5];
+                counts[0] = host[0];
+                counts[1] = host[1];
+                return host[2] ? host[2] : ORBFE_OK;
+            }
+            // restore the frame's slots and take the CSR path
+            ORBFE_HIP(hipMemcpyAsync(d_frame_mp, m->s1.p, (size_t)N * 4, hipMemcpyDeviceToDevice, m->stream));
+            ORBFE_HIP(hipMemcpyAsync(d_frame_mp_obs, m->s2.p, (size_t)N * 4, hipMemcpyDeviceToDevice, m->stream));
+            ++m->capacity_retries;
+        }
         bool retried = false;
         std::function<int()> attempt = [&]() -> int {
         ORBFE_HIP(hipMemsetAsync(m->scal.p, 0, 16, m->stream));
