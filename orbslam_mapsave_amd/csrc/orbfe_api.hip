@@ -172,6 +172,10 @@ struct orbfe_extractor {
     // plan / workspace buffer: set_plan and a growing ensure_frames drop the graph.
     hipGraphExec_t g1 = nullptr;
     const void* g1_key[8] = {};  // the buffers and plan the graph was captured with
+    // K4 fused into K5 per keypoint window (default), or its own pass over every level with
+    // K5 reading the blurred levels (ORBFE_PREBLUR=1: describe 0.30 -> 0.20 ms per 256 frames,
+    // but the pass costs 0.19 ms; profiles/r02/experiments/preblur.json)
+    bool fused_blur = std::getenv("ORBFE_PREBLUR") == nullptr;
     bool graph_broken = std::getenv("ORBFE_NO_GRAPH") != nullptr;  // capture failed once (or
                                  // disabled for A/B runs): keep to the launch path
 
@@ -385,7 +389,26 @@ struct orbfe_extractor {
         oa.sort_cap = g.sort_cap;
         oa.lds_keys = g.oct_keys;
         ORBFE_LAUNCH(prof, ORBFE_STAGE_OCTREE, octree_kernel, dim3(n, L), dim3(kOctBlockSize), g.oct_lds, stream, oa);
-        // K4 (the blur) is fused into K5: each keypoint's window is blurred in LDS
+        // K4 blur: fused into K5, where each keypoint's window is blurred in LDS, or (PREBLUR)
+        // every level of every frame, read by the pre-blurred describe
+        if (!fused_blur) {
+            BlurArgs ba;
+            ba.nlevels = L;
+            for (int l = 0; l < L; ++l) {
+                ba.w[l] = g.geo.lv[l].w;
+                ba.h[l] = g.geo.lv[l].h;
+                ba.src[l] = lp[l];
+                ba.dst[l] = bp[l];
+                ba.simd_xb[l] = x86() ? sse2_body_blur(g.geo.lv[l].w) : 0;
+                ba.bt_begin[l] = g.bt_begin[l];
+                ba.bt_cw[l] = g.bt_cw[l];
+            }
+            for (int i = 0; i < 4; ++i) ba.taps[i] = tab.taps[i];
+            if (x86())
+                ORBFE_LAUNCH(prof, ORBFE_STAGE_BLUR, blur_band_kernel<true>, dim3(g.bt_total, n), dim3(64), 0, stream, ba);
+            else
+                ORBFE_LAUNCH(prof, ORBFE_STAGE_BLUR, blur_band_kernel<false>, dim3(g.bt_total, n), dim3(64), 0, stream, ba);
+        }
         // K5 describe
         DescArgs da;
         da.nlevels = L;
@@ -396,6 +419,7 @@ struct orbfe_extractor {
             da.scale[l] = g.geo.lv[l].scale;
             da.size[l] = g.geo.lv[l].size;
             da.pyr[l] = lp[l];
+            da.blur[l] = bp[l];
             da.w[l] = g.geo.lv[l].w;
             da.h[l] = g.geo.lv[l].h;
             da.simd_xb[l] = x86() ? sse2_body_blur(da.w[l]) : 0;
@@ -412,16 +436,19 @@ struct orbfe_extractor {
         const int group = n >= kDescSmallBatch ? kDescGroupSize : kDescGroupSmall;
         const int per_block = (kDescBlockSize / 64) * group;  // slots per workgroup
         const dim3 dgrid((g.geo.out_total + per_block - 1) / per_block, n);
-        if (group == kDescGroupSize) {
-            if (x86())
-                ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, (describe_kernel<kDescGroupSize, true>), dgrid, dim3(kDescBlockSize), 0, stream, da);
-            else
-                ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, (describe_kernel<kDescGroupSize, false>), dgrid, dim3(kDescBlockSize), 0, stream, da);
-        } else {
-            if (x86())
-                ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, (describe_kernel<kDescGroupSmall, true>), dgrid, dim3(kDescBlockSize), 0, stream, da);
-            else
-                ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, (describe_kernel<kDescGroupSmall, false>), dgrid, dim3(kDescBlockSize), 0, stream, da);
+        const int variant = (group == kDescGroupSize ? 4 : 0) | (x86() ? 2 : 0) | (fused_blur ? 0 : 1);
+        switch (variant) {
+#define ORBFE_DESC_CASE(V, G, X, P) \
+            case V: ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, (describe_kernel<G, X, P>), dgrid, dim3(kDescBlockSize), 0, stream, da); break;
+            ORBFE_DESC_CASE(0, kDescGroupSmall, false, false)
+            ORBFE_DESC_CASE(1, kDescGroupSmall, false, true)
+            ORBFE_DESC_CASE(2, kDescGroupSmall, true, false)
+            ORBFE_DESC_CASE(3, kDescGroupSmall, true, true)
+            ORBFE_DESC_CASE(4, kDescGroupSize, false, false)
+            ORBFE_DESC_CASE(5, kDescGroupSize, false, true)
+            ORBFE_DESC_CASE(6, kDescGroupSize, true, false)
+            ORBFE_DESC_CASE(7, kDescGroupSize, true, true)
+#undef ORBFE_DESC_CASE
         }
         ORBFE_HIP(hipGetLastError());
         last_n = n;
@@ -1035,20 +1062,24 @@ int orbfe_get_blurred_level(orbfe_extractor* h, int frame, int level, uint8_t* o
     const Plan& g = h->plan;
     const LevelGeo& lv = g.geo.lv[level];
     LevelPtr bp{h->blur.as<uint8_t>() + lv.off, g.slab, lv.pitch};
-    if (out) {  // K4 on demand: the extraction path blurs keypoint windows inside K5
+    if (out) {  // K4 on demand (the default extraction path blurs keypoint windows inside K5)
         DeviceGuard dg(h->device);
         BlurArgs ba;
         ba.nlevels = g.geo.nlevels;
         for (int l = 0; l < ba.nlevels; ++l) {
-            ba.tile_begin[l] = g.tile_begin[l];
             ba.w[l] = g.geo.lv[l].w;
             ba.h[l] = g.geo.lv[l].h;
             ba.src[l] = h->last_pyr[l];
             ba.dst[l] = LevelPtr{h->blur.as<uint8_t>() + g.geo.lv[l].off, g.slab, g.geo.lv[l].pitch};
             ba.simd_xb[l] = h->x86() ? sse2_body_blur(g.geo.lv[l].w) : 0;
+            ba.bt_begin[l] = g.bt_begin[l];
+            ba.bt_cw[l] = g.bt_cw[l];
         }
         for (int i = 0; i < 4; ++i) ba.taps[i] = h->tab.taps[i];
-        hipLaunchKernelGGL(blur_kernel, dim3(g.tiles_total, h->last_n), dim3(256), 0, h->stream, ba);
+        if (h->x86())
+            hipLaunchKernelGGL(blur_band_kernel<true>, dim3(g.bt_total, h->last_n), dim3(64), 0, h->stream, ba);
+        else
+            hipLaunchKernelGGL(blur_band_kernel<false>, dim3(g.bt_total, h->last_n), dim3(64), 0, h->stream, ba);
         ORBFE_HIP(hipGetLastError());
     }
     return copy_level(h, bp, frame, level, out, w, hgt);

@@ -10,7 +10,7 @@
 //                       (764-831); one workgroup per (frame, cell)
 //   K3 octree_kernel    DistributeOctTree (538-762) as a data-parallel list emulation; one
 //                       workgroup per (frame, level)
-//   K4 blur_kernel      GaussianBlur 7x7 sigma 2 REFLECT_101 (1088-1089), integer path
+//   K4 blur_band_kernel GaussianBlur 7x7 sigma 2 REFLECT_101 (1088-1089), integer path
 //   K5 describe_kernel  IC_Angle (76-103) + rBRIEF (107-146) + level scaling (1098-1104);
 //                       one wave per keypoint, 256 tests packed with 4 ballots
 #include <hip/hip_runtime.h>
@@ -718,7 +718,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds& s, 
     int seq_base = nini;
     bool finished = false;
     bool phase2 = false;
-    int npass = 0, nround = 0;
+    [[maybe_unused]] int npass = 0, nround = 0;  // read by the ORBFE_OCT_TIMING build
 
     // ---- phase 1: split every open node per pass (593-671)
     for (int pass = 0; pass < 64 && !finished && !phase2; ++pass) {
@@ -1112,141 +1112,170 @@ __device__ __forceinline__ uint32_t blur_round_bit(uint32_t v, bool even) {
     return even ? ((v - 0x7fffu) >> 16) & 1u : 1u;
 }
 
-// K4 — GaussianBlur(7x7, sigma 2, REFLECT_101) integer path: row pass R = sum k_i I (<= 65535,
-// kept as u16), column pass (sum k_j R + 2^15) >> 16 saturated (App. A.2).  128 x 32 output
-// tile per workgroup of 32 x 8 threads; each thread makes 4 x 4 pixels from dword LDS reads.
-constexpr int kBlurTW = kBlurTileW, kBlurTH = kBlurTileH;
-constexpr int kBlurRPT = kBlurTH / 8;  // output rows per thread (256 threads = 8 x 32)
 // cv::borderInterpolate(p, len, BORDER_REFLECT_101) (App. A.2), any distance from the edge.
 __device__ __forceinline__ int reflect101(int p, int len) {
     if (len == 1) return 0;
     while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - p - 2;
     return p;
 }
-constexpr int kBlurIW = kBlurTW + 8;   // input row: image cols [ox-4, ox+TW+4)
-constexpr int kBlurIQ = (kBlurIW + 15) / 16;  // 16-byte chunks per input row (9)
-constexpr int kBlurIP = 16 * kBlurIQ;  // LDS row pitch (144, 16-byte aligned)
-constexpr int kBlurIR = kBlurTH + 6;   // input rows [oy-3, oy+TH+3)
-constexpr int kBlurRPW = 64 / kBlurIQ;  // input rows per wave per step (7)
-__global__ __launch_bounds__(256) void blur_kernel(BlurArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t in[kBlurIR * kBlurIP];
-    __shared__ __attribute__((aligned(16))) uint16_t rowp[kBlurIR * kBlurTW];  // row pairs, u16x2
-    int t, f, l = 0;
+// K4 — GaussianBlur(7x7, sigma 2, REFLECT_101), integer path (App. A.2): row pass R = sum k_i I
+// (<= 65535, exact in u16), column pass (sum k_j R + 2^15) >> 16 saturated; x86 mode rounds the
+// SIMD body half to even (H6) as a vertical sweep without LDS: lane q of a (level, 32-row band, 64-lane column
+// wave) tile owns output columns 8q .. 8q+7.  It walks its band's 38 input rows: one 16-byte
+// load per row (the window of columns 8q-4 .. 8q+11, straight from the level; kBandAhead rows
+// in flight ahead of the row being used), the row pass is two v_dot4_u32_u8 per column, rows
+// 2k, 2k+1 are packed as u16 pairs, and output rows 2m, 2m+1 are four v_dot2_u32_u16 each over
+// the pairs m .. m+3 held in registers (the sweep is unrolled, so the windows rotate without
+// moves).  Rows are reflected (REFLECT_101) by index.  A lane whose window leaves the row
+// loads the 16 bytes at ls = clamp(8q-4, 0, w-16) instead; every window byte's reflected
+// column then lies in that load, and v_perm_b32 pairs (selectors fixed per lane) rebuild it.
+constexpr int kBandAhead = 8;
+__device__ __forceinline__ int reflect101_1(int p, int len) {  // |overshoot| < len - 1
+    return p < 0 ? -p : (p >= len ? 2 * len - 2 - p : p);
+}
+template <bool kX86>
+__global__ __launch_bounds__(64) void blur_band_kernel(BlurArgs a) {
+    int t, f;
     xcd_block(t, f);
-    while (l + 1 < a.nlevels && t >= a.tile_begin[l + 1]) ++l;
-    t -= a.tile_begin[l];
+    int l = 0;
+    while (l + 1 < a.nlevels && t >= a.bt_begin[l + 1]) ++l;
+    t -= a.bt_begin[l];
+    const int cw = a.bt_cw[l];
+    const int band = t / cw;
+    const int x = 8 * ((t - band * cw) * 64 + (int)threadIdx.x);
     const int w = a.w[l], h = a.h[l];
-    const int tx = (w + kBlurTW - 1) / kBlurTW;
-    const int ox = (t % tx) * kBlurTW, oy = (t / tx) * kBlurTH;
-    const LevelPtr sp = a.src[l];
+    if (x >= w) return;
+    const LevelPtr sp = a.src[l], dp = a.dst[l];
     const uint8_t* src = sp.base + f * sp.fpitch;
-    const int tid = threadIdx.x;
-    // Staging: lane (row rr = lane / 9, chunk q = lane % 9) of every wave copies 16 bytes; the
-    // four waves walk the 38 input rows 7 at a time.  Rows are reflected (REFLECT_101) by the
-    // row pointer; a chunk that leaves [0, w) is assembled byte by byte with reflected columns
-    // (tiles at the left / right edge only).  Level sizes are >= 4.
-    {
-        const int lane = tid & 63, wid = tid >> 6;
-        const int rr = lane / kBlurIQ, q = lane - rr * kBlurIQ;
-        const int x = ox - 4 + 16 * q;
-        const bool inside = x >= 0 && x + 16 <= w;
-        for (int r = wid * kBlurRPW + rr; rr < kBlurRPW && r < kBlurIR; r += 4 * kBlurRPW) {
-            const int yy = reflect101(oy - 3 + r, h);
-            const uint8_t* row = src + (long long)yy * sp.pitch;
-            uint4 v;
-            if (inside) {
-                v = load16_a4(row + x);  // pitch % 4 == 0, x % 4 == 0
-            } else {
-                uint32_t b[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    b[k >> 2] |= (uint32_t)row[reflect101(x + k, w)] << (8 * (k & 3));
+    uint8_t* dst = const_cast<uint8_t*>(dp.base) + f * dp.fpitch;
+    const int y0 = band * kBlurBandRows, yend = min(y0 + kBlurBandRows, h);
+    const uint32_t KLO = (uint32_t)(a.taps[0] | (a.taps[1] << 8) | (a.taps[2] << 16) | (a.taps[3] << 24));
+    const uint32_t KHI = (uint32_t)(a.taps[2] | (a.taps[1] << 8) | (a.taps[0] << 16));
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    const unsigned short k0 = (unsigned short)a.taps[0], k1 = (unsigned short)a.taps[1],
+                         k2 = (unsigned short)a.taps[2], k3 = (unsigned short)a.taps[3];
+    const us2 T01 = us2{k0, k1}, T23 = us2{k2, k3}, T21 = us2{k2, k1}, T0L = us2{k0, 0},
+              T0H = us2{0, k0}, T12 = us2{k1, k2}, T32 = us2{k3, k2}, T10 = us2{k1, k0};
+    const bool even0 = kX86 && x < a.simd_xb[l], even1 = kX86 && x + 4 < a.simd_xb[l];
+    auto round_sat = [&](uint32_t v, bool even) {
+        // sums carry 0x7fff; + 1 (scalar FixedPtCastEx) or the half-to-even bit (x86 SIMD body)
+        if constexpr (kX86) v += blur_round_bit(v, even);
+        else v += 1u;
+        return min(v, 0xffffffu);  // byte 2 = min(acc >> 16, 255)
+    };
+    if (w < 16) {  // levels narrower than 16 px: each pixel directly, on reflected indices
+        for (int y = y0; y < yend; ++y)
+            for (int c = x; c < min(x + 8, w); ++c) {
+                uint32_t acc = 0x7fffu;
+                for (int i = -3; i <= 3; ++i) {
+                    const uint8_t* row = src + (long long)reflect101(y + i, h) * sp.pitch;
+                    uint32_t rs = 0;
+                    for (int j = -3; j <= 3; ++j)
+                        rs += (uint32_t)a.taps[3 - (j < 0 ? -j : j)] * row[reflect101(c + j, w)];
+                    acc += (uint32_t)a.taps[3 - (i < 0 ? -i : i)] * rs;
                 }
-                v = make_uint4(b[0], b[1], b[2], b[3]);
+                dst[(long long)y * dp.pitch + c] = (uint8_t)(round_sat(acc, kX86 && c < a.simd_xb[l]) >> 16);
             }
-            *reinterpret_cast<uint4*>(in + r * kBlurIP + 16 * q) = v;
-        }
+        return;
     }
-    __syncthreads();
-    // Row pass on bytes: output col c = dot4(bytes c+1..c+4, k0 k1 k2 k3) + dot4(bytes c+5..c+8,
-    // k2 k1 k0 0) (v_dot4_u32_u8), exact in u16 (max 255 * 257).  A work item makes 4 columns
-    // of two consecutive input rows and stores them as dwords (row 2i in the low half, row 2i+1
-    // in the high half), so the column pass reads row pairs for v_dot2_u32_u16.
-    const int k0 = a.taps[0], k1 = a.taps[1], k2 = a.taps[2], k3 = a.taps[3];
-    const uint32_t KLO = (uint32_t)(k0 | (k1 << 8) | (k2 << 16) | (k3 << 24));
-    const uint32_t KHI = (uint32_t)(k2 | (k1 << 8) | (k0 << 16));
-    constexpr int NPAIR = kBlurIR / 2;
-    for (int it = tid; it < NPAIR * (kBlurTW / 4); it += 256) {
-        const int pr = it >> 5, q = it & 31;
-        uint32_t h[2][4];
+    const bool edge = x < 4 || x + 12 > w;
+    const int ls = min(max(x - 4, 0), w - 16);
+    // edge lanes: window dword k = v_perm(v.y, v.x, selA_k) | v_perm(v.w, v.z, selB_k), the
+    // selector bytes of the pair not holding a byte's source being 0x0c (-> 0)
+    uint32_t selA[4] = {0u, 0u, 0u, 0u}, selB[4] = {0u, 0u, 0u, 0u};
+    if (edge) {
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const uint32_t* row = reinterpret_cast<const uint32_t*>(in + (2 * pr + e) * kBlurIP) + q;
-            const uint32_t w0 = row[0], w1 = row[1], w2 = row[2];
+        for (int k = 0; k < 4; ++k)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const uint32_t lo = j < 3 ? __builtin_amdgcn_alignbyte(w1, w0, j + 1) : w1;
-                const uint32_t hi = j < 3 ? __builtin_amdgcn_alignbyte(w2, w1, j + 1) : w2;
-                h[e][j] = __builtin_amdgcn_udot4(hi, KHI, __builtin_amdgcn_udot4(lo, KLO, 0u, false), false);
+                const int b = reflect101_1(x - 4 + 4 * k + j, w) - ls;  // in [0, 16)
+                selA[k] |= (uint32_t)(b < 8 ? b : 0x0c) << (8 * j);
+                selB[k] |= (uint32_t)(b >= 8 ? b - 8 : 0x0c) << (8 * j);
             }
-        }
-        *reinterpret_cast<uint4*>(rowp + (pr * kBlurTW + 4 * q) * 2) =
-            make_uint4(h[0][0] | (h[1][0] << 16), h[0][1] | (h[1][1] << 16),
-                       h[0][2] | (h[1][2] << 16), h[0][3] | (h[1][3] << 16));
     }
-    __syncthreads();
-    // Column pass: output row j (input rows j .. j+6) as four v_dot2_u32_u16 over row pairs,
-    // the rounding constant folded into the first; rows j even / odd pair differently.
-    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-    const us2 T01 = us2{(unsigned short)k0, (unsigned short)k1}, T23 = us2{(unsigned short)k2, (unsigned short)k3},
-              T21 = us2{(unsigned short)k2, (unsigned short)k1}, T12 = us2{(unsigned short)k1, (unsigned short)k2},
-              T32 = us2{(unsigned short)k3, (unsigned short)k2}, T10 = us2{(unsigned short)k1, (unsigned short)k0},
-              T0L = us2{(unsigned short)k0, 0}, T0H = us2{0, (unsigned short)k0};
-    const LevelPtr dp = a.dst[l];
-    uint8_t* dst = const_cast<uint8_t*>(dp.base) + f * dp.fpitch;
-    const int ltx = tid & 31, lty = tid >> 5;
-    uint4 Pq[kBlurRPT / 2 + 3];
+    auto load_row = [&](int r) -> uint4 {
+        return load16_a1(src + (long long)reflect101_1(r, h) * sp.pitch + ls);
+    };
+    // row pass at the lane's 8 columns: column x + j from window bytes j+1 .. j+7
+    auto rowpass = [&](uint4 v, uint32_t (&o)[8]) {
+        if (edge) {
+            uint32_t e[4];
 #pragma unroll
-    for (int i = 0; i < kBlurRPT / 2 + 3; ++i)
-        Pq[i] = *reinterpret_cast<const uint4*>(rowp + (((kBlurRPT / 2) * lty + i) * kBlurTW + 4 * ltx) * 2);
-    const int x = ox + 4 * ltx;
-    // x86 arithmetic: the 4 columns lie wholly in the SIMD body or wholly in the tail (both
-    // x and simd_xb are multiples of 4)
-    const bool even = x < a.simd_xb[l];
-#pragma unroll
-    for (int j = 0; j < kBlurRPT; ++j) {
-        const int y = oy + kBlurRPT * lty + j;
-        if (y >= h) break;
-        const int b = j >> 1;
-        uint32_t acc[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const uint32_t p0 = (&Pq[b].x)[c], p1 = (&Pq[b + 1].x)[c], p2 = (&Pq[b + 2].x)[c],
-                           p3 = (&Pq[b + 3].x)[c];
-            uint32_t v;
-            if ((j & 1) == 0) {
-                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T01, 0x7fffu, false);
-                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), T23, v, false);
-                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), T21, v, false);
-                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), T0L, v, false);
-            } else {
-                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T0H, 0x7fffu, false);
-                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), T12, v, false);
-                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), T32, v, false);
-                v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), T10, v, false);
-            }
-            acc[c] = min(v + blur_round_bit(v, even), 0xffffffu);  // byte 2 = min(acc >> 16, 255)
+            for (int k = 0; k < 4; ++k)
+                e[k] = __builtin_amdgcn_perm(v.y, v.x, selA[k]) | __builtin_amdgcn_perm(v.w, v.z, selB[k]);
+            v = make_uint4(e[0], e[1], e[2], e[3]);
         }
-        const uint32_t packed = __builtin_amdgcn_perm(acc[1], acc[0], 0x0c0c0602u) |
-                                __builtin_amdgcn_perm(acc[3], acc[2], 0x06020c0cu);
+        const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int b = j + 1;
+            const uint32_t lo_ = (b & 3) ? __builtin_amdgcn_alignbyte(d[(b >> 2) + 1], d[b >> 2], b & 3) : d[b >> 2];
+            const int b2 = b + 4;
+            const uint32_t hi_ = (b2 & 3) ? __builtin_amdgcn_alignbyte(d[(b2 >> 2) + 1], d[b2 >> 2], b2 & 3) : d[b2 >> 2];
+            o[j] = __builtin_amdgcn_udot4(hi_, KHI, __builtin_amdgcn_udot4(lo_, KLO, 0u, false), false);
+        }
+    };
+    auto out_row = [&](int y, const uint32_t (&acc)[8]) {
+        const uint32_t lw = __builtin_amdgcn_perm(acc[1], acc[0], 0x0c0c0602u) |
+                            __builtin_amdgcn_perm(acc[3], acc[2], 0x06020c0cu);
+        const uint32_t hw = __builtin_amdgcn_perm(acc[5], acc[4], 0x0c0c0602u) |
+                            __builtin_amdgcn_perm(acc[7], acc[6], 0x06020c0cu);
         uint8_t* d = dst + (long long)y * dp.pitch + x;
-        if (x + 4 <= w) {
-            *reinterpret_cast<uint32_t*>(d) = packed;
+        if (x + 8 <= w) {
+            *reinterpret_cast<uint2*>(d) = make_uint2(lw, hw);
         } else {
-            for (int c = 0; c < 4 && x + c < w; ++c) d[c] = (uint8_t)(packed >> (8 * c));
+            const unsigned long long v = ((unsigned long long)hw << 32) | lw;
+            for (int c = 0; c < 8 && x + c < w; ++c) d[c] = (uint8_t)(v >> (8 * c));
         }
+    };
+    constexpr int kPairsB = kBlurBandRows / 2 + 3;  // 19 input row pairs
+    constexpr int kAheadP = kBandAhead / 2;          // pairs in flight
+    uint4 ring[kAheadP][2];
+#pragma unroll
+    for (int i = 0; i < kAheadP; ++i) {
+        ring[i][0] = load_row(y0 - 3 + 2 * i);
+        ring[i][1] = load_row(y0 - 2 + 2 * i);
+    }
+    uint32_t P[4][8];  // pairs m .. m+3: rows y0-3+2k (low halves), y0-2+2k (high)
+#pragma unroll
+    for (int k = 0; k < kPairsB; ++k) {
+        const uint4 c0 = ring[k % kAheadP][0], c1 = ring[k % kAheadP][1];
+        if (k + kAheadP < kPairsB) {
+            ring[k % kAheadP][0] = load_row(y0 - 3 + 2 * (k + kAheadP));
+            ring[k % kAheadP][1] = load_row(y0 - 2 + 2 * (k + kAheadP));
+        }
+        uint32_t e[8], o[8];
+        rowpass(c0, e);
+        rowpass(c1, o);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) P[k & 3][c] = __builtin_amdgcn_perm(o[c], e[c], 0x05040100u);
+        if (k < 3) continue;
+        const int m = k - 3;
+        const uint32_t* p0 = P[m & 3];
+        const uint32_t* p1 = P[(m + 1) & 3];
+        const uint32_t* p2 = P[(m + 2) & 3];
+        const uint32_t* p3 = P[(m + 3) & 3];
+        uint32_t ev[8], od[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const bool even = c < 4 ? even0 : even1;
+            uint32_t v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0[c]), T01, 0x7fffu, false);
+            v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1[c]), T23, v, false);
+            v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2[c]), T21, v, false);
+            v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3[c]), T0L, v, false);
+            ev[c] = round_sat(v, even);
+            uint32_t u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0[c]), T0H, 0x7fffu, false);
+            u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1[c]), T12, u, false);
+            u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2[c]), T32, u, false);
+            u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3[c]), T10, u, false);
+            od[c] = round_sat(u, even);
+        }
+        if (y0 + 2 * m < yend) out_row(y0 + 2 * m, ev);
+        if (y0 + 2 * m + 1 < yend) out_row(y0 + 2 * m + 1, od);
     }
 }
+template __global__ void blur_band_kernel<false>(BlurArgs);
+template __global__ void blur_band_kernel<true>(BlurArgs);
 
 // ---------------------------------------------------------------------------------------------
 // K5 — IC angle (76-103) on the unblurred level, rBRIEF (107-146) on the blurred level and
@@ -1266,7 +1295,9 @@ constexpr int kDescWinRows = 2 * kDescWinR + 1;      // 37
 constexpr int kDescWinP = 48;                        // bytes per window row (3 x 16)
 constexpr int kDescWinBytes = kDescWinRows * kDescWinP;
 typedef float float2v __attribute__((ext_vector_type(2)));
-template <int kDescGroup, bool kX86>
+// kPre: the levels were blurred by K4 (a.blur); the wave copies each keypoint's 37-row
+// blurred window straight into LDS instead of blurring a raw window.
+template <int kDescGroup, bool kX86, bool kPre>
 __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
     int bx, f;
     xcd_block(bx, f);
@@ -1387,7 +1418,7 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
     // raw rows x 3 chunks of 16 bytes from x0-4 into LDS (loads of the next keypoint in flight
     // during the current one) and blurs window cols 0..39 of all 37 rows; when a
     // sampled pixel's 7x7 support leaves the level, or a chunk would leave the row, the raw
-    // window is assembled byte by byte with reflect101 indices instead.  Then blur_kernel's
+    // window is assembled byte by byte with reflect101 indices instead.  Then K4's
     // integer passes: rows by v_dot4 into u16 row pairs, columns by v_dot2 + 2^15 >> 16.
     uint32_t my_kc = 0;
     int my_x0 = 0;
@@ -1412,10 +1443,11 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
     constexpr int kBlurQ = 10;
     // The raw window is dead once the row pass has read it and the blurred window is written
     // after that (same wave, LDS ops in order), so the two share one buffer.
-    constexpr int kRawWinBytes = kRawRows * kRawP > kDescWinBytes ? kRawRows * kRawP : kDescWinBytes;
+    constexpr int kRawWinBytes = kPre ? kDescWinBytes
+                                      : kRawRows * kRawP > kDescWinBytes ? kRawRows * kRawP : kDescWinBytes;
     __shared__ __attribute__((aligned(16))) uint8_t raw_all[kDescBlock / 64][kRawWinBytes];
     constexpr int kRowpP = 4 * kBlurQ;                 // u16 row-pair pitch: window cols 0..39
-    __shared__ __attribute__((aligned(16))) uint32_t rowp_all[kDescBlock / 64][kPairs * kRowpP];
+    __shared__ __attribute__((aligned(16))) uint32_t rowp_all[kDescBlock / 64][kPre ? 4 : kPairs * kRowpP];
     uint8_t* raw = raw_all[threadIdx.x >> 6];
     uint32_t* rowp = rowp_all[threadIdx.x >> 6];
     uint8_t* wb = raw;
@@ -1454,18 +1486,48 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
             }
         }
     };
-    load_raw(__ffsll((long long)vmask) - 1);
+    // kPre: blurred window chunk c = lane + 64 i (i < 2, c < 37 * 3): window row c / 3, 16-byte
+    // part c % 3, at LDS byte 16 c.  Keypoints lie >= 19 px inside their level, so rows
+    // y - 18 .. y + 18 are level rows; the bytes of a row past the level width (< 16, never
+    // sampled) stay inside the slab (the last row read is h - 2).
+    auto load_win = [&](int j) {
+        const int kl = __builtin_amdgcn_readlane(my_l, j);
+        const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane(my_key, j);
+        const int x = key_x(kk), y = key_y(kk), x0 = (x - kDescWinR) & ~3;
+        const LevelPtr bp = a.blur[kl];
+        const uint8_t* fb = bp.base + f * bp.fpitch + (long long)(y - kDescWinR) * bp.pitch + x0;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int c = lane + 64 * i, r = c / 3, part = c - 3 * r;
+            rv[i] = make_uint4(0u, 0u, 0u, 0u);
+            if (r < kDescWinRows) rv[i] = load16_a4(fb + (long long)r * bp.pitch + 16 * part);
+        }
+    };
+    if constexpr (kPre) load_win(__ffsll((long long)vmask) - 1);
+    else load_raw(__ffsll((long long)vmask) - 1);
     for (unsigned long long m = vmask; m; m &= m - 1) {
         const int j = __ffsll((long long)m) - 1;
+        if constexpr (kPre) {
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const int c = lane + 64 * i;
-            if (c / kRawQ < kRawRows - 1) *reinterpret_cast<uint4*>(raw + 16 * c) = rv[i];
+            for (int i = 0; i < 2; ++i) {
+                const int c = lane + 64 * i;
+                if (c < 3 * kDescWinRows) *reinterpret_cast<uint4*>(wb + 16 * c) = rv[i];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const int c = lane + 64 * i;
+                if (c / kRawQ < kRawRows - 1) *reinterpret_cast<uint4*>(raw + 16 * c) = rv[i];
+            }
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         const unsigned long long rest = m & (m - 1);
-        if (rest) load_raw(__ffsll((long long)rest) - 1);  // next keypoint's raw window in flight
+        if (rest) {  // next keypoint's window in flight
+            if constexpr (kPre) load_win(__ffsll((long long)rest) - 1);
+            else load_raw(__ffsll((long long)rest) - 1);
+        }
+        if constexpr (!kPre) {
         // row pass: item (pair pr, quad q) -> window cols 4q..4q+3 of raw rows 2pr, 2pr+1.
         // Items it = lane + 64 i: (pr, q) advance by (6, 4) or, when q wraps, (7, -6), and the
         // raw offset with them (no division or multiply in the loop); (pr, q) sits at dword
@@ -1544,6 +1606,7 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        }  // !kPre
         const float cj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ca), j));
         const float sj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, sa), j));
         const uint32_t kc = (uint32_t)__builtin_amdgcn_readlane((int)my_kc, j);
@@ -1663,7 +1726,7 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
     g.h = h;
     g.geo.nlevels = L;
     long long slab = 0, keys = 0;
-    int out = 0, ncap_max = 0, tiles = 0;
+    int out = 0, ncap_max = 0;
     g.cells.clear();
     g.xtab.clear();
     g.ytab.clear();
@@ -1731,9 +1794,10 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
         lv.out_off = out;
         out += lv.ncap;
         ncap_max = std::max(ncap_max, lv.ncap);
-        // blur tiles
-        g.tile_begin[l] = tiles;
-        tiles += ((lv.w + kBlurTW - 1) / kBlurTW) * ((lv.h + kBlurTH - 1) / kBlurTH);
+        // blur band tiles
+        g.bt_begin[l] = g.bt_total;
+        g.bt_cw[l] = ((lv.w + 7) / 8 + 63) / 64;
+        g.bt_total += g.bt_cw[l] * ((lv.h + kBlurBandRows - 1) / kBlurBandRows);
         // resize tables for level l from level l-1 (App. A.1)
         if (l > 0) {
             const LevelGeo& sv = g.geo.lv[l - 1];
@@ -1812,7 +1876,6 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
     g.geo.out_total = out;
     g.slab = slab;
     g.ncap_max = ncap_max;
-    g.tiles_total = tiles;
     int sort_cap = 1;
     while (sort_cap < ncap_max) sort_cap <<= 1;
     g.sort_cap = sort_cap;

@@ -122,12 +122,13 @@ struct OctArgs {
 
 struct BlurArgs {
     int nlevels;
-    int tile_begin[kMaxLevels];
     int w[kMaxLevels], h[kMaxLevels];
     int taps[4];
     LevelPtr src[kMaxLevels];
     LevelPtr dst[kMaxLevels];
     int simd_xb[kMaxLevels];  // x86 arithmetic: columns [0, simd_xb) round half to even (H6)
+    int bt_begin[kMaxLevels];  // blur_band_kernel: first band tile of each level
+    int bt_cw[kMaxLevels];     // blur_band_kernel: 64-quad column waves per band of each level
 };
 
 struct DescArgs {
@@ -143,6 +144,7 @@ struct DescArgs {
     uint8_t* desc;
     int32_t* n_out;
     int simd_xb[kMaxLevels];  // as BlurArgs::simd_xb, for the fused per-keypoint blur
+    LevelPtr blur[kMaxLevels];  // blurred levels (K4 output), read by the pre-blurred variant
 };
 
 // Pixels [0, n) of a w-pixel row that OpenCV 3.3's x86 SSE2 vertical kernels produce (the rest
@@ -180,8 +182,8 @@ struct Plan {
     std::vector<int> xtab, ytab;
     int xoff[kMaxLevels] = {}, yoff[kMaxLevels] = {};
     long long slab = 0;
-    int ncap_max = 0, sort_cap = 0, tiles_total = 0;
-    int tile_begin[kMaxLevels] = {};
+    int ncap_max = 0, sort_cap = 0;
+    int bt_total = 0, bt_begin[kMaxLevels] = {}, bt_cw[kMaxLevels] = {};  // blur_band_kernel tiles
     size_t oct_lds = 0;
     int oct_keys = 0;      // LDS key capacity of the oct-tree kernel
     int roi_pitch = 0, roi_rows = 0, cand_max = 0;
@@ -201,7 +203,7 @@ template <bool kX86> __global__ void resize_tail_kernel(ResizeTailArgs);
 template <int kP> __global__ void fast_kernel(FastArgs);
 constexpr int kFastPitch = 48;  // fast_kernel<kFastPitch>: ROI pitch known at compile time
 __global__ void octree_kernel(OctArgs);
-__global__ void blur_kernel(BlurArgs);
+template <bool kX86> __global__ void blur_band_kernel(BlurArgs);
 template <int kDescGroup, bool kX86> __global__ void describe_kernel(DescArgs);
 extern __constant__ int c_umax[16];
 
@@ -221,6 +223,6 @@ constexpr int kDescBlockSize = ORBFE_DESC_BLOCK;
 constexpr int kDescSmallBatch = 8;  // batches below this use kDescGroupSmall keypoints per wave
 constexpr int kTailMinFrames = 8;   // batches below this skip the one-workgroup-per-frame tail
 constexpr int kDescGroupSize = ORBFE_DESC_GROUP;  // oct-tree output slots per describe wave
-constexpr int kBlurTileW = 128, kBlurTileH = 32;
+constexpr int kBlurBandRows = 32;  // output rows per blur_band_kernel lane
 
 }  // namespace orbfe

@@ -164,3 +164,23 @@ def test_unsupported_inputs_are_refused():
             e(np.zeros(shape, np.uint8))
         assert ei.value.status == ORBFE_ERR_UNSUPPORTED
     e.close()
+
+
+@pytest.mark.parametrize("size", [(643, 481), (1281, 722), (331, 247), (97, 73), (61, 44)])
+def test_blur_levels_odd_sizes(size):
+    """K4 (blur_band_kernel) on level widths of every residue mod 8 / mod 16, including levels
+    narrower than 16 and than 6 px (the byte-gather and all-edge-column paths), against the
+    oracle's GaussianBlur 7x7 REFLECT_101 (ORBextractor.cc:1088-1089)."""
+    from orbslam_mapsave_amd.native import ORBextractor
+    w, h = size
+    p = oracle.params(**CFG)
+    e = ORBextractor(1000, 1.2, 8, 32, 7, device=0, max_width=w, max_height=h)
+    try:
+        img = synthetic_frame(11, w, h)
+        e(img)
+        for l, lev in enumerate(oracle.pyramid(p, img)):
+            gb, ob = e.get_blurred_level(l), oracle.gaussian_blur(lev)
+            assert gb.shape == ob.shape
+            assert np.array_equal(gb, ob), f"{size} level {l} {lev.shape}: {(gb != ob).sum()} px differ"
+    finally:
+        e.close()
