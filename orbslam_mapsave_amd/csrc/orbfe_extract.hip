@@ -445,6 +445,9 @@ __device__ __forceinline__ int fast_emit(const uint8_t* S, const uint16_t* list,
 
 // kP: the ROI pitch as a compile-time constant (48 for every cell width up to 45 px, i.e. the
 // common frame sizes), so the 16 circle offsets of fast_S become LDS immediates; 0 = runtime.
+// Measured and dropped (profiles/r02/experiments/fast_variants.json): several cells per wave
+// with the next ROI prefetched into registers, and 4-pixel groups scored from aligned dwords
+// (conflict-free LDS reads, but 1.6x the VALU per survivor: 0.29 -> 0.35 ms).
 template <int kP>
 __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char fast_lds[];
@@ -545,10 +548,17 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
                 };
                 int pos = (int)below(b3, below(b2, below(b1, below(b0, (uint32_t)cnt))));
                 const int ob = cr * P + gx - X0;  // ROI offset of byte 0's window
-                if (fl & 0x80u) list[pos++] = (uint16_t)ob;
-                if (fl & 0x8000u) list[pos++] = (uint16_t)(ob + 1);
-                if (fl & 0x800000u) list[pos++] = (uint16_t)(ob + 2);
-                if (fl & 0x80000000u) list[pos] = (uint16_t)(ob + 3);
+                // unconditional stores (no exec-mask branch per byte): a byte that is not a
+                // survivor writes the lane's trash slot past the list
+                const int tr = a.cand_max + lane;
+                const int f0 = (fl >> 7) & 1, f1 = (fl >> 15) & 1, f2 = (fl >> 23) & 1, f3 = fl >> 31;
+                list[f0 ? pos : tr] = (uint16_t)ob;
+                pos += f0;
+                list[f1 ? pos : tr] = (uint16_t)(ob + 1);
+                pos += f1;
+                list[f2 ? pos : tr] = (uint16_t)(ob + 2);
+                pos += f2;
+                list[f3 ? pos : tr] = (uint16_t)(ob + 3);
             }
             cnt += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
         }
@@ -1871,7 +1881,7 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
     // ROI + zero-bordered score plane at the ROI pitch + candidate list of u16 ROI offsets
     if ((long long)rmax * g.roi_pitch >= 65536) return ORBFE_ERR_UNSUPPORTED;
     g.fast_lds = (size_t)rmax * g.roi_pitch + (((rmax - 4) * g.roi_pitch + 15) & ~15) +
-                 2 * (size_t)g.cand_max + 16;
+                 2 * (size_t)g.cand_max + 16 + 128;  // + a trash slot per lane
     g.geo.key_total = keys;
     g.geo.out_total = out;
     g.slab = slab;
