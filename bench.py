@@ -178,14 +178,17 @@ def run_c5(args) -> None:
     d_keys = torch.from_numpy(keys.view(np.uint8).copy()).to(dev)
     d_desc = torch.from_numpy(np.ascontiguousarray(desc)).to(dev)
     d_inv = torch.zeros(M, dtype=torch.uint8, device=dev)
-    fmp0, fobs0 = T["frame_mp"].clone(), T["frame_mp_obs"].clone()
+    # the frame's MapPoint slots and their Observations() side by side, so the per-step reset
+    # (the call writes them) is one copy
+    slots = torch.stack([T["frame_mp"], T["frame_mp_obs"]]).contiguous()
+    T["frame_mp"], T["frame_mp_obs"] = slots[0], slots[1]
+    slots0 = slots.clone()
     mt = ORBmatcher(0.8, False, device=local)
     mt.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     out = {}
 
     def step():
-        T["frame_mp"].copy_(fmp0)
-        T["frame_mp_obs"].copy_(fobs0)
+        slots.copy_(slots0)
         out["r"] = mt.search_local_points_device(
             len(keys), d_keys.data_ptr(), d_desc.data_ptr(), None, W, H, scale, lm["tcw"], cam,
             log_scale, 0.5, M, T["xyz"].data_ptr(), T["normal"].data_ptr(),

@@ -53,7 +53,7 @@ struct GreedyArgs {
     const int* fobs0;     // their Observations(); NULL: any held point blocks
     int* T[3];
     int* dec;             // decision per point (-2 before round 0, -1 = none)
-    int* chg;             // changed decisions per round
+    int* chg;             // per round: nonzero iff a decision changed
     int* last;            // per slot: last acceptor
     int* nm;
     // orientation filter
@@ -89,6 +89,9 @@ struct GreedyAcc {
     int best = 256, bl = -1, second = 256, sl = -1, bi = -1;
     __device__ __forceinline__ void add(const GreedyArgs& a, const int* Tc, int i, int2 c) {
         if (Tc[c.x] < i) return;
+        add_unblocked(a, c);
+    }
+    __device__ __forceinline__ void add_unblocked(const GreedyArgs& a, int2 c) {
         const int d = c.y & 0xffff;
         if (a.mode == kGreedyLocal) {
             const int lv = c.y >> 16;
@@ -125,7 +128,21 @@ __device__ __forceinline__ int greedy_decide(const GreedyArgs& a, const int* Tc,
     GreedyAcc acc;
     int e0, e1;
     greedy_range(a, i, e0, e1);
-    for (int e = e0; e < e1; ++e) acc.add(a, Tc, i, a.cand[e]);
+    // 4 candidates and their 4 T lookups in flight at a time (the lookups depend on the
+    // candidates, the accumulation on both; acc.add keeps the reference's order)
+    int e = e0;
+    for (; e + 4 <= e1; e += 4) {
+        int2 c[4];
+        int tv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c[k] = a.cand[e + k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) tv[k] = Tc[c[k].x];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (tv[k] >= i) acc.add_unblocked(a, c[k]);
+    }
+    for (; e < e1; ++e) acc.add(a, Tc, i, a.cand[e]);
     return acc.result(a);
 }
 
@@ -154,6 +171,27 @@ __device__ __forceinline__ int greedy_decide_cached(const GreedyArgs& a, const i
 // Round r: decisions from T[r % 3], first blocking acceptors into T[(r + 1) % 3] (holding the
 // pre-blocked state), T[(r + 2) % 3] reset for round r + 1.  A round after a round without
 // changes is a no-op (the fixed point is reached).
+// Fixed-slot layout (kfix): the count, the first 4 candidates (one 32-byte load, read before
+// the count is known: their slot indices are clamped, entries past the count ignored) and the
+// point's own state are in flight together, then the 4 T lookups: two dependent global
+// latencies per point instead of four.
+__device__ __forceinline__ int greedy_decide_fix(const GreedyArgs& a, const int* Tc, int i) {
+    const int n = a.fcnt[i];
+    const int2* cp = a.cand + (size_t)i * a.kfix;
+    const uint4 p0 = reinterpret_cast<const uint4*>(cp)[0], p1 = reinterpret_cast<const uint4*>(cp)[1];
+    const int2 c[4] = {make_int2((int)p0.x, (int)p0.y), make_int2((int)p0.z, (int)p0.w),
+                       make_int2((int)p1.x, (int)p1.y), make_int2((int)p1.z, (int)p1.w)};
+    int tv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tv[k] = Tc[min(max(c[k].x, 0), max(a.nkp - 1, 0))];  // T holds >= 1 entry
+    GreedyAcc acc;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (k < n && tv[k] >= i) acc.add_unblocked(a, c[k]);
+    for (int e = 4; e < n; ++e) acc.add(a, Tc, i, cp[e]);
+    return acc.result(a);
+}
+
 __global__ __launch_bounds__(kGreedyBlock) void greedy_round_kernel(GreedyArgs a, int r) {
     if (r > 0 && a.chg[r - 1] == 0) return;
     const int t = blockIdx.x * kGreedyBlock + threadIdx.x;
@@ -163,19 +201,51 @@ __global__ __launch_bounds__(kGreedyBlock) void greedy_round_kernel(GreedyArgs a
     if (t < a.nkp) Tz[t] = greedy_preblocked(a, t) ? -1 : INT_MAX;
     bool changed = false;
     if (t < a.m) {
-        const int d = greedy_decide(a, Tc, t);
-        if (d >= 0 && (!a.nobs || a.nobs[t] > 0)) atomicMin(&Tn[d], t);
-        changed = d != a.dec[t];
+        const int prev = a.dec[t];
+        const bool blocks = !a.nobs || a.nobs[t] > 0;
+        const int d = a.kfix ? greedy_decide_fix(a, Tc, t) : greedy_decide(a, Tc, t);
+        // contended slots: an acceptor whose index cannot lower the slot's minimum (as read
+        // now; a stale read only costs the atomic) skips the atomic
+        if (d >= 0 && blocks && __hip_atomic_load(&Tn[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > t)
+            atomicMin(&Tn[d], t);
+        changed = d != prev;
         if (changed) a.dec[t] = d;
     }
+    // chg[r] only needs to be nonzero when something changed: one atomic per wave until a
+    // wave sees it set (one counter hit by every wave serialised the first rounds)
     const unsigned long long b = __ballot(changed);
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(&a.chg[r], __popcll(b));
+    if ((threadIdx.x & 63) == 0 && b &&
+        __hip_atomic_load(&a.chg[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+        atomicOr(&a.chg[r], 1);
 }
 
-// G2: acceptances -> last acceptor per slot, nmatches, rotation bins.
-__global__ __launch_bounds__(kGreedyBlock) void greedy_accept_kernel(GreedyArgs a) {
+// G2: acceptances -> last acceptor per slot, nmatches, rotation bins.  kRound: the launch is
+// also round r of the resolver (the fused path's last blind round): when round r - 1 changed
+// nothing the round is a no-op and the decisions are final; otherwise this round's decisions
+// are accepted and chg[r] != 0 reports that they may not be (the host then reruns the call).
+// Either way a point's acceptance needs only its own decision, so no second launch.
+template <bool kRound>
+__global__ __launch_bounds__(kGreedyBlock) void greedy_accept_kernel(GreedyArgs a, int r) {
     const int i = blockIdx.x * kGreedyBlock + threadIdx.x;
     bool acc = false;
+    if (kRound && !(r > 0 && a.chg[r - 1] == 0)) {
+        const int* Tc = a.T[r % 3];
+        int* Tn = a.T[(r + 1) % 3];
+        bool changed = false;
+        if (i < a.m) {
+            const int prev = a.dec[i];
+            const bool blocks = !a.nobs || a.nobs[i] > 0;
+            const int d = a.kfix ? greedy_decide_fix(a, Tc, i) : greedy_decide(a, Tc, i);
+            if (d >= 0 && blocks && __hip_atomic_load(&Tn[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > i)
+                atomicMin(&Tn[d], i);
+            changed = d != prev;
+            if (changed) a.dec[i] = d;
+        }
+        const unsigned long long b = __ballot(changed);
+        if ((threadIdx.x & 63) == 0 && b &&
+            __hip_atomic_load(&a.chg[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+            atomicOr(&a.chg[r], 1);
+    }
     if (i < a.m) {
         const int s = a.dec[i];
         acc = s >= 0;
@@ -203,18 +273,44 @@ __global__ __launch_bounds__(kGreedyBlock) void greedy_accept_kernel(GreedyArgs 
     __syncthreads();
     if (!is_last) return;
     __threadfence();
-    for (int s = threadIdx.x; s < a.nkp; s += kGreedyBlock) {
-        const int j = __hip_atomic_load(&a.last[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (j < 0) continue;
-        a.fmp[s] = a.ids ? a.ids[j] : j;
-        if (a.fobs) a.fobs[s] = a.nobs ? a.nobs[j] : 1;
+    // the slots and the tallies in batches whose loads are all issued before any is used (one
+    // workgroup does this work alone: a dependent load chain per element would be serial)
+    for (int s0 = 0; s0 < a.nkp; s0 += 4 * kGreedyBlock) {
+        int j[4], id[4], ob[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int s = s0 + threadIdx.x + kGreedyBlock * b;
+            j[b] = s < a.nkp ? __hip_atomic_load(&a.last[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : -1;
+        }
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            id[b] = j[b] >= 0 ? (a.ids ? a.ids[j[b]] : j[b]) : 0;
+            ob[b] = j[b] >= 0 && a.fobs ? (a.nobs ? a.nobs[j[b]] : 1) : 0;
+        }
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int s = s0 + threadIdx.x + kGreedyBlock * b;
+            if (j[b] < 0) continue;
+            a.fmp[s] = id[b];
+            if (a.fobs) a.fobs[s] = ob[b];
+        }
     }
     if (threadIdx.x < 64) {
         int in = 0, ovf = 0, bad = 0;
-        for (int k = threadIdx.x; k < a.nblk; k += 64) {
-            in += a.blk[3 * k];
-            ovf += a.blk[3 * k + 1];
-            bad += a.blk[3 * k + 2];
+        for (int k0 = 0; k0 < a.nblk; k0 += 4 * 64) {
+            int v[4][3];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int k = k0 + threadIdx.x + 64 * b;
+#pragma unroll
+                for (int q = 0; q < 3; ++q) v[b][q] = k < a.nblk ? a.blk[3 * k + q] : 0;
+            }
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                in += v[b][0];
+                ovf += v[b][1];
+                bad += v[b][2];
+            }
         }
         in = wave_sum(in);
         ovf = wave_sum(ovf);
@@ -376,6 +472,14 @@ __global__ __launch_bounds__(kGreedySmallBlock) void greedy_small_kernel(GreedyA
 // makes the host rerun the call through the CSR path.
 constexpr int kSbpFix = 16;
 constexpr int kSbpFixKp = 2048;
+// kSbpLpp lanes per map point: the point's window cells are dealt round-robin over them in the
+// reference's (ix-major, iy) order, so 256 points make a 1024-thread workgroup (16 waves per
+// CU instead of 4: the per-point walk is LDS-latency bound).
+#ifndef ORBFE_SBP_LPP
+#define ORBFE_SBP_LPP 4
+#endif
+constexpr int kSbpLpp = ORBFE_SBP_LPP;
+constexpr int kSbpPts = 1024 / kSbpLpp;  // map points per workgroup
 struct SbpFusedArgs {
     FrustumArgs fr;        // in_view is written; px / py / pxr / lvl / vcos are not
     SbpLocalArgs s;        // f, mp.m, mp.desc, th, nlevels, cnt, cand
@@ -384,17 +488,32 @@ struct SbpFusedArgs {
     GreedyArgs g;          // initialised here (greedy_init_kernel's work)
     int rounds;            // g.chg[0 .. rounds] cleared
 };
-__global__ __launch_bounds__(256) void sbp_local_fused_kernel(SbpFusedArgs fa) {
+// exclusive / total sum over the kSbpLpp lanes of a point (aligned sub-groups of the wave)
+__device__ __forceinline__ int sub_scan(int x, int& total) {
+    int inc = x;
+#pragma unroll
+    for (int d = 1; d < kSbpLpp; d <<= 1) {
+        const int y = __shfl_up(inc, d, kSbpLpp);
+        if ((threadIdx.x & (kSbpLpp - 1)) >= d) inc += y;
+    }
+    total = __shfl(inc, kSbpLpp - 1, kSbpLpp);
+    return inc - x;
+}
+__global__ __launch_bounds__(1024) void sbp_local_fused_kernel(SbpFusedArgs fa) {
     const SbpLocalArgs& a = fa.s;
     __shared__ int cs[kGridCells + 1];
     __shared__ int ci[kSbpFixKp];
     __shared__ float2 kxy[kSbpFixKp];
     __shared__ int8_t koct[kSbpFixKp];
     __shared__ int tally[3];
+    // the frame's descriptors (2 x uint4 per keypoint, F.n of them: dynamic LDS sized by the
+    // host), so a candidate's Hamming distance reads LDS instead of waiting on a global load
+    extern __shared__ uint4 fdesc[];
     const DevFrame& F = a.f;
     const int tid = threadIdx.x;
-    const int i = blockIdx.x * 256 + tid;
-    {   // greedy_init_kernel's work, spread over the grid (which covers max(m, nkp) threads)
+    const int sub = tid & (kSbpLpp - 1);
+    const int i = blockIdx.x * kSbpPts + tid / kSbpLpp;
+    if (sub == 0) {  // greedy_init_kernel's work, spread over the grid (max(m, nkp) points)
         const GreedyArgs& g = fa.g;
         if (i < g.nkp) {
             const int v = greedy_preblocked(g, i) ? -1 : INT_MAX;
@@ -409,27 +528,72 @@ __global__ __launch_bounds__(256) void sbp_local_fused_kernel(SbpFusedArgs fa) {
         if (i == 0) *g.nm = 0;
     }
     if (tid < 3) tally[tid] = 0;
-    for (int c = tid; c <= kGridCells; c += 256) cs[c] = F.cstart[c];
-    for (int k = tid; k < F.n; k += 256) {
-        const orbfe_keypoint kp = F.k[k];
-        kxy[k] = make_float2(kp.x, kp.y);
-        koct[k] = (int8_t)min(max(kp.octave, -128), 127);
+    // Staging: every load of a batch is issued before its LDS stores (one global latency per
+    // batch, not one per element).  The grid items are read up to F.n (total <= F.n).
+    {
+        constexpr int kCsIt = (kGridCells + 1 + 1023) / 1024;
+        int v[kCsIt];
+#pragma unroll
+        for (int k = 0; k < kCsIt; ++k) {
+            const int c = tid + 1024 * k;
+            v[k] = c <= kGridCells ? F.cstart[c] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < kCsIt; ++k) {
+            const int c = tid + 1024 * k;
+            if (c <= kGridCells) cs[c] = v[k];
+        }
+    }
+    for (int k0 = 0; k0 < F.n; k0 += 2 * 1024) {
+        float kx[2], ky[2];
+        int ko[2], it[2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int k = k0 + tid + 1024 * b;
+            if (k < F.n) {
+                kx[b] = F.k[k].x;
+                ky[b] = F.k[k].y;
+                ko[b] = F.k[k].octave;
+                it[b] = F.citems[k];
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int k = k0 + tid + 1024 * b;
+            if (k < F.n) {
+                kxy[k] = make_float2(kx[b], ky[b]);
+                koct[k] = (int8_t)min(max(ko[b], -128), 127);
+                ci[k] = it[b];
+            }
+        }
+    }
+    for (int q0 = 0; q0 < 2 * F.n; q0 += 4 * 1024) {
+        uint4 d[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int q = q0 + tid + 1024 * b;
+            if (q < 2 * F.n) d[b] = F.desc[q];
+        }
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int q = q0 + tid + 1024 * b;
+            if (q < 2 * F.n) fdesc[q] = d[b];
+        }
     }
     __syncthreads();
-    const int total = cs[kGridCells];
-    for (int e = tid; e < total; e += 256) ci[e] = F.citems[e];
-    __syncthreads();
     int in = 0, ovf = 0, bad_level = 0;
-    if (i < a.mp.m) {
-        fa.fr.in_view[i] = 0;  // isInFrustum starts with mbTrackInView = false (Frame.cc:389)
+    if (i < a.mp.m) {  // every lane of the point evaluates the (cheap, uniform) frustum test
+        if (sub == 0) fa.fr.in_view[i] = 0;  // isInFrustum starts with mbTrackInView = false (Frame.cc:389)
         FrustumOut o;
         int n = 0;
         if (frustum_eval(fa.fr, i, o)) {
-            fa.fr.in_view[i] = 1;
-            in = 1;
+            if (sub == 0) {
+                fa.fr.in_view[i] = 1;
+                in = 1;
+            }
             const int pl = o.lvl;
             if (pl < 0 || pl >= a.nlevels) {  // F.mvScaleFactors[nPredictedLevel] out of range
-                bad_level = 1;
+                bad_level = sub == 0;
             } else {
                 float r = o.vc > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos (131-137)
                 if (a.th != 1.0) r *= a.th;
@@ -438,44 +602,54 @@ __global__ __launch_bounds__(256) void sbp_local_fused_kernel(SbpFusedArgs fa) {
                 int2* out = a.cand + (size_t)i * kSbpFix;
                 // GetFeaturesInArea(x, y, rs, pl - 1, pl) (Frame.cc:445-498) on the LDS copy, in
                 // features_in_area's order (ix-major, iy, insertion); the level check is on
-                // (maxLevel = pl >= 0)
+                // (maxLevel = pl >= 0).  Lane sub takes window cells sub, sub + kSbpLpp, ..;
+                // a sub-group scan of the per-cell counts gives each candidate its rank.
                 const int cx0 = max(0, (int)floorf((x - F.minx - rs) * F.gwi));
                 const int cx1 = min(kGridCols - 1, (int)ceilf((x - F.minx + rs) * F.gwi));
                 const int cy0 = max(0, (int)floorf((y - F.miny - rs) * F.ghi));
                 const int cy1 = min(kGridRows - 1, (int)ceilf((y - F.miny + rs) * F.ghi));
                 if (cx0 < kGridCols && cx1 >= 0 && cy0 < kGridRows && cy1 >= 0) {
-                    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
-                    bool qd = false;
-                    for (int ix = cx0; ix <= cx1; ++ix)
-                        for (int iy = cy0; iy <= cy1; ++iy) {
-                            const int c = ix * kGridRows + iy;
-                            for (int e = cs[c], e1 = cs[c + 1]; e < e1; ++e) {
-                                const int idx = ci[e];
-                                const int oct = koct[idx];
-                                if (oct < pl - 1 || oct > pl) continue;
-                                const float2 kp = kxy[idx];
-                                if (!(fabsf(kp.x - x) < rs && fabsf(kp.y - y) < rs)) continue;
-                                if (F.ur && F.ur[idx] > 0) {  // stereo consistency (91-96)
-                                    const float er = fabsf(o.ur - F.ur[idx]);
-                                    if (er > r * fa.scalev[pl]) continue;
-                                }
-                                if (n < kSbpFix) {
-                                    if (!qd) {
-                                        q0 = a.mp.desc[2 * i];
-                                        q1 = a.mp.desc[2 * i + 1];
-                                        qd = true;
-                                    }
-                                    const uint4* d = F.desc + 2 * idx;
-                                    out[n] = make_int2(idx, hamming256(q0, q1, d[0], d[1]) | (oct << 16));
-                                }
-                                ++n;
-                            }
+                    const uint4 q0 = a.mp.desc[2 * i], q1 = a.mp.desc[2 * i + 1];
+                    const int ny = cy1 - cy0 + 1, ncell = (cx1 - cx0 + 1) * ny;
+                    auto pass = [&](int idx) {
+                        const int oct = koct[idx];
+                        if (oct < pl - 1 || oct > pl) return false;
+                        const float2 kp = kxy[idx];
+                        if (!(fabsf(kp.x - x) < rs && fabsf(kp.y - y) < rs)) return false;
+                        if (F.ur && F.ur[idx] > 0) {  // stereo consistency (91-96)
+                            const float er = fabsf(o.ur - F.ur[idx]);
+                            if (er > r * fa.scalev[pl]) return false;
                         }
+                        return true;
+                    };
+                    for (int t0 = 0; t0 < ncell; t0 += kSbpLpp) {
+                        const int t = t0 + sub;
+                        int e0 = 0, e1 = 0, cnt = 0;
+                        if (t < ncell) {
+                            const int c = (cx0 + t / ny) * kGridRows + cy0 + t % ny;
+                            e0 = cs[c];
+                            e1 = cs[c + 1];
+                            for (int e = e0; e < e1; ++e) cnt += pass(ci[e]);
+                        }
+                        int tot;
+                        int rank = n + sub_scan(cnt, tot);
+                        if (cnt)
+                            for (int e = e0; e < e1; ++e) {
+                                const int idx = ci[e];
+                                if (!pass(idx)) continue;
+                                if (rank < kSbpFix) {
+                                    const uint4* d = fdesc + 2 * idx;
+                                    out[rank] = make_int2(idx, hamming256(q0, q1, d[0], d[1]) | ((int)koct[idx] << 16));
+                                }
+                                ++rank;
+                            }
+                        n += tot;
+                    }
                 }
-                ovf = n > kSbpFix;
+                ovf = sub == 0 && n > kSbpFix;
             }
         }
-        a.cnt[i] = min(n, kSbpFix);
+        if (sub == 0) a.cnt[i] = min(n, kSbpFix);
     }
     const int w_in = wave_sum(in), w_ovf = wave_sum(ovf), w_bad = wave_sum(bad_level);
     if ((tid & 63) == 0) {

@@ -349,7 +349,7 @@ struct orbfe_matcher {
             if (r > M) return ORBFE_ERR_HIP;  // cannot happen: the correct prefix grows every round
             batch = std::min(batch * 2, 64);
         }
-        hipLaunchKernelGGL(greedy_accept_kernel, dim3(mblocks), dim3(kGreedyBlock), 0, stream, g);
+        hipLaunchKernelGGL(greedy_accept_kernel<false>, dim3(mblocks), dim3(kGreedyBlock), 0, stream, g, 0);
         hipLaunchKernelGGL(greedy_slots_kernel, dim3(nblocks), dim3(kGreedyBlock), 0, stream, g);
         if (g.check_ori)
             hipLaunchKernelGGL(greedy_ori_kernel, dim3(mblocks), dim3(kGreedyBlock), 0, stream, g);
@@ -940,9 +940,6 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
         int st;
         const int M = n_mp, N = frame->n;
         if ((st = m->scal.ensure(64))) return st;
-        if ((st = m->m_f4.ensure(std::max<size_t>(16, (size_t)frame->nlevels * 4)))) return st;
-        ORBFE_HIP(hipMemcpyAsync(m->m_f4.p, frame->scale_factors, (size_t)frame->nlevels * 4,
-                                 hipMemcpyHostToDevice, m->stream));
         for (DevBuf* b : {&m->o_f0, &m->o_f1, &m->o_f2, &m->o_f3, &m->o_i})
             if ((st = b->ensure(std::max<size_t>(16, (size_t)M * 4)))) return st;
         int* d_cnt = m->scal.as<int>() + 1;     // nToMatch
@@ -956,7 +953,7 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
         // rounds (rare) restores the slots saved by the fused kernel and takes the CSR path.
         if (N <= kSbpFixKp && frame->nlevels <= kMaxLevels && M > 0) {
             constexpr int kBlindRounds = 6;
-            const int fblocks = (std::max(std::max(M, N), kBlindRounds + 1) + 255) / 256;
+            const int fblocks = (std::max(std::max(M, N), kBlindRounds + 1) + kSbpPts - 1) / kSbpPts;
             if ((st = m->cand.ensure((size_t)M * kSbpFix * sizeof(int2)))) return st;
             if ((st = m->cnt.ensure((size_t)M * sizeof(int)))) return st;
             if ((st = m->s1.ensure(std::max(N, 1) * sizeof(int)))) return st;
@@ -967,7 +964,7 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
             if ((st = m->g_t2.ensure(std::max(N, 1) * sizeof(int)))) return st;
             if ((st = m->g_last.ensure(std::max(N, 1) * sizeof(int)))) return st;
             if ((st = m->g_dec.ensure((size_t)M * sizeof(int)))) return st;
-            if ((st = m->g_chg.ensure((size_t)(M + 2) * sizeof(int)))) return st;
+            if ((st = m->g_chg.ensure((size_t)std::max(M + 2, kBlindRounds + 2) * sizeof(int)))) return st;
             if (!m->done_ctr.p) {  // the accept kernel's counter: zero once, reset by its user
                 if ((st = m->done_ctr.ensure(64))) return st;
                 ORBFE_HIP(hipMemsetAsync(m->done_ctr.p, 0, 64, m->stream));
@@ -1033,12 +1030,13 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
             g.nblk = fblocks;
             g.stats = m->scal.as<int>();
             g.conv_round = kBlindRounds - 1;
-            hipLaunchKernelGGL(sbp_local_fused_kernel, dim3(fblocks), dim3(256), 0, m->stream, fu);
+            hipLaunchKernelGGL(sbp_local_fused_kernel, dim3(fblocks), dim3(1024), (size_t)N * 32, m->stream, fu);
             const int rblocks = std::max(1, (std::max(std::max(M, N), 32) + kGreedyBlock - 1) / kGreedyBlock);
-            for (int r = 0; r < kBlindRounds; ++r)
+            for (int r = 0; r < kBlindRounds - 1; ++r)
                 hipLaunchKernelGGL(greedy_round_kernel, dim3(rblocks), dim3(kGreedyBlock), 0, m->stream, g, r);
-            hipLaunchKernelGGL(greedy_accept_kernel, dim3((M + kGreedyBlock - 1) / kGreedyBlock),
-                               dim3(kGreedyBlock), 0, m->stream, g);
+            // the last blind round and the acceptances in one launch
+            hipLaunchKernelGGL(greedy_accept_kernel<true>, dim3((M + kGreedyBlock - 1) / kGreedyBlock),
+                               dim3(kGreedyBlock), 0, m->stream, g, kBlindRounds - 1);
             ORBFE_HIP(hipGetLastError());
             m->rounds_on_device = false;
             int host[6] = {0, 0, 0, 0, 0, 0};
@@ -1056,6 +1054,10 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
             ++m->capacity_retries;
         }
         bool retried = false;
+        // (the fast path above passes mvScaleFactors in its kernel arguments)
+        if ((st = m->m_f4.ensure(std::max<size_t>(16, (size_t)frame->nlevels * 4)))) return st;
+        ORBFE_HIP(hipMemcpyAsync(m->m_f4.p, frame->scale_factors, (size_t)frame->nlevels * 4,
+                                 hipMemcpyHostToDevice, m->stream));
         std::function<int()> attempt = [&]() -> int {
         ORBFE_HIP(hipMemsetAsync(m->scal.p, 0, 16, m->stream));
         // Tracking::SearchLocalPoints: isInFrustum(pMP, 0.5) over the local map (1425-1438)
