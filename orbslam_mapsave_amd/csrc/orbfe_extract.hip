@@ -162,7 +162,11 @@ __device__ __forceinline__ uint32_t resize_px(uint32_t t0, uint32_t t1, uint32_t
     return min(sse2 ? sv : sc, 255u);
 }
 
-constexpr int kRsTW = 128, kRsTH = 32;
+#ifndef ORBFE_RS_TH
+#define ORBFE_RS_TH 32
+#endif
+constexpr int kRsTW = 128, kRsTH = ORBFE_RS_TH;  // output tile; 8 thread rows of kRsTH / 8
+constexpr int kRsRPT = kRsTH / 8;
 template <bool kX86>
 __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
@@ -229,8 +233,8 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
     }
     uint8_t* dst = const_cast<uint8_t*>(a.dst.base) + f * a.dst.fpitch;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int y = oy + 4 * ty + j;
+    for (int j = 0; j < kRsRPT; ++j) {
+        const int y = oy + kRsRPT * ty + j;
         if (y >= a.dh) break;
         const int ry0 = a.yt[3 * y] - sy0, ry1 = a.yt[3 * y + 1] - sy0, bb = a.yt[3 * y + 2];
         const int b0 = bb & 0xffff, b1 = (int)((unsigned)bb >> 16);
