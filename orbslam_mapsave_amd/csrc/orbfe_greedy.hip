@@ -148,7 +148,7 @@ __device__ __forceinline__ int greedy_decide(const GreedyArgs& a, const int* Tc,
 
 // The first kCandCache candidates of a point held in registers across the rounds of the
 // single-workgroup resolver (a round then costs LDS lookups only, no global load chain).
-constexpr int kCandCache = 8;
+constexpr int kCandCache = 16;
 struct CandCache {
     int e0, e1;
     int2 c[kCandCache];
@@ -386,10 +386,14 @@ __global__ __launch_bounds__(kGreedySmallBlock) void greedy_small_kernel(GreedyA
         T[1][s] = v;
         last[s] = -1;
     }
-    for (int i = tid; i < a.m; i += kGreedySmallBlock) a.dec[i] = -2;
-    CandCache cc;  // the candidates of point tid (most calls have <= one point per thread)
+    for (int i = tid + kGreedySmallBlock; i < a.m; i += kGreedySmallBlock) a.dec[i] = -2;
+    // point tid (most calls have <= one point per thread): its candidates, its decision and
+    // whether it blocks held in registers across the rounds; further points go through memory
+    CandCache cc;
     if (tid < a.m) cand_cache_load(a, tid, cc);
     else cc.e0 = cc.e1 = 0;
+    int my_dec = -2;
+    const bool my_blocks = tid < a.m && (!a.nobs || a.nobs[tid] > 0);
     if (tid < 30) h[tid] = 0;
     if (tid == 0) nm = 0;
     __syncthreads();
@@ -400,8 +404,16 @@ __global__ __launch_bounds__(kGreedySmallBlock) void greedy_small_kernel(GreedyA
         const int* Tc = T[cur];
         int* Tn = T[cur ^ 1];
         bool ch = false;
-        for (int i = tid; i < a.m; i += kGreedySmallBlock) {
-            const int d = i == tid ? greedy_decide_cached(a, Tc, i, cc) : greedy_decide(a, Tc, i);
+        if (tid < a.m) {
+            const int d = greedy_decide_cached(a, Tc, tid, cc);
+            if (d >= 0 && my_blocks) atomicMin(&Tn[d], tid);
+            if (d != my_dec) {
+                my_dec = d;
+                ch = true;
+            }
+        }
+        for (int i = tid + kGreedySmallBlock; i < a.m; i += kGreedySmallBlock) {
+            const int d = greedy_decide(a, Tc, i);
             if (d >= 0 && (!a.nobs || a.nobs[i] > 0)) atomicMin(&Tn[d], i);
             if (d != a.dec[i]) {
                 a.dec[i] = d;
@@ -418,8 +430,9 @@ __global__ __launch_bounds__(kGreedySmallBlock) void greedy_small_kernel(GreedyA
         __syncthreads();
     }
     // G2: last acceptor per slot, nmatches, rotation bins
+    if (tid < a.m) a.dec[tid] = my_dec;  // read back by the host path's ori / slot passes
     for (int i = tid; i < a.m; i += kGreedySmallBlock) {
-        const int s = a.dec[i];
+        const int s = i == tid ? my_dec : a.dec[i];
         if (s < 0) continue;
         atomicMax(&last[s], i);
         atomicAdd(&nm, 1);
@@ -443,7 +456,7 @@ __global__ __launch_bounds__(kGreedySmallBlock) void greedy_small_kernel(GreedyA
         if (tid == 0) three_maxima(h, top[0], top[1], top[2]);
         __syncthreads();
         for (int i = tid; i < a.m; i += kGreedySmallBlock) {
-            const int s = a.dec[i];
+            const int s = i == tid ? my_dec : a.dec[i];
             if (s < 0) continue;
             const int bin = a.bins[i];
             if (bin != top[0] && bin != top[1] && bin != top[2]) {
