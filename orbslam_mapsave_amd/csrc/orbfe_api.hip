@@ -129,7 +129,7 @@ struct orbfe_extractor {
     Plan plan;
     bool planned = false;
     int frames_cap = 0;
-    DevBuf cells, xtab, ytab;
+    DevBuf cells, xtab, ytab, bslot;
     DevBuf pyr, blur, cell_cnt, cell_keys, keys, act, oct_out, oct_cnt, level_keys;
     DevBuf out_kps, out_desc, out_n;  // staging for the host-pointer entry points
     DevBuf stage, rects;              // host colour frames / rectangle masks (level-0 inputs)
@@ -254,12 +254,18 @@ struct orbfe_extractor {
         if ((st = cells.ensure(std::max<size_t>(1, g.cells.size()) * sizeof(CellDesc)))) return st;
         if ((st = xtab.ensure(std::max<size_t>(1, g.xtab.size()) * sizeof(int)))) return st;
         if ((st = ytab.ensure(std::max<size_t>(1, g.ytab.size()) * sizeof(int)))) return st;
+        if ((st = bslot.ensure(kBlurFragBytes + g.bitems.size() * sizeof(uint32_t)))) return st;
         ORBFE_HIP(hipMemcpyAsync(cells.p, g.cells.data(), g.cells.size() * sizeof(CellDesc),
                                  hipMemcpyHostToDevice, stream));
         ORBFE_HIP(hipMemcpyAsync(xtab.p, g.xtab.data(), g.xtab.size() * sizeof(int),
                                  hipMemcpyHostToDevice, stream));
         ORBFE_HIP(hipMemcpyAsync(ytab.p, g.ytab.data(), g.ytab.size() * sizeof(int),
                                  hipMemcpyHostToDevice, stream));
+        // blur_mfma_kernel: its constant fragments, then its work list
+        std::vector<uint8_t> bb(kBlurFragBytes + g.bitems.size() * sizeof(uint32_t));
+        blur_frags(tab.taps, bb.data());
+        std::memcpy(bb.data() + kBlurFragBytes, g.bitems.data(), g.bitems.size() * sizeof(uint32_t));
+        ORBFE_HIP(hipMemcpyAsync(bslot.p, bb.data(), bb.size(), hipMemcpyHostToDevice, stream));
         ORBFE_HIP(hipStreamSynchronize(stream));
         plan = std::move(g);
         planned = true;
@@ -400,14 +406,15 @@ struct orbfe_extractor {
                 ba.src[l] = lp[l];
                 ba.dst[l] = bp[l];
                 ba.simd_xb[l] = x86() ? sse2_body_blur(g.geo.lv[l].w) : 0;
-                ba.bt_begin[l] = g.bt_begin[l];
-                ba.bt_cw[l] = g.bt_cw[l];
             }
+            ba.frags = bslot.as<uint4>();
+            ba.items = reinterpret_cast<const uint32_t*>(bslot.as<uint8_t>() + kBlurFragBytes);
+            ba.nitems = (int)g.bitems.size();
             for (int i = 0; i < 4; ++i) ba.taps[i] = tab.taps[i];
             if (x86())
-                ORBFE_LAUNCH(prof, ORBFE_STAGE_BLUR, blur_band_kernel<true>, dim3(g.bt_total, n), dim3(64), 0, stream, ba);
+                ORBFE_LAUNCH(prof, ORBFE_STAGE_BLUR, blur_mfma_kernel<true>, dim3(ba.nitems, n), dim3(256), 0, stream, ba);
             else
-                ORBFE_LAUNCH(prof, ORBFE_STAGE_BLUR, blur_band_kernel<false>, dim3(g.bt_total, n), dim3(64), 0, stream, ba);
+                ORBFE_LAUNCH(prof, ORBFE_STAGE_BLUR, blur_mfma_kernel<false>, dim3(ba.nitems, n), dim3(256), 0, stream, ba);
         }
         // K5 describe
         DescArgs da;
@@ -560,7 +567,7 @@ struct orbfe_extractor {
     }
 
     ~orbfe_extractor() {
-        for (DevBuf* b : {&cells, &xtab, &ytab, &pyr, &blur, &cell_cnt, &cell_keys, &keys, &act,
+        for (DevBuf* b : {&cells, &xtab, &ytab, &bslot, &pyr, &blur, &cell_cnt, &cell_keys, &keys, &act,
                           &oct_out, &oct_cnt, &level_keys, &out_kps, &out_desc, &out_n, &stage, &rects, &st_off, &st_items,
                           &st_sad, &st_status, &st_kl, &st_dl, &st_kr, &st_dr, &st_n, &st_ur, &st_dp})
             b->release();
@@ -1072,14 +1079,15 @@ int orbfe_get_blurred_level(orbfe_extractor* h, int frame, int level, uint8_t* o
             ba.src[l] = h->last_pyr[l];
             ba.dst[l] = LevelPtr{h->blur.as<uint8_t>() + g.geo.lv[l].off, g.slab, g.geo.lv[l].pitch};
             ba.simd_xb[l] = h->x86() ? sse2_body_blur(g.geo.lv[l].w) : 0;
-            ba.bt_begin[l] = g.bt_begin[l];
-            ba.bt_cw[l] = g.bt_cw[l];
         }
+        ba.frags = h->bslot.as<uint4>();
+        ba.items = reinterpret_cast<const uint32_t*>(h->bslot.as<uint8_t>() + kBlurFragBytes);
+        ba.nitems = (int)g.bitems.size();
         for (int i = 0; i < 4; ++i) ba.taps[i] = h->tab.taps[i];
         if (h->x86())
-            hipLaunchKernelGGL(blur_band_kernel<true>, dim3(g.bt_total, h->last_n), dim3(64), 0, h->stream, ba);
+            hipLaunchKernelGGL(blur_mfma_kernel<true>, dim3(ba.nitems, h->last_n), dim3(256), 0, h->stream, ba);
         else
-            hipLaunchKernelGGL(blur_band_kernel<false>, dim3(g.bt_total, h->last_n), dim3(64), 0, h->stream, ba);
+            hipLaunchKernelGGL(blur_mfma_kernel<false>, dim3(ba.nitems, h->last_n), dim3(256), 0, h->stream, ba);
         ORBFE_HIP(hipGetLastError());
     }
     return copy_level(h, bp, frame, level, out, w, hgt);

@@ -10,7 +10,7 @@
 //                       (764-831); one workgroup per (frame, cell)
 //   K3 octree_kernel    DistributeOctTree (538-762) as a data-parallel list emulation; one
 //                       workgroup per (frame, level)
-//   K4 blur_band_kernel GaussianBlur 7x7 sigma 2 REFLECT_101 (1088-1089), integer path
+//   K4 blur_mfma_kernel GaussianBlur 7x7 sigma 2 REFLECT_101 (1088-1089), integer path
 //   K5 describe_kernel  IC_Angle (76-103) + rBRIEF (107-146) + level scaling (1098-1104);
 //                       one wave per keypoint, 256 tests packed with 4 ballots
 #include <hip/hip_runtime.h>
@@ -371,6 +371,48 @@ typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ half2v fast_h2(uint32_t b) {
     return __builtin_bit_cast(half2v, b * 0x10001u + 0x64006400u);
 }
+#ifndef ORBFE_FAST_DENORM
+#define ORBFE_FAST_DENORM 1
+#endif
+#if ORBFE_FAST_DENORM
+// The same S with every byte taken as the f16 DENORMAL of its bit pattern, b * 2^-24: the
+// zero-extended ds_read_u8 result is the operand as loaded (op_sel_hi = 0 puts its low half in
+// both halves, neg_lo negates one), so the 17 per-byte conversions vanish.  f16 denormals are
+// not flushed (the kernel's f16/f64 denormal mode is IEEE), minimum / maximum order them as the
+// integers they encode, and every sum below stays under 1024 units (|q| + |v| <= 510), so each
+// value is exact; the result's sign-magnitude bits are S + 1 directly.
+__device__ __forceinline__ _Float16 fast_dn(uint32_t b) {
+    return __builtin_bit_cast(_Float16, (unsigned short)b);
+}
+__device__ __forceinline__ int fast_S(const uint8_t* p, int st) {
+    const _Float16 V = fast_dn(p[0]);
+    const uint32_t x[16] = {p[3 * st],      p[3 * st + 1],  p[2 * st + 2],  p[st + 3],
+                            p[3],           p[-st + 3],     p[-2 * st + 2], p[-3 * st + 1],
+                            p[-3 * st],     p[-3 * st - 1], p[-2 * st - 2], p[-st - 3],
+                            p[-3],          p[st - 3],      p[2 * st - 2],  p[3 * st - 1]};
+    half2v e[16], m3[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const _Float16 X = fast_dn(x[k]);
+        e[k] = half2v{-X, X};
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        m3[k] = __builtin_elementwise_minimum(__builtin_elementwise_minimum(e[k], e[(k + 1) & 15]),
+                                              e[(k + 2) & 15]);
+    half2v q = __builtin_elementwise_minimum(__builtin_elementwise_minimum(m3[0], m3[3]), m3[6]);
+#pragma unroll
+    for (int k = 1; k < 16; ++k) {
+        const half2v m9 = __builtin_elementwise_minimum(
+            __builtin_elementwise_minimum(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15]);
+        q = __builtin_elementwise_maximum(q, m9);
+    }
+    q = q + half2v{V, -V};
+    const uint32_t bits = __builtin_bit_cast(unsigned short, __builtin_elementwise_maximum(q.x, q.y));
+    const int mag = (int)(bits & 0x3ffu);
+    return ((bits & 0x8000u) ? -mag : mag) - 1;
+}
+#else
 __device__ __forceinline__ int fast_S(const uint8_t* p, int st) {
     const half2v V = fast_h2(p[0]);
     const uint32_t x[16] = {p[3 * st],      p[3 * st + 1],  p[2 * st + 2],  p[st + 3],
@@ -400,6 +442,7 @@ __device__ __forceinline__ int fast_S(const uint8_t* p, int st) {
     q = q + half2v{V.x, -V.y};
     return (int)(float)__builtin_elementwise_maximum(q.x, q.y) - 1;
 }
+#endif
 
 // Necessary condition for a corner at t (the pre-test): a 9-arc always holds two consecutive
 // cardinal points (0/4/8/12), so both must be brighter than v + t or both darker than v - t.
@@ -1134,162 +1177,178 @@ __device__ __forceinline__ int reflect101(int p, int len) {
 }
 // K4 — GaussianBlur(7x7, sigma 2, REFLECT_101), integer path (App. A.2): row pass R = sum k_i I
 // (<= 65535, exact in u16), column pass (sum k_j R + 2^15) >> 16 saturated; x86 mode rounds the
-// SIMD body half to even (H6) as a vertical sweep without LDS: lane q of a (level, 32-row band, 64-lane column
-// wave) tile owns output columns 8q .. 8q+7.  It walks its band's 38 input rows: one 16-byte
-// load per row (the window of columns 8q-4 .. 8q+11, straight from the level; kBandAhead rows
-// in flight ahead of the row being used), the row pass is two v_dot4_u32_u8 per column, rows
-// 2k, 2k+1 are packed as u16 pairs, and output rows 2m, 2m+1 are four v_dot2_u32_u16 each over
-// the pairs m .. m+3 held in registers (the sweep is unrolled, so the windows rotate without
-// moves).  Rows are reflected (REFLECT_101) by index.  A lane whose window leaves the row
-// loads the 16 bytes at ls = clamp(8q-4, 0, w-16) instead; every window byte's reflected
-// column then lies in that load, and v_perm_b32 pairs (selectors fixed per lane) rebuild it.
-constexpr int kBandAhead = 8;
+// SIMD body half to even (H6).  Both passes are banded integer GEMMs on the i8 matrix cores:
+//   row pass     R (32 rows x 32 cols)  = (I - 128) . T + 128 * 257     (v_mfma_i32_32x32x32_i8)
+//   column pass  O^T (32 x 32) = (R^T split into hi / lo bytes, each - 128) . V^T, two MFMAs,
+//                the hi result shifted by 8 into the lo MFMA's C input, + 0x8000 rounding,
+// where T[k][x] = tap(k - 3 - x) and V[y][r] = tap(r - 3 - y) are constant fragments (taps as
+// i8, |tap| <= 55), and every sum is exact in i32.  A wave's tile is 26 output rows x 24 output
+// columns: its 32 R rows (y - 3 .. y + 28) are one M-tile, its 30 input columns fit one K
+// block.  The row pass's accumulator tile has its column on the lane and its rows in the
+// registers, so it is the column pass's A operand (R^T: rows = columns x) after a byte split,
+// with no lane movement — the column pass's K order is the accumulator's register order, and
+// V's fragment follows it.  Memory stays row-contiguous: a workgroup (4 waves, 4 tiles side by
+// side: 96 output columns) stages each 32-row input band in LDS with 112-byte row loads (all
+// bands' loads issued up front), and writes its 26 x 96 output
+// band to LDS and then to the level with 16-byte row stores — per-lane row-strided accesses
+// (one row per lane) would make the texture addresser the bound.  Chunks that leave the level
+// gather reflected bytes one by one (edge workgroups only).
+constexpr int kBlurTileW = 24, kBlurTileH = 26, kBlurChunk = 8;
+constexpr int kBlurGroupW = 4 * kBlurTileW;   // output columns per workgroup
+constexpr int kBlurInP = 112;                 // LDS input row: columns X0 - 3 .. X0 + 108
+constexpr int kBlurInQ = kBlurInP / 16;       // 16-byte chunks per input row
 __device__ __forceinline__ int reflect101_1(int p, int len) {  // |overshoot| < len - 1
     return p < 0 ? -p : (p >= len ? 2 * len - 2 - p : p);
 }
+typedef int i32x4b __attribute__((ext_vector_type(4)));
+typedef int i32x16b __attribute__((ext_vector_type(16)));
 template <bool kX86>
-__global__ __launch_bounds__(64) void blur_band_kernel(BlurArgs a) {
-    int t, f;
-    xcd_block(t, f);
-    int l = 0;
-    while (l + 1 < a.nlevels && t >= a.bt_begin[l + 1]) ++l;
-    t -= a.bt_begin[l];
-    const int cw = a.bt_cw[l];
-    const int band = t / cw;
-    const int x = 8 * ((t - band * cw) * 64 + (int)threadIdx.x);
-    const int w = a.w[l], h = a.h[l];
-    if (x >= w) return;
-    const LevelPtr sp = a.src[l], dp = a.dst[l];
+__global__ __launch_bounds__(256) void blur_mfma_kernel(BlurArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t in_lds[2][32 * kBlurInP];
+    __shared__ __attribute__((aligned(16))) uint8_t out_lds[kBlurTileH * kBlurGroupW];
+    int it, f;
+    xcd_block(it, f);
+    const uint32_t item = a.items[it];
+    const int lv = (int)(item & 15u), gx = (int)((item >> 4) & 0x1ffu), ty0 = (int)((item >> 13) & 0x1ffu),
+              nt = (int)(item >> 22);
+    const LevelPtr sp = a.src[lv], dp = a.dst[lv];
+    const int w = a.w[lv], h = a.h[lv], xb = a.simd_xb[lv];
     const uint8_t* src = sp.base + f * sp.fpitch;
     uint8_t* dst = const_cast<uint8_t*>(dp.base) + f * dp.fpitch;
-    const int y0 = band * kBlurBandRows, yend = min(y0 + kBlurBandRows, h);
-    const uint32_t KLO = (uint32_t)(a.taps[0] | (a.taps[1] << 8) | (a.taps[2] << 16) | (a.taps[3] << 24));
-    const uint32_t KHI = (uint32_t)(a.taps[2] | (a.taps[1] << 8) | (a.taps[0] << 16));
-    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-    const unsigned short k0 = (unsigned short)a.taps[0], k1 = (unsigned short)a.taps[1],
-                         k2 = (unsigned short)a.taps[2], k3 = (unsigned short)a.taps[3];
-    const us2 T01 = us2{k0, k1}, T23 = us2{k2, k3}, T21 = us2{k2, k1}, T0L = us2{k0, 0},
-              T0H = us2{0, k0}, T12 = us2{k1, k2}, T32 = us2{k3, k2}, T10 = us2{k1, k0};
-    const bool even0 = kX86 && x < a.simd_xb[l], even1 = kX86 && x + 4 < a.simd_xb[l];
-    auto round_sat = [&](uint32_t v, bool even) {
-        // sums carry 0x7fff; + 1 (scalar FixedPtCastEx) or the half-to-even bit (x86 SIMD body)
-        if constexpr (kX86) v += blur_round_bit(v, even);
-        else v += 1u;
-        return min(v, 0xffffffu);  // byte 2 = min(acc >> 16, 255)
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, col = lane & 31, hh = lane >> 5;
+    const int X0 = gx * kBlurGroupW;
+    // constant B fragments (blur_frags, built on the host): T (row pass, K = input column
+    // X - 3 + k) and V^T (column pass, K = the row pass's accumulator order)
+    const uint4 tq = a.frags[lane], vq = a.frags[64 + lane];
+    const i32x4b Tf = i32x4b{(int)tq.x, (int)tq.y, (int)tq.z, (int)tq.w};
+    const i32x4b Vf = i32x4b{(int)vq.x, (int)vq.y, (int)vq.z, (int)vq.w};
+    // Rows and columns past h + 2 / w + 2 feed only outputs outside the level: clamped there,
+    // one reflection suffices (levels of >= 5 px; smaller ones take the general loop)
+    auto refl = [](int p, int len) {
+        p = min(p, len + 2);
+        return len >= 5 ? reflect101_1(p, len) : reflect101(p, len);
     };
-    if (w < 16) {  // levels narrower than 16 px: each pixel directly, on reflected indices
-        for (int y = y0; y < yend; ++y)
-            for (int c = x; c < min(x + 8, w); ++c) {
-                uint32_t acc = 0x7fffu;
-                for (int i = -3; i <= 3; ++i) {
-                    const uint8_t* row = src + (long long)reflect101(y + i, h) * sp.pitch;
-                    uint32_t rs = 0;
-                    for (int j = -3; j <= 3; ++j)
-                        rs += (uint32_t)a.taps[3 - (j < 0 ? -j : j)] * row[reflect101(c + j, w)];
-                    acc += (uint32_t)a.taps[3 - (i < 0 ? -i : i)] * rs;
+    // band loader: thread -> (input row lr, 16-byte chunk lc) of the band's 32 x 112 bytes
+    const int lr = tid / kBlurInQ, lc = tid - lr * kBlurInQ;
+    const int lx = X0 - 3 + 16 * lc;
+    const bool ledge = lx < 0 || lx + 15 >= w;
+    auto load_band = [&](int t) -> uint4 {
+        if (lr >= 32) return make_uint4(0u, 0u, 0u, 0u);
+        const uint8_t* row = src + (long long)refl((ty0 + t) * kBlurTileH - 3 + lr, h) * sp.pitch;
+        if (ledge) {
+            uint32_t bb[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                bb[k >> 2] |= (uint32_t)row[refl(lx + k, w)] << (8 * (k & 3));
+            return make_uint4(bb[0], bb[1], bb[2], bb[3]);
+        }
+        return load16_a1(row + lx);
+    };
+    const i32x16b zero = {};
+    constexpr uint32_t kRound = kX86 ? 0x7fffu : 0x8000u;
+    // hi pass: sum V (Rh - 128) = Dh - 128 * 257; the lo pass's C input restores both offsets
+    constexpr uint32_t kC2 = 128u * 257u * 256u + 128u * 257u + kRound;
+    // every band's loads are issued up front: a band's compute is far shorter than a global
+    // round trip, so one band of prefetch leaves the workgroup waiting on each load
+    uint4 pre[kBlurChunk];
+#pragma unroll
+    for (int t = 0; t < kBlurChunk; ++t)
+        if (t < nt) pre[t] = load_band(t);
+#pragma unroll
+    for (int t = 0; t < kBlurChunk; ++t) {
+        if (t >= nt) break;
+        uint8_t* inb = in_lds[t & 1];
+        if (lr < 32) *reinterpret_cast<uint4*>(inb + lr * kBlurInP + 16 * lc) = pre[t];
+        __syncthreads();
+        // A fragment: R row `col`, input columns X - 3 + 16 hh .. + 15, X = X0 + 24 wv
+        const uint8_t* ap = inb + col * kBlurInP + kBlurTileW * wv + 16 * hh;  // 8-byte aligned
+        const uint2 a0 = *reinterpret_cast<const uint2*>(ap), a1 = *reinterpret_cast<const uint2*>(ap + 8);
+        const i32x4b av = i32x4b{(int)(a0.x ^ 0x80808080u), (int)(a0.y ^ 0x80808080u),
+                                 (int)(a1.x ^ 0x80808080u), (int)(a1.y ^ 0x80808080u)};
+        // R - 128 * 257 (the sum of T's column is 257 for the 24 output columns)
+        const i32x16b R0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, Tf, zero, 0, 0, 0);
+        i32x4b rlo, rhi;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t e0 = (uint32_t)R0[4 * q] + 128u * 257u, e1 = (uint32_t)R0[4 * q + 1] + 128u * 257u,
+                           e2 = (uint32_t)R0[4 * q + 2] + 128u * 257u, e3 = (uint32_t)R0[4 * q + 3] + 128u * 257u;
+            rlo[q] = (int)((__builtin_amdgcn_perm(e1, e0, 0x0c0c0400u) |
+                            __builtin_amdgcn_perm(e3, e2, 0x04000c0cu)) ^ 0x80808080u);
+            rhi[q] = (int)((__builtin_amdgcn_perm(e1, e0, 0x0c0c0501u) |
+                            __builtin_amdgcn_perm(e3, e2, 0x05010c0cu)) ^ 0x80808080u);
+        }
+        const i32x16b Dh = __builtin_amdgcn_mfma_i32_32x32x32_i8(rhi, Vf, zero, 0, 0, 0);
+        i32x16b c2;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) c2[e] = (int)(((uint32_t)Dh[e] << 8) + kC2);
+        const i32x16b O = __builtin_amdgcn_mfma_i32_32x32x32_i8(rlo, Vf, c2, 0, 0, 0);
+        // O^T: output row `col` of the band, columns 24 wv + 8 g + 4 hh + i in registers 4 g + i
+        if (col < kBlurTileH) {
+#pragma unroll
+            for (int g = 0; g < 3; ++g) {
+                const int xo = kBlurTileW * wv + 8 * g + 4 * hh;
+                uint32_t s4[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    uint32_t sm = (uint32_t)O[4 * g + i];
+                    if constexpr (kX86) sm += blur_round_bit(sm, X0 + xo + i < xb);
+                    s4[i] = min(sm, 0xffffffu);  // byte 2 = min(sum >> 16, 255)
                 }
-                dst[(long long)y * dp.pitch + c] = (uint8_t)(round_sat(acc, kX86 && c < a.simd_xb[l]) >> 16);
+                *reinterpret_cast<uint32_t*>(out_lds + col * kBlurGroupW + xo) =
+                    __builtin_amdgcn_perm(s4[1], s4[0], 0x0c0c0602u) | __builtin_amdgcn_perm(s4[3], s4[2], 0x06020c0cu);
             }
-        return;
-    }
-    const bool edge = x < 4 || x + 12 > w;
-    const int ls = min(max(x - 4, 0), w - 16);
-    // edge lanes: window dword k = v_perm(v.y, v.x, selA_k) | v_perm(v.w, v.z, selB_k), the
-    // selector bytes of the pair not holding a byte's source being 0x0c (-> 0)
-    uint32_t selA[4] = {0u, 0u, 0u, 0u}, selB[4] = {0u, 0u, 0u, 0u};
-    if (edge) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int b = reflect101_1(x - 4 + 4 * k + j, w) - ls;  // in [0, 16)
-                selA[k] |= (uint32_t)(b < 8 ? b : 0x0c) << (8 * j);
-                selB[k] |= (uint32_t)(b >= 8 ? b - 8 : 0x0c) << (8 * j);
+        }
+        __syncthreads();
+        // the band's 26 output rows x 96 columns, 16 bytes per thread
+        if (tid < kBlurTileH * (kBlurGroupW / 16)) {
+            const int r = tid / (kBlurGroupW / 16), c = tid - r * (kBlurGroupW / 16);
+            const int yo = (ty0 + t) * kBlurTileH + r, xo = X0 + 16 * c;
+            if (yo < h && xo < w) {
+                const uint4 o = *reinterpret_cast<const uint4*>(out_lds + r * kBlurGroupW + 16 * c);
+                uint8_t* d = dst + (long long)yo * dp.pitch + xo;
+                if (xo + 16 <= w) {
+                    *reinterpret_cast<uint4*>(d) = o;  // blurred slab rows: 64-B aligned, X0 % 16 == 0
+                } else {
+                    const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+                    for (int i = 0; i < 16 && xo + i < w; ++i) d[i] = (uint8_t)(ow[i >> 2] >> (8 * (i & 3)));
+                }
             }
-    }
-    auto load_row = [&](int r) -> uint4 {
-        return load16_a1(src + (long long)reflect101_1(r, h) * sp.pitch + ls);
-    };
-    // row pass at the lane's 8 columns: column x + j from window bytes j+1 .. j+7
-    auto rowpass = [&](uint4 v, uint32_t (&o)[8]) {
-        if (edge) {
-            uint32_t e[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                e[k] = __builtin_amdgcn_perm(v.y, v.x, selA[k]) | __builtin_amdgcn_perm(v.w, v.z, selB[k]);
-            v = make_uint4(e[0], e[1], e[2], e[3]);
         }
-        const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int b = j + 1;
-            const uint32_t lo_ = (b & 3) ? __builtin_amdgcn_alignbyte(d[(b >> 2) + 1], d[b >> 2], b & 3) : d[b >> 2];
-            const int b2 = b + 4;
-            const uint32_t hi_ = (b2 & 3) ? __builtin_amdgcn_alignbyte(d[(b2 >> 2) + 1], d[b2 >> 2], b2 & 3) : d[b2 >> 2];
-            o[j] = __builtin_amdgcn_udot4(hi_, KHI, __builtin_amdgcn_udot4(lo_, KLO, 0u, false), false);
-        }
-    };
-    auto out_row = [&](int y, const uint32_t (&acc)[8]) {
-        const uint32_t lw = __builtin_amdgcn_perm(acc[1], acc[0], 0x0c0c0602u) |
-                            __builtin_amdgcn_perm(acc[3], acc[2], 0x06020c0cu);
-        const uint32_t hw = __builtin_amdgcn_perm(acc[5], acc[4], 0x0c0c0602u) |
-                            __builtin_amdgcn_perm(acc[7], acc[6], 0x06020c0cu);
-        uint8_t* d = dst + (long long)y * dp.pitch + x;
-        if (x + 8 <= w) {
-            *reinterpret_cast<uint2*>(d) = make_uint2(lw, hw);
-        } else {
-            const unsigned long long v = ((unsigned long long)hw << 32) | lw;
-            for (int c = 0; c < 8 && x + c < w; ++c) d[c] = (uint8_t)(v >> (8 * c));
-        }
-    };
-    constexpr int kPairsB = kBlurBandRows / 2 + 3;  // 19 input row pairs
-    constexpr int kAheadP = kBandAhead / 2;          // pairs in flight
-    uint4 ring[kAheadP][2];
-#pragma unroll
-    for (int i = 0; i < kAheadP; ++i) {
-        ring[i][0] = load_row(y0 - 3 + 2 * i);
-        ring[i][1] = load_row(y0 - 2 + 2 * i);
-    }
-    uint32_t P[4][8];  // pairs m .. m+3: rows y0-3+2k (low halves), y0-2+2k (high)
-#pragma unroll
-    for (int k = 0; k < kPairsB; ++k) {
-        const uint4 c0 = ring[k % kAheadP][0], c1 = ring[k % kAheadP][1];
-        if (k + kAheadP < kPairsB) {
-            ring[k % kAheadP][0] = load_row(y0 - 3 + 2 * (k + kAheadP));
-            ring[k % kAheadP][1] = load_row(y0 - 2 + 2 * (k + kAheadP));
-        }
-        uint32_t e[8], o[8];
-        rowpass(c0, e);
-        rowpass(c1, o);
-#pragma unroll
-        for (int c = 0; c < 8; ++c) P[k & 3][c] = __builtin_amdgcn_perm(o[c], e[c], 0x05040100u);
-        if (k < 3) continue;
-        const int m = k - 3;
-        const uint32_t* p0 = P[m & 3];
-        const uint32_t* p1 = P[(m + 1) & 3];
-        const uint32_t* p2 = P[(m + 2) & 3];
-        const uint32_t* p3 = P[(m + 3) & 3];
-        uint32_t ev[8], od[8];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const bool even = c < 4 ? even0 : even1;
-            uint32_t v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0[c]), T01, 0x7fffu, false);
-            v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1[c]), T23, v, false);
-            v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2[c]), T21, v, false);
-            v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3[c]), T0L, v, false);
-            ev[c] = round_sat(v, even);
-            uint32_t u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0[c]), T0H, 0x7fffu, false);
-            u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1[c]), T12, u, false);
-            u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2[c]), T32, u, false);
-            u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3[c]), T10, u, false);
-            od[c] = round_sat(u, even);
-        }
-        if (y0 + 2 * m < yend) out_row(y0 + 2 * m, ev);
-        if (y0 + 2 * m + 1 < yend) out_row(y0 + 2 * m + 1, od);
     }
 }
-template __global__ void blur_band_kernel<false>(BlurArgs);
-template __global__ void blur_band_kernel<true>(BlurArgs);
+template __global__ void blur_mfma_kernel<false>(BlurArgs);
+template __global__ void blur_mfma_kernel<true>(BlurArgs);
+
+// Host: blur_mfma_kernel's work list — per level, per 96-column group of four 24-px tiles,
+// runs of up to kBlurChunk 26-row bands.  Item bits: 0-3 level, 4-12 column group, 13-21 first
+// band, 22-31 band count.
+void blur_items(const Geo& geo, std::vector<uint32_t>& s) {
+    s.clear();
+    for (int l = 0; l < geo.nlevels; ++l) {
+        const int ntx = (geo.lv[l].w + kBlurGroupW - 1) / kBlurGroupW;
+        const int nty = (geo.lv[l].h + kBlurTileH - 1) / kBlurTileH;
+        for (int tx = 0; tx < ntx; ++tx)
+            for (int ty = 0; ty < nty; ty += kBlurChunk)
+                s.push_back((uint32_t)l | ((uint32_t)tx << 4) | ((uint32_t)ty << 13) |
+                            ((uint32_t)std::min(kBlurChunk, nty - ty) << 22));
+    }
+}
+
+// Host: blur_mfma_kernel's constant B fragments, lane l = col + 32 hh, byte j of its 16:
+// [0, 64)  T[k = 16 hh + j][x = col]  = tap(k - 3 - x)          (row pass)
+// [64,128) V^T[slot 16 hh + j][y = col] = tap(rho - 3 - y), rho = (j & 3) + 8 (j >> 2) + 4 hh
+//          (the row pass's accumulator row held in register j of lane half hh)
+void blur_frags(const int taps[4], uint8_t out[128 * 16]) {
+    auto tap = [&](int d) { return d < -3 || d > 3 ? 0 : taps[3 - (d < 0 ? -d : d)]; };
+    for (int l = 0; l < 64; ++l) {
+        const int col = l & 31, hh = l >> 5;
+        for (int j = 0; j < 16; ++j) {
+            out[16 * l + j] = (uint8_t)tap(16 * hh + j - 3 - col);
+            const int rho = (j & 3) + 8 * (j >> 2) + 4 * hh;
+            out[16 * (64 + l) + j] = (uint8_t)tap(rho - 3 - col);
+        }
+    }
+}
 
 // ---------------------------------------------------------------------------------------------
 // K5 — IC angle (76-103) on the unblurred level, rBRIEF (107-146) on the blurred level and
@@ -1808,10 +1867,6 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
         lv.out_off = out;
         out += lv.ncap;
         ncap_max = std::max(ncap_max, lv.ncap);
-        // blur band tiles
-        g.bt_begin[l] = g.bt_total;
-        g.bt_cw[l] = ((lv.w + 7) / 8 + 63) / 64;
-        g.bt_total += g.bt_cw[l] * ((lv.h + kBlurBandRows - 1) / kBlurBandRows);
         // resize tables for level l from level l-1 (App. A.1)
         if (l > 0) {
             const LevelGeo& sv = g.geo.lv[l - 1];
@@ -1887,6 +1942,7 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
     g.fast_lds = (size_t)rmax * g.roi_pitch + (((rmax - 4) * g.roi_pitch + 15) & ~15) +
                  2 * (size_t)g.cand_max + 16 + 128;  // + a trash slot per lane
     g.geo.key_total = keys;
+    blur_items(g.geo, g.bitems);
     g.geo.out_total = out;
     g.slab = slab;
     g.ncap_max = ncap_max;

@@ -127,8 +127,9 @@ struct BlurArgs {
     LevelPtr src[kMaxLevels];
     LevelPtr dst[kMaxLevels];
     int simd_xb[kMaxLevels];  // x86 arithmetic: columns [0, simd_xb) round half to even (H6)
-    int bt_begin[kMaxLevels];  // blur_band_kernel: first band tile of each level
-    int bt_cw[kMaxLevels];     // blur_band_kernel: 64-quad column waves per band of each level
+    const uint32_t* items;     // blur_mfma_kernel: the plan's work list (blur_items)
+    int nitems;
+    const uint4* frags;        // blur_mfma_kernel: constant B fragments (blur_frags)
 };
 
 struct DescArgs {
@@ -183,7 +184,7 @@ struct Plan {
     int xoff[kMaxLevels] = {}, yoff[kMaxLevels] = {};
     long long slab = 0;
     int ncap_max = 0, sort_cap = 0;
-    int bt_total = 0, bt_begin[kMaxLevels] = {}, bt_cw[kMaxLevels] = {};  // blur_band_kernel tiles
+    std::vector<uint32_t> bitems;  // blur_mfma_kernel work items (blur_items)
     size_t oct_lds = 0;
     int oct_keys = 0;      // LDS key capacity of the oct-tree kernel
     int roi_pitch = 0, roi_rows = 0, cand_max = 0;
@@ -203,7 +204,10 @@ template <bool kX86> __global__ void resize_tail_kernel(ResizeTailArgs);
 template <int kP> __global__ void fast_kernel(FastArgs);
 constexpr int kFastPitch = 48;  // fast_kernel<kFastPitch>: ROI pitch known at compile time
 __global__ void octree_kernel(OctArgs);
-template <bool kX86> __global__ void blur_band_kernel(BlurArgs);
+template <bool kX86> __global__ void blur_mfma_kernel(BlurArgs);
+void blur_items(const Geo& geo, std::vector<uint32_t>& s);
+void blur_frags(const int taps[4], uint8_t out[128 * 16]);
+constexpr size_t kBlurFragBytes = 128 * 16;
 template <int kDescGroup, bool kX86> __global__ void describe_kernel(DescArgs);
 extern __constant__ int c_umax[16];
 
@@ -223,6 +227,5 @@ constexpr int kDescBlockSize = ORBFE_DESC_BLOCK;
 constexpr int kDescSmallBatch = 8;  // batches below this use kDescGroupSmall keypoints per wave
 constexpr int kTailMinFrames = 8;   // batches below this skip the one-workgroup-per-frame tail
 constexpr int kDescGroupSize = ORBFE_DESC_GROUP;  // oct-tree output slots per describe wave
-constexpr int kBlurBandRows = 32;  // output rows per blur_band_kernel lane
 
 }  // namespace orbfe

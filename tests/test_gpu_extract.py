@@ -166,10 +166,10 @@ def test_unsupported_inputs_are_refused():
     e.close()
 
 
-@pytest.mark.parametrize("size", [(643, 481), (1281, 722), (331, 247), (97, 73), (61, 44)])
+@pytest.mark.parametrize("size", [(643, 481), (1281, 722), (331, 247), (97, 73), (61, 44), (40, 30)])
 def test_blur_levels_odd_sizes(size):
-    """K4 (blur_band_kernel) on level widths of every residue mod 8 / mod 16, including levels
-    narrower than 16 and than 6 px (the byte-gather and all-edge-column paths), against the
+    """K4 (blur_row_kernel) on level widths of every residue mod 4 / mod 8 / mod 16, including
+    levels narrower than 16 px or lower than 8 rows (the per-pixel "tiny" slots), against the
     oracle's GaussianBlur 7x7 REFLECT_101 (ORBextractor.cc:1088-1089)."""
     from orbslam_mapsave_amd.native import ORBextractor
     w, h = size
@@ -182,5 +182,30 @@ def test_blur_levels_odd_sizes(size):
             gb, ob = e.get_blurred_level(l), oracle.gaussian_blur(lev)
             assert gb.shape == ob.shape
             assert np.array_equal(gb, ob), f"{size} level {l} {lev.shape}: {(gb != ob).sum()} px differ"
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("size", [(640, 480), (643, 481), (1920, 1080), (331, 247)])
+def test_preblur_path(size, monkeypatch):
+    """ORBFE_PREBLUR=1: K4 over every level (blur_row_kernel), describe reading the blurred
+    levels; keypoints and descriptors stay bit-exact against the oracle, batch and single."""
+    from orbslam_mapsave_amd.native import ORBextractor
+    w, h = size
+    monkeypatch.setenv("ORBFE_PREBLUR", "1")
+    nf = 2000 if w > 1000 else 1000
+    e = ORBextractor(nf, 1.2, 8, 20, 7, device=0, max_width=w, max_height=h)
+    pp = oracle.params(nf, 1.2, 8, 20, 7)
+    try:
+        imgs = np.stack([synthetic_frame(s + w, w, h) for s in range(3)])
+        kps, desc, cnt = e.extract_batch(imgs)
+        for f in range(3):
+            okps, odesc = oracle.extract(pp, imgs[f])
+            _assert_same_keys(kps[f, :cnt[f]], okps)
+            assert np.array_equal(desc[f, :cnt[f]], odesc)
+        k1, d1 = e(imgs[0])
+        okps, odesc = oracle.extract(pp, imgs[0])
+        _assert_same_keys(k1, okps)
+        assert np.array_equal(d1, odesc)
     finally:
         e.close()
