@@ -1195,8 +1195,10 @@ __device__ __forceinline__ int reflect101(int p, int len) {
 // gather reflected bytes one by one (edge workgroups only).
 constexpr int kBlurTileW = 24, kBlurTileH = 26, kBlurChunk = 8;
 constexpr int kBlurGroupW = 4 * kBlurTileW;   // output columns per workgroup
-constexpr int kBlurInP = 112;                 // LDS input row: columns X0 - 3 .. X0 + 108
-constexpr int kBlurInQ = kBlurInP / 16;       // 16-byte chunks per input row
+constexpr int kBlurInQ = 7;                   // 16-byte input chunks per row: X0 - 3 .. X0 + 108
+constexpr int kBlurInP = 104;                 // LDS input row (columns X0 - 3 .. X0 + 100 are
+                                              // read; 26 dwords: 2-way bank aliasing at most)
+constexpr int kBlurOutP = 100;                // LDS output row (25 dwords: conflict-free)
 __device__ __forceinline__ int reflect101_1(int p, int len) {  // |overshoot| < len - 1
     return p < 0 ? -p : (p >= len ? 2 * len - 2 - p : p);
 }
@@ -1205,7 +1207,7 @@ typedef int i32x16b __attribute__((ext_vector_type(16)));
 template <bool kX86>
 __global__ __launch_bounds__(256) void blur_mfma_kernel(BlurArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t in_lds[2][32 * kBlurInP];
-    __shared__ __attribute__((aligned(16))) uint8_t out_lds[kBlurTileH * kBlurGroupW];
+    __shared__ __attribute__((aligned(16))) uint8_t out_lds[kBlurTileH * kBlurOutP];
     int it, f;
     xcd_block(it, f);
     const uint32_t item = a.items[it];
@@ -1232,17 +1234,39 @@ __global__ __launch_bounds__(256) void blur_mfma_kernel(BlurArgs a) {
     const int lr = tid / kBlurInQ, lc = tid - lr * kBlurInQ;
     const int lx = X0 - 3 + 16 * lc;
     const bool ledge = lx < 0 || lx + 15 >= w;
+    // a chunk that leaves the row (level >= 16 px wide) loads the row's first or last 16 bytes
+    // instead: every reflected column it needs lies there, and v_perm pairs with per-lane
+    // selectors rebuild it (chunk byte k <- loaded byte of column refl(lx + k))
+    const bool tiny = w < 16;
+    const int ls = lx < 0 ? 0 : (lx + 15 >= w ? w - 16 : lx);
+    uint32_t selA[4] = {0u, 0u, 0u, 0u}, selB[4] = {0u, 0u, 0u, 0u};
+    if (ledge && !tiny) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int b = refl(lx + k, w) - ls;  // in [0, 16)
+            selA[k >> 2] |= (uint32_t)(b < 8 ? b : 0x0c) << (8 * (k & 3));
+            selB[k >> 2] |= (uint32_t)(b >= 8 ? b - 8 : 0x0c) << (8 * (k & 3));
+        }
+    }
     auto load_band = [&](int t) -> uint4 {
         if (lr >= 32) return make_uint4(0u, 0u, 0u, 0u);
         const uint8_t* row = src + (long long)refl((ty0 + t) * kBlurTileH - 3 + lr, h) * sp.pitch;
-        if (ledge) {
+        if (tiny) {  // levels narrower than 16 px: byte by byte
             uint32_t bb[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
             for (int k = 0; k < 16; ++k)
                 bb[k >> 2] |= (uint32_t)row[refl(lx + k, w)] << (8 * (k & 3));
             return make_uint4(bb[0], bb[1], bb[2], bb[3]);
         }
-        return load16_a1(row + lx);
+        uint4 v = load16_a1(row + ls);
+        if (ledge) {
+            uint32_t e[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                e[k] = __builtin_amdgcn_perm(v.y, v.x, selA[k]) | __builtin_amdgcn_perm(v.w, v.z, selB[k]);
+            v = make_uint4(e[0], e[1], e[2], e[3]);
+        }
+        return v;
     };
     const i32x16b zero = {};
     constexpr uint32_t kRound = kX86 ? 0x7fffu : 0x8000u;
@@ -1258,7 +1282,11 @@ __global__ __launch_bounds__(256) void blur_mfma_kernel(BlurArgs a) {
     for (int t = 0; t < kBlurChunk; ++t) {
         if (t >= nt) break;
         uint8_t* inb = in_lds[t & 1];
-        if (lr < 32) *reinterpret_cast<uint4*>(inb + lr * kBlurInP + 16 * lc) = pre[t];
+        if (lr < 32) {  // two 8-byte writes (rows are 8-byte aligned); chunk 6 keeps its first half
+            uint2* q = reinterpret_cast<uint2*>(inb + lr * kBlurInP + 16 * lc);
+            q[0] = make_uint2(pre[t].x, pre[t].y);
+            if (lc < kBlurInQ - 1) q[1] = make_uint2(pre[t].z, pre[t].w);
+        }
         __syncthreads();
         // A fragment: R row `col`, input columns X - 3 + 16 hh .. + 15, X = X0 + 24 wv
         const uint8_t* ap = inb + col * kBlurInP + kBlurTileW * wv + 16 * hh;  // 8-byte aligned
@@ -1294,7 +1322,7 @@ __global__ __launch_bounds__(256) void blur_mfma_kernel(BlurArgs a) {
                     if constexpr (kX86) sm += blur_round_bit(sm, X0 + xo + i < xb);
                     s4[i] = min(sm, 0xffffffu);  // byte 2 = min(sum >> 16, 255)
                 }
-                *reinterpret_cast<uint32_t*>(out_lds + col * kBlurGroupW + xo) =
+                *reinterpret_cast<uint32_t*>(out_lds + col * kBlurOutP + xo) =
                     __builtin_amdgcn_perm(s4[1], s4[0], 0x0c0c0602u) | __builtin_amdgcn_perm(s4[3], s4[2], 0x06020c0cu);
             }
         }
@@ -1304,7 +1332,8 @@ __global__ __launch_bounds__(256) void blur_mfma_kernel(BlurArgs a) {
             const int r = tid / (kBlurGroupW / 16), c = tid - r * (kBlurGroupW / 16);
             const int yo = (ty0 + t) * kBlurTileH + r, xo = X0 + 16 * c;
             if (yo < h && xo < w) {
-                const uint4 o = *reinterpret_cast<const uint4*>(out_lds + r * kBlurGroupW + 16 * c);
+                const uint32_t* op = reinterpret_cast<const uint32_t*>(out_lds + r * kBlurOutP + 16 * c);
+                const uint4 o = make_uint4(op[0], op[1], op[2], op[3]);
                 uint8_t* d = dst + (long long)yo * dp.pitch + xo;
                 if (xo + 16 <= w) {
                     *reinterpret_cast<uint4*>(d) = o;  // blurred slab rows: 64-B aligned, X0 % 16 == 0
