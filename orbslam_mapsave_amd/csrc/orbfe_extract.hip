@@ -170,13 +170,8 @@ constexpr int kRsRPT = kRsTH / 8;
 template <bool kX86>
 __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
-    // the tile's table entries, staged once: {x0 - sx0, x1 - sx0, a0 | a1 << 16} per output
-    // column and {y0 - sy0, y1 - sy0, b0 | b1 << 16} per output row (as per-thread global
-    // loads they were 24 VMEM instructions per thread, the kernel's texture-addresser bound)
-    __shared__ int4 xts[kRsTW], yts[kRsTH];
     int bx, f;
     xcd_block(bx, f);
-    const int tid = threadIdx.x;
     const int ox = (bx % a.tiles_x) * kRsTW, oy = (bx / a.tiles_x) * kRsTH;
     const int ex = min(ox + kRsTW, a.dw) - 1, ey = min(oy + kRsTH, a.dh) - 1;
     const int sy0 = a.yt[3 * oy], sy1 = a.yt[3 * ey + 1];
@@ -184,13 +179,6 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
     const int nrow = sy1 - sy0 + 1, P = a.lds_pitch;  // P % 16 == 0
     const int cpr = ((sx1 - sx0) >> 4) + 1;                 // 16-byte chunks per source row
     const uint8_t* src = a.src.base + f * a.src.fpitch;
-    if (tid < kRsTW) {
-        const int dx = min(ox + tid, a.dw - 1);
-        xts[tid] = make_int4(a.xt[3 * dx] - sx0, a.xt[3 * dx + 1] - sx0, a.xt[3 * dx + 2], 0);
-    } else if (tid < kRsTW + kRsTH) {
-        const int dy = min(oy + tid - kRsTW, a.dh - 1);
-        yts[tid - kRsTW] = make_int4(a.yt[3 * dy] - sy0, a.yt[3 * dy + 1] - sy0, a.yt[3 * dy + 2], 0);
-    }
     // source rows -> LDS in 16-byte chunks (global dwordx4 needs 4-byte alignment: sx0 % 4 ==
     // 0, pitch % 4 == 0); four chunks per thread in flight before any LDS store.  A chunk
     // reaching past the row end is assembled from dwords / bytes (level 0 may be the caller's
@@ -200,7 +188,7 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
         uint4 v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int i = base + 256 * u + tid;
+            const int i = base + 256 * u + (int)threadIdx.x;
             if (i >= total) continue;
             const int r = i / cpr, c = i - r * cpr;
             const uint8_t* row = src + (long long)(sy0 + r) * a.src.pitch;
@@ -222,35 +210,36 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int i = base + 256 * u + tid;
+            const int i = base + 256 * u + (int)threadIdx.x;
             if (i >= total) continue;
             const int r = i / cpr, c = i - r * cpr;
             *reinterpret_cast<uint4*>(rs_lds + r * P + 16 * c) = v[u];
         }
     }
     __syncthreads();
-    const int tx = tid & 31, ty = tid >> 5;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
     const int x = ox + 4 * tx;
     if (x >= a.dw) return;
     const int n = min(4, a.dw - x);
     int x0[4], x1[4], a0[4], a1[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const int4 e = xts[4 * tx + k];
-        x0[k] = e.x;
-        x1[k] = e.y;
-        a0[k] = e.z & 0xffff;
-        a1[k] = (int)((unsigned)e.z >> 16);
+        const int dx = min(x + k, a.dw - 1);
+        x0[k] = a.xt[3 * dx] - sx0;
+        x1[k] = a.xt[3 * dx + 1] - sx0;
+        const int aa = a.xt[3 * dx + 2];
+        a0[k] = aa & 0xffff;
+        a1[k] = (int)((unsigned)aa >> 16);
     }
     uint8_t* dst = const_cast<uint8_t*>(a.dst.base) + f * a.dst.fpitch;
 #pragma unroll
     for (int j = 0; j < kRsRPT; ++j) {
         const int y = oy + kRsRPT * ty + j;
         if (y >= a.dh) break;
-        const int4 e = yts[kRsRPT * ty + j];
-        const int b0 = e.z & 0xffff, b1 = (int)((unsigned)e.z >> 16);
-        const uint8_t* s0 = rs_lds + e.x * P;
-        const uint8_t* s1 = rs_lds + e.y * P;
+        const int ry0 = a.yt[3 * y] - sy0, ry1 = a.yt[3 * y + 1] - sy0, bb = a.yt[3 * y + 2];
+        const int b0 = bb & 0xffff, b1 = (int)((unsigned)bb >> 16);
+        const uint8_t* s0 = rs_lds + ry0 * P;
+        const uint8_t* s1 = rs_lds + ry1 * P;
         uint32_t packed = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
