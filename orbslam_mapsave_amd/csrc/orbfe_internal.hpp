@@ -220,8 +220,12 @@ constexpr int kOctLdsKeys = 4096;  // max oct-tree keys of one level held in LDS
 #ifndef ORBFE_DESC_BLOCK
 #define ORBFE_DESC_BLOCK 256
 #endif
+// 4 keypoints per describe wave: a frame spreads over twice the waves, so ~3.5 frames are in
+// flight per XCD instead of ~7 and each frame's level windows stay in that XCD's 4 MB L2 —
+// describe traffic 1.70x -> 0.69x of its algorithmic bytes for +2 % kernel time
+// (profiles/r02/experiments/describe_group.json)
 #ifndef ORBFE_DESC_GROUP
-#define ORBFE_DESC_GROUP 8
+#define ORBFE_DESC_GROUP 4
 #endif
 constexpr int kDescBlockSize = ORBFE_DESC_BLOCK;
 constexpr int kDescSmallBatch = 8;  // batches below this use kDescGroupSmall keypoints per wave
