@@ -1429,20 +1429,29 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
     const int s0 = (bx * (kDescBlock / 64) + (threadIdx.x >> 6)) * kDescGroup;
     if (s0 >= a.out_total) return;
 
-    // lane j < kDescGroup: slot s0 + j -> level, key, output index
+    // lane j < kDescGroup: slot s0 + j -> level, key, output index.  The level key counts are
+    // one load (lane q holds level q's) and their exclusive prefix a wave scan, so a wave's
+    // start is one global round trip, not a chain of dependent loads.  The group's slots lie in
+    // the level of s0 or the next one (every level has >= 20 slots).
+    const int cq = lane < a.nlevels ? max(cnt[lane], 0) : 0;
+    const int pre = wave_inclusive_sum(cq) - cq;
+    int l0 = 0;
+    while (l0 + 1 < a.nlevels && s0 >= a.out_off[l0 + 1]) ++l0;  // uniform: scalar loads
+    const int l1 = min(l0 + 1, a.nlevels - 1);
+    const int off0 = a.out_off[l0], off1 = l1 > l0 ? a.out_off[l1] : a.out_total;
+    const int c0 = __builtin_amdgcn_readlane(cq, l0), c1 = __builtin_amdgcn_readlane(cq, l1);
+    const int p0 = __builtin_amdgcn_readlane(pre, l0), p1 = __builtin_amdgcn_readlane(pre, l1);
     int my_l = 0, my_key = 0, my_o = 0;
     bool valid = false;
     if (lane < kDescGroup && s0 + lane < a.out_total) {
         const int slot = s0 + lane;
-        int l = 0;
-        while (l + 1 < a.nlevels && slot >= a.out_off[l + 1]) ++l;
-        const int idx = slot - a.out_off[l];
-        if (idx < cnt[l]) {
-            int o = idx;
-            for (int q = 0; q < l; ++q) o += max(cnt[q], 0);
+        const bool nx = slot >= off1;
+        const int idx = slot - (nx ? off1 : off0);
+        if (idx < (nx ? c1 : c0)) {
+            const int o = idx + (nx ? p1 : p0);
             if (o < a.kps_cap) {
                 valid = true;
-                my_l = l;
+                my_l = nx ? l1 : l0;
                 my_o = o;
                 my_key = (int)a.oct_out[f * a.out_total + slot];
             }
@@ -1511,8 +1520,11 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
     const float ang = angle * (float)(3.14159265358979323846 / 180.f);
     float ca = 1.f, sa = 0.f;
     if (valid) {
-        ca = (float)cos((double)ang);
-        sa = (float)sin((double)ang);
+        // one shared argument reduction (OCML's sin and cos are the two halves of its sincos)
+        double sd, cd;
+        sincos((double)ang, &sd, &cd);
+        ca = (float)cd;
+        sa = (float)sd;
     }
 
     // 3. rBRIEF: lane handles pairs lane + 64 q; bit k of byte i = pair 8 i + k (122-143).
