@@ -535,7 +535,8 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
     const int nr = rows - 6, nc = cols - 6;  // candidates: ROI rows/cols 3 .. n-4
     const int ncand = (nr > 0 && nc > 0) ? nr * nc : 0;
     // score plane: ROI pitch, rows -1 .. nr of the candidates, zero border
-    for (int i = lane; i < (ncand ? ((nr + 2) * P) >> 2 : 0); i += 64) reinterpret_cast<uint32_t*>(S)[i] = 0u;
+    // (16-byte stores: S is 16-byte aligned and (nr + 2) * P a multiple of 16)
+    for (int i = lane; i < (ncand ? ((nr + 2) * P) >> 4 : 0); i += 64) reinterpret_cast<uint4*>(S)[i] = make_uint4(0u, 0u, 0u, 0u);
     const unsigned inv_p = 0xffffffffu / (unsigned)P + 1u;  // r = umulhi(o, inv_p) for o < 2^16
     // Pre-test lanes: (candidate row lr, 4-pixel group lg).  Group g holds ROI-row bytes
     // [4g, 4g + 4) of roi_base (dword aligned, P % 16 == 0); candidate columns are
