@@ -1207,8 +1207,9 @@ __device__ __forceinline__ int reflect101(int p, int len) {
 // side: 96 output columns) stages each 32-row input band in LDS with 112-byte row loads (all
 // bands' loads issued up front), and writes its 26 x 96 output
 // band to LDS and then to the level with 16-byte row stores — per-lane row-strided accesses
-// (one row per lane) would make the texture addresser the bound.  Chunks that leave the level
-// gather reflected bytes one by one (edge workgroups only).
+// (one row per lane) would make the texture addresser the bound.  A chunk that leaves the
+// level loads the row's first / last 16 bytes and v_perm rebuilds the reflected bytes; levels
+// narrower than 16 px gather them one by one.
 constexpr int kBlurTileW = 24, kBlurTileH = 26, kBlurChunk = 8;
 constexpr int kBlurGroupW = 4 * kBlurTileW;   // output columns per workgroup
 constexpr int kBlurInQ = 7;                   // 16-byte input chunks per row: X0 - 3 .. X0 + 108
