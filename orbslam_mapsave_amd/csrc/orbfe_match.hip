@@ -278,6 +278,202 @@ __global__ __launch_bounds__(kBfBlock) void bf_match_kernel(
     }
 }
 
+// The same brute force on the FP4 matrix cores (v_mfma_scale_f32_32x32x64_f8f6f4, e2m1 A and B):
+// a reference bit is the FP4 value 0 or 1 (nibble 0x0 / 0x2), a query bit +1 or -1 (0x2 /
+// 0xA) and the B block scale 2^6 makes it +-64, so each accumulator is again 64 X + p exactly
+// (f32 holds every integer below 2^24).  One instruction covers 64 descriptor bits at the
+// cycles the i8 form spends on 32, so a 32 x 32 tile is a chain of 4 MFMAs instead of 8.
+// Lane half h of chunk c (bits 64 c .. 64 c + 63) holds descriptor dword 2 c + h as 32 nibbles;
+// the nibble order inside the lane is the same permutation for references and queries (a K
+// permutation common to A and B leaves the product unchanged): bit 8 q + b -> dword q, byte b,
+// low nibble; bit 8 q + 4 + b -> the high nibble.  Ranking as above, on f32 keys (min / med3 of
+// exact integers), converted to the 32-bit keys when a tile closes.
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr float kBfNoneF = 32767.f;
+// 8 bits (s .. s+7 of w) as 8 nibbles of one dword, each 0 or 1 (bit s+b -> byte b low nibble,
+// bit s+4+b -> byte b high nibble)
+__device__ __forceinline__ uint32_t bits8_nib(uint32_t w, int s) {
+    return nibble01(w, s) | (nibble01(w, s + 4) << 4);
+}
+__device__ __forceinline__ i32x4 ref_fp4(uint32_t w) {  // 0 -> 0.0, 1 -> 1.0 (0x2)
+    return i32x4{(int)(bits8_nib(w, 0) << 1), (int)(bits8_nib(w, 8) << 1),
+                 (int)(bits8_nib(w, 16) << 1), (int)(bits8_nib(w, 24) << 1)};
+}
+__device__ __forceinline__ i32x4 qry_fp4(uint32_t w) {  // 0 -> +1.0 (0x2), 1 -> -1.0 (0xA)
+    return i32x4{(int)((bits8_nib(w, 0) << 3) | 0x22222222u), (int)((bits8_nib(w, 8) << 3) | 0x22222222u),
+                 (int)((bits8_nib(w, 16) << 3) | 0x22222222u), (int)((bits8_nib(w, 24) << 3) | 0x22222222u)};
+}
+struct BfLaneF {
+    float tb, ts;
+    int best, second;
+    __device__ __forceinline__ void push(float k) {
+        // exact integers, never NaN: plain v_min_f32 (fminf would canonicalize its operands)
+        ts = __builtin_amdgcn_fmed3f(tb, ts, k);
+        float m;
+        asm("v_min_f32 %0, %1, %2" : "=v"(m) : "v"(tb), "v"(k));
+        tb = m;
+    }
+    __device__ __forceinline__ void close(int base) {
+        const int ib = (int)tb, is = (int)ts;
+        const int kb = ((ib >> 6) << 16) + base + (ib & 63), ks = (is >> 6) << 16;
+        second = kmin(kmin(second, ks), kmax(best, kb));
+        best = kmin(best, kb);
+        tb = ts = kBfNoneF;
+    }
+};
+__global__ __launch_bounds__(kBfBlock) void bf_match_fp4_kernel(
+    const uint8_t* q, long long q_pitch, const int* nq_arr, int nq_cap, const uint8_t* r,
+    long long r_pitch, const int* nr_arr, int* out) {
+    __shared__ i32x4 tile[2][8][kBfRefs];  // [buffer][descriptor dword][row]
+    const int b = blockIdx.y;
+    const int nq = min(nq_arr[b], nq_cap);
+    const int nr = r_pitch >= 32 ? min((long long)nr_arr[b], r_pitch / 32) : nr_arr[b];
+    if ((int)blockIdx.x * kBfBlock >= nq) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int col = lane & 31, h = lane >> 5;
+    const int q0 = blockIdx.x * kBfBlock + w * 64;
+    const uint8_t* R = r + b * r_pitch;
+    i32x4 bq[2][4];
+    int popc[2];
+    BfLaneF st[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+        const int qi = q0 + 32 * nt + col;
+        uint4 d0 = make_uint4(0, 0, 0, 0), d1 = d0;
+        if (qi < nq) {
+            const uint4* Q = reinterpret_cast<const uint4*>(q + b * q_pitch) + 2 * qi;
+            d0 = Q[0];
+            d1 = Q[1];
+        }
+        const uint32_t dw[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+        int pc = 0;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) pc += __popc(dw[c]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) bq[nt][c] = qry_fp4(dw[2 * c + h]);
+        popc[nt] = pc;
+        st[nt].best = st[nt].second = (256 - pc) << 16;
+        st[nt].tb = st[nt].ts = kBfNoneF;
+    }
+    f32x16 pos[2];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        pos[0][e] = (float)bf_pos(0, e);
+        pos[1][e] = (float)bf_pos(1, e);
+    }
+    const int lrow = tid & 63, lcp = tid >> 6;
+    struct Raw { uint32_t w[kBfWords]; };
+    auto fetch = [&](int t) {
+        const int j = t * kBfRefs + lrow;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(
+            R + (long long)min(j, max(nr - 1, 0)) * 32 + 4 * kBfWords * lcp);
+        Raw v;
+        if constexpr (kBfWords == 2) {
+            const uint2 u = *reinterpret_cast<const uint2*>(src);
+            v.w[0] = j < nr ? u.x : 0u;
+            v.w[1] = j < nr ? u.y : 0u;
+        } else {
+            v.w[0] = j < nr ? src[0] : 0u;
+        }
+        return v;
+    };
+    const int nfull = nr / kBfRefs, ntiles = (nr + kBfRefs - 1) / kBfRefs;
+    if (nr) {
+        const Raw v = fetch(0);
+#pragma unroll
+        for (int j = 0; j < kBfWords; ++j) tile[0][kBfWords * lcp + j][lrow] = ref_fp4(v.w[j]);
+    }
+    __syncthreads();
+    Raw raw = fetch(1);
+    f32x16 accp;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) accp[e] = kBfNoneF;
+    const int scale_a = 127, scale_b = 127 + 6;  // e8m0: 1 and 2^6
+    auto step = [&](int t, auto partial_tag) {
+        constexpr bool partial = decltype(partial_tag)::value;
+        const int cur = t & 1;
+        const Raw raw2 = fetch(t + 2);
+        const int valid = nr - t * kBfRefs - 4 * h;
+        // fragment ring, two reads ahead: fragment f = 4 p + c is chunk c of m-tile p & 1
+        auto frag = [&](int f) { return tile[cur][2 * (f & 3) + h][32 * ((f >> 2) & 1) + col]; };
+        i32x4 a = frag(0), a1 = frag(1);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int mt = p & 1, nt = p >> 1;
+            const int pmt = (p + 3) & 1, pnt = ((p + 3) & 3) >> 1;
+            f32x16 acc;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int f = 4 * p + c;
+                i32x4 a2 = a1;
+                if (f + 2 < 16) a2 = frag(f + 2);
+                const i32x8 av = i32x8{a[0], a[1], a[2], a[3], 0, 0, 0, 0};
+                const i32x8 bv = i32x8{bq[nt][c][0], bq[nt][c][1], bq[nt][c][2], bq[nt][c][3], 0, 0, 0, 0};
+                acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, bv, c ? acc : pos[mt], 4, 4, 0,
+                                                                       scale_a, 0, scale_b);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int e = 4 * c + u;
+                    float k = accp[e];
+                    if (partial && p > 0 && bf_pos(pmt, e) >= valid) k = kBfNoneF;
+                    st[pnt].push(k);
+                }
+                // next tile's expansion: word f / 8 of this thread's kBfWords at gap f % 8 == 7
+                if (f % 8 == 7 && (f >> 3) < kBfWords)
+                    tile[cur ^ 1][kBfWords * lcp + (f >> 3)][lrow] = ref_fp4(raw.w[f >> 3]);
+                a = a1;
+                a1 = a2;
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // fragment read, 2 ahead
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);  // fillers
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if (p == 0) st[1].close((t - 1) * kBfRefs);
+            if (p == 2) st[0].close(t * kBfRefs);
+            accp = acc;
+        }
+        raw = raw2;
+        __syncthreads();
+    };
+    for (int t = 0; t < nfull; ++t) step(t, std::false_type{});
+    if (nfull < ntiles) step(nfull, std::true_type{});
+    if (ntiles) {
+        const int valid = nr - (ntiles - 1) * kBfRefs - 4 * h;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) st[1].push(bf_pos(1, e) < valid ? accp[e] : kBfNoneF);
+        st[1].close((ntiles - 1) * kBfRefs);
+    }
+    int best[2] = {st[0].best, st[1].best}, second[2] = {st[0].second, st[1].second};
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+        const int kb = best[nt] + 4 * h, ks = second[nt];
+        const int ob = __shfl_xor(kb, 32), os = __shfl_xor(ks, 32);
+        second[nt] = kmin(kmin(ks, os), kmax(kb, ob));
+        best[nt] = kmin(kb, ob);
+    }
+    const int qi = q0 + 32 * h + col;
+    if (qi < nq) {
+        const int kb = h ? best[1] : best[0], ks = h ? second[1] : second[0];
+        const int pc = h ? popc[1] : popc[0];
+        const int db = (kb >> 16) + pc;
+        int* o = out + ((long long)b * nq_cap + qi) * 3;
+        o[0] = db >= 256 ? -1 : (kb & 0xffff);
+        o[1] = db;
+        o[2] = (ks >> 16) + pc;
+    }
+}
+
+// the brute-force kernel the ABI launches (ORBFE_BF_FP4: the FP4 form)
+#ifndef ORBFE_BF_FP4
+#define ORBFE_BF_FP4 1
+#endif
+#if ORBFE_BF_FP4
+#define ORBFE_BF_KERNEL bf_match_fp4_kernel
+#else
+#define ORBFE_BF_KERNEL bf_match_kernel
+#endif
+
 // ---------------------------------------------------------------------------------------------
 // Grid as CSR.  cellof[i] = -1 for keypoints outside the 64 x 48 grid (PosInGrid, 500-510).
 constexpr int kGridBlock = 1024;

@@ -463,7 +463,7 @@ int orbfe_bf_match(orbfe_matcher* m, const uint8_t* q, int nq, const uint8_t* r,
         if ((st = m->out.ensure((size_t)nq * 3 * sizeof(int)))) return st;
         if (nr >= 65536) return ORBFE_ERR_UNSUPPORTED;
         if ((st = m->flush())) return st;
-        hipLaunchKernelGGL(bf_match_kernel, dim3((nq + kBfBlock - 1) / kBfBlock, 1), dim3(kBfBlock),
+        hipLaunchKernelGGL(ORBFE_BF_KERNEL, dim3((nq + kBfBlock - 1) / kBfBlock, 1), dim3(kBfBlock),
                            0, m->stream, m->q.as<uint8_t>(), 0ll, m->nq.as<int>(), nq,
                            m->r.as<uint8_t>(), 0ll, m->nq.as<int>() + 1, m->out.as<int>());
         std::vector<int> tri((size_t)nq * 3);
@@ -486,7 +486,7 @@ int orbfe_bf_match_batch_device(orbfe_matcher* m, const uint8_t* d_q, size_t q_p
     if (nb == 0 || nq_cap == 0) return ORBFE_OK;
     if ((q_pitch | r_pitch) & 15) return ORBFE_ERR_ARG;
     return guarded(m, [&]() {
-        ORBFE_LAUNCH(m->prof, 0, bf_match_kernel, dim3((nq_cap + kBfBlock - 1) / kBfBlock, nb),
+        ORBFE_LAUNCH(m->prof, 0, ORBFE_BF_KERNEL, dim3((nq_cap + kBfBlock - 1) / kBfBlock, nb),
                      dim3(kBfBlock), 0, m->stream, d_q, (long long)q_pitch, d_nq, nq_cap, d_r,
                      (long long)r_pitch, d_nr, d_out);
         ORBFE_HIP(hipGetLastError());
