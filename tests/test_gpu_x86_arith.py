@@ -120,3 +120,26 @@ def test_mode_switch_keeps_single_frame_graph_honest(p):
                 okps, odesc = oracle.extract(p, img)
             same(kps, desc, okps, odesc)
     e.close()
+
+
+def test_x86_preblur_path(p, monkeypatch):
+    """ORBFE_PREBLUR=1 in x86 mode: blur_mfma_kernel<true> (half-to-even column rounding on the
+    SIMD body) feeding the pre-blurred describe, batch and single frame, against the oracle's
+    x86 reading."""
+    from orbslam_mapsave_amd.native import ORBextractor
+    monkeypatch.setenv("ORBFE_PREBLUR", "1")
+    e = ORBextractor(1000, 1.2, 8, 32, 7, device=0, max_width=643, max_height=481)
+    e.set_arithmetic(e.ARITH_X86_SIMD)
+    try:
+        imgs = np.stack([synthetic_frame(40 + s, 643, 481) for s in range(2)])
+        kps, desc, cnt = e.extract_batch(imgs)
+        for f in range(2):
+            with oracle.variant(X86):
+                okps, odesc = oracle.extract(p, imgs[f])
+            same(kps[f, :cnt[f]], desc[f, :cnt[f]], okps, odesc)
+        k1, d1 = e(imgs[1])
+        with oracle.variant(X86):
+            okps, odesc = oracle.extract(p, imgs[1])
+        same(k1, d1, okps, odesc)
+    finally:
+        e.close()
