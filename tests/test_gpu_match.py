@@ -30,8 +30,9 @@ def test_hamming_random(mt):
     assert mt.DescriptorDistance(a[0], ~a[0]) == 256
 
 
-@pytest.mark.parametrize("nq,nr", [(1000, 2000), (1, 1), (300, 7), (513, 1500)])
+@pytest.mark.parametrize("nq,nr", [(1000, 2000), (1, 1), (300, 7), (513, 1500), (40, 4097), (100, 65535)])
 def test_bf_match_random(mt, nq, nr):
+    """(100, 65535): the largest reference set the 16-bit index field of the keys holds."""
     rng = np.random.Generator(np.random.PCG64(nq + nr))
     q, r = S.random_desc(rng, nq), S.random_desc(rng, nr)
     got = mt.bf_match(q, r)
