@@ -29,6 +29,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+ARITH = {"scalar": 0, "x86": 1}  # orbfe_set_arithmetic: ORBFE_ARITH_SCALAR / ORBFE_ARITH_X86_SIMD
 METRIC = "frames/sec ORB extract+match, 640×480 @1000 kp, 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md "HBM3E peak BW 8.0 TB/s spec"
 STAGES = ("mask", "resize", "fast", "octree", "blur", "describe", "bf_match")
@@ -85,21 +86,26 @@ def host_cpu() -> dict:
 
 
 def cpu_baseline(frames: np.ndarray, ref_desc: np.ndarray | None, budget_s: float,
-                 nfeatures: int = 1000, what: str = "") -> dict:
+                 nfeatures: int = 1000, what: str = "", match: bool = True,
+                 arith: str = "scalar") -> dict:
     """The CPU oracle (a port of the reference CPU path, oracle/orb_oracle.cpp, -O3) on the
     bench's own frames, BASELINE.md §2: (i) one thread, frames in sequence, after 50 warm-up
     frames, until >= 1000 frames or `budget_s`; (ii) all cores of this job's host share, one
     extractor state per thread (ctypes releases the GIL), for ~budget_s / 3.  Each frame is
     extract(nfeatures) + brute-force match against `ref_desc` (or against the previous frame's
-    descriptors when ref_desc is None: config 4's f vs f-1)."""
+    descriptors when ref_desc is None: config 4's f vs f-1); extract only with match=False
+    (config 2).  arith "x86" switches the oracle to the x86 build's reading (H4/H5/H6)."""
     import concurrent.futures as cf
     import oracle  # test infrastructure: the cpu_baseline leg is allowed to load it
+    oracle.set_variant(0 if arith == "scalar" else
+                       oracle.VAR_H4_FMA | oracle.VAR_H5_SSE2 | oracle.VAR_H6_SIMD)
     p = oracle.params(nfeatures, 1.2, 8, 32, 7)
     host = host_cpu()
 
     def one(i, prev):
         kps, desc = oracle.extract(p, frames[i % len(frames)])
-        oracle.bf_match(desc, ref_desc if ref_desc is not None else prev)
+        if match:
+            oracle.bf_match(desc, ref_desc if ref_desc is not None else prev)
         return desc
 
     prev = oracle.extract(p, frames[-1])[1]
@@ -196,24 +202,51 @@ def run_c5(args) -> None:
             T["nobs"].data_ptr(), T["bad"].data_ptr(), T["skip"].data_ptr(), T["ids"].data_ptr(),
             0.8, 1.0, T["frame_mp"].data_ptr(), T["frame_mp_obs"].data_ptr(), d_inv.data_ptr())
 
+    # A14 alone ("time A17+A14 together and A14 alone"): the same
+    # frame and map with isInFrustum's outputs already in HBM (computed once, untimed) —
+    # SearchByProjection(F, vpLocalMapPoints, th) by itself
+    sf_np = np.asarray(scale, np.float32)
+    inv, px, py, pxr, pl, vc = mt.is_in_frustum(lm["xyz"], lm["normal"], lm["min_dist"],
+                                                lm["max_dist"], lm["tcw"], cam,
+                                                (0.0, float(W), 0.0, float(H)), log_scale, 0.5)
+    inv[(lm["skip"] > 0) | (lm["bad"] > 0)] = 0
+    A = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+         for k, v in dict(inv=inv, px=px, py=py, pxr=pxr, pl=pl, vc=vc).items()}
+
+    def step_a14():
+        slots.copy_(slots0)
+        out["a14"] = mt.search_by_projection_local_device(
+            len(keys), d_keys.data_ptr(), d_desc.data_ptr(), None, W, H, sf_np, M,
+            A["inv"].data_ptr(), T["bad"].data_ptr(), A["px"].data_ptr(), A["py"].data_ptr(),
+            A["pxr"].data_ptr(), A["pl"].data_ptr(), A["vc"].data_ptr(), T["desc"].data_ptr(),
+            T["nobs"].data_ptr(), T["ids"].data_ptr(), 0.8, 1.0, T["frame_mp"].data_ptr(),
+            T["frame_mp_obs"].data_ptr())
+
     def barrier():
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    for _ in range(max(args.warmup, 1)):
-        step()
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    def timed(fn):
+        for _ in range(max(args.warmup, 1)):
+            fn()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    dt_a14 = timed(step_a14)
+    fmp_a14 = slots.clone()
+    dt = timed(step)
+    same_a14 = bool(torch.equal(fmp_a14, slots))  # both legs reach the same assignment
     if rank == 0:
         K = args.steps
         value = world * K / dt
@@ -228,7 +261,7 @@ def run_c5(args) -> None:
             import oracle  # test infrastructure: the cpu_baseline leg is allowed to load it
             from orbslam_mapsave_amd.abi import Frame
             fr = Frame(keys, desc, W, H, scale)
-            done, c0 = 0, time.perf_counter()
+            done, c0, t_sbp = 0, time.perf_counter(), 0.0
             while True:
                 inv, px, py, pxr, pl, vc = oracle.is_in_frustum(
                     lm["xyz"], lm["normal"], lm["min_dist"], lm["max_dist"], lm["tcw"], cam,
@@ -236,17 +269,26 @@ def run_c5(args) -> None:
                 inv[(lm["skip"] > 0) | (lm["bad"] > 0)] = 0
                 mps = MapPoints(px, py, pl, vc, lm["desc"], lm["nobs"], track_in_view=inv,
                                 is_bad=lm["bad"], proj_xr=pxr)
+                s0 = time.perf_counter()
                 oracle.search_by_projection_local(fr, mps, 1.0, 0.8, lm["frame_mp"],
                                                   lm["frame_mp_obs"], lm["ids"])
+                t_sbp += time.perf_counter() - s0
                 done += 1
                 el = time.perf_counter() - c0
                 if el >= min(args.cpu_budget, 10.0) and done >= 3:
                     break
             cpu = {"value": round(done / el, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+                   "a14_alone_value": round(done / t_sbp, 3),
                    "sample": f"{done} calls of the same frame + 50k-point local map, isInFrustum "
                              f"+ SearchByProjection, 1 thread, oracle/orb_oracle.cpp -O3, "
                              f"{el:.1f} s"}
         nm, nto = out["r"]
+        a14 = {"calls_per_s": round(world * K / dt_a14, 2),
+               "ms_per_call": round(dt_a14 / K * 1e3, 4), "nmatches": out["a14"],
+               "same_assignment_as_fused": same_a14,
+               "note": "orbfe_search_by_projection_local_device: isInFrustum outputs resident in "
+                       "HBM (computed once, untimed); grid + candidates (count/scan/fill) + "
+                       "greedy rounds + one synchronisation per batch of rounds"}
         line = {
             "metric": C5_METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
@@ -255,6 +297,7 @@ def run_c5(args) -> None:
                     "world-space map points (synth.synthetic_local_map), resident in HBM",
             "config": {"workload": "configs[4]: Tracking::SearchLocalPoints (isInFrustum + "
                                    "SearchByProjection th=1, nnratio 0.8) vs 50k-MapPoint local map",
+                       "arith": args.arith,
                        "map_points": M, "keypoints": int(len(keys)), "nToMatch": nto,
                        "nmatches": nm, "greedy_rounds": mt.last_rounds(),
                        "parallelism": f"replicas x{world}"},
@@ -264,6 +307,7 @@ def run_c5(args) -> None:
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
                          "bytes_per_launch": nbytes, "avg_launch_ms": round(ms, 4)},
             "cpu_baseline": cpu,
+            "a14_alone": a14,
         }
         if cpu:
             line["gpu_over_cpu"] = round(value / cpu["value"], 1)
@@ -286,7 +330,16 @@ def e2e_bytes(w: int, h: int, nf: int, nq: int = 0, nr: int = 0) -> int:
 
 def parse_args():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one process per GPU); when WORLD_SIZE is unset and N > 1, "
+                         "bench.py starts the N rank processes itself")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the multi-rank launch: gloo backend, no GPU, the "
+                         "config-4 exchange step on small random descriptor slabs")
+    ap.add_argument("--arith", default="scalar", choices=["scalar", "x86"],
+                    help="arithmetic reading of the extractor (orbfe_set_arithmetic): OpenCV's "
+                         "scalar paths, or the SSE2 resize / blur bodies + FMA rotation of an "
+                         "x86 build (DESIGN.md §2)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="frames per rank per step (c3)")
@@ -295,10 +348,11 @@ def parse_args():
                     help="c4: frames per rank (default 256 / world; 32 rehearses the 8-GPU "
                          "per-rank shape on one GPU)")
     ap.add_argument("--distinct", type=int, default=32, help="distinct synthetic seeds (cycled)")
-    ap.add_argument("--streams", type=int, default=1,
+    ap.add_argument("--streams", type=int, default=0,
                     help="sub-batches per rank, each on its own HIP stream and extractor handle "
                          "(2 overlaps the sub-batches' kernels: more frames/s, but per-launch "
-                         "durations then measure a shared chip)")
+                         "durations then measure a shared chip); 0 = 1 for c2/c3, 2 for c4 "
+                         "(sub-batch A's all-gather runs while B is extracted)")
     ap.add_argument("--probe-steps", type=int, default=2,
                     help="steps after the warmup with events on every kernel, for the per-stage "
                          "table and the choice of the dominant kernel")
@@ -328,7 +382,7 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
 
     frames_np = synthetic_batch(B, W, H, first_seed=1000 * rank, distinct=args.distinct)
     frames = torch.from_numpy(frames_np).to(dev)
-    S = max(1, min(args.streams, B))
+    S = max(1, min(args.streams or (2 if mode == "pred" else 1), B))
     while B % S:
         S -= 1
     C = B // S  # frames per sub-batch
@@ -337,6 +391,7 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
     exs = []
     for k in range(S):
         e = ORBextractor(NF, 1.2, 8, 32, 7, device=local, max_width=W, max_height=H, max_batch=C)
+        e.set_arithmetic(ARITH[args.arith])
         e.set_stream(streams[k].cuda_stream)
         exs.append(e)
     mt = ORBmatcher(0.9, True, device=local)
@@ -350,6 +405,7 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
     if mode == "ref":  # reference frame (config 3): the 2x-feature extractor, once on the GPU
         ref_np = synthetic_frame(999_999, W, H)
         ex_ref = ORBextractor(NREF, 1.2, 8, 32, 7, device=local, max_width=W, max_height=H)
+        ex_ref.set_arithmetic(ARITH[args.arith])
         ref_kps, ref_desc_np = ex_ref(ref_np)
         ex_ref.close()
         ref_desc = torch.from_numpy(np.ascontiguousarray(ref_desc_np)).to(dev)
@@ -364,7 +420,9 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
             mt.bf_match_batch_device(q.data_ptr(), cap * 32, qn.data_ptr(), cap, r.data_ptr(),
                                      cap * 32, rn.data_ptr(), q.shape[0], out.data_ptr())
 
-        pm = PredecessorMatch(rank, world, B, cap, dev, bf)
+        # one exchange part per sub-batch stream: part k's all-gather is queued behind stream
+        # k's extraction, so it runs while the later sub-batches are still being extracted
+        pm = PredecessorMatch(rank, world, B, cap, dev, bf, parts=S)
 
     J = max(1, min(args.chunks, C))
     while C % J:
@@ -399,12 +457,16 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
                         ev[j] = torch.cuda.Event()
                         ev[j].record(streams[0])
             skew_next[0] = False
-        else:  # extraction on the sub-streams, then exchange + match on the main stream
+        else:  # sub-batch k: extract on stream k, then its all-gather behind it (RCCL's
+            # stream waits for stream k only); the match runs on the main stream once every
+            # part has arrived
             for k in range(S):
                 extract_chunk(k)
+                with torch.cuda.stream(streams[k]):
+                    pm.gather_part(k, d_desc, d_n)
             for k in range(S):
                 main_stream.wait_stream(streams[k])
-            pm.step(d_desc, d_n, d_out)
+            pm.finish(d_desc, d_n, d_out)
             for k in range(S):
                 streams[k].wait_stream(main_stream)
 
@@ -470,14 +532,22 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
     nref = float(len(ref_desc_np)) if mode == "ref" else nkp
     bytes_per_step = algorithmic_bytes(dom, W, H, nkp, nref) * B if dom else 0.0
     achieved = bytes_per_step / (dom_ms / K / 1e3) / 1e9 if dom_ms > 0 else 0.0
-    traffic = None
+    # HBM traffic of the dominant kernel per launch: PMC counters cannot be read inside this
+    # process, so it comes from the rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the same
+    # command committed under profiles/ (traffic_source names the file and round)
+    traffic, tsrc = None, None
     tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
-    if os.path.exists(tpath) and args.config != "c2":
+    if os.path.exists(tpath) and dom:
         with open(tpath) as fh:
-            traffic = json.load(fh).get(dom) if dom else None
+            tj = json.load(fh)
+        key = dom if args.arith == "scalar" else f"{dom}@{args.arith}"
+        if isinstance(tj.get(key), (int, float)) and tj.get("frames_per_launch") == B:
+            traffic = tj[key]
+            tsrc = f"profiles/traffic_{args.config}.json ({tj.get('source', 'rocprofv3 --pmc')})"
     roof = {"bound": "hbm", "kernel": f"{dom}_kernel" if dom else None,
             "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "traffic_source": tsrc,
             "bytes_per_launch": round(bytes_per_step * K / max(dom_launches, 1)),
             "avg_launch_ms": round(dom_ms / max(dom_launches, 1), 4)}
     value = world * B * K / dt
@@ -492,16 +562,150 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
                            "model": "SURVEY.md §8(d) algorithmic bytes per frame x frames/s"}}
 
 
+def launch_ranks(args) -> int:
+    """`--gpus N` without a launcher: start N rank processes (this script again, with RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* set, rendezvous on 127.0.0.1) and return the worst exit
+    code.  Runs before anything touches the GPU: the parent imports no torch, so every rank
+    owns its device from the start."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]],
+                                      env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in pending:  # one rank failed: the others would wait forever
+                    q.terminate()
+        time.sleep(0.05)
+    return rc if rc >= 0 else 1
+
+
+def _cpu_bf(desc, counts, prev, prev_n, out) -> None:
+    """Dry-run stand-in for the GPU matcher (first-wins best / second per query over a popcount
+    table); only `--dry-run` uses it."""
+    table = np.array([bin(i).count("1") for i in range(256)], np.int32)
+    out.fill_(-1)
+    for j in range(desc.shape[0]):
+        q = desc[j, :int(counts[j])].numpy()
+        r = prev[j, :int(prev_n[j])].numpy()
+        if len(q) == 0 or len(r) == 0:
+            continue
+        d = table[q[:, None, :] ^ r[None, :, :]].sum(-1)
+        bi = d.argmin(1)
+        bd = d[np.arange(len(q)), bi]
+        d[np.arange(len(q)), bi] = 257
+        res = np.stack([bi, bd, d.min(1)], 1).astype(np.int32)
+        out[j, :len(q)] = torch_from_numpy(res)
+
+
+def torch_from_numpy(a):
+    import torch
+    return torch.from_numpy(a)
+
+
+def run_dry(args) -> None:
+    """`--dry-run`: the multi-rank plumbing on CPU (gloo) — rendezvous, world-size check, the
+    config-4 exchange (shard.PredecessorMatch in `parts` sub-batches), barrier-bracketed timing
+    and the max over ranks — on small random descriptor slabs.  Not a GPU measurement."""
+    import torch
+    import torch.distributed as dist
+    from orbslam_mapsave_amd.shard import PredecessorMatch, global_frame
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    if rank == 0 and world != args.gpus:
+        print(f"bench.py: {world} ranks running but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(3)
+    B, cap = max(2, 8 // world), 64  # a global batch of 8 frames (so results compare)
+    desc = torch.zeros((B, cap, 32), dtype=torch.uint8)
+    cnt = torch.zeros(B, dtype=torch.int32)
+    for j in range(B):
+        rng = np.random.default_rng(global_frame(rank, world, j))
+        desc[j] = torch.from_numpy(rng.integers(0, 256, (cap, 32), dtype=np.uint8))
+        cnt[j] = int(rng.integers(cap // 2, cap + 1))
+    out = torch.zeros((B, cap, 3), dtype=torch.int32)
+    parts = 2
+    pm = PredecessorMatch(rank, world, B, cap, "cpu", _cpu_bf, parts=parts)
+
+    def step():
+        for p in range(parts):
+            pm.gather_part(p, desc, cnt)
+        pm.finish(desc, cnt, out)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    # a checksum over every global frame's matches, identical for every world size
+    chk = torch.tensor([sum(int(global_frame(rank, world, j) + 1) * int(out[j].long().sum())
+                            for j in range(B))], dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(chk)
+    if rank == 0:
+        K = args.steps
+        print(json.dumps({
+            "metric": C4_METRIC + " [dry run: CPU gloo plumbing rehearsal]",
+            "match_checksum": int(chk.item()),
+            "value": round(world * B * K / dt, 2), "unit": "frames/s", "n_gpus": world,
+            "steps": K, "warmup": args.warmup, "ms_per_step": round(dt / K * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": f"synthetic random descriptor slabs ({B} frames x 64 x 32 B per rank)",
+            "dry_run": True,
+            "config": {"workload": "config-4 exchange step on CPU: gloo all-gather in 2 "
+                                   "sub-batches + frame f vs f-1 brute force",
+                       "frames_per_rank_per_step": B, "global_batch": B * world,
+                       "parallelism": f"frame-sharded x{world} + gloo all-gather"}}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main() -> None:
     args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    if args.dry_run:
+        return run_dry(args)
     import torch
     import torch.distributed as dist
 
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if int(os.environ.get("RANK", "0")) == 0 and world != args.gpus:
+        print(f"bench.py: {world} ranks running but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(3)
     if args.config == "c5":
         return run_c5(args)
 
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -553,15 +757,17 @@ def main() -> None:
         if world == 1 and args.cpu_budget > 0:
             if args.config == "c4":
                 cpu = cpu_baseline(r["frames_np"][:min(args.distinct, 8)], None, args.cpu_budget,
-                                   NF, "(1920x1080, extract 2000 kp + BF match vs frame f-1)")
+                                   NF, "(1920x1080, extract 2000 kp + BF match vs frame f-1)",
+                                   arith=args.arith)
             elif args.config == "c3":
                 cpu = cpu_baseline(r["frames_np"][:args.distinct], r["ref_desc_np"],
                                    args.cpu_budget, NF,
-                                   "(640x480, extract 1000 kp + BF match vs the 2000-kp reference)")
+                                   "(640x480, extract 1000 kp + BF match vs the 2000-kp reference)",
+                                   arith=args.arith)
             else:
                 cpu = cpu_baseline(r["frames_np"][:args.distinct], None, args.cpu_budget, NF,
-                                   "(640x480, extract 1000 kp + BF match vs frame f-1)")
-                cpu["sample"] += " [the CPU leg matches f vs f-1: an upper bound on extract-only]"
+                                   "(640x480, extract 1000 kp, no match)", match=False,
+                                   arith=args.arith)
         K, S, J = r["K"], r["S"], r["J"]
         line = {
             "metric": metric, "value": round(r["value"], 2), "unit": "frames/s", "n_gpus": world,
@@ -570,7 +776,8 @@ def main() -> None:
             "vs_baseline": None, "dtype": "u8",
             "data": f"synthetic: seeded textured {W}x{H} u8 frames ({args.distinct} distinct "
                     f"seeds per rank, cycled), resident in HBM",
-            "config": {"workload": workload, "frames_per_rank_per_step": B,
+            "config": {"workload": workload, "arith": args.arith,
+                       "frames_per_rank_per_step": B,
                        "streams_per_rank": S, "chunks_per_stream": J,
                        "stream_skew": bool(args.skew) and S > 1 and J >= S,
                        "global_batch": B * world, "nfeatures": NF, "reference_kp": r["ref_kp"],

@@ -295,7 +295,8 @@ int orbfe_bf_match(orbfe_matcher* m, const uint8_t* q, int nq, const uint8_t* r,
 /* Device-resident batched form: `nb` independent (query-set, reference-set) problems;
  * problem b reads d_q + b*q_pitch (nq_b = d_nq[b] rows) against d_r + b*r_pitch
  * (nr_b = d_nr[b] rows) and writes d_out + b*nq_cap*3 as (best_idx, best, second) triples.
- * Reference sets hold fewer than 65536 rows. */
+ * Reference sets hold fewer than 65536 rows: the kernels search the first 65,535 rows of a
+ * larger set (indices are 16-bit fields of the ranking keys). */
 int orbfe_bf_match_batch_device(orbfe_matcher* m, const uint8_t* d_q, size_t q_pitch,
                                 const int32_t* d_nq, int nq_cap, const uint8_t* d_r,
                                 size_t r_pitch, const int32_t* d_nr, int nb, int32_t* d_out);
@@ -358,6 +359,18 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
                                      const int32_t* d_mp_ids, float nnratio, float th,
                                      int32_t* d_frame_mp, int32_t* d_frame_mp_obs,
                                      uint8_t* d_in_view, int32_t* counts);
+/* ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th) (ORBmatcher.cc:45-129)
+ * alone, on device-resident data: the isInFrustum outputs (mbTrackInView, mTrackProjX/Y/XR,
+ * mnTrackScaleLevel, mTrackViewCos — Tracking.cc:1425-1438 computed them) are already in HBM.
+ * `frame` as for orbfe_search_local_points_device (device keys_un / desc / u_right, host
+ * scale_factors); every pointer in `d_mps` and d_mp_ids (or NULL) is a device pointer;
+ * d_frame_mp / d_frame_mp_obs are updated in place; *nmatches (host).  A tracked point whose
+ * predicted level is outside the pyramid returns ORBFE_ERR_UNSUPPORTED.  Synchronous. */
+int orbfe_search_by_projection_local_device(orbfe_matcher* m, float nnratio,
+                                            const orbfe_frame_view* frame, int32_t* d_frame_mp,
+                                            int32_t* d_frame_mp_obs,
+                                            const orbfe_mappoint_view* d_mps,
+                                            const int32_t* d_mp_ids, float th, int32_t* nmatches);
 /* Jacobi rounds the most recent SearchByProjection / SearchForInitialization resolution took
  * (diagnostics). */
 int orbfe_matcher_last_rounds(const orbfe_matcher* m);

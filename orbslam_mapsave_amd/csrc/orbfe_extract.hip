@@ -1409,6 +1409,10 @@ void blur_frags(const int taps[4], uint8_t out[128 * 16]) {
 //      in 4 registers across the group) and 4 ballots make the 256-bit descriptor.
 constexpr int kDescBlock = kDescBlockSize;
 constexpr int kDescGroupSmall = 2;  // small batches (single-frame latency): 4x the waves
+// the group's slot -> level lookup assumes a group spans at most two levels, which holds while
+// a group is no larger than the smallest per-level slot capacity (ncap >= 20)
+static_assert(kDescGroupSize <= 20 && kDescGroupSmall <= 20,
+              "describe groups larger than the minimum per-level ncap (20) can span 3 levels");
 constexpr int kDescWinR = 18;                        // rotated pattern radius bound (< 18.5)
 constexpr int kDescWinRows = 2 * kDescWinR + 1;      // 37
 constexpr int kDescWinP = 48;                        // bytes per window row (3 x 16)

@@ -538,7 +538,15 @@ __global__ __launch_bounds__(1024) void sbp_local_fused_kernel(SbpFusedArgs fa) 
         }
         if (i < g.m) g.dec[i] = -2;
         if (i <= fa.rounds) g.chg[i] = 0;
-        if (i == 0) *g.nm = 0;
+        if (i == 0) {
+            *g.nm = 0;
+            // the accept kernel's last-workgroup counter starts every call at 0, and its
+            // convergence word reads "not converged" until that last workgroup overwrites it:
+            // an accept launch that never completes sends the host to the CSR fallback instead
+            // of returning a previous call's tallies
+            *g.done = 0;
+            g.stats[4] = -1;
+        }
     }
     if (tid < 3) tally[tid] = 0;
     // Staging: every load of a batch is issued before its LDS stores (one global latency per

@@ -71,7 +71,8 @@ __global__ __launch_bounds__(256) void hamming_kernel(const uint4* a, const uint
 // MFMA gaps of the next chain, beside a slice of the next tile's expansion (about 5 single-issue
 // instructions per gap, pinned with sched_group_barrier).  Lane half h holds rows 4h.. of each
 // C/D row group; its keys carry the position without the +4, added when the halves merge.
-// nr < 65536.
+// nr < 65536 (kBfMaxRefs).
+constexpr int kBfMaxRefs = 65535;
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 constexpr int kBfBlock = 256;               // 4 waves x 64 queries
@@ -121,7 +122,10 @@ __global__ __launch_bounds__(kBfBlock) void bf_match_kernel(
     // counts above the slab capacities (an extraction reports its true count when it holds
     // more keypoints than kps_cap) are clamped to the rows the slabs hold
     const int nq = min(nq_arr[b], nq_cap);
-    const int nr = r_pitch >= 32 ? min((long long)nr_arr[b], r_pitch / 32) : nr_arr[b];
+    // and to kBfMaxRefs: a row index must fit the keys' 16-bit field (past it the index would
+    // carry into the distance bits); the ABI documents that rows past it are not searched
+    const int nr = (int)min((long long)kBfMaxRefs,
+                            r_pitch >= 32 ? min((long long)nr_arr[b], r_pitch / 32) : (long long)nr_arr[b]);
     if ((int)blockIdx.x * kBfBlock >= nq) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int col = lane & 31, h = lane >> 5;
@@ -328,7 +332,10 @@ __global__ __launch_bounds__(kBfBlock) void bf_match_fp4_kernel(
     __shared__ i32x4 tile[2][8][kBfRefs];  // [buffer][descriptor dword][row]
     const int b = blockIdx.y;
     const int nq = min(nq_arr[b], nq_cap);
-    const int nr = r_pitch >= 32 ? min((long long)nr_arr[b], r_pitch / 32) : nr_arr[b];
+    // and to kBfMaxRefs: a row index must fit the keys' 16-bit field (past it the index would
+    // carry into the distance bits); the ABI documents that rows past it are not searched
+    const int nr = (int)min((long long)kBfMaxRefs,
+                            r_pitch >= 32 ? min((long long)nr_arr[b], r_pitch / 32) : (long long)nr_arr[b]);
     if ((int)blockIdx.x * kBfBlock >= nq) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int col = lane & 31, h = lane >> 5;
@@ -464,15 +471,11 @@ __global__ __launch_bounds__(kBfBlock) void bf_match_fp4_kernel(
     }
 }
 
-// the brute-force kernel the ABI launches (ORBFE_BF_FP4: the FP4 form)
-#ifndef ORBFE_BF_FP4
-#define ORBFE_BF_FP4 1
-#endif
-#if ORBFE_BF_FP4
-#define ORBFE_BF_KERNEL bf_match_fp4_kernel
-#else
-#define ORBFE_BF_KERNEL bf_match_kernel
-#endif
+// The brute-force kernel the ABI launches: the FP4 form, or the i8 form (the measured
+// alternative) for a matcher created with ORBFE_BF_I8=1 in the environment (the
+// GPU suite runs the brute-force parity tests on both).
+using BfKernel = void (*)(const uint8_t*, long long, const int*, int, const uint8_t*, long long,
+                          const int*, int*);
 
 // ---------------------------------------------------------------------------------------------
 // Grid as CSR.  cellof[i] = -1 for keypoints outside the 64 x 48 grid (PosInGrid, 500-510).

@@ -7,6 +7,7 @@
 #include <climits>
 #include <functional>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -52,6 +53,7 @@ struct orbfe_matcher {
     int last_rounds = 0;  // rounds the most recent greedy resolution took (diagnostics)
     int capacity_retries = 0;  // calls rerun because the candidates outgrew the buffer
     bool rounds_on_device = false;  // single-workgroup form: the count sits in g_chg[0]
+    BfKernel bf_kernel = bf_match_fp4_kernel;  // ORBFE_BF_I8=1 at creation: bf_match_kernel
 
     ~orbfe_matcher() {
         for (DevBuf* b : {&fa_k, &fa_d, &fa_ur, &fa_cs, &fa_ci, &fa_co, &fb_k, &fb_d, &fb_ur,
@@ -406,6 +408,8 @@ orbfe_matcher* orbfe_matcher_create(int device, int* status) {
             DeviceGuard dg(device);
             m = new orbfe_matcher();
             m->device = device;
+            const char* i8 = std::getenv("ORBFE_BF_I8");
+            if (i8 && i8[0] == '1') m->bf_kernel = bf_match_kernel;
             if (hipStreamCreateWithFlags(&m->own, hipStreamNonBlocking) != hipSuccess) st = ORBFE_ERR_HIP;
             m->stream = m->own;
         } catch (...) {
@@ -463,7 +467,7 @@ int orbfe_bf_match(orbfe_matcher* m, const uint8_t* q, int nq, const uint8_t* r,
         if ((st = m->out.ensure((size_t)nq * 3 * sizeof(int)))) return st;
         if (nr >= 65536) return ORBFE_ERR_UNSUPPORTED;
         if ((st = m->flush())) return st;
-        hipLaunchKernelGGL(ORBFE_BF_KERNEL, dim3((nq + kBfBlock - 1) / kBfBlock, 1), dim3(kBfBlock),
+        hipLaunchKernelGGL(m->bf_kernel, dim3((nq + kBfBlock - 1) / kBfBlock, 1), dim3(kBfBlock),
                            0, m->stream, m->q.as<uint8_t>(), 0ll, m->nq.as<int>(), nq,
                            m->r.as<uint8_t>(), 0ll, m->nq.as<int>() + 1, m->out.as<int>());
         std::vector<int> tri((size_t)nq * 3);
@@ -486,7 +490,7 @@ int orbfe_bf_match_batch_device(orbfe_matcher* m, const uint8_t* d_q, size_t q_p
     if (nb == 0 || nq_cap == 0) return ORBFE_OK;
     if ((q_pitch | r_pitch) & 15) return ORBFE_ERR_ARG;
     return guarded(m, [&]() {
-        ORBFE_LAUNCH(m->prof, 0, ORBFE_BF_KERNEL, dim3((nq_cap + kBfBlock - 1) / kBfBlock, nb),
+        ORBFE_LAUNCH(m->prof, 0, m->bf_kernel, dim3((nq_cap + kBfBlock - 1) / kBfBlock, nb),
                      dim3(kBfBlock), 0, m->stream, d_q, (long long)q_pitch, d_nq, nq_cap, d_r,
                      (long long)r_pitch, d_nr, d_out);
         ORBFE_HIP(hipGetLastError());
@@ -965,10 +969,8 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
             if ((st = m->g_last.ensure(std::max(N, 1) * sizeof(int)))) return st;
             if ((st = m->g_dec.ensure((size_t)M * sizeof(int)))) return st;
             if ((st = m->g_chg.ensure((size_t)std::max(M + 2, kBlindRounds + 2) * sizeof(int)))) return st;
-            if (!m->done_ctr.p) {  // the accept kernel's counter: zero once, reset by its user
-                if ((st = m->done_ctr.ensure(64))) return st;
-                ORBFE_HIP(hipMemsetAsync(m->done_ctr.p, 0, 64, m->stream));
-            }
+            // the accept kernel's counter (zeroed by sbp_local_fused_kernel on every call)
+            if ((st = m->done_ctr.ensure(64))) return st;
             SbpFusedArgs fu{};
             FrustumArgs& fa = fu.fr;
             fa.n = M;
@@ -1143,6 +1145,83 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
         counts[0] = host[0];  // nmatches
         counts[1] = host[1];  // nToMatch
         return host[2] ? host[2] : ORBFE_OK;
+        };
+        return attempt();
+    });
+}
+
+int orbfe_search_by_projection_local_device(orbfe_matcher* m, float nnratio,
+                                            const orbfe_frame_view* frame, int32_t* d_frame_mp,
+                                            int32_t* d_frame_mp_obs,
+                                            const orbfe_mappoint_view* d_mps,
+                                            const int32_t* d_mp_ids, float th, int32_t* nmatches) {
+    if (!frame_ok(frame) || !d_mps || d_mps->m < 0 || !nmatches ||
+        (frame->n && (!d_frame_mp || !d_frame_mp_obs)))
+        return ORBFE_ERR_ARG;
+    const int M = d_mps->m;
+    if (M && (!d_mps->track_in_view || !d_mps->is_bad || !d_mps->proj_x || !d_mps->proj_y ||
+              !d_mps->proj_xr || !d_mps->pred_level || !d_mps->view_cos || !d_mps->desc ||
+              !d_mps->n_obs))
+        return ORBFE_ERR_ARG;
+    return guarded(m, [&]() {
+        int st;
+        const int N = frame->n;
+        if ((st = m->scal.ensure(64))) return st;
+        if ((st = m->m_f4.ensure(std::max<size_t>(16, (size_t)frame->nlevels * 4)))) return st;
+        ORBFE_HIP(hipMemcpyAsync(m->m_f4.p, frame->scale_factors, (size_t)frame->nlevels * 4,
+                                 hipMemcpyHostToDevice, m->stream));
+        bool retried = false;
+        std::function<int()> attempt = [&]() -> int {
+            ORBFE_HIP(hipMemsetAsync(m->scal.p, 0, 16, m->stream));
+            SbpLocalArgs a;
+            if ((st = m->frame_device(frame, a.f))) return st;  // AssignFeaturesToGrid
+            a.mp = SbpMps{M, d_mps->track_in_view, d_mps->is_bad, d_mps->proj_x, d_mps->proj_y,
+                          d_mps->proj_xr, d_mps->pred_level, d_mps->view_cos,
+                          reinterpret_cast<const uint4*>(d_mps->desc), d_mps->n_obs};
+            a.scale = m->m_f4.as<float>();
+            a.th = th;
+            a.nlevels = frame->nlevels;
+            a.status = m->scal.as<int>() + 2;  // a predicted level outside the pyramid
+            // count -> scan -> fill bounded by the grow-only capacity; checked after the first
+            // batch of greedy rounds, redone once with the exact total if it did not fit
+            const size_t cap = std::max(m->cand.bytes / sizeof(int2), (size_t)16 * std::max(M, 1));
+            if ((st = m->cand.ensure(cap * sizeof(int2)))) return st;
+            if ((st = m->cnt.ensure(std::max(M, 1) * sizeof(int)))) return st;
+            if ((st = m->off.ensure((M + 1) * sizeof(int)))) return st;
+            a.cnt = m->cnt.as<int>();
+            a.off = m->off.as<int>();
+            a.cand = m->cand.as<int2>();
+            a.cand_cap = (long long)cap;
+            const int qb = std::max(1, (M + 255) / 256);
+            hipLaunchKernelGGL(sbp_local_cand_kernel<false>, dim3(qb), dim3(256), 0, m->stream, a);
+            hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, m->stream, m->cnt.as<int>(), M, m->off.as<int>());
+            hipLaunchKernelGGL(sbp_local_cand_kernel<true>, dim3(qb), dim3(256), 0, m->stream, a);
+            int total = 0;
+            ORBFE_HIP(hipMemcpyAsync(&total, m->off.as<int>() + M, sizeof(int), hipMemcpyDeviceToHost, m->stream));
+            GreedyArgs g{};
+            g.m = M;
+            g.nkp = N;
+            g.mode = kGreedyLocal;
+            g.nnratio = nnratio;
+            g.off = m->off.as<int>();
+            g.cand = m->cand.as<int2>();
+            g.nobs = d_mps->n_obs;
+            g.fmp0 = g.fmp = d_frame_mp;
+            g.fobs0 = g.fobs = d_frame_mp_obs;
+            g.ids = d_mp_ids;
+            st = m->greedy(g, 8, &total, cap);
+            if (st == ORBFE_ERR_CAPACITY && !retried) {
+                if ((st = m->cand.ensure((size_t)total * sizeof(int2)))) return st;
+                retried = true;
+                ++m->capacity_retries;
+                return attempt();
+            }
+            if (st) return st;
+            int host[3] = {0, 0, 0};
+            ORBFE_HIP(hipMemcpyAsync(host, m->scal.p, sizeof(host), hipMemcpyDeviceToHost, m->stream));
+            ORBFE_HIP(hipStreamSynchronize(m->stream));
+            *nmatches = host[0];
+            return host[2] ? host[2] : ORBFE_OK;
         };
         return attempt();
     });

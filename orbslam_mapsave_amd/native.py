@@ -18,7 +18,7 @@ import os
 import numpy as np
 
 from .abi import (KEYPOINT_DTYPE, ORBFE_ERR_CAPACITY, ORBFE_OK, Camera, Frame, FrameView,
-                  MapPoints, OrbfeError, Params, ptr)
+                  MapPoints, MapPointView, OrbfeError, Params, ptr)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # ORBFE_LIB selects another build of the same library (A/B runs of build variants)
@@ -40,6 +40,7 @@ EXPORTED = [
     "orbfe_search_by_projection_local", "orbfe_search_by_projection_last",
     "orbfe_search_by_projection_keyframe", "orbfe_distinctive_descriptors",
     "orbfe_distinctive_descriptors_device", "orbfe_search_local_points_device",
+    "orbfe_search_by_projection_local_device",
     "orbfe_matcher_last_rounds", "orbfe_matcher_capacity_retries", "orbfe_features_in_area", "orbfe_is_in_frustum", "orbfe_vocabulary_load_text",
     "orbfe_vocabulary_create", "orbfe_vocabulary_destroy", "orbfe_vocabulary_info",
     "orbfe_vocabulary_set_stream", "orbfe_bow_transform", "orbfe_bow_transform_batch_device",
@@ -616,6 +617,31 @@ class ORBmatcher:
             vp(d_mdesc), vp(d_nobs), vp(d_bad), vp(d_skip), vp(d_ids), C.c_float(nnratio),
             C.c_float(th), vp(d_fmp), vp(d_fobs), vp(d_in_view), ptr(counts)))
         return int(counts[0]), int(counts[1])
+
+    def search_by_projection_local_device(self, n_kp: int, d_keys: int, d_desc: int,
+                                          d_u_right: int | None, width: int, height: int,
+                                          scale_factors: np.ndarray, n_mp: int,
+                                          d_in_view: int, d_bad: int, d_px: int, d_py: int,
+                                          d_pxr: int, d_lvl: int, d_vcos: int, d_mdesc: int,
+                                          d_nobs: int, d_ids: int | None, nnratio: float,
+                                          th: float, d_fmp: int, d_fobs: int) -> int:
+        """SearchByProjection(F, vpLocalMapPoints, th) alone on device-resident isInFrustum
+        outputs (orbfe_search_by_projection_local_device) -> nmatches."""
+        sf = np.ascontiguousarray(scale_factors, np.float32)
+        gw = np.float32(64) / np.float32(width)
+        gh = np.float32(48) / np.float32(height)
+        fv = FrameView(n_kp, C.c_void_p(d_keys), C.c_void_p(d_desc),
+                       C.c_void_p(d_u_right) if d_u_right else None, 0.0, float(width), 0.0,
+                       float(height), float(gw), float(gh), ptr(sf), len(sf))
+        vp = lambda p: C.c_void_p(p) if p else None  # noqa: E731
+        mv = MapPointView(n_mp, vp(d_in_view), vp(d_bad), vp(d_px), vp(d_py), vp(d_pxr),
+                          vp(d_lvl), vp(d_vcos), vp(d_mdesc), vp(d_nobs))
+        nm = C.c_int32(0)
+        _check("orbfe_search_by_projection_local_device",
+               lib().orbfe_search_by_projection_local_device(
+                   self._h, C.c_float(nnratio), C.byref(fv), vp(d_fmp), vp(d_fobs), C.byref(mv),
+                   vp(d_ids), C.c_float(th), C.byref(nm)))
+        return nm.value
 
     def last_rounds(self) -> int:
         return lib().orbfe_matcher_last_rounds(self._h)

@@ -173,3 +173,78 @@ def test_device_path_refuses_short_capacity():
         assert got.tobytes() == okps.tobytes()
         assert np.array_equal(d_desc[i, :c].cpu().numpy(), odesc)
     ex.close()
+
+
+def _chain_case(L, seed=3):
+    """A contended local map whose greedy resolution needs L + 1 Jacobi rounds: L map points
+    at the same projection all rank the same L keypoints in the same order (distances 2, 8, 14,
+    ... from one descriptor; octaves alternate 1 / 2, so best and second never share a level and
+    the ratio test never rejects), and each blocks what it takes (Observations() = 1), so point
+    j ends on keypoint j only after round j.  Added to a real frame + a 300-point map."""
+    from orbslam_mapsave_amd.abi import KEYPOINT_DTYPE, Frame
+    f = S.extract_frame(seed, 1000)
+    far = (np.abs(f.keys["x"] - 320) > 12) | (np.abs(f.keys["y"] - 240) > 12)
+    rng = np.random.default_rng(seed)
+    D = rng.integers(0, 256, 32, dtype=np.uint8)
+    ck = np.zeros(L, KEYPOINT_DTYPE)
+    ck["x"] = 320 + 0.05 * np.arange(L)
+    ck["y"] = 240
+    ck["size"] = 31
+    ck["octave"] = 1 + np.arange(L) % 2
+    ck["class_id"] = -1
+    cd = np.unpackbits(np.tile(D, (L, 1)), axis=1)
+    for j in range(L):
+        cd[j, :2 + 6 * j] ^= 1
+    keys = np.concatenate([f.keys[far], ck])
+    desc = np.concatenate([f.desc[far], np.packbits(cd, axis=1)])
+    fr = Frame(keys, desc, S.W, S.H, f.scale_factors)
+    lm = synthetic_local_map(f.keys[far], f.desc[far], 300, seed=seed)  # none near the chain
+    lm["frame_mp"] = np.concatenate([lm["frame_mp"], np.full(L, -1, np.int32)])
+    lm["frame_mp_obs"] = np.concatenate([lm["frame_mp_obs"], np.zeros(L, np.int32)])
+    z, s = 4.0, np.float64(np.float32(1.2))
+    maxd = z * s ** 1.5  # PredictScale -> level 2
+    add = dict(xyz=np.tile([0.0, 0.0, z], (L, 1)), normal=np.tile([0.0, 0.0, 1.0], (L, 1)),
+               min_dist=np.full(L, maxd / s ** 7), max_dist=np.full(L, maxd),
+               desc=np.tile(D, (L, 1)), nobs=np.ones(L), bad=np.zeros(L), skip=np.zeros(L),
+               ids=np.arange(L) + 900_000)
+    for k, v in add.items():
+        lm[k] = np.concatenate([lm[k], v.astype(lm[k].dtype)])
+    return fr, lm
+
+
+@pytest.mark.parametrize("L", [4, 5, 6, 12])
+def test_local_points_round_limit(L):
+    """The fused SearchLocalPoints path runs 6 blind greedy rounds, the last merged into the
+    accept kernel (round index 5).  A chain converging by round 5 (L <= 5; L = 5 is decided in
+    the merged round itself) is returned from the fused path; a longer one (L >= 6: the map
+    still changes in round 5) restores the slots and reruns on the CSR path — both bit-exact
+    against the in-order oracle, and the fallback counted by orbfe_matcher_capacity_retries."""
+    import torch
+    from test_local_points import LOG_SCALE, oracle_search_local_points
+    fr, lm = _chain_case(L)
+    cam = S.camera()
+    inv, fmp, fobs, nm, nto = oracle_search_local_points(fr, lm, cam, 1.0)
+    M = len(lm["xyz"])
+    # the chain resolved in order: chain point j holds chain keypoint j
+    assert np.array_equal(fmp[-L:], lm["ids"][-L:])
+    dev = torch.device("cuda", 0)
+    T = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in lm.items()}
+    d_keys = torch.from_numpy(fr.keys.view(np.uint8).copy()).to(dev)
+    d_desc = torch.from_numpy(fr.desc).to(dev)
+    d_inv = torch.zeros(M, dtype=torch.uint8, device=dev)
+    m = fresh_matcher(0.8, False)
+    torch.cuda.synchronize()
+    gnm, gnto = m.search_local_points_device(
+        fr.n, d_keys.data_ptr(), d_desc.data_ptr(), None, S.W, S.H, fr.scale_factors,
+        lm["tcw"], cam, LOG_SCALE, 0.5, M, T["xyz"].data_ptr(), T["normal"].data_ptr(),
+        T["min_dist"].data_ptr(), T["max_dist"].data_ptr(), T["desc"].data_ptr(),
+        T["nobs"].data_ptr(), T["bad"].data_ptr(), T["skip"].data_ptr(), T["ids"].data_ptr(),
+        0.8, 1.0, T["frame_mp"].data_ptr(), T["frame_mp_obs"].data_ptr(), d_inv.data_ptr())
+    assert (gnm, gnto) == (nm, nto)
+    assert np.array_equal(d_inv.cpu().numpy(), inv)
+    assert np.array_equal(T["frame_mp"].cpu().numpy(), fmp)
+    assert np.array_equal(T["frame_mp_obs"].cpu().numpy(), fobs)
+    assert m.capacity_retries() == (1 if L >= 6 else 0)
+    if L >= 6:
+        assert m.last_rounds() >= L + 1
+    m.close()

@@ -22,6 +22,25 @@ def mt():
     m.close()
 
 
+@pytest.fixture(scope="module", params=["fp4", "i8"])
+def bf(request):
+    """A matcher per brute-force kernel: the FP4 MFMA form (default) and the i8 MFMA form
+    (ORBFE_BF_I8=1 at creation)."""
+    import os
+    from orbslam_mapsave_amd.native import ORBmatcher
+    old = os.environ.pop("ORBFE_BF_I8", None)
+    if request.param == "i8":
+        os.environ["ORBFE_BF_I8"] = "1"
+    try:
+        m = ORBmatcher(0.9, True, device=0)
+    finally:
+        os.environ.pop("ORBFE_BF_I8", None)
+        if old is not None:
+            os.environ["ORBFE_BF_I8"] = old
+    yield m
+    m.close()
+
+
 def test_hamming_random(mt):
     rng = np.random.Generator(np.random.PCG64(1))
     a, b = S.random_desc(rng, 5000), S.random_desc(rng, 5000)
@@ -31,27 +50,27 @@ def test_hamming_random(mt):
 
 
 @pytest.mark.parametrize("nq,nr", [(1000, 2000), (1, 1), (300, 7), (513, 1500), (40, 4097), (100, 65535)])
-def test_bf_match_random(mt, nq, nr):
+def test_bf_match_random(bf, nq, nr):
     """(100, 65535): the largest reference set the 16-bit index field of the keys holds."""
     rng = np.random.Generator(np.random.PCG64(nq + nr))
     q, r = S.random_desc(rng, nq), S.random_desc(rng, nr)
-    got = mt.bf_match(q, r)
+    got = bf.bf_match(q, r)
     exp = oracle.bf_match(q, r)
     for g, e in zip(got, exp):
         assert np.array_equal(g, e)
 
 
-def test_bf_match_ties(mt):
+def test_bf_match_ties(bf):
     rng = np.random.Generator(np.random.PCG64(3))
     base = S.random_desc(rng, 4)
     r = base[rng.integers(0, 4, 700)]       # many exact duplicates: first-wins ties
     q = S.flip_bits(base[rng.integers(0, 4, 300)], rng, 0.02)
-    for g, e in zip(mt.bf_match(q, r), oracle.bf_match(q, r)):
+    for g, e in zip(bf.bf_match(q, r), oracle.bf_match(q, r)):
         assert np.array_equal(g, e)
 
 
 @pytest.mark.parametrize("nq,nr", [(257, 64), (64, 65), (31, 63), (2, 128), (700, 129)])
-def test_bf_match_extremes(mt, nq, nr):
+def test_bf_match_extremes(bf, nq, nr):
     """Partial tiles and blocks, all-zero / all-one / complementary descriptors (distances 0 and
     256: a distance-256 reference never wins), duplicates (first-wins)."""
     rng = np.random.Generator(np.random.PCG64(7 * nq + nr))
@@ -60,18 +79,18 @@ def test_bf_match_extremes(mt, nq, nr):
     r[:] = np.where(rng.random((nr, 1)) < 0.2, ~q[rng.integers(0, nq, nr)], r)
     r[nr // 2], r[-1] = 0, 255
     r[nr // 3] = q[1]
-    got = mt.bf_match(q, r)
+    got = bf.bf_match(q, r)
     exp = oracle.bf_match(q, r)
     for g, e in zip(got, exp):
         assert np.array_equal(g, e)
     assert got[1][0] == 0 and got[1][-1] == 0                # zero / all-one references exist
-    z = mt.bf_match(np.zeros((3, 32), np.uint8), np.full((5, 32), 255, np.uint8))
+    z = bf.bf_match(np.zeros((3, 32), np.uint8), np.full((5, 32), 255, np.uint8))
     assert (z[0] == -1).all() and (z[1] == 256).all() and (z[2] == 256).all()
 
 
-def test_bf_match_extracted(mt):
+def test_bf_match_extracted(bf):
     f1, f2 = S.extract_frame(0, 1000), S.extract_frame(1, 2000)
-    for g, e in zip(mt.bf_match(f1.desc, f2.desc), oracle.bf_match(f1.desc, f2.desc)):
+    for g, e in zip(bf.bf_match(f1.desc, f2.desc), oracle.bf_match(f1.desc, f2.desc)):
         assert np.array_equal(g, e)
 
 

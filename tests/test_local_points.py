@@ -69,3 +69,44 @@ def test_gpu_search_local_points(seed, m, th, stereo):
     assert np.array_equal(T["frame_mp_obs"].cpu().numpy(), fobs)
     print(f"rounds={mt.last_rounds()} nmatches={nm} nToMatch={nto}")
     mt.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,m,th,stereo", [(0, 50000, 1.0, False), (2, 20000, 1.0, True),
+                                              (3, 1000, 5.0, False)])
+def test_gpu_search_by_projection_local_device(seed, m, th, stereo):
+    """A14 alone on device-resident isInFrustum outputs (orbfe_search_by_projection_local_device,
+    config 5's "A14 alone" leg): slots, Observations and nmatches exact vs the oracle."""
+    import torch
+    from orbslam_mapsave_amd.native import ORBmatcher
+    f = S.extract_frame(seed, 1000, u_right=stereo)
+    lm = synthetic_local_map(f.keys, f.desc, m, seed=seed)
+    cam = S.camera()
+    inv, px, py, pxr, pl, vc = oracle.is_in_frustum(
+        lm["xyz"], lm["normal"], lm["min_dist"], lm["max_dist"], lm["tcw"], cam,
+        (0.0, float(S.W), 0.0, float(S.H)), LOG_SCALE, 0.5)
+    inv[(lm["skip"] > 0) | (lm["bad"] > 0)] = 0
+    mps = MapPoints(px, py, pl, vc, lm["desc"], lm["nobs"], track_in_view=inv,
+                    is_bad=lm["bad"], proj_xr=pxr)
+    fmp, fobs, nm = oracle.search_by_projection_local(f, mps, th, 0.8, lm["frame_mp"],
+                                                      lm["frame_mp_obs"], lm["ids"])
+    dev = torch.device("cuda", 0)
+    up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    D = {k: up(v) for k, v in dict(inv=inv, bad=lm["bad"], px=px, py=py, pxr=pxr, pl=pl, vc=vc,
+                                   desc=lm["desc"], nobs=lm["nobs"], ids=lm["ids"],
+                                   fmp=lm["frame_mp"], fobs=lm["frame_mp_obs"]).items()}
+    d_keys = up(f.keys.view(np.uint8))
+    d_desc = up(f.desc)
+    d_ur = up(f.u_right) if f.u_right is not None else None
+    mt = ORBmatcher(0.8, False, device=0)
+    torch.cuda.synchronize()
+    gnm = mt.search_by_projection_local_device(
+        f.n, d_keys.data_ptr(), d_desc.data_ptr(), d_ur.data_ptr() if d_ur is not None else None,
+        S.W, S.H, f.scale_factors, m, D["inv"].data_ptr(), D["bad"].data_ptr(),
+        D["px"].data_ptr(), D["py"].data_ptr(), D["pxr"].data_ptr(), D["pl"].data_ptr(),
+        D["vc"].data_ptr(), D["desc"].data_ptr(), D["nobs"].data_ptr(), D["ids"].data_ptr(), 0.8,
+        th, D["fmp"].data_ptr(), D["fobs"].data_ptr())
+    assert gnm == nm
+    assert np.array_equal(D["fmp"].cpu().numpy(), fmp)
+    assert np.array_equal(D["fobs"].cpu().numpy(), fobs)
+    mt.close()

@@ -16,18 +16,25 @@ from orbslam_mapsave_amd.shard import (gather_slabs, global_frame, gathered_row,
 
 def test_predecessor_mapping():
     for world in (1, 2, 4, 8):
-        per = 5
+        per = 6
         total = world * per
-        seen = set()
-        for r in range(world):
-            rows = predecessor_index(r, world, per)
-            for j, row in enumerate(rows):
-                f = global_frame(r, world, j)
-                seen.add(f)
-                p = (f - 1) % total
-                assert row == gathered_row(p, world, per)
-                assert (row // per) == p % world and row % per == p // world
-        assert seen == set(range(total))
+        for parts in (1, 2, 3):
+            pp = per // parts
+            seen, rows_all = set(), set()
+            for r in range(world):
+                rows = predecessor_index(r, world, per, parts)
+                for j, row in enumerate(rows):
+                    f = global_frame(r, world, j)
+                    seen.add(f)
+                    p = (f - 1) % total
+                    assert row == gathered_row(p, world, per, parts)
+                    # part-major, then rank-major: the row is where part (p // world) // pp of
+                    # rank p % world lands
+                    part, jj = divmod(p // world, pp)
+                    assert row == part * world * pp + (p % world) * pp + jj
+                    rows_all.add(row)
+            assert seen == set(range(total))
+            assert rows_all == set(range(total))  # a permutation of the gathered rows
 
 
 def _free_port():

@@ -51,7 +51,7 @@ def oracle_match(desc, counts, prev, prev_n, out):
         out[j, :len(q)] = torch.from_numpy(np.stack([bi, bd, sd], 1).astype(np.int32))
 
 
-def _worker(rank, world, port, desc, cnt, res):
+def _worker(rank, world, port, desc, cnt, res, parts=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -60,19 +60,22 @@ def _worker(rank, world, port, desc, cnt, res):
     d = torch.from_numpy(desc[mine].copy())
     n = torch.from_numpy(cnt[mine].copy())
     out = torch.zeros((per, CAP, 3), dtype=torch.int32)
-    PredecessorMatch(rank, world, per, CAP, "cpu", oracle_match).step(d, n, out)
+    pm = PredecessorMatch(rank, world, per, CAP, "cpu", oracle_match, parts=parts)
+    for p in range(parts):  # the overlapped order bench.py --config c4 issues
+        pm.gather_part(p, d, n)
+    pm.finish(d, n, out)
     res[rank] = {f: out[j].numpy().tobytes() for j, f in enumerate(mine)}
     if world > 1:
         dist.destroy_process_group()
 
 
-def run_world(world, desc, cnt):
+def run_world(world, desc, cnt, parts=1):
     if world == 1:
         res = {}
-        _worker(0, 1, 0, desc, cnt, res)
+        _worker(0, 1, 0, desc, cnt, res, parts)
         return res[0]
     out = mp.Manager().dict()
-    mp.spawn(_worker, args=(world, _free_port(), desc, cnt, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), desc, cnt, out, parts), nprocs=world, join=True)
     merged = {}
     for r in range(world):
         merged.update(out[r])
@@ -92,3 +95,7 @@ def test_c4_step_identical_across_world_sizes(slabs):
         assert np.array_equal(got, np.stack([bi, bd, sd], 1))
     for world in (2, 4):
         assert run_world(world, desc, cnt) == base, f"world {world} differs from world 1"
+    # the overlapped exchange: two sub-batches per rank gathered separately (world 4 has one
+    # frame per rank, so one part)
+    for world, parts in ((1, 2), (2, 2), (1, 4)):
+        assert run_world(world, desc, cnt, parts) == base, f"world {world} parts {parts}"

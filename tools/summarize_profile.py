@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Turns gpurun_out/prof_<round>/ (tools/profile_round.sh) into the committed summaries under
-profiles/<round>/ and profiles/traffic_c3.json (read by bench.py for roofline.traffic).
+"""Turns gpurun_out/prof_<name>/ (tools/profile_round.sh <name> [bench args]) into the committed
+summaries under profiles/<name>/ and profiles/traffic_<config>.json (read by bench.py for
+roofline.traffic; keys "<stage>" for the scalar reading, "<stage>@x86" for --arith x86).
 
 Traffic per launch = 2 x FETCH_SIZE + WRITE_SIZE (KB -> bytes): on gfx950 FETCH_SIZE counts half
 of the bytes of a coalesced streaming read (MI355X_MICROARCH.md §HBM).  The guide calibrates 16-B
@@ -14,9 +15,9 @@ import re
 import shutil
 import sys
 
-R = sys.argv[1] if len(sys.argv) > 1 else "r01"
+R = sys.argv[1] if len(sys.argv) > 1 else "r03"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "gpurun_out", f"prof_{R}")
+SRC = os.path.join(ROOT, "gpurun_out", "prof_" + R.replace("/", "_"))
 DST = os.path.join(ROOT, "profiles", R)
 os.makedirs(DST, exist_ok=True)
 
@@ -25,7 +26,9 @@ def short(name):
 
 # kernel stats (copy + a compact table)
 shutil.copy(os.path.join(SRC, "trace", "run_kernel_stats.csv"), os.path.join(DST, "kernel_stats.csv"))
-for f in ("bench.json", "trace_bench.json"):
+for f in ("bench.json", "trace_bench.json", "bench_args.txt"):
+    if not os.path.exists(os.path.join(SRC, f)):
+        continue
     shutil.copy(os.path.join(SRC, f), os.path.join(DST, f))
 
 # Bench-shape launches: the timed launches of bench.py process one sub-batch of FRAMES frames
@@ -86,7 +89,18 @@ for n in sorted(fetch):
     stage = n.replace("_kernel", "")
     traffic[stage] = round(2 * f + w)
 json.dump(summary, open(os.path.join(DST, "pmc_summary.json"), "w"), indent=1)
-json.dump(traffic, open(os.path.join(ROOT, "profiles", "traffic_c3.json"), "w"), indent=1)
+CONF = next((c for c in ("c2", "c3", "c4") if f"--config {c}" in open(
+    os.path.join(SRC, "bench_args.txt")).read()), "c3") if os.path.exists(
+    os.path.join(SRC, "bench_args.txt")) else "c3"
+ARITH = _cfg.get("arith", "scalar")
+tpath = os.path.join(ROOT, "profiles", f"traffic_{CONF}.json")
+tj = json.load(open(tpath)) if os.path.exists(tpath) else {}
+if tj.get("frames_per_launch") not in (None, FRAMES):
+    tj = {}
+tj.update({(k if ARITH == "scalar" else f"{k}@{ARITH}"): v for k, v in traffic.items()})
+tj["frames_per_launch"] = FRAMES
+tj["source"] = f"profiles/{R}: rocprofv3 --pmc, 2 x FETCH_SIZE + WRITE_SIZE per launch"
+json.dump(tj, open(tpath, "w"), indent=1)
 for n, v in summary.items():
     print(n, v)
 
