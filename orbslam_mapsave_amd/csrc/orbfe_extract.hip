@@ -22,6 +22,7 @@
 #include <memory>
 #include <mutex>
 #include <new>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/orbfe.h"
@@ -371,9 +372,6 @@ typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ half2v fast_h2(uint32_t b) {
     return __builtin_bit_cast(half2v, b * 0x10001u + 0x64006400u);
 }
-#ifndef ORBFE_FAST_PAIRS
-#define ORBFE_FAST_PAIRS 0
-#endif
 #ifndef ORBFE_FAST_DENORM
 #define ORBFE_FAST_DENORM 1
 #endif
@@ -558,6 +556,22 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
     // Pass at iniThFAST: only pixels passing the pre-test at that threshold can have S >= t,
     // and every other pixel counts as 0 in the NMS, so S is computed for those alone.
     uint32_t* out = a.cell_keys + f * a.cell_cap_total + cell.slot;
+    // S for list entries [from, to)
+    auto score = [&](int from, int to) {
+#pragma unroll 2
+        for (int i = from + lane; i < to; i += 64) {
+            const int o = list[i];
+            // S < 0 is never a corner for t >= 0: clamp to -1 so S + 1 fits a byte
+            S[o + P + 1] = (uint8_t)(max(fast_S(roi + o + 3 * P + 3, P), -1) + 1);
+        }
+    };
+    // The list holds cand_max entries (not one per candidate pixel: ~22 % pass the pre-test on
+    // textured frames, and the LDS it would take bounds the kernel's occupancy).  Before a
+    // sweep that could overflow it, the entries so far are scored and those of rows up to
+    // r0 - 2 — whose 3 x 3 neighbourhoods are complete — are emitted; the last pre-tested row's
+    // entries move to the front (<= nc <= 66 of them; a sweep adds <= rps * nc <= 256, so
+    // cand_max >= 322 always makes progress).
+    const int sweep_max = rps * nc;
     int total = 0;
     for (int pass = 0; pass < 2 && total == 0; ++pass) {
         const int t = pass ? a.min_th : a.ini_th;  // rerun at minThFAST when empty (811-815)
@@ -569,8 +583,24 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
         // corner needs (b0 | b8) & (b4 | b12) of one polarity.
         const uint32_t R1 = (t & 1) ? 0x01010101u : 0u;
         const uint32_t M = (uint32_t)(128 - ((t + 1) >> 1)) * 0x01010101u;
-        int cnt = 0;
+        int cnt = 0, scored = 0, emitted = 0;
         for (int r0 = 0; r0 < nr; r0 += rps) {
+            if (cnt + sweep_max > a.cand_max) {  // wave-uniform
+                __syncthreads();
+                score(scored, cnt);
+                __syncthreads();
+                const int lim = (r0 - 1) * P;  // entries of rows <= r0 - 2 lie below
+                int k = 0;
+                for (int i0 = 0; i0 < cnt; i0 += 64)
+                    k += __popcll(__ballot(i0 + lane < cnt && list[i0 + lane] < lim));
+                emitted += fast_emit(S, list, k, P, inv_p, t, cell, out + emitted, cell.cap - emitted);
+                const int n1 = cnt - k;
+                const int e0 = lane < n1 ? list[k + lane] : 0, e1 = lane + 64 < n1 ? list[k + 64 + lane] : 0;
+                __syncthreads();
+                if (lane < n1) list[lane] = (uint16_t)e0;
+                if (lane + 64 < n1) list[lane + 64] = (uint16_t)e1;
+                cnt = scored = n1;
+            }
             const int cr = r0 + lr;
             uint32_t fl = 0;
             if (vmask && cr < nr) {
@@ -614,26 +644,9 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
             cnt += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
         }
         __syncthreads();
-#if ORBFE_FAST_PAIRS
-        // two candidates per lane per iteration, their 34 circle reads issued together (a
-        // second slot past cnt repeats the first: same value to the same byte)
-        for (int i = lane; i < cnt; i += 128) {
-            const int o0 = list[i];
-            const int o1 = i + 64 < cnt ? list[i + 64] : o0;
-            const int s0 = fast_S(roi + o0 + 3 * P + 3, P), s1 = fast_S(roi + o1 + 3 * P + 3, P);
-            S[o0 + P + 1] = (uint8_t)(max(s0, -1) + 1);
-            S[o1 + P + 1] = (uint8_t)(max(s1, -1) + 1);
-        }
-#else
-#pragma unroll 2
-        for (int i = lane; i < cnt; i += 64) {
-            const int o = list[i];
-            // S < 0 is never a corner for t >= 0: clamp to -1 so S + 1 fits a byte
-            S[o + P + 1] = (uint8_t)(max(fast_S(roi + o + 3 * P + 3, P), -1) + 1);
-        }
-#endif
+        score(scored, cnt);
         __syncthreads();
-        total = fast_emit(S, list, cnt, P, inv_p, t, cell, out, cell.cap);
+        total = emitted + fast_emit(S, list, cnt, P, inv_p, t, cell, out + emitted, cell.cap - emitted);
         __syncthreads();
     }
     if (lane == 0) {
@@ -664,27 +677,50 @@ template __global__ void fast_kernel<kFastPitch>(FastArgs);
 // response, first (lowest original index) on ties (741-759).
 constexpr int kOctBlock = kOctBlockSize;
 
-struct OctLds {  // carve of the dynamic LDS region (sizes in elements)
-    // two node lists (b = 0 / 1), 5 arrays of NC each: box x0 | x1 << 16, boy y0 | y1 << 16,
-    // key count, creation seq, key (single-key nodes); addressed by arithmetic, since a
+// Carve of the dynamic LDS region (sizes in elements).  IT is the type of the per-node key
+// counts, single-key indices and quadrant keys / child positions: u16 when the level's keys
+// sit in LDS (<= kOctLdsKeys keys, < 2^16 nodes), int on the global-array path (any count).
+// With u16 the four quadrant counters of a node are two packed u32 LDS atomics.  The narrow
+// form is what lets six trees share a CU (DESIGN.md "oct-tree").
+template <class IT>
+struct OctLds {
+    // two node lists (b = 0 / 1): box x0 | x1 << 16, boy y0 | y1 << 16, creation seq (int);
+    // key count, key of a single-key node (IT); addressed by arithmetic, since a
     // runtime-indexed pointer array would live in scratch
     int* lists;
+    IT* ilists;
     int nc;
-    __device__ __forceinline__ int* box(int b) const { return lists + (b * 5 + 0) * nc; }
-    __device__ __forceinline__ int* boy(int b) const { return lists + (b * 5 + 1) * nc; }
-    __device__ __forceinline__ int* cnt(int b) const { return lists + (b * 5 + 2) * nc; }
-    __device__ __forceinline__ int* seq(int b) const { return lists + (b * 5 + 3) * nc; }
-    __device__ __forceinline__ int* key(int b) const { return lists + (b * 5 + 4) * nc; }
-    int* qc;        // 4 per node: keys per quadrant
-    int* qk;        // 4 per node: a key of the quadrant, then the child's new list position
+    __device__ __forceinline__ int* box(int b) const { return lists + (b * 3 + 0) * nc; }
+    __device__ __forceinline__ int* boy(int b) const { return lists + (b * 3 + 1) * nc; }
+    __device__ __forceinline__ int* seq(int b) const { return lists + (b * 3 + 2) * nc; }
+    __device__ __forceinline__ IT* cnt(int b) const { return ilists + (b * 2 + 0) * nc; }
+    __device__ __forceinline__ IT* key(int b) const { return ilists + (b * 2 + 1) * nc; }
+    static constexpr bool kPacked = sizeof(IT) == 2;
+    static constexpr int kQcWords = kPacked ? 2 : 4;  // u32 words of quadrant counters per node
+    uint32_t* qc;   // keys per quadrant (kPacked: quadrants 2w, 2w + 1 in the halves of word w)
+    IT* qk;         // 4 per node: a key of the quadrant, then the child's new list position
     int* aux;       // per node: scan offsets / kept position / processed flag
     int* aux2;
     unsigned long long* s64;  // sort keys (phase 2) / best response (final)
     int* tmp;
     int* scal;      // scalars
-    uint32_t* keys;  // kOctLdsKeys packed keys (LDS form)
-    short* node;     // kOctLdsKeys node positions (LDS form)
+    __device__ __forceinline__ int qcount(int node, int q) const {
+        if constexpr (kPacked) return (int)((qc[node * 2 + (q >> 1)] >> (16 * (q & 1))) & 0xffffu);
+        else return (int)qc[node * 4 + q];
+    }
+    __device__ __forceinline__ void qinc(int node, int q) const {
+        if constexpr (kPacked) atomicAdd(&qc[node * 2 + (q >> 1)], 1u << (16 * (q & 1)));
+        else atomicAdd(&qc[node * 4 + q], 1u);
+    }
 };
+
+// Bytes of the carve: the LDS form (keys and node positions in LDS, u16 node fields) and the
+// global-array form (wider node fields in place of the keys); the launch takes the larger.
+constexpr size_t oct_lds_bytes(bool in_lds, int ncap, int sort_cap, int lds_keys) {
+    const size_t it = in_lds ? 2 : 4;
+    return (size_t)sort_cap * 8 + (in_lds ? (size_t)lds_keys * 6 : 0) +
+           (size_t)ncap * (6 * 4 + 4 * it + (in_lds ? 8 : 16) + 4 * it + 8) + (64 + 16) * 4 + 16;
+}
 
 __device__ __forceinline__ int quadrant(int box, int boy, int x, int y) {
     const int x0 = box & 0xffff, x1 = box >> 16, y0 = boy & 0xffff, y1 = boy >> 16;
@@ -733,8 +769,8 @@ __device__ __forceinline__ void oct_sweep(const KT* K, const NT* NODE, int nkeys
 }
 
 // The tree of one (frame, level) after its keys are in K (nkeys, original order).
-template <class KT, class NT>
-__device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds& s, const LevelGeo& L, KT* K,
+template <class IT, class KT, class NT>
+__device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>& s, const LevelGeo& L, KT* K,
                              NT* NODE, int nkeys, uint32_t* out, int* out_cnt,
                                               long long* tm) {
     const int tid = threadIdx.x;
@@ -748,14 +784,14 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds& s, 
     const float hX = L.hx;
     const int H = L.bh;
     for (int i = tid; i < nini; i += kOctBlock) {
-        s.qc[i] = 0;
-        s.qk[i] = -1;
+        s.qc[i] = 0u;  // per initial node here (nini <= NC / 4 entries)
+        s.qk[i] = (IT)-1;
     }
     __syncthreads();
     for (int k = tid; k < nkeys; k += kOctBlock) {
         const int node = min((int)((float)key_x(K[k]) / hX), nini - 1);  // vpIniNodes[kp.pt.x/hX] (568)
-        atomicAdd(&s.qc[node], 1);
-        s.qk[node] = k;
+        atomicAdd(&s.qc[node], 1u);
+        s.qk[node] = (IT)k;
     }
     __syncthreads();
     int size;
@@ -763,7 +799,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds& s, 
         int total = 0;
         for (int base = 0; base < nini; base += kOctBlock) {
             const int i = base + tid;
-            const int ne = i < nini && s.qc[i] > 0;
+            const int ne = i < nini && s.qc[i] > 0u;
             int chunk_total;
             const int off = block_exclusive_scan<kOctBlock>(ne, s.tmp, chunk_total);
             if (ne) {
@@ -771,9 +807,9 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds& s, 
                 const int x0 = (int)(hX * (float)i), x1 = (int)(hX * (float)(i + 1));
                 s.box(0)[pos] = x0 | (x1 << 16);
                 s.boy(0)[pos] = 0 | (H << 16);
-                s.cnt(0)[pos] = s.qc[i];
+                s.cnt(0)[pos] = (IT)s.qc[i];
                 s.seq(0)[pos] = i;
-                s.key(0)[pos] = s.qc[i] == 1 ? s.qk[i] : -1;
+                s.key(0)[pos] = s.qc[i] == 1u ? s.qk[i] : (IT)-1;
                 s.aux[i] = pos;
             }
             total += chunk_total;
@@ -783,7 +819,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds& s, 
     __syncthreads();
     for (int k = tid; k < nkeys; k += kOctBlock) {
         const int node = s.aux[min((int)((float)key_x(K[k]) / hX), nini - 1)];
-        NODE[k] = s.cnt(0)[node] >= 2 ? node : -1;
+        NODE[k] = (int)s.cnt(0)[node] >= 2 ? node : -1;
     }
     __syncthreads();
     OCT_MARK(tm, 3);
@@ -797,15 +833,15 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds& s, 
     for (int pass = 0; pass < 64 && !finished && !phase2; ++pass) {
         const int prev = size;
         const int nxt = cur ^ 1;
-        for (int i = tid; i < 4 * size; i += kOctBlock) s.qc[i] = 0;
+        for (int i = tid; i < OctLds<IT>::kQcWords * size; i += kOctBlock) s.qc[i] = 0u;
         __syncthreads();
         {
             const int *bx = s.box(cur), *by = s.boy(cur);
-            int *qc = s.qc, *qk = s.qk;
+            const OctLds<IT> ss = s;
             oct_sweep(K, NODE, nkeys, [=](int k, uint32_t kk, int node) {
                 const int q = quadrant(bx[node], by[node], key_x(kk), key_y(kk));
-                atomicAdd(&qc[node * 4 + q], 1);
-                qk[node * 4 + q] = k;
+                ss.qinc(node, q);
+                ss.qk[node * 4 + q] = (IT)k;
             });
         }
         __syncthreads();
@@ -815,10 +851,10 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds& s, 
             const int i = base + tid;
             int nch = 0, keep = 0, ne = 0;
             if (i < size) {
-                if (s.cnt(cur)[i] >= 2) {
+                if ((int)s.cnt(cur)[i] >= 2) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const int qn = s.qc[i * 4 + q];
+                        const int qn = s.qcount(i, q);
                         nch += qn > 0;
                         ne += qn > 1;
                     }
@@ -847,21 +883,21 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds& s, 
         }
         __syncthreads();
         for (int i = tid; i < size; i += kOctBlock) {
-            if (s.cnt(cur)[i] >= 2) {
+            if ((int)s.cnt(cur)[i] >= 2) {
                 int cp = s.aux[i];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const int qn = s.qc[i * 4 + q];
+                    const int qn = s.qcount(i, q);
                     if (!qn) continue;
                     const int np = csize - 1 - cp;
                     int cbx, cby;
                     child_box(s.box(cur)[i], s.boy(cur)[i], q, cbx, cby);
                     s.box(nxt)[np] = cbx;
                     s.boy(nxt)[np] = cby;
-                    s.cnt(nxt)[np] = qn;
+                    s.cnt(nxt)[np] = (IT)qn;
                     s.seq(nxt)[np] = seq_base + cp;
-                    s.key(nxt)[np] = qn == 1 ? s.qk[i * 4 + q] : -1;
-                    s.qk[i * 4 + q] = np;
+                    s.key(nxt)[np] = qn == 1 ? s.qk[i * 4 + q] : (IT)-1;
+                    s.qk[i * 4 + q] = (IT)np;
                     ++cp;
                 }
             } else {
@@ -875,10 +911,11 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds& s, 
         }
         __syncthreads();
         {
-            const int *bx = s.box(cur), *by = s.boy(cur), *qk = s.qk, *ncnt = s.cnt(nxt);
+            const int *bx = s.box(cur), *by = s.boy(cur);
+            const IT *qk = s.qk, *ncnt = s.cnt(nxt);
             oct_sweep(K, NODE, nkeys, [=](int k, uint32_t kk, int node) {
-                const int np = qk[node * 4 + quadrant(bx[node], by[node], key_x(kk), key_y(kk))];
-                NODE[k] = ncnt[np] >= 2 ? np : -1;
+                const int np = (int)qk[node * 4 + quadrant(bx[node], by[node], key_x(kk), key_y(kk))];
+                NODE[k] = (int)ncnt[np] >= 2 ? np : -1;
             });
         }
         __syncthreads();
@@ -899,9 +936,9 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds& s, 
         if (tid == 0) { flag_sh[0] = 0; *rmin_sh = 0x7fffffff; }
         __syncthreads();
         for (int i = tid; i < size; i += kOctBlock)
-            if (s.cnt(cur)[i] >= 2) {
+            if ((int)s.cnt(cur)[i] >= 2) {
                 const int slot = atomicAdd(&flag_sh[0], 1);
-                s.s64[slot] = ((unsigned long long)s.cnt(cur)[i] << 40) |
+                s.s64[slot] = ((unsigned long long)(unsigned)s.cnt(cur)[i] << 40) |
                               ((unsigned long long)(unsigned)s.seq(cur)[i] << 14) | (unsigned)i;
             }
         __syncthreads();
@@ -926,8 +963,8 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds& s, 
         } else {
             // rank sort (the keys are distinct: seq is unique): an entry's rank is the number of
             // larger keys; every thread scans all m keys (LDS broadcast reads), two barriers
-            // instead of a bitonic network's log2(P)(log2(P)+1)/2.  qc (4 NC ints) holds the
-            // sorted copy until it is cleared below.
+            // instead of a bitonic network's log2(P)(log2(P)+1)/2.  qc (>= 8 NC bytes, 8-byte
+            // aligned) holds the sorted copy until it is cleared below.
             unsigned long long* srt = reinterpret_cast<unsigned long long*>(s.qc);
             for (int j = tid; j < m; j += kOctBlock) {
                 const unsigned long long v = s.s64[j];
@@ -939,15 +976,15 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds& s, 
             for (int j = tid; j < m; j += kOctBlock) s.s64[j] = srt[j];
             __syncthreads();
         }
-        for (int i = tid; i < 4 * size; i += kOctBlock) s.qc[i] = 0;
+        for (int i = tid; i < OctLds<IT>::kQcWords * size; i += kOctBlock) s.qc[i] = 0u;
         __syncthreads();
         {
             const int *bx = s.box(cur), *by = s.boy(cur);
-            int *qc = s.qc, *qk = s.qk;
+            const OctLds<IT> ss = s;
             oct_sweep(K, NODE, nkeys, [=](int k, uint32_t kk, int node) {
                 const int q = quadrant(bx[node], by[node], key_x(kk), key_y(kk));
-                atomicAdd(&qc[node * 4 + q], 1);
-                qk[node * 4 + q] = k;
+                ss.qinc(node, q);
+                ss.qk[node * 4 + q] = (IT)k;
             });
         }
         __syncthreads();
@@ -959,7 +996,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds& s, 
                 int delta = 0;
                 if (j < m) {
                     const int i = (int)(s.s64[j] & 0x3fff);
-                    for (int q = 0; q < 4; ++q) delta += s.qc[i * 4 + q] > 0;
+                    for (int q = 0; q < 4; ++q) delta += s.qcount(i, q) > 0;
                     delta -= 1;
                 }
                 int t;
@@ -979,7 +1016,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds& s, 
             int nch = 0, i = -1;
             if (j <= r) {
                 i = (int)(s.s64[j] & 0x3fff);
-                for (int q = 0; q < 4; ++q) nch += s.qc[i * 4 + q] > 0;
+                for (int q = 0; q < 4; ++q) nch += s.qcount(i, q) > 0;
             }
             int t;
             const int o = block_exclusive_scan<kOctBlock>(nch, s.tmp, t);
@@ -1010,17 +1047,17 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds& s, 
                 int cp = s.aux[i];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const int qn = s.qc[i * 4 + q];
+                    const int qn = s.qcount(i, q);
                     if (!qn) continue;
                     const int np = csize - 1 - cp;
                     int cbx, cby;
                     child_box(s.box(cur)[i], s.boy(cur)[i], q, cbx, cby);
                     s.box(nxt)[np] = cbx;
                     s.boy(nxt)[np] = cby;
-                    s.cnt(nxt)[np] = qn;
+                    s.cnt(nxt)[np] = (IT)qn;
                     s.seq(nxt)[np] = seq_base + cp;
-                    s.key(nxt)[np] = qn == 1 ? s.qk[i * 4 + q] : -1;
-                    s.qk[i * 4 + q] = np;
+                    s.key(nxt)[np] = qn == 1 ? s.qk[i * 4 + q] : (IT)-1;
+                    s.qk[i * 4 + q] = (IT)np;
                     ++cp;
                 }
             } else {
@@ -1035,13 +1072,13 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds& s, 
         }
         __syncthreads();
         {
-            const int *bx = s.box(cur), *by = s.boy(cur), *qk = s.qk, *aux = s.aux,
-                      *aux2 = s.aux2, *ncnt = s.cnt(nxt);
+            const int *bx = s.box(cur), *by = s.boy(cur), *aux = s.aux, *aux2 = s.aux2;
+            const IT *qk = s.qk, *ncnt = s.cnt(nxt);
             oct_sweep(K, NODE, nkeys, [=](int k, uint32_t kk, int node) {
                 const int np = aux2[node] > 0
-                                   ? qk[node * 4 + quadrant(bx[node], by[node], key_x(kk), key_y(kk))]
+                                   ? (int)qk[node * 4 + quadrant(bx[node], by[node], key_x(kk), key_y(kk))]
                                    : aux[node];
-                NODE[k] = ncnt[np] >= 2 ? np : -1;
+                NODE[k] = (int)ncnt[np] >= 2 ? np : -1;
             });
         }
         __syncthreads();
@@ -1064,7 +1101,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds& s, 
     }
     __syncthreads();
     for (int i = tid; i < size; i += kOctBlock) {
-        const int k = s.cnt(cur)[i] == 1 ? s.key(cur)[i]
+        const int k = (int)s.cnt(cur)[i] == 1 ? (int)s.key(cur)[i]
                                           : (int)(0xffffffffu - (unsigned)(s.s64[i] & 0xffffffffu));
         const uint32_t kk = K[k];
         out[i] = pack_key(key_x(kk) + kMinBorder, key_y(kk) + kMinBorder, key_score(kk));
@@ -1084,24 +1121,28 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
     const LevelGeo& L = a.geo.lv[level];
     const int NC = a.ncap_max;
     const int tid = threadIdx.x;
-    OctLds s;
-    {
-        int* p = reinterpret_cast<int*>(lds_raw);
-        s.s64 = reinterpret_cast<unsigned long long*>(p);
-        p += 2 * a.sort_cap;
-        s.keys = reinterpret_cast<uint32_t*>(p);
-        p += a.lds_keys;
-        s.lists = p;
+    // carve: sort keys | tmp | scalars | the path's region (oct_lds_bytes)
+    unsigned long long* s64 = reinterpret_cast<unsigned long long*>(lds_raw);
+    int* tmp = reinterpret_cast<int*>(s64 + a.sort_cap);
+    int* scal = tmp + 64;
+    unsigned char* region = reinterpret_cast<unsigned char*>(scal + 16);
+    auto carve = [&](auto& s, unsigned char* p) {
+        using IT = std::remove_pointer_t<decltype(s.qk)>;
+        s.s64 = s64;
+        s.tmp = tmp;
+        s.scal = scal;
         s.nc = NC;
-        p += 10 * NC;
-        s.qc = p; p += 4 * NC;
-        s.qk = p; p += 4 * NC;
-        s.aux = p; p += NC;
-        s.aux2 = p; p += NC;
-        s.tmp = p; p += 64;
-        s.scal = p; p += 16;
-        s.node = reinterpret_cast<short*>(p);
-    }
+        s.lists = reinterpret_cast<int*>(p);
+        p += 6 * 4 * (size_t)NC;
+        s.qc = reinterpret_cast<uint32_t*>(p);  // 8-byte aligned: the rank sort's u64 copy
+        p += (size_t)std::remove_reference_t<decltype(s)>::kQcWords * 4 * NC;
+        s.ilists = reinterpret_cast<IT*>(p);
+        p += 4 * sizeof(IT) * (size_t)NC;
+        s.qk = reinterpret_cast<IT*>(p);
+        p += 4 * sizeof(IT) * (size_t)NC;
+        s.aux = reinterpret_cast<int*>(p);
+        s.aux2 = s.aux + NC;
+    };
     uint32_t* out = a.oct_out + f * a.geo.out_total + L.out_off;
     int* out_cnt = a.oct_cnt + f * a.geo.nlevels + level;
     long long* tm = nullptr;
@@ -1111,9 +1152,9 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
     OCT_MARK(tm, 0);
 
     // ---- 1. this level's key count (summed by the FAST kernel; reset for the next call)
-    if (tid == 0) s.scal[0] = a.level_keys[f * kMaxLevels + level];
+    if (tid == 0) scal[0] = a.level_keys[f * kMaxLevels + level];
     __syncthreads();
-    const int total = s.scal[0];
+    const int total = scal[0];
     if (tid == 0) a.level_keys[f * kMaxLevels + level] = 0;
     if (total == 0 || L.nini < 1) {
         if (tid == 0) *out_cnt = 0;
@@ -1124,7 +1165,9 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
     // ---- 2. compact the cell outputs into original key order (LDS when they fit): a thread
     // per cell copies the cell's keys to its scanned offset, loads batched 8 at a time
     const bool in_lds = total <= a.lds_keys;
-    uint32_t* K = in_lds ? s.keys : a.keys + f * a.geo.key_total + L.key_off;
+    uint32_t* lkeys = reinterpret_cast<uint32_t*>(region);  // LDS form: keys, node positions
+    short* lnode = reinterpret_cast<short*>(lkeys + a.lds_keys);
+    uint32_t* K = in_lds ? lkeys : a.keys + f * a.geo.key_total + L.key_off;
     const uint32_t* src = a.cell_keys + f * a.cell_cap_total;
     int nkeys = 0;
     // the first two chunks' counts and slots are loaded together (one global round trip for
@@ -1155,7 +1198,7 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
             slot = a.cells[c].slot;
         }
         int chunk_total;
-        const int off = nkeys + block_exclusive_scan<kOctBlock>(n, s.tmp, chunk_total);
+        const int off = nkeys + block_exclusive_scan<kOctBlock>(n, tmp, chunk_total);
         for (int i0 = 0; i0 < n; i0 += 8) {
             uint32_t v[8];
 #pragma unroll
@@ -1170,8 +1213,12 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
     __syncthreads();
     OCT_MARK(tm, 2);
     if (in_lds) {
-        octree_level(a, s, L, s.keys, s.node, nkeys, out, out_cnt, tm);
+        OctLds<uint16_t> s;
+        carve(s, reinterpret_cast<unsigned char*>(lnode + a.lds_keys));
+        octree_level(a, s, L, lkeys, lnode, nkeys, out, out_cnt, tm);
     } else {  // more keys than LDS holds: the same passes over global arrays
+        OctLds<int> s;
+        carve(s, region);
         int* node = reinterpret_cast<int*>(a.act) + (f * a.geo.key_total + L.key_off);
         octree_level(a, s, L, K, node, nkeys, out, out_cnt, tm);
     }
@@ -1408,6 +1455,10 @@ void blur_frags(const int taps[4], uint8_t out[128 * 16]) {
 //   3. per keypoint, lane k evaluates the rotated pattern pairs k + 64 r (pattern held packed
 //      in 4 registers across the group) and 4 ballots make the 256-bit descriptor.
 constexpr int kDescBlock = kDescBlockSize;
+#ifndef ORBFE_DESC_SKIP
+#define ORBFE_DESC_SKIP 0  // attribution experiments only (wrong descriptors): 1 blur passes,
+#endif                     // 2 IC, 4 samples, 8 window loads, 16 trig
+constexpr int kDescSkip = ORBFE_DESC_SKIP;
 constexpr int kDescGroupSmall = 2;  // small batches (single-frame latency): 4x the waves
 // the group's slot -> level lookup assumes a group spans at most two levels, which holds while
 // a group is no larger than the smallest per-level slot capacity (ncap >= 20)
@@ -1496,7 +1547,7 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
         for (int jb = 0; jb < kIcBatch; ++jb) {
             const int j = j0 + jb;
             px[jb] = make_uint4(0u, 0u, 0u, 0u);
-            if (((vmask >> j) & 1) && r < 31) {
+            if (!(kDescSkip & 2) && ((vmask >> j) & 1) && r < 31) {
                 const int kl = __builtin_amdgcn_readlane(my_l, j);
                 const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane(my_key, j);
                 const LevelPtr pp = a.pyr[kl];
@@ -1525,7 +1576,7 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
     const float angle = fast_atan2((float)M01, (float)M10);
     const float ang = angle * (float)(3.14159265358979323846 / 180.f);
     float ca = 1.f, sa = 0.f;
-    if (valid) {
+    if (valid && !(kDescSkip & 16)) {
         // one shared argument reduction (OCML's sin and cos are the two halves of its sincos)
         double sd, cd;
         sincos((double)ang, &sd, &cd);
@@ -1608,7 +1659,7 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
         for (int i = 0; i < 3; ++i) {
             const int c = lane + 64 * i, r = c / kRawQ, part = c - kRawQ * r;
             rv[i] = make_uint4(0u, 0u, 0u, 0u);
-            if (r >= kRawRows - 1) continue;
+            if (r >= kRawRows - 1 || (kDescSkip & 8)) continue;
             if (fast) {
                 rv[i] = load16_a4(fb + (long long)(y - 21 + r) * pp.pitch + x0 - 4 + 16 * part);
             } else {
@@ -1662,7 +1713,7 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
             if constexpr (kPre) load_win(__ffsll((long long)rest) - 1);
             else load_raw(__ffsll((long long)rest) - 1);
         }
-        if constexpr (!kPre) {
+        if constexpr (!kPre && !(kDescSkip & 1)) {
         // row pass: item (pair pr, quad q) -> window cols 4q..4q+3 of raw rows 2pr, 2pr+1.
         // Items it = lane + 64 i: (pr, q) advance by (6, 4) or, when q wraps, (7, -6), and the
         // raw offset with them (no division or multiply in the loop); (pr, q) sits at dword
@@ -1767,8 +1818,13 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
             // (__builtin_bit_cast of an ext-vector element reads element 0 in this clang:
             // go through __float_as_uint on copied scalars)
             const float r0y = r0.x, r0x = r0.y, r1y = r1.x, r1x = r1.y;
+            if constexpr (kDescSkip & 4) {
+                i0[q] = (int)(__float_as_uint(r0y) ^ __float_as_uint(r1x));
+                i1[q] = (int)(__float_as_uint(r1y) + kc);
+            } else {
             i0[q] = wb[__umul24(__float_as_uint(r0y), (uint32_t)kDescWinP) + __float_as_uint(r0x) + kc];
             i1[q] = wb[__umul24(__float_as_uint(r1y), (uint32_t)kDescWinP) + __float_as_uint(r1x) + kc];
+            }
         }
         unsigned long long words[4];
 #pragma unroll
@@ -1998,7 +2054,8 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
     }
     g.roi_rows = rmax;
     g.roi_pitch = (cmax + 3 + 15) & ~15;  // + alignment shift, 16-byte rows for b128 LDS writes
-    g.cand_max = (rmax - 6) * (cmax - 6);
+    // FAST survivor list: every candidate pixel up to kFastListCap, else flushed (fast_kernel)
+    g.cand_max = std::min((rmax - 6) * (cmax - 6), kFastListCap);
     // ROI + zero-bordered score plane at the ROI pitch + candidate list of u16 ROI offsets
     if ((long long)rmax * g.roi_pitch >= 65536) return ORBFE_ERR_UNSUPPORTED;
     g.fast_lds = (size_t)rmax * g.roi_pitch + (((rmax - 4) * g.roi_pitch + 15) & ~15) +
@@ -2008,17 +2065,18 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
     g.geo.out_total = out;
     g.slab = slab;
     g.ncap_max = ncap_max;
-    int sort_cap = 1;
-    while (sort_cap < ncap_max) sort_cap <<= 1;
-    g.sort_cap = sort_cap;
-    // LDS-resident keys per level: ~10x the largest level budget covers the FAST lists of
-    // textured frames (640x480 @1000: <= 1,900 keys per level; 1080p @2000: <= 3,300), at
-    // most kOctLdsKeys; a level with more runs on global arrays
+    // phase-2 sort keys: <= one per node (rank sort), 64 for the one-wave bitonic sort
+    g.sort_cap = std::max(ncap_max, 64);
+    // LDS-resident keys per level: ~9x the largest level budget covers the FAST lists of
+    // textured frames (640x480 @1000: <= 1,900 keys per level of 2,048; 1080p @2000: <= 3,300
+    // of 4,096), at most kOctLdsKeys; a level with more runs on global arrays.  At 640x480
+    // @1000 the carve is 26.8 KB (six trees per CU; 33.9 KB and four before the u16 node
+    // fields and the 10x key capacity)
     int nf_max = 0;
     for (int l = 0; l < L; ++l) nf_max = std::max(nf_max, g.geo.lv[l].nfeat);
-    g.oct_keys = std::min(kOctLdsKeys, std::max(1024, (10 * nf_max + 255) & ~255));
-    g.oct_lds = (size_t)2 * sort_cap * 4 + (size_t)g.oct_keys * 4 +
-                (size_t)ncap_max * 4 * (10 + 8 + 2) + 64 * 4 + 16 * 4 + (size_t)g.oct_keys * 2;
+    g.oct_keys = std::min(kOctLdsKeys, std::max(1024, (9 * nf_max + 255) & ~255));
+    g.oct_lds = std::max(oct_lds_bytes(true, ncap_max, g.sort_cap, g.oct_keys),
+                         oct_lds_bytes(false, ncap_max, g.sort_cap, g.oct_keys));
     return ORBFE_OK;
 }
 

@@ -212,6 +212,14 @@ template <int kDescGroup, bool kX86> __global__ void describe_kernel(DescArgs);
 extern __constant__ int c_umax[16];
 
 constexpr int kFastBlockSize = 64;
+// FAST survivor-list entries per cell (>= 322: a pre-test sweep adds <= 256 entries and a
+// flush keeps <= 66).  512 covers the ~22 % pre-test pass rate of textured cells without a
+// flush and brings the kernel's LDS to ~4.8 KB per wave (32 waves per CU, from ~25)
+#ifndef ORBFE_FAST_LIST
+#define ORBFE_FAST_LIST 512
+#endif
+constexpr int kFastListCap = ORBFE_FAST_LIST;
+static_assert(kFastListCap >= 322, "a FAST list flush must make progress");
 #ifndef ORBFE_OCT_BLOCK
 #define ORBFE_OCT_BLOCK 256  // 128: 248K, 256: 254K, 512: 243K, 1024: 220K frames/s (c3)
 #endif

@@ -1,0 +1,48 @@
+"""fast_kernel's bounded survivor list (orbfe_extract.hip K2): a cell's pre-test survivors are
+kept in a list of kFastListCap (512) entries; a sweep that could overflow it first scores the
+entries so far and emits those of rows whose 3x3 neighbourhoods are complete.  Frames where
+nearly every candidate pixel passes the pre-test (noise at a low threshold: ~992 candidates per
+31 x 32 cell) take that flush path many times per cell; the per-level FAST lists (order
+included) and the final keypoints / descriptors must stay the oracle's
+(ORBextractor.cc:764-831, cv::FAST with its 3x3 NMS)."""
+import numpy as np
+import pytest
+
+import oracle
+from orbslam_mapsave_amd.synth import synthetic_frame
+
+pytestmark = pytest.mark.gpu
+
+
+def noise_frame(seed, w, h):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    return rng.integers(0, 256, (h, w), dtype=np.uint8)
+
+
+def checker_frame(w, h, period):
+    y, x = np.mgrid[0:h, 0:w]
+    return np.where(((x // period) + (y // period)) % 2 == 0, 40, 215).astype(np.uint8)
+
+
+@pytest.mark.parametrize("kind,ini,mn", [("noise", 5, 3), ("noise", 20, 7), ("noise", 60, 1),
+                                         ("checker2", 7, 3), ("checker3", 20, 7),
+                                         ("textured", 1, 1)])
+def test_fast_lists_with_flushes(kind, ini, mn):
+    from orbslam_mapsave_amd.native import ORBextractor
+    w, h = 640, 480
+    if kind == "noise":
+        img = noise_frame(11, w, h)
+    elif kind.startswith("checker"):
+        img = checker_frame(w, h, int(kind[-1]))
+    else:
+        img = synthetic_frame(12, w, h)
+    p = oracle.params(1000, 1.2, 8, ini, mn)
+    ex = ORBextractor(1000, 1.2, 8, ini, mn, device=0)
+    kps, desc = ex(img)
+    okps, odesc = oracle.extract(p, img)
+    for lv, plane in enumerate(oracle.pyramid(p, img)):
+        assert np.array_equal(ex.get_fast_keys(lv), oracle.fast_keys(p, plane)), lv
+    assert len(kps) == len(okps)
+    assert kps.tobytes() == okps.tobytes()
+    assert np.array_equal(desc, odesc)
+    ex.close()

@@ -1,5 +1,5 @@
 """The oct-tree's global-array path (orbfe_extract.hip octree_kernel): a level whose FAST list
-holds more keys than the plan's LDS key capacity (oct_keys = min(4096, max(1024, 10 x the
+holds more keys than the plan's LDS key capacity (oct_keys = min(4096, max(1024, 9 x the
 largest level budget rounded up to 256)), orbfe_extract.hip plan) keeps its keys and node lists
 in global memory instead of LDS.  These frames are built so that such a level exists — asserted
 from the oracle's FAST lists before the GPU runs — and the extraction must stay bit-exact
@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 
 def oct_keys(p) -> int:
     nf = int(max(oracle.tables(p)["nfeat"]))
-    return min(4096, max(1024, (10 * nf + 255) & ~255))
+    return min(4096, max(1024, (9 * nf + 255) & ~255))
 
 
 def noise_frame(seed, w, h):
