@@ -176,6 +176,14 @@ struct orbfe_extractor {
     // K5 reading the blurred levels (ORBFE_PREBLUR=1: describe 0.30 -> 0.20 ms per 256 frames,
     // but the pass costs 0.19 ms; profiles/r02/experiments/preblur.json)
     bool fused_blur = std::getenv("ORBFE_PREBLUR") == nullptr;
+    // ORBFE_PREBLUR with ORBFE_PRE_MASK=<hex>: the describe reads blurred windows only for the
+    // levels in the mask and blurs the others per keypoint (experiments)
+    uint32_t pre_mask_env = std::getenv("ORBFE_PRE_MASK") ? (uint32_t)std::strtoul(std::getenv("ORBFE_PRE_MASK"), nullptr, 16) : 0xffffffffu;
+    // ORBFE_RESIZE_BLUR=1: levels made by per-level resize launches are blurred by them
+    // (resize_blur_kernel) and describe reads their blurred windows.  Bit-exact, but measured
+    // slower overall (resize +0.125 ms, describe -0.076 ms per 256 frames;
+    // profiles/r03/experiments/resize_blur.json), so off by default.
+    bool resize_blur = std::getenv("ORBFE_RESIZE_BLUR") && std::strcmp(std::getenv("ORBFE_RESIZE_BLUR"), "1") == 0;
     bool graph_broken = std::getenv("ORBFE_NO_GRAPH") != nullptr;  // capture failed once (or
                                  // disabled for A/B runs): keep to the launch path
 
@@ -313,6 +321,10 @@ struct orbfe_extractor {
         // top levels (tail_start ..) in one K1b launch, a workgroup per frame
         // (a batch of a few frames would leave most CUs idle in the tail: per-level launches)
         const int ts = n >= kTailMinFrames ? std::min(g.tail_start, L) : L;
+        // levels 1 .. ts-1 blurred with their resize (K1 + K4 fused) unless K4 runs as its own
+        // pass (PREBLUR) or ORBFE_RESIZE_BLUR=0
+        const bool rb = fused_blur && resize_blur;
+        uint32_t pre_mask = 0;
         for (int l = 1; l < ts; ++l) {
             ResizeArgs ra;
             ra.src = lp[l - 1];
@@ -326,12 +338,26 @@ struct orbfe_extractor {
             ra.xt = xtab.as<int>() + g.xoff[l];
             ra.yt = ytab.as<int>() + g.yoff[l];
             ra.simd_xb = x86() ? sse2_body_resize(ra.dw) : 0;
-            if (x86())
+            if (rb) {  // the level and its blur (describe reads this level's blurred windows)
+                ra.lds_pitch = g.rb_pitch[l];
+                ra.lds_e = g.rb_lds_e[l];
+                ra.bdst = bp[l];
+                ra.blur_xb = x86() ? sse2_body_blur(ra.dw) : 0;
+                for (int i = 0; i < 4; ++i) ra.taps[i] = tab.taps[i];
+                pre_mask |= 1u << l;
+                if (x86())
+                    ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resize_blur_kernel<true>, dim3(g.rs_tiles[l], n),
+                                 dim3(256), g.rb_lds[l], stream, ra);
+                else
+                    ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resize_blur_kernel<false>, dim3(g.rs_tiles[l], n),
+                                 dim3(256), g.rb_lds[l], stream, ra);
+            } else if (x86()) {
                 ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resize_kernel<true>, dim3(g.rs_tiles[l], n),
                              dim3(256), g.rs_lds[l], stream, ra);
-            else
+            } else {
                 ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resize_kernel<false>, dim3(g.rs_tiles[l], n),
                              dim3(256), g.rs_lds[l], stream, ra);
+            }
         }
         if (ts < L) {
             ResizeTailArgs ta;
@@ -437,13 +463,15 @@ struct orbfe_extractor {
         da.kps = d_kps;
         da.desc = d_desc;
         da.n_out = d_n;
+        const bool all_pre = !fused_blur && pre_mask_env == 0xffffffffu;
+        da.pre_mask = fused_blur ? pre_mask : pre_mask_env;
         // a wave takes kDescGroupSize keypoints (the trig and pattern loads amortised over the
         // group); small batches take kDescGroupSmall, for four times the waves in flight
         // (x86 arithmetic: the rotation FMA-contracted, kFma)
         const int group = n >= kDescSmallBatch ? kDescGroupSize : kDescGroupSmall;
         const int per_block = (kDescBlockSize / 64) * group;  // slots per workgroup
         const dim3 dgrid((g.geo.out_total + per_block - 1) / per_block, n);
-        const int variant = (group == kDescGroupSize ? 4 : 0) | (x86() ? 2 : 0) | (fused_blur ? 0 : 1);
+        const int variant = (group == kDescGroupSize ? 4 : 0) | (x86() ? 2 : 0) | (all_pre ? 1 : 0);
         switch (variant) {
 #define ORBFE_DESC_CASE(V, G, X, P) \
             case V: ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, (describe_kernel<G, X, P>), dgrid, dim3(kDescBlockSize), 0, stream, da); break;
@@ -1069,7 +1097,10 @@ int orbfe_get_blurred_level(orbfe_extractor* h, int frame, int level, uint8_t* o
     const Plan& g = h->plan;
     const LevelGeo& lv = g.geo.lv[level];
     LevelPtr bp{h->blur.as<uint8_t>() + lv.off, g.slab, lv.pitch};
-    if (out) {  // K4 on demand (the default extraction path blurs keypoint windows inside K5)
+    // K4 on demand (the default extraction path blurs level 0 and the tail levels inside K5);
+    // ORBFE_PROBE_AS_EXTRACTED=1 copies the slab as the extraction left it (the levels
+    // resize_blur_kernel made)
+    if (out && !std::getenv("ORBFE_PROBE_AS_EXTRACTED")) {
         DeviceGuard dg(h->device);
         BlurArgs ba;
         ba.nlevels = g.geo.nlevels;

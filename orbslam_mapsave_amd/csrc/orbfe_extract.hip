@@ -259,6 +259,251 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
     }
 }
 
+// Column-pass rounding.  The sums carry 0x7fff; the scalar FixedPtCastEx (sum + 2^15) >> 16
+// adds one more, the x86 SIMD body (H6: float sum, exact below 2^24, _mm_cvtps_epi32) rounds
+// half to even: (sum + 0x7fff + bit 16 of sum) >> 16.  v = sum + 0x7fff.
+__device__ __forceinline__ uint32_t blur_round_bit(uint32_t v, bool even) {
+    return even ? ((v - 0x7fffu) >> 16) & 1u : 1u;
+}
+
+// cv::borderInterpolate(p, len, BORDER_REFLECT_101) (App. A.2), any distance from the edge.
+__device__ __forceinline__ int reflect101(int p, int len) {
+    if (len == 1) return 0;
+    while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - p - 2;
+    return p;
+}
+__device__ __forceinline__ int reflect101_1(int p, int len) {  // |overshoot| < len - 1
+    return p < 0 ? -p : (p >= len ? 2 * len - 2 - p : p);
+}
+// K1 + K4 fused — the level's 128 x 32 tile AND its GaussianBlur (7x7, sigma 2, REFLECT_101,
+// ORBextractor.cc:1088-1089; K4's exact integer passes, App. A.2), so describe reads blurred
+// windows for this level instead of blurring one per keypoint.  The tile's resize outputs are
+// made for the rows / columns the blur reaches (3 beyond every edge, clipped to the level:
+// 1.24x the tile's resize work) into an LDS image E whose column 0 is level column ox - 4 and
+// row 0 level row oy - 3; positions outside the level are then copied from their reflect-101
+// images (which lie inside E: tiles are >= 4 px from the far edge's reflection).  Rows pass:
+// v_dot4 on dword-aligned E reads into u16 row pairs (the source staging region is dead by
+// then and holds them); columns pass: v_dot2 + 2^15 >> 16 saturated (x86: half to even on
+// the SIMD body, H6) straight to the blurred slab.  The level itself is written as by
+// resize_kernel.
+constexpr int kRbEP = 144;                 // E row pitch: level columns ox - 4 .. ox + 139
+constexpr int kRbERows = kRsTH + 8;        // E rows: oy - 3 .. oy + th + 2, + pad rows for pairs
+constexpr int kRbQ = kRsTW / 4 + 2;        // 34 column quads of E computed (ox - 4 .. ox + 131)
+constexpr int kRbPairs = (kRsTH + 6 + 1) / 2;  // 19 u16 row pairs of the rows pass
+constexpr int kRbRowpBytes = kRbPairs * (kRsTW / 4) * 16;
+template <bool kX86>
+__global__ __launch_bounds__(256) void resize_blur_kernel(ResizeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
+    int bx, f;
+    xcd_block(bx, f);
+    const int ox = (bx % a.tiles_x) * kRsTW, oy = (bx / a.tiles_x) * kRsTH;
+    const int ex = min(ox + kRsTW, a.dw) - 1, ey = min(oy + kRsTH, a.dh) - 1;
+    const int th = ey - oy + 1, tw = ex - ox + 1;
+    // the level rows / columns the blur reaches, clipped (their reflections lie inside)
+    const int er0 = max(oy - 3, 0), er1 = min(ey + 3, a.dh - 1);
+    const int ec0 = max(ox - 3, 0), ec1 = min(ex + 3, a.dw - 1);
+    const int sy0 = a.yt[3 * er0], sy1 = a.yt[3 * er1 + 1];
+    const int sx0 = a.xt[3 * ec0] & ~3, sx1 = a.xt[3 * ec1 + 1];
+    const int nrow = sy1 - sy0 + 1, P = a.lds_pitch;  // P % 16 == 0
+    const int cpr = ((sx1 - sx0) >> 4) + 1;
+    uint8_t* E = rs_lds + a.lds_e;                      // 16-byte aligned, kRbEP % 16 == 0
+    int* ys = reinterpret_cast<int*>(E + kRbERows * kRbEP);  // y tables of rows er0 .. er1
+    const uint8_t* src = a.src.base + f * a.src.fpitch;
+    const int nyt = 3 * (er1 - er0 + 1);
+    const int yv = threadIdx.x < nyt ? a.yt[3 * er0 + threadIdx.x] : 0;
+    if (threadIdx.x < nyt) ys[threadIdx.x] = yv;
+    const int total = nrow * cpr;
+    for (int base = 0; base < total; base += 4 * 256) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = base + 256 * u + (int)threadIdx.x;
+            if (i >= total) continue;
+            const int r = i / cpr, c = i - r * cpr;
+            const uint8_t* row = src + (long long)(sy0 + r) * a.src.pitch;
+            const int x = sx0 + 16 * c;
+            if (x + 16 <= a.sw) {
+                v[u] = load16_a4(row + x);
+            } else {
+                uint32_t w[4];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const int xd = x + 4 * d;
+                    w[d] = 0;
+                    if (xd + 4 <= a.sw) w[d] = *reinterpret_cast<const uint32_t*>(row + xd);
+                    else
+                        for (int q = 0; q < 4 && xd + q < a.sw; ++q) w[d] |= (uint32_t)row[xd + q] << (8 * q);
+                }
+                v[u] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = base + 256 * u + (int)threadIdx.x;
+            if (i >= total) continue;
+            const int r = i / cpr, c = i - r * cpr;
+            *reinterpret_cast<uint4*>(rs_lds + r * P + 16 * c) = v[u];
+        }
+    }
+    __syncthreads();
+    // resize outputs: thread -> (E quad k, row phase rp); quads 1 .. 32 are the tile's columns
+    uint8_t* dst = const_cast<uint8_t*>(a.dst.base) + f * a.dst.fpitch;
+    if (threadIdx.x < kRbQ * 7) {
+        const int k = threadIdx.x % kRbQ, rp = threadIdx.x / kRbQ;
+        const int x = ox - 4 + 4 * k;  // level column of the quad's byte 0
+        int x0[4], x1[4], a0[4], a1[4];
+        bool in[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            in[q] = x + q >= ec0 && x + q <= ec1;
+            const int dx = min(max(x + q, 0), a.dw - 1);
+            x0[q] = a.xt[3 * dx] - sx0;
+            x1[q] = a.xt[3 * dx + 1] - sx0;
+            const int aa = a.xt[3 * dx + 2];
+            a0[q] = aa & 0xffff;
+            a1[q] = (int)((unsigned)aa >> 16);
+        }
+        const bool tile_col = k >= 1 && k <= kRsTW / 4 && x < a.dw;
+        const int n = min(4, a.dw - x);
+        if (in[0] || in[1] || in[2] || in[3]) {
+#pragma unroll
+            for (int j = 0; j < (kRsTH + 6 + 6) / 7; ++j) {
+                const int y = er0 + rp + 7 * j;
+                if (y > er1) break;
+                const int* yy = ys + 3 * (y - er0);
+                const int ry0 = yy[0] - sy0, ry1 = yy[1] - sy0, bb = yy[2];
+                const int b0 = bb & 0xffff, b1 = (int)((unsigned)bb >> 16);
+                const uint8_t* s0 = rs_lds + ry0 * P;
+                const uint8_t* s1 = rs_lds + ry1 * P;
+                uint32_t packed = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (!in[q]) continue;
+                    const uint32_t t0 = __umul24(s0[x0[q]], a0[q]) + __umul24(s0[x1[q]], a1[q]);
+                    const uint32_t t1 = __umul24(s1[x0[q]], a0[q]) + __umul24(s1[x1[q]], a1[q]);
+                    packed |= resize_px<kX86>(t0, t1, b0, b1, x + q < a.simd_xb) << (8 * q);
+                }
+                *reinterpret_cast<uint32_t*>(E + (y - oy + 3) * kRbEP + 4 * k) = packed;
+                if (tile_col && y >= oy && y <= ey) {
+                    uint8_t* d = dst + (long long)y * a.dst.pitch + x;
+                    if (n >= 4) {
+                        *reinterpret_cast<uint32_t*>(d) = packed;
+                    } else {
+                        for (int q = 0; q < n; ++q) d[q] = (uint8_t)(packed >> (8 * q));
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // border tiles: E positions outside the level take their reflect-101 images
+    // (the strips: 3 rows above / below the tile across its width + 6, 3 columns left / right
+    // across its height + 6; corners are written by both with the same in-level image)
+    if (oy < 3 || ey + 3 >= a.dh || ox < 3 || ex + 3 >= a.dw) {
+        const int er = th + 6, ecn = tw + 6;
+        auto fix = [&](int r, int c) {
+            const int y = oy - 3 + r, x = ox - 3 + c;
+            if (y >= 0 && y < a.dh && x >= 0 && x < a.dw) return;
+            const int yr = reflect101_1(y, a.dh), xr = reflect101_1(x, a.dw);
+            E[r * kRbEP + c + 1] = E[(yr - oy + 3) * kRbEP + (xr - ox + 4)];
+        };
+        for (int c = threadIdx.x; c < ecn; c += 256) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                fix(r, c);
+                fix(er - 1 - r, c);
+            }
+        }
+        for (int r = threadIdx.x; r < er; r += 256) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                fix(r, c);
+                fix(r, ecn - 1 - c);
+            }
+        }
+        __syncthreads();
+    }
+    // rows pass: item (pair pr, quad q) -> E rows 2pr, 2pr + 1, output columns 4q .. 4q + 3
+    uint32_t* rowp = reinterpret_cast<uint32_t*>(rs_lds);
+    const uint32_t KLO = (uint32_t)(a.taps[0] | (a.taps[1] << 8) | (a.taps[2] << 16) | (a.taps[3] << 24));
+    const uint32_t KHI = (uint32_t)(a.taps[2] | (a.taps[1] << 8) | (a.taps[0] << 16));
+    const int npairs = (th + 7) >> 1, nq = (tw + 3) >> 2;
+#pragma unroll
+    for (int u = 0; u < (kRbPairs * (kRsTW / 4) + 255) / 256; ++u) {
+        const int it = threadIdx.x + 256 * u;
+        const int pr = it >> 5, q = it & 31;
+        if (pr >= npairs || q >= nq) continue;
+        uint32_t hh[2][4];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const uint32_t* row = reinterpret_cast<const uint32_t*>(E + (2 * pr + e) * kRbEP + 4 * q);
+            const uint32_t w0 = row[0], w1 = row[1], w2 = row[2];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                const uint32_t lo = jj < 3 ? __builtin_amdgcn_alignbyte(w1, w0, jj + 1) : w1;
+                const uint32_t hi = jj < 3 ? __builtin_amdgcn_alignbyte(w2, w1, jj + 1) : w2;
+                hh[e][jj] = __builtin_amdgcn_udot4(hi, KHI, __builtin_amdgcn_udot4(lo, KLO, 0u, false), false);
+            }
+        }
+        *reinterpret_cast<uint4*>(rowp + 4 * it) =
+            make_uint4(__builtin_amdgcn_perm(hh[1][0], hh[0][0], 0x05040100u),
+                       __builtin_amdgcn_perm(hh[1][1], hh[0][1], 0x05040100u),
+                       __builtin_amdgcn_perm(hh[1][2], hh[0][2], 0x05040100u),
+                       __builtin_amdgcn_perm(hh[1][3], hh[0][3], 0x05040100u));
+    }
+    __syncthreads();
+    // columns pass: item (output rows 2jp, 2jp + 1; quad q) from pairs jp .. jp + 3
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    const unsigned short k0 = (unsigned short)a.taps[0], k1 = (unsigned short)a.taps[1],
+                         k2 = (unsigned short)a.taps[2], k3 = (unsigned short)a.taps[3];
+    const us2 T01 = us2{k0, k1}, T23 = us2{k2, k3}, T21 = us2{k2, k1}, T0L = us2{k0, 0},
+              T0H = us2{0, k0}, T12 = us2{k1, k2}, T32 = us2{k3, k2}, T10 = us2{k1, k0};
+    constexpr uint32_t kRnd = kX86 ? 0x7fffu : 0x8000u;
+    uint8_t* bdst = const_cast<uint8_t*>(a.bdst.base) + f * a.bdst.fpitch;
+#pragma unroll
+    for (int u = 0; u < (kRsTH / 2) * (kRsTW / 4) / 256; ++u) {
+        const int it = threadIdx.x + 256 * u;
+        const int jp = it >> 5, q = it & 31;
+        if (2 * jp >= th || q >= nq) continue;
+        const int x = ox + 4 * q;
+        const bool even = x < a.blur_xb;
+        uint4 P4[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) P4[i] = *reinterpret_cast<const uint4*>(rowp + 4 * (it + i * (kRsTW / 4)));
+        uint32_t ev[4], od[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t p0 = (&P4[0].x)[c], p1 = (&P4[1].x)[c], p2 = (&P4[2].x)[c], p3 = (&P4[3].x)[c];
+            uint32_t v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T01, kRnd, false);
+            v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), T23, v, false);
+            v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), T21, v, false);
+            v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), T0L, v, false);
+            if constexpr (kX86) v += blur_round_bit(v, even);
+            ev[c] = min(v, 0xffffffu);  // byte 2 = min(acc >> 16, 255)
+            uint32_t u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T0H, kRnd, false);
+            u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), T12, u, false);
+            u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), T32, u, false);
+            u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), T10, u, false);
+            if constexpr (kX86) u += blur_round_bit(u, even);
+            od[c] = min(u, 0xffffffu);
+        }
+        const uint32_t pe = __builtin_amdgcn_perm(ev[1], ev[0], 0x0c0c0602u) | __builtin_amdgcn_perm(ev[3], ev[2], 0x06020c0cu);
+        const uint32_t po = __builtin_amdgcn_perm(od[1], od[0], 0x0c0c0602u) | __builtin_amdgcn_perm(od[3], od[2], 0x06020c0cu);
+        const int y = oy + 2 * jp, n = min(4, a.dw - x);
+        uint8_t* d = bdst + (long long)y * a.bdst.pitch + x;
+        if (n == 4) {
+            *reinterpret_cast<uint32_t*>(d) = pe;
+            if (y + 1 <= ey) *reinterpret_cast<uint32_t*>(d + a.bdst.pitch) = po;
+        } else {
+            for (int i = 0; i < n; ++i) d[i] = (uint8_t)(pe >> (8 * i));
+            if (y + 1 <= ey)
+                for (int i = 0; i < n; ++i) d[a.bdst.pitch + i] = (uint8_t)(po >> (8 * i));
+        }
+    }
+}
+template __global__ void resize_blur_kernel<false>(ResizeArgs);
+template __global__ void resize_blur_kernel<true>(ResizeArgs);
+
 // K1b — the small top levels in one launch: one 1024-thread workgroup per frame copies level
 // ts-1 into LDS, then makes levels ts .. L-1 one after the other, each from the previous one
 // held in LDS (two buffers, ping-pong), writing every level to the pyramid as well.  Same
@@ -1225,19 +1470,6 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Column-pass rounding.  The sums carry 0x7fff; the scalar FixedPtCastEx (sum + 2^15) >> 16
-// adds one more, the x86 SIMD body (H6: float sum, exact below 2^24, _mm_cvtps_epi32) rounds
-// half to even: (sum + 0x7fff + bit 16 of sum) >> 16.  v = sum + 0x7fff.
-__device__ __forceinline__ uint32_t blur_round_bit(uint32_t v, bool even) {
-    return even ? ((v - 0x7fffu) >> 16) & 1u : 1u;
-}
-
-// cv::borderInterpolate(p, len, BORDER_REFLECT_101) (App. A.2), any distance from the edge.
-__device__ __forceinline__ int reflect101(int p, int len) {
-    if (len == 1) return 0;
-    while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - p - 2;
-    return p;
-}
 // K4 — GaussianBlur(7x7, sigma 2, REFLECT_101), integer path (App. A.2): row pass R = sum k_i I
 // (<= 65535, exact in u16), column pass (sum k_j R + 2^15) >> 16 saturated; x86 mode rounds the
 // SIMD body half to even (H6).  Both passes are banded integer GEMMs on the i8 matrix cores:
@@ -1263,9 +1495,6 @@ constexpr int kBlurInQ = 7;                   // 16-byte input chunks per row: X
 constexpr int kBlurInP = 104;                 // LDS input row (columns X0 - 3 .. X0 + 100 are
                                               // read; 26 dwords: 2-way bank aliasing at most)
 constexpr int kBlurOutP = 100;                // LDS output row (25 dwords: conflict-free)
-__device__ __forceinline__ int reflect101_1(int p, int len) {  // |overshoot| < len - 1
-    return p < 0 ? -p : (p >= len ? 2 * len - 2 - p : p);
-}
 typedef int i32x4b __attribute__((ext_vector_type(4)));
 typedef int i32x16b __attribute__((ext_vector_type(16)));
 template <bool kX86>
@@ -1689,11 +1918,25 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
             if (r < kDescWinRows) rv[i] = load16_a4(fb + (long long)r * bp.pitch + 16 * part);
         }
     };
-    if constexpr (kPre) load_win(__ffsll((long long)vmask) - 1);
-    else load_raw(__ffsll((long long)vmask) - 1);
+    // a keypoint of a level whose bit is set in pre_mask reads its blurred window (the level
+    // was blurred by the pyramid kernels); the others blur a raw window here.  The choice is
+    // wave-uniform per keypoint.
+    auto is_pre = [&](int j) {
+        return kPre || ((a.pre_mask >> __builtin_amdgcn_readlane(my_l, j)) & 1u) != 0u;
+    };
+    auto load_kp = [&](int j) {
+        if (is_pre(j)) {
+            load_win(j);
+            rv[2] = make_uint4(0u, 0u, 0u, 0u);
+        } else {
+            load_raw(j);
+        }
+    };
+    load_kp(__ffsll((long long)vmask) - 1);
     for (unsigned long long m = vmask; m; m &= m - 1) {
         const int j = __ffsll((long long)m) - 1;
-        if constexpr (kPre) {
+        const bool pre_j = is_pre(j);
+        if (pre_j) {
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 const int c = lane + 64 * i;
@@ -1709,11 +1952,8 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         const unsigned long long rest = m & (m - 1);
-        if (rest) {  // next keypoint's window in flight
-            if constexpr (kPre) load_win(__ffsll((long long)rest) - 1);
-            else load_raw(__ffsll((long long)rest) - 1);
-        }
-        if constexpr (!kPre && !(kDescSkip & 1)) {
+        if (rest) load_kp(__ffsll((long long)rest) - 1);  // next keypoint's window in flight
+        if (!kPre && !(kDescSkip & 1) && !pre_j) {
         // row pass: item (pair pr, quad q) -> window cols 4q..4q+3 of raw rows 2pr, 2pr+1.
         // Items it = lane + 64 i: (pr, q) advance by (6, 4) or, when q wraps, (7, -6), and the
         // raw offset with them (no division or multiply in the loop); (pr, q) sits at dword
@@ -2015,6 +2255,25 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
                     const int ex = std::min(ox + kRsTW, dw) - 1;
                     const int a0 = g.xtab[xb + 3 * ox] & ~3, a1 = g.xtab[xb + 3 * ex + 1];
                     need_w = std::max(need_w, ((a1 - a0) >> 2) + 1);
+                }
+                {   // resize_blur_kernel: the source of the rows / columns 3 beyond the tile
+                    int rb_rows = 0, rb_w = 0;
+                    for (int oy = 0; oy < dh; oy += kRsTH) {
+                        const int e0 = std::max(oy - 3, 0), e1 = std::min(std::min(oy + kRsTH, dh) - 1 + 3, dh - 1);
+                        auto sy = [&](int dy) { return (int)std::floor((float)((dy + 0.5) * scale_y - 0.5)); };
+                        const int r0 = std::min(std::max(sy(e0), 0), sh - 1), r1 = std::min(std::max(sy(e1) + 1, 0), sh - 1);
+                        rb_rows = std::max(rb_rows, r1 - r0 + 1);
+                    }
+                    for (int ox = 0; ox < dw; ox += kRsTW) {
+                        const int e0 = std::max(ox - 3, 0), e1 = std::min(std::min(ox + kRsTW, dw) - 1 + 3, dw - 1);
+                        const int a0 = g.xtab[xb + 3 * e0] & ~3, a1 = g.xtab[xb + 3 * e1 + 1];
+                        rb_w = std::max(rb_w, ((a1 - a0) >> 2) + 1);
+                    }
+                    g.rb_pitch[l] = 16 * ((rb_w + 3) / 4);
+                    const size_t stage = std::max((size_t)rb_rows * g.rb_pitch[l], (size_t)kRbRowpBytes);
+                    g.rb_lds_e[l] = (int)((stage + 15) & ~(size_t)15);
+                    g.rb_lds[l] = (size_t)g.rb_lds_e[l] + (size_t)kRbERows * kRbEP + 3 * (kRsTH + 6) * sizeof(int);
+                    if (g.rb_lds[l] > 64 * 1024) return ORBFE_ERR_UNSUPPORTED;
                 }
                 g.rs_tiles_x[l] = (dw + kRsTW - 1) / kRsTW;
                 g.rs_tiles[l] = g.rs_tiles_x[l] * ((dh + kRsTH - 1) / kRsTH);

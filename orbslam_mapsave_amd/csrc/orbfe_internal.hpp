@@ -76,6 +76,11 @@ struct ResizeArgs {
     const int* xt;
     const int* yt;
     int simd_xb;           // x86 arithmetic: columns [0, simd_xb) use the SSE2 rounding (H5)
+    // resize_blur_kernel: the blurred level, its x86 SIMD-body bound (H6), taps, LDS offset of E
+    LevelPtr bdst;
+    int blur_xb;
+    int taps[4];
+    int lds_e;
 };
 
 struct ResizeTailArgs {
@@ -146,6 +151,7 @@ struct DescArgs {
     int32_t* n_out;
     int simd_xb[kMaxLevels];  // as BlurArgs::simd_xb, for the fused per-keypoint blur
     LevelPtr blur[kMaxLevels];  // blurred levels (K4 output), read by the pre-blurred variant
+    uint32_t pre_mask;          // levels whose blurred plane exists (bit l): windows read from it
 };
 
 // Pixels [0, n) of a w-pixel row that OpenCV 3.3's x86 SSE2 vertical kernels produce (the rest
@@ -191,6 +197,9 @@ struct Plan {
     size_t fast_lds = 0;
     int rs_tiles_x[kMaxLevels] = {}, rs_tiles[kMaxLevels] = {}, rs_pitch[kMaxLevels] = {};
     size_t rs_lds[kMaxLevels] = {};
+    // resize_blur_kernel: staging pitch / LDS bytes, offset of its E image
+    int rb_pitch[kMaxLevels] = {}, rb_lds_e[kMaxLevels] = {};
+    size_t rb_lds[kMaxLevels] = {};
     int tail_start = kMaxLevels;  // levels >= tail_start come from resize_tail_kernel
 };
 
@@ -201,6 +210,7 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g);
 __global__ void level0_kernel(Level0Args);
 template <bool kX86> __global__ void resize_kernel(ResizeArgs);
 template <bool kX86> __global__ void resize_tail_kernel(ResizeTailArgs);
+template <bool kX86> __global__ void resize_blur_kernel(ResizeArgs);
 template <int kP> __global__ void fast_kernel(FastArgs);
 constexpr int kFastPitch = 48;  // fast_kernel<kFastPitch>: ROI pitch known at compile time
 __global__ void octree_kernel(OctArgs);
