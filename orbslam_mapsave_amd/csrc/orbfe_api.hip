@@ -129,7 +129,7 @@ struct orbfe_extractor {
     Plan plan;
     bool planned = false;
     int frames_cap = 0;
-    DevBuf cells, xtab, ytab, bslot;
+    DevBuf cells, xtab, ytab, bslot, ptab;
     DevBuf pyr, blur, cell_cnt, cell_keys, keys, act, oct_out, oct_cnt, level_keys;
     DevBuf out_kps, out_desc, out_n;  // staging for the host-pointer entry points
     DevBuf stage, rects;              // host colour frames / rectangle masks (level-0 inputs)
@@ -184,6 +184,11 @@ struct orbfe_extractor {
     // slower overall (resize +0.125 ms, describe -0.076 ms per 256 frames;
     // profiles/r03/experiments/resize_blur.json), so off by default.
     bool resize_blur = std::getenv("ORBFE_RESIZE_BLUR") && std::strcmp(std::getenv("ORBFE_RESIZE_BLUR"), "1") == 0;
+    // the pyramid in one launch (pyramid_kernel); ORBFE_PYR=0: per-level resize launches + the
+    // one-workgroup tail
+    bool use_pyr = !(std::getenv("ORBFE_PYR") && std::strcmp(std::getenv("ORBFE_PYR"), "0") == 0);
+    // ORBFE_PYR=2: the band kernel even where its plan recomputes many seam rows (tests, A/B)
+    bool force_pyr = std::getenv("ORBFE_PYR") && std::strcmp(std::getenv("ORBFE_PYR"), "2") == 0;
     bool graph_broken = std::getenv("ORBFE_NO_GRAPH") != nullptr;  // capture failed once (or
                                  // disabled for A/B runs): keep to the launch path
 
@@ -263,6 +268,17 @@ struct orbfe_extractor {
         if ((st = xtab.ensure(std::max<size_t>(1, g.xtab.size()) * sizeof(int)))) return st;
         if ((st = ytab.ensure(std::max<size_t>(1, g.ytab.size()) * sizeof(int)))) return st;
         if ((st = bslot.ensure(kBlurFragBytes + g.bitems.size() * sizeof(uint32_t)))) return st;
+        if ((st = ptab.ensure(std::max<size_t>(16, g.ptab.size() * sizeof(uint32_t))))) return st;
+        if (!g.ptab.empty())
+            ORBFE_HIP(hipMemcpyAsync(ptab.p, g.ptab.data(), g.ptab.size() * sizeof(uint32_t),
+                                     hipMemcpyHostToDevice, stream));
+        if (g.pyr_ok) {  // dynamic LDS above 64 KB must be allowed per kernel
+            const int mx = (int)std::max(g.pyr_lds[0], g.pyr_lds[1]);
+            hipFuncSetAttribute(reinterpret_cast<const void*>(&pyramid_kernel<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+            hipFuncSetAttribute(reinterpret_cast<const void*>(&pyramid_kernel<true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        }
         ORBFE_HIP(hipMemcpyAsync(cells.p, g.cells.data(), g.cells.size() * sizeof(CellDesc),
                                  hipMemcpyHostToDevice, stream));
         ORBFE_HIP(hipMemcpyAsync(xtab.p, g.xtab.data(), g.xtab.size() * sizeof(int),
@@ -325,7 +341,33 @@ struct orbfe_extractor {
         // pass (PREBLUR) or ORBFE_RESIZE_BLUR=0
         const bool rb = fused_blur && resize_blur;
         uint32_t pre_mask = 0;
-        for (int l = 1; l < ts; ++l) {
+        // K1 as one launch (pyramid_kernel): every level of a band of every frame in LDS
+        const int which = n >= kTailMinFrames ? 0 : 1;
+        const bool one_pyr = g.pyr_ok && (g.pyr_use[which] || force_pyr) && !rb && use_pyr && L >= 2;
+        if (one_pyr) {
+            PyrArgs pa;
+            pa.src = lp[0];
+            pa.nlevels = L;
+            for (int l = 0; l < L; ++l) {
+                pa.dst[l] = lp[l];
+                pa.w[l] = g.geo.lv[l].w;
+                pa.lp[l] = g.pyr_lp[l];
+                pa.gtab[l] = ptab.as<uint4>() + g.gtab_off[l];
+                pa.yt[l] = ytab.as<int>() + g.yoff[l];
+                pa.simd_xb[l] = x86() ? sse2_body_resize(pa.w[l]) : 0;
+            }
+            pa.buf_b = g.pyr_bufb[which];
+            pa.ybuf = g.pyr_ybuf[which];
+            pa.ymax = g.pyr_ymax[which];
+            pa.bands = reinterpret_cast<const int4*>(ptab.as<uint4>() + g.band_off[which]);
+            if (x86())
+                ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, pyramid_kernel<true>, dim3(g.nbands[which], n),
+                             dim3(kPyrBlockSize), g.pyr_lds[which], stream, pa);
+            else
+                ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, pyramid_kernel<false>, dim3(g.nbands[which], n),
+                             dim3(kPyrBlockSize), g.pyr_lds[which], stream, pa);
+        }
+        for (int l = 1; l < (one_pyr ? 1 : ts); ++l) {
             ResizeArgs ra;
             ra.src = lp[l - 1];
             ra.dst = lp[l];
@@ -359,7 +401,7 @@ struct orbfe_extractor {
                              dim3(256), g.rs_lds[l], stream, ra);
             }
         }
-        if (ts < L) {
+        if (!one_pyr && ts < L) {
             ResizeTailArgs ta;
             ta.src = lp[ts - 1];
             ta.sh = g.geo.lv[ts - 1].h;
@@ -595,7 +637,7 @@ struct orbfe_extractor {
     }
 
     ~orbfe_extractor() {
-        for (DevBuf* b : {&cells, &xtab, &ytab, &bslot, &pyr, &blur, &cell_cnt, &cell_keys, &keys, &act,
+        for (DevBuf* b : {&cells, &xtab, &ytab, &bslot, &ptab, &pyr, &blur, &cell_cnt, &cell_keys, &keys, &act,
                           &oct_out, &oct_cnt, &level_keys, &out_kps, &out_desc, &out_n, &stage, &rects, &st_off, &st_items,
                           &st_sad, &st_status, &st_kl, &st_dl, &st_kr, &st_dr, &st_n, &st_ur, &st_dp})
             b->release();

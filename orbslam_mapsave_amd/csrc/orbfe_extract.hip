@@ -504,6 +504,167 @@ __global__ __launch_bounds__(256) void resize_blur_kernel(ResizeArgs a) {
 template __global__ void resize_blur_kernel<false>(ResizeArgs);
 template __global__ void resize_blur_kernel<true>(ResizeArgs);
 
+// K1 as one launch — the whole pyramid of a horizontal band of every frame per workgroup.
+// The host partitions every level's rows into nbands bands (proportionally) and derives, top
+// level down, the rows each band must COMPUTE at each level: its own rows plus the source rows
+// its rows of the level above read (a few rows of halo, recomputed by the neighbouring band).
+// The workgroup stages its level-0 rows in LDS, then makes level 1 .. L-1 one after the other,
+// each from the previous one held in LDS (two buffers, ping-pong; every level's y-table rows
+// staged beside them), writing only its own rows of each level to the pyramid.  So the levels
+// never make a round trip through HBM between launches and one launch replaces nlevels - 1.
+// Horizontal pass (App. A.1): a thread makes 4 output pixels of a row, whose source columns
+// x0[k], x1[k] lie in 8 bytes from x0[0] (checked on the host for the plan's scale factor): 3
+// dword LDS reads per source row, two v_alignbyte make the 8-byte window, one v_perm per pixel
+// pairs its two source bytes as u16 and v_dot2 applies (a0, a1) — instead of 4 byte gathers,
+// 2 multiplies and an add per pixel.  Vertical pass and rounding: resize_px, as resize_kernel.
+constexpr int kPyrBlock = kPyrBlockSize;
+#ifndef ORBFE_PYR_ROWS
+#define ORBFE_PYR_ROWS 1  // 2 and 4 measured no faster (profiles/r03/experiments/pyramid.json)
+#endif
+constexpr int kPyrRows = ORBFE_PYR_ROWS;
+template <bool kX86>
+__global__ __launch_bounds__(kPyrBlock) void pyramid_kernel(PyrArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char py_lds[];
+    const int band = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    const int L = a.nlevels;
+    const int4* bt = a.bands + band * L;
+    // (LDS addresses by offset arithmetic from py_lds: a pointer picked from an array would be
+    // a generic pointer, and every access a flat instruction)
+    {   // level 0 rows c0 .. c1 -> buf[0] (16-byte chunks; a chunk past the row end is assembled
+        // from dwords / bytes: level 0 may be the caller's buffer)
+        const int4 b0 = bt[0];
+        const int w = a.w[0], P = a.lp[0];
+        const uint8_t* src = a.src.base + f * a.src.fpitch;
+        const int cpr = (w + 15) >> 4, total = (b0.y - b0.x + 1) * cpr;
+        for (int base = 0; base < total; base += 4 * kPyrBlock) {
+            uint4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = base + kPyrBlock * u + tid;
+                if (i >= total) continue;
+                const int r = i / cpr, c = i - r * cpr;
+                const uint8_t* row = src + (long long)(b0.x + r) * a.src.pitch;
+                const int x = 16 * c;
+                if (x + 16 <= w) {
+                    v[u] = load16_a4(row + x);
+                } else {
+                    uint32_t wd[4];
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) {
+                        const int xd = x + 4 * d;
+                        wd[d] = 0;
+                        if (xd + 4 <= w) wd[d] = *reinterpret_cast<const uint32_t*>(row + xd);
+                        else
+                            for (int q = 0; q < 4 && xd + q < w; ++q) wd[d] |= (uint32_t)row[xd + q] << (8 * q);
+                    }
+                    v[u] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = base + kPyrBlock * u + tid;
+                if (i >= total) continue;
+                const int r = i / cpr, c = i - r * cpr;
+                *reinterpret_cast<uint4*>(py_lds + r * P + 16 * c) = v[u];
+            }
+        }
+    }
+    for (int l = 1; l < L; ++l) {
+        const int4 bs = bt[l - 1], bl = bt[l];
+        const int nrows = bl.y - bl.x + 1;  // may be 0 for a thin band of a small level
+        const int w = a.w[l], gpr = (w + 3) >> 2, rps = kPyrBlock / gpr;
+        const int gx = tid % gpr, ry = tid / gpr;
+        // this level's y-table rows, and the thread's column group (issued before the barrier)
+        int* yb = reinterpret_cast<int*>(py_lds + a.ybuf) + ((l & 1) ? 3 * a.ymax : 0);
+        for (int i = tid; i < 3 * nrows; i += kPyrBlock) yb[i] = a.yt[l][3 * bl.x + i];
+        uint4 g0 = make_uint4(0u, 0u, 0u, 0u), g1 = g0, g2 = g0;
+        if (ry < rps && nrows > 0) {
+            const uint4* gp = a.gtab[l] + 3 * gx;
+            g0 = gp[0];
+            g1 = gp[1];
+            g2 = gp[2];
+        }
+        __syncthreads();
+        if (ry >= rps || nrows <= 0) continue;
+        const uint8_t* s = py_lds + (((l - 1) & 1) ? a.buf_b : 0);
+        uint8_t* d = py_lds + ((l & 1) ? a.buf_b : 0);
+        const int sp = a.lp[l - 1], dpitch = a.lp[l];
+        const int xbase = (int)g0.x, wofs = (xbase >> 2) << 2, sh = xbase & 3;
+        const uint32_t sel[4] = {g0.y, g0.z, g0.w, g1.x};
+        typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+        const us2 cf[4] = {__builtin_bit_cast(us2, g1.y), __builtin_bit_cast(us2, g1.z),
+                           __builtin_bit_cast(us2, g1.w), __builtin_bit_cast(us2, g2.x)};
+        const int x = 4 * gx, n = min(4, w - x);
+        const int xb = a.simd_xb[l];
+        const LevelPtr dp = a.dst[l];
+        uint8_t* dst = const_cast<uint8_t*>(dp.base) + f * dp.fpitch;
+        auto hsum = [&](int r, uint32_t (&t)[4]) {  // horizontal sums of source row r (LDS row)
+            const uint32_t* row = reinterpret_cast<const uint32_t*>(s + r * sp + wofs);
+            const uint32_t w0 = row[0], w1 = row[1], w2 = row[2];
+            const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh), hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                t[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(hi, lo, sel[k])), cf[k], 0u, false);
+        };
+        auto row_out = [&](int r) {
+            const int* yy = yb + 3 * (r - bl.x);
+            const int bb = yy[2];
+            const uint32_t b0 = (uint32_t)bb & 0xffffu, b1 = (uint32_t)bb >> 16;
+            uint32_t t0[4], t1[4];
+            hsum(yy[0] - bs.x, t0);
+            hsum(yy[1] - bs.x, t1);
+            uint32_t packed = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) packed |= resize_px<kX86>(t0[k], t1[k], b0, b1, x + k < xb) << (8 * k);
+            *reinterpret_cast<uint32_t*>(d + (r - bl.x) * dpitch + x) = packed;
+            if (r >= bl.z && r < bl.w) {
+                uint8_t* o = dst + (long long)r * dp.pitch + x;
+                if (n == 4) {
+                    *reinterpret_cast<uint32_t*>(o) = packed;
+                } else {
+                    for (int k = 0; k < n; ++k) o[k] = (uint8_t)(packed >> (8 * k));
+                }
+            }
+        };
+        // kPyrRows rows per iteration: their LDS reads are issued together
+        int r = bl.x + ry;
+        for (; r + (kPyrRows - 1) * rps <= bl.y; r += kPyrRows * rps) {
+#pragma unroll
+            for (int j = 0; j < kPyrRows; ++j) row_out(r + j * rps);
+        }
+        for (; r <= bl.y; r += rps) row_out(r);
+    }
+}
+template __global__ void pyramid_kernel<false>(PyrArgs);
+template __global__ void pyramid_kernel<true>(PyrArgs);
+
+// Host: pyramid_kernel's per-level column-group tables (3 uint4 per group of 4 output columns:
+// x0[0], the 4 perm selectors pairing bytes x0[k] - x0[0], x1[k] - x0[0] as u16 (0x0c = zero),
+// the 4 (a0 | a1 << 16) coefficient pairs).  False when a group's source bytes do not fit 8
+// bytes from x0[0] (scale factors well above 1.2): the per-level kernels are used instead.
+static bool pyramid_group_table(const std::vector<int>& xtab, int xoff, int dw, std::vector<uint32_t>& out) {
+    for (int gx = 0; gx < (dw + 3) / 4; ++gx) {
+        uint32_t e[12] = {};
+        int x0[4], x1[4], c[4];
+        for (int k = 0; k < 4; ++k) {
+            const int dx = std::min(4 * gx + k, dw - 1);
+            x0[k] = xtab[xoff + 3 * dx];
+            x1[k] = xtab[xoff + 3 * dx + 1];
+            c[k] = xtab[xoff + 3 * dx + 2];
+        }
+        e[0] = (uint32_t)x0[0];
+        for (int k = 0; k < 4; ++k) {
+            const int o0 = x0[k] - x0[0], o1 = x1[k] - x0[0];
+            if (o0 < 0 || o1 < 0 || o0 > 7 || o1 > 7) return false;
+            const uint32_t sv = (uint32_t)o0 | (0x0cu << 8) | ((uint32_t)o1 << 16) | (0x0cu << 24);
+            e[1 + k] = sv;        // sel[0..3] = g0.y, g0.z, g0.w, g1.x
+            e[5 + k] = (uint32_t)c[k];  // coefficient pairs: g1.y .. g2.x
+        }
+        out.insert(out.end(), e, e + 12);
+    }
+    return true;
+}
+
 // K1b — the small top levels in one launch: one 1024-thread workgroup per frame copies level
 // ts-1 into LDS, then makes levels ts .. L-1 one after the other, each from the previous one
 // held in LDS (two buffers, ping-pong), writing every level to the pyramid as well.  Same
@@ -517,7 +678,6 @@ __global__ __launch_bounds__(kTailBlock) void resize_tail_kernel(ResizeTailArgs 
     __shared__ __attribute__((aligned(16))) uint8_t lds[kTailLds];
     const int f = blockIdx.x;
     const int tid = threadIdx.x;
-    uint8_t* buf[2] = {lds, lds + a.buf_b};
     {   // level ts-1 from the pyramid in 16-byte chunks (LDS pitch lp[0] % 16 == 0, inside the
         // slab's 64-byte row pitch), four per thread in flight before the LDS stores
         const LevelPtr sp = a.src;
@@ -537,7 +697,7 @@ __global__ __launch_bounds__(kTailBlock) void resize_tail_kernel(ResizeTailArgs 
                 const int i = base + kTailBlock * u + tid;
                 if (i >= total) continue;
                 const int r = i / cpr, c = i - r * cpr;
-                *reinterpret_cast<uint4*>(buf[0] + r * a.lp[0] + 16 * c) = v[u];
+                *reinterpret_cast<uint4*>(lds + r * a.lp[0] + 16 * c) = v[u];
             }
         }
     }
@@ -546,8 +706,9 @@ __global__ __launch_bounds__(kTailBlock) void resize_tail_kernel(ResizeTailArgs 
     // otherwise wait on three dependent global loads per iteration
     __shared__ int yts[3 * kTailRows];
     for (int k = 0; k < a.nt; ++k) {
-        const uint8_t* s = buf[k & 1];
-        uint8_t* d = buf[(k + 1) & 1];
+        // (offsets from lds, not a pointer array: that would make every access a flat one)
+        const uint8_t* s = lds + ((k & 1) ? a.buf_b : 0);
+        uint8_t* d = lds + (((k + 1) & 1) ? a.buf_b : 0);
         const int sp_l = a.lp[k], dp_l = a.lp[k + 1];
         const int dw = a.dw[k], dh = a.dh[k], xb = a.simd_xb[k];
         const int* xt = a.xt[k];
@@ -1449,9 +1610,16 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
 #pragma unroll
             for (int i = 0; i < 8; ++i)
                 if (i0 + i < n) v[i] = src[slot + i0 + i];
+            // (uniform branch: a store through the selected pointer would be a flat store)
+            if (in_lds) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
-                if (i0 + i < n) K[off + i0 + i] = v[i];
+                for (int i = 0; i < 8; ++i)
+                    if (i0 + i < n) lkeys[off + i0 + i] = v[i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    if (i0 + i < n) K[off + i0 + i] = v[i];
+            }
         }
         nkeys += chunk_total;
     }
@@ -2305,6 +2473,81 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
             g.tail_start = ts;
         }
         if (L - g.tail_start < 2) g.tail_start = L;  // a single level gains nothing
+    }
+    {   // pyramid_kernel: column-group tables, then two band plans (batches >= kTailMinFrames:
+        // the fewest bands whose LDS fits kPyrLdsCap; single frames / small batches: bands of
+        // ~kPyrSmallRows level-0 rows, for more workgroups)
+        const int L = g.geo.nlevels;
+        g.ptab.clear();
+        g.pyr_ok = L >= 2;
+        for (int l = 1; l < L && g.pyr_ok; ++l) {
+            g.gtab_off[l] = (int)(g.ptab.size() / 4);
+            g.pyr_ok = pyramid_group_table(g.xtab, g.xoff[l], g.geo.lv[l].w, g.ptab);
+        }
+        for (int l = 0; l < L; ++l) g.pyr_lp[l] = ((g.geo.lv[l].w + 15) & ~15) + 16;
+        double work = 0, own = 0;  // pixels computed by the bands vs the pyramid's
+        for (int l = 1; l < L; ++l) own += (double)g.geo.lv[l].w * g.geo.lv[l].h;
+        auto plan_bands = [&](int nb, std::vector<int>& bt, size_t& lds, int& bufb, int& ybuf, int& ymax) {
+            bt.assign((size_t)nb * L * 4, 0);
+            size_t A = 0, B = 0;
+            work = 0;
+            ymax = 1;
+            for (int b = 0; b < nb; ++b) {
+                auto R = [&](int l, int bb) { return (int)((long long)bb * g.geo.lv[l].h / nb); };
+                int c0[kMaxLevels], c1[kMaxLevels];
+                c0[L - 1] = R(L - 1, b);
+                c1[L - 1] = R(L - 1, b + 1) - 1;
+                for (int l = L - 1; l >= 1; --l) {
+                    const int o0 = R(l - 1, b), o1 = R(l - 1, b + 1) - 1;
+                    if (c1[l] >= c0[l]) {  // y tables are monotone: the sources of rows c0 .. c1
+                        const int s0 = g.ytab[g.yoff[l] + 3 * c0[l]], s1 = g.ytab[g.yoff[l] + 3 * c1[l] + 1];
+                        c0[l - 1] = o1 >= o0 ? std::min(o0, s0) : s0;
+                        c1[l - 1] = o1 >= o0 ? std::max(o1, s1) : s1;
+                    } else {
+                        c0[l - 1] = o0;
+                        c1[l - 1] = o1;
+                    }
+                }
+                for (int l = 0; l < L; ++l) {
+                    int* e = &bt[((size_t)b * L + l) * 4];
+                    e[0] = c0[l];
+                    e[1] = c1[l];
+                    e[2] = R(l, b);
+                    e[3] = R(l, b + 1);
+                    const size_t n = (size_t)std::max(0, c1[l] - c0[l] + 1);
+                    (l & 1 ? B : A) = std::max(l & 1 ? B : A, n * g.pyr_lp[l]);
+                    if (l) ymax = std::max(ymax, (int)n);
+                    if (l) work += (double)n * g.geo.lv[l].w;
+                }
+            }
+            bufb = (int)((A + 15) & ~(size_t)15);
+            ybuf = bufb + (int)((B + 15) & ~(size_t)15);
+            lds = (size_t)ybuf + 2 * 3 * (size_t)ymax * sizeof(int);
+        };
+        const char* cap_env = std::getenv("ORBFE_PYR_LDS_KB");
+        const size_t cap = (cap_env ? (size_t)std::atoi(cap_env) : (size_t)kPyrLdsCapKB) * 1024;
+        std::vector<int> bt[2];
+        const int h0 = g.geo.lv[0].h, htop = g.geo.lv[L - 1].h;
+        int nb = 1;
+        for (int which = 0; which < 2 && g.pyr_ok; ++which) {
+            nb = which == 0 ? 1 : std::max(1, std::min(std::min(64, htop), h0 / kPyrSmallRows));
+            for (;; ++nb) {
+                plan_bands(nb, bt[which], g.pyr_lds[which], g.pyr_bufb[which], g.pyr_ybuf[which], g.pyr_ymax[which]);
+                if (g.pyr_lds[which] <= cap) break;
+                if (nb >= htop) { g.pyr_ok = false; break; }  // no band fits: per-level kernels
+            }
+            g.nbands[which] = nb;
+            // thin bands recompute too many seam rows: at 1920x1080 the per-level kernels win
+            // (c4: 1.11 vs 1.25-1.45 ms per step), at 640x480 the band kernel (0.135 vs 0.17)
+            g.pyr_use[which] = g.pyr_ok && work <= own * (which == 0 ? kPyrMaxWork : kPyrMaxWorkSmall);
+        }
+        if (g.pyr_ok) {
+            for (int which = 0; which < 2; ++which) {
+                while (g.ptab.size() % 4) g.ptab.push_back(0u);
+                g.band_off[which] = (int)(g.ptab.size() / 4);  // int4 units
+                for (int v : bt[which]) g.ptab.push_back((uint32_t)v);
+            }
+        }
     }
     int rmax = 7, cmax = 7;
     for (const CellDesc& c : g.cells) {

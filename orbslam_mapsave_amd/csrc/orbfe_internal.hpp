@@ -83,6 +83,19 @@ struct ResizeArgs {
     int lds_e;
 };
 
+struct PyrArgs {
+    LevelPtr src;                  // level 0
+    LevelPtr dst[kMaxLevels];      // pyramid levels (index = level; 0 unused)
+    int nlevels;
+    int w[kMaxLevels];             // level widths
+    int lp[kMaxLevels];            // LDS row pitch per level
+    int buf_b, ybuf, ymax;         // LDS offsets: second level buffer, y-table rows (2 x ymax)
+    const int4* bands;             // [band][level] {c0, c1, w0, w1}: rows computed / written
+    const uint4* gtab[kMaxLevels]; // per level >= 1: 3 uint4 per column group
+    const int* yt[kMaxLevels];     // per level >= 1: the resize y table
+    int simd_xb[kMaxLevels];
+};
+
 struct ResizeTailArgs {
     LevelPtr src;                 // level ts-1
     int sh;                       // its rows
@@ -201,6 +214,15 @@ struct Plan {
     int rb_pitch[kMaxLevels] = {}, rb_lds_e[kMaxLevels] = {};
     size_t rb_lds[kMaxLevels] = {};
     int tail_start = kMaxLevels;  // levels >= tail_start come from resize_tail_kernel
+    // pyramid_kernel: column-group tables (all levels) then the band tables of the two band
+    // plans (batches >= kTailMinFrames / smaller), in one device table of u32
+    bool pyr_ok = false;
+    bool pyr_use[2] = {false, false};  // per band plan: the band kernel is the faster path
+    std::vector<uint32_t> ptab;
+    int gtab_off[kMaxLevels] = {};  // in uint4 units
+    int band_off[2] = {}, nbands[2] = {}, pyr_bufb[2] = {}, pyr_ybuf[2] = {}, pyr_ymax[2] = {};
+    int pyr_lp[kMaxLevels] = {};
+    size_t pyr_lds[2] = {};
 };
 
 int make_tables(const orbfe_params& p, HostTables& t);
@@ -211,6 +233,7 @@ __global__ void level0_kernel(Level0Args);
 template <bool kX86> __global__ void resize_kernel(ResizeArgs);
 template <bool kX86> __global__ void resize_tail_kernel(ResizeTailArgs);
 template <bool kX86> __global__ void resize_blur_kernel(ResizeArgs);
+template <bool kX86> __global__ void pyramid_kernel(PyrArgs);
 template <int kP> __global__ void fast_kernel(FastArgs);
 constexpr int kFastPitch = 48;  // fast_kernel<kFastPitch>: ROI pitch known at compile time
 __global__ void octree_kernel(OctArgs);
@@ -221,6 +244,14 @@ constexpr size_t kBlurFragBytes = 128 * 16;
 template <int kDescGroup, bool kX86> __global__ void describe_kernel(DescArgs);
 extern __constant__ int c_umax[16];
 
+// pyramid_kernel band plans: LDS per workgroup for large batches (80 KB: two 1024-thread
+// workgroups per CU; ORBFE_PYR_LDS_KB overrides), level-0 rows per band for small ones
+constexpr int kPyrLdsCapKB = 80;
+constexpr int kPyrBlockSize = 1024;
+constexpr int kPyrSmallRows = 12;
+// band plans whose rows computed exceed the pyramid's by more than this use the per-level
+// kernels instead (large batches: throughput; small ones: latency)
+constexpr double kPyrMaxWork = 1.25, kPyrMaxWorkSmall = 3.0;
 constexpr int kFastBlockSize = 64;
 // FAST survivor-list entries per cell (>= 322: a pre-test sweep adds <= 256 entries and a
 // flush keeps <= 66).  512 covers the ~22 % pre-test pass rate of textured cells without a

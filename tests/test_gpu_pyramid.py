@@ -1,0 +1,103 @@
+"""pyramid_kernel (orbfe_extract.hip): the whole cascaded pyramid (ORBextractor.cc:1110-1135,
+cv::resize INTER_LINEAR) in one launch, a horizontal band of every frame per workgroup, each
+level made from the previous one in LDS.  Every level of every frame must be byte-exact against
+the oracle — band seams (rows recomputed by two bands), thin bands of the top levels, odd
+widths, single frames (the small-batch band plan) and batches, both arithmetic readings —
+and identical to the per-level kernels (ORBFE_PYR=0).  ORBFE_PYR=2 forces the band kernel
+where the default plan would pick the per-level kernels (thin bands at 1080p).  Scale factors whose source columns do
+not fit the kernel's 8-byte window fall back to the per-level kernels."""
+import numpy as np
+import pytest
+
+import oracle
+from orbslam_mapsave_amd.synth import synthetic_frame
+
+pytestmark = pytest.mark.gpu
+
+
+def _levels_exact(e, p, imgs, var):
+    for f, img in enumerate(imgs):
+        with oracle.variant(var):
+            levels = oracle.pyramid(p, img)
+        for l, lev in enumerate(levels):
+            g = e.get_level(l, f)
+            assert g.shape == lev.shape
+            bad = np.argwhere(g != lev)
+            assert bad.size == 0, f"frame {f} level {l} {lev.shape}: {len(bad)} px differ, first {bad[:4].tolist()}"
+
+
+@pytest.mark.parametrize("size", [(640, 480), (643, 481), (1920, 1080), (331, 247), (97, 73), (1281, 722)])
+@pytest.mark.parametrize("batch", [1, 9])
+@pytest.mark.parametrize("arith", ["scalar", "x86"])
+def test_levels_bit_exact(size, batch, arith, monkeypatch):
+    from orbslam_mapsave_amd.native import ORBextractor
+    monkeypatch.setenv("ORBFE_PYR", "2")  # the band kernel at every size (thin bands included)
+    w, h = size
+    nf = 2000 if w > 1000 else 1000
+    p = oracle.params(nf, 1.2, 8, 20, 7)
+    e = ORBextractor(nf, 1.2, 8, 20, 7, device=0, max_width=w, max_height=h)
+    var = oracle.VAR_H5_SSE2 if arith == "x86" else 0
+    if arith == "x86":
+        e.set_arithmetic(e.ARITH_X86_SIMD)
+    try:
+        imgs = np.stack([synthetic_frame(3 * w + s, w, h) for s in range(batch)])
+        if batch == 1:
+            e(imgs[0])
+        else:
+            e.extract_batch(imgs)
+        _levels_exact(e, p, imgs, var)
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("lds_kb", ["30", "40", "150"])
+def test_band_plans(lds_kb, monkeypatch):
+    """Other LDS caps -> other band counts (more seams, or one band per frame half)."""
+    from orbslam_mapsave_amd.native import ORBextractor
+    monkeypatch.setenv("ORBFE_PYR_LDS_KB", lds_kb)
+    monkeypatch.setenv("ORBFE_PYR", "2")
+    p = oracle.params(1000, 1.2, 8, 20, 7)
+    e = ORBextractor(1000, 1.2, 8, 20, 7, device=0, max_width=640, max_height=480)
+    try:
+        imgs = np.stack([synthetic_frame(90 + s, 640, 480) for s in range(8)])
+        kps, desc, cnt = e.extract_batch(imgs)
+        _levels_exact(e, p, imgs, 0)
+        okps, odesc = oracle.extract(p, imgs[3])
+        assert kps[3, :cnt[3]].tobytes() == okps.tobytes()
+        assert np.array_equal(desc[3, :cnt[3]], odesc)
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("sf,nl", [(1.5, 5), (2.0, 4), (1.1, 10)])
+def test_other_scale_factors(sf, nl, monkeypatch):
+    """Fallback (or band kernel, where the window fits) for other scale factors."""
+    from orbslam_mapsave_amd.native import ORBextractor
+    monkeypatch.setenv("ORBFE_PYR", "2")
+    p = oracle.params(1000, sf, nl, 20, 7)
+    e = ORBextractor(1000, sf, nl, 20, 7, device=0, max_width=640, max_height=480)
+    try:
+        imgs = np.stack([synthetic_frame(120 + s, 640, 480) for s in range(8)])
+        e.extract_batch(imgs)
+        _levels_exact(e, p, imgs[:2], 0)
+    finally:
+        e.close()
+
+
+def test_per_level_path_identical(monkeypatch):
+    from orbslam_mapsave_amd.native import ORBextractor
+    imgs = np.stack([synthetic_frame(150 + s, 640, 480) for s in range(8)])
+    outs = []
+    for flag in ("2", "0"):
+        monkeypatch.setenv("ORBFE_PYR", flag)
+        e = ORBextractor(1000, 1.2, 8, 20, 7, device=0, max_width=640, max_height=480)
+        try:
+            kps, desc, cnt = e.extract_batch(imgs)
+            outs.append((kps.copy(), desc.copy(), cnt.copy()))
+        finally:
+            e.close()
+    assert np.array_equal(outs[0][2], outs[1][2])
+    for f in range(len(imgs)):
+        n = outs[0][2][f]
+        assert outs[0][0][f, :n].tobytes() == outs[1][0][f, :n].tobytes()
+        assert np.array_equal(outs[0][1][f, :n], outs[1][1][f, :n])
