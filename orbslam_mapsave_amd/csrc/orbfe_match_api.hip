@@ -24,6 +24,26 @@ struct UpScatter {
     const uint8_t* src[kMaxUpSeg];
     uint32_t bytes[kMaxUpSeg];
 };
+// Results of a host-form call go the other way in one launch: each segment copies device
+// bytes into the (device-mapped) pinned staging buffer, so a call ends with this kernel and
+// one stream synchronisation instead of a DMA per output array.
+__global__ __launch_bounds__(256) void download_gather_kernel(UpScatter a) {
+    const int s = blockIdx.y;
+    if (s >= a.n) return;
+    const uint32_t nb = a.bytes[s];
+    const uint8_t* src = a.src[s];
+    uint8_t* dst = a.dst[s];
+    // dword copies when both ends are 4-byte aligned (device buffers and 256-B staging slots)
+    if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 3) == 0) {
+        const uint32_t n4 = nb >> 2;
+        const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
+        uint32_t* d4 = reinterpret_cast<uint32_t*>(dst);
+        for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) d4[i] = s4[i];
+        if (blockIdx.x == 0 && threadIdx.x < (nb & 3)) dst[4 * n4 + threadIdx.x] = src[4 * n4 + threadIdx.x];
+    } else {
+        for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nb; i += gridDim.x * 256) dst[i] = src[i];
+    }
+}
 __global__ __launch_bounds__(256) void upload_scatter_kernel(UpScatter a) {
     const int s = blockIdx.y;
     if (s >= a.n) return;
@@ -53,6 +73,8 @@ struct orbfe_matcher {
     int last_rounds = 0;  // rounds the most recent greedy resolution took (diagnostics)
     int capacity_retries = 0;  // calls rerun because the candidates outgrew the buffer
     bool rounds_on_device = false;  // single-workgroup form: the count sits in g_chg[0]
+    // ORBFE_ZERO_COPY=0: uploads and downloads as DMA copies (the staging buffer unmapped)
+    bool zero_copy_off = std::getenv("ORBFE_ZERO_COPY") && std::strcmp(std::getenv("ORBFE_ZERO_COPY"), "0") == 0;
     BfKernel bf_kernel = bf_match_fp4_kernel;  // ORBFE_BF_I8=1 at creation: bf_match_kernel
 
     ~orbfe_matcher() {
@@ -71,7 +93,10 @@ struct orbfe_matcher {
     // host-form entry point starts with begin() and ends with sync(), which completes the
     // deferred downloads; the staging memory is reused from call to call.
     uint8_t* pin = nullptr;
+    uint8_t* pin_dev = nullptr;  // the staging buffer's device-mapped address (null: DMA path)
     size_t pin_cap = 0, pin_used = 0;
+    struct DnSeg { const uint8_t* src; uint8_t* dst; size_t bytes; };
+    std::vector<DnSeg> dnq;  // downloads not yet gathered (zero-copy path)
     std::vector<uint8_t*> pin_retired;  // outgrown buffers, freed once the stream is idle
     struct Pending { void* dst; const uint8_t* src; size_t bytes; };
     std::vector<Pending> pend;
@@ -86,16 +111,23 @@ struct orbfe_matcher {
         pin_used = 0;
         pend.clear();
         upq.clear();
+        dnq.clear();
         cand_check = false;
     }
     // Copies the staged uploads to their device buffers (call before any kernel reads them).
+    // With a device-mapped staging buffer the scatter kernel reads the pinned bytes itself
+    // (zero-copy: no DMA in front of it); otherwise one H2D copy into d_stage first.
     int flush() {
         if (upq.empty()) return ORBFE_OK;
         size_t lo = upq[0].off, hi = 0;
         for (const UpSeg& u : upq) { lo = std::min(lo, u.off); hi = std::max(hi, u.off + u.bytes); }
         int st;
-        if ((st = d_stage.ensure(pin_cap))) return st;
-        ORBFE_HIP(hipMemcpyAsync(d_stage.as<uint8_t>() + lo, pin + lo, hi - lo, hipMemcpyHostToDevice, stream));
+        const uint8_t* sbase = pin_dev;
+        if (!sbase) {
+            if ((st = d_stage.ensure(pin_cap))) return st;
+            ORBFE_HIP(hipMemcpyAsync(d_stage.as<uint8_t>() + lo, pin + lo, hi - lo, hipMemcpyHostToDevice, stream));
+            sbase = d_stage.as<uint8_t>();
+        }
         for (size_t b = 0; b < upq.size(); b += kMaxUpSeg) {
             UpScatter a;
             a.n = (int)std::min<size_t>(kMaxUpSeg, upq.size() - b);
@@ -103,7 +135,7 @@ struct orbfe_matcher {
             for (int i = 0; i < a.n; ++i) {
                 const UpSeg& u = upq[b + i];
                 a.dst[i] = u.dst;
-                a.src[i] = d_stage.as<uint8_t>() + u.off;
+                a.src[i] = sbase + u.off;
                 a.bytes[i] = (uint32_t)u.bytes;
                 mx = std::max(mx, u.bytes);
             }
@@ -124,6 +156,8 @@ struct orbfe_matcher {
             if (pin) pin_retired.push_back(pin);  // in-flight copies may still read it
             pin = static_cast<uint8_t*>(q);
             pin_cap = cap;
+            void* dq = nullptr;
+            pin_dev = (!zero_copy_off && hipHostGetDevicePointer(&dq, q, 0) == hipSuccess) ? static_cast<uint8_t*>(dq) : nullptr;
             pin_used = 0;
             return stage(bytes);
         }
@@ -140,17 +174,41 @@ struct orbfe_matcher {
         upq.push_back(UpSeg{b.as<uint8_t>(), (size_t)(q - pin), bytes});
         return ORBFE_OK;
     }
-    int down(void* dst, const DevBuf& b, size_t bytes) {
+    int down(void* dst, const DevBuf& b, size_t bytes) { return down_ptr(dst, b.p, bytes); }
+    int down_ptr(void* dst, const void* src, size_t bytes) {
         if (!bytes) return ORBFE_OK;
         uint8_t* q = stage(bytes);
         if (!q) return ORBFE_ERR_NOMEM;
-        ORBFE_HIP(hipMemcpyAsync(q, b.p, bytes, hipMemcpyDeviceToHost, stream));
+        if (pin_dev) {  // gathered at sync() by one kernel
+            dnq.push_back(DnSeg{static_cast<const uint8_t*>(src), pin_dev + (q - pin), bytes});
+        } else {
+            ORBFE_HIP(hipMemcpyAsync(q, src, bytes, hipMemcpyDeviceToHost, stream));
+        }
         pend.push_back(Pending{dst, q, bytes});
+        return ORBFE_OK;
+    }
+    int gather() {
+        for (size_t b = 0; b < dnq.size(); b += kMaxUpSeg) {
+            UpScatter a;
+            a.n = (int)std::min<size_t>(kMaxUpSeg, dnq.size() - b);
+            size_t mx = 0;
+            for (int i = 0; i < a.n; ++i) {
+                a.src[i] = dnq[b + i].src;
+                a.dst[i] = dnq[b + i].dst;
+                a.bytes[i] = (uint32_t)dnq[b + i].bytes;
+                mx = std::max(mx, dnq[b + i].bytes);
+            }
+            const int gx = (int)std::min<size_t>(64, std::max<size_t>(1, (mx / 4 + 255) / 256));
+            hipLaunchKernelGGL(download_gather_kernel, dim3(gx, a.n), dim3(256), 0, stream, a);
+        }
+        dnq.clear();
+        ORBFE_HIP(hipGetLastError());
         return ORBFE_OK;
     }
     int sync() {
         int st;
         if ((st = flush())) return st;
+        if ((st = gather())) return st;
         ORBFE_HIP(hipStreamSynchronize(stream));
         if (cand_check) {  // csr_async: the candidates must have fit before results count
             int total = 0;
@@ -260,10 +318,7 @@ struct orbfe_matcher {
         hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, stream, cnt.as<int>(), nq, off.as<int>());
         hipLaunchKernelGGL(fk, dim3(blocks), dim3(256), 0, stream, a);
         ORBFE_HIP(hipGetLastError());
-        uint8_t* q = stage(sizeof(int));
-        if (!q) return ORBFE_ERR_NOMEM;
-        ORBFE_HIP(hipMemcpyAsync(q, off.as<int>() + nq, sizeof(int), hipMemcpyDeviceToHost, stream));
-        pend.push_back(Pending{&cand_total, q, sizeof(int)});
+        if ((st = down_ptr(&cand_total, off.as<int>() + nq, sizeof(int)))) return st;
         cand_cap_used = cap;
         cand_check = true;
         return ORBFE_OK;
