@@ -150,20 +150,23 @@ struct orbfe_extractor {
     // copies.  Rebuilt when the plan or any buffer it captured changes.
     struct Pinned {
         uint8_t* p = nullptr;
+        uint8_t* d = nullptr;  // device-mapped address (kernels read / write it over PCIe)
         size_t bytes = 0;
         int ensure(size_t n) {
             if (n <= bytes) return ORBFE_OK;
             if (p) hipHostFree(p);
-            p = nullptr;
+            p = d = nullptr;
             bytes = 0;
             if (hipHostMalloc(reinterpret_cast<void**>(&p), n, hipHostMallocDefault) != hipSuccess)
                 return ORBFE_ERR_NOMEM;
+            void* dq = nullptr;
+            d = hipHostGetDevicePointer(&dq, p, 0) == hipSuccess ? static_cast<uint8_t*>(dq) : nullptr;
             bytes = n;
             return ORBFE_OK;
         }
         void release() {
             if (p) hipHostFree(p);
-            p = nullptr;
+            p = d = nullptr;
             bytes = 0;
         }
     };
@@ -189,6 +192,17 @@ struct orbfe_extractor {
     bool use_pyr = !(std::getenv("ORBFE_PYR") && std::strcmp(std::getenv("ORBFE_PYR"), "0") == 0);
     // ORBFE_PYR=2: the band kernel even where its plan recomputes many seam rows (tests, A/B)
     bool force_pyr = std::getenv("ORBFE_PYR") && std::strcmp(std::getenv("ORBFE_PYR"), "2") == 0;
+    // ORBFE_ZERO_COPY=0: the single-frame host call copies its frame in and its outputs out
+    // with DMA copies instead of kernels reading / writing the pinned buffers
+    bool zero_copy = !(std::getenv("ORBFE_ZERO_COPY") && std::strcmp(std::getenv("ORBFE_ZERO_COPY"), "0") == 0);
+    // run(): the pyramid kernel reads level 0 from l0_stage and writes it to the slab level 0
+    LevelPtr l0_stage{};
+    bool l0_from_stage = false;
+    bool pyr_path(int n) const {  // run() makes the pyramid with pyramid_kernel for n frames
+        const int which = n >= kTailMinFrames ? 0 : 1;
+        return plan.pyr_ok && (plan.pyr_use[which] || force_pyr) && use_pyr &&
+               !(fused_blur && resize_blur) && plan.geo.nlevels >= 2;
+    }
     bool graph_broken = std::getenv("ORBFE_NO_GRAPH") != nullptr;  // capture failed once (or
                                  // disabled for A/B runs): keep to the launch path
 
@@ -224,17 +238,34 @@ struct orbfe_extractor {
                 graph_broken = true;
                 return ORBFE_OK;
             }
-            bool ok = hipMemcpy2DAsync(pyr.as<uint8_t>() + l0.off, l0.pitch, pin_in.p, w, w, h,
-                                       hipMemcpyHostToDevice, stream) == hipSuccess;
+            // zero-copy: the pyramid kernel reads the frame from the pinned staging buffer and
+            // writes level 0 into the slab as it goes (no H2D copy), describe writes keypoints,
+            // descriptors and the count straight into the pinned outputs (no D2H copies)
+            const bool zc_out = zero_copy && pin_kps.d && pin_desc.d && pin_n.d;
+            const bool zc_in = zero_copy && pin_in.d && pyr_path(1);
             LevelPtr lp0{pyr.as<uint8_t>() + l0.off, g.slab, l0.pitch};
-            ok = ok && run(1, lp0, out_kps.as<orbfe_keypoint>(), cap, out_desc.as<uint8_t>(),
-                           out_n.as<int32_t>()) == ORBFE_OK;
-            ok = ok && hipMemcpyAsync(pin_n.p, out_n.p, sizeof(int32_t), hipMemcpyDeviceToHost,
-                                      stream) == hipSuccess;
-            ok = ok && hipMemcpyAsync(pin_kps.p, out_kps.p, (size_t)cap * sizeof(orbfe_keypoint),
-                                      hipMemcpyDeviceToHost, stream) == hipSuccess;
-            ok = ok && hipMemcpyAsync(pin_desc.p, out_desc.p, (size_t)cap * 32,
-                                      hipMemcpyDeviceToHost, stream) == hipSuccess;
+            bool ok = true;
+            if (zc_in) {
+                l0_stage = LevelPtr{pin_in.d, (long long)w * h, w};
+                l0_from_stage = true;
+            } else {
+                ok = hipMemcpy2DAsync(pyr.as<uint8_t>() + l0.off, l0.pitch, pin_in.p, w, w, h,
+                                      hipMemcpyHostToDevice, stream) == hipSuccess;
+            }
+            if (zc_out) {
+                ok = ok && run(1, lp0, reinterpret_cast<orbfe_keypoint*>(pin_kps.d), cap, pin_desc.d,
+                               reinterpret_cast<int32_t*>(pin_n.d)) == ORBFE_OK;
+            } else {
+                ok = ok && run(1, lp0, out_kps.as<orbfe_keypoint>(), cap, out_desc.as<uint8_t>(),
+                               out_n.as<int32_t>()) == ORBFE_OK;
+                ok = ok && hipMemcpyAsync(pin_n.p, out_n.p, sizeof(int32_t), hipMemcpyDeviceToHost,
+                                          stream) == hipSuccess;
+                ok = ok && hipMemcpyAsync(pin_kps.p, out_kps.p, (size_t)cap * sizeof(orbfe_keypoint),
+                                          hipMemcpyDeviceToHost, stream) == hipSuccess;
+                ok = ok && hipMemcpyAsync(pin_desc.p, out_desc.p, (size_t)cap * 32,
+                                          hipMemcpyDeviceToHost, stream) == hipSuccess;
+            }
+            l0_from_stage = false;
             const bool ended = hipStreamEndCapture(stream, &graph) == hipSuccess;
             ok = ok && ended && graph &&
                  hipGraphInstantiate(&g1, graph, nullptr, nullptr, 0) == hipSuccess;
@@ -343,10 +374,12 @@ struct orbfe_extractor {
         uint32_t pre_mask = 0;
         // K1 as one launch (pyramid_kernel): every level of a band of every frame in LDS
         const int which = n >= kTailMinFrames ? 0 : 1;
-        const bool one_pyr = g.pyr_ok && (g.pyr_use[which] || force_pyr) && !rb && use_pyr && L >= 2;
+        const bool one_pyr = pyr_path(n);
+        if (l0_from_stage && !one_pyr) return ORBFE_ERR_ARG;  // callers check pyr_path first
         if (one_pyr) {
             PyrArgs pa;
-            pa.src = lp[0];
+            pa.src = l0_from_stage ? l0_stage : lp[0];
+            pa.l0_copy = l0_from_stage ? lp[0] : LevelPtr{nullptr, 0, 0};
             pa.nlevels = L;
             for (int l = 0; l < L; ++l) {
                 pa.dst[l] = lp[l];

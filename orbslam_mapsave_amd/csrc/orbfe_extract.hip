@@ -566,6 +566,11 @@ __global__ __launch_bounds__(kPyrBlock) void pyramid_kernel(PyrArgs a) {
                 if (i >= total) continue;
                 const int r = i / cpr, c = i - r * cpr;
                 *reinterpret_cast<uint4*>(py_lds + r * P + 16 * c) = v[u];
+                // the band's own level-0 rows to the slab (the 16-byte chunk stays inside the
+                // slab's 64-byte row pitch)
+                if (a.l0_copy.base && b0.x + r >= b0.z && b0.x + r < b0.w)
+                    *reinterpret_cast<uint4*>(const_cast<uint8_t*>(a.l0_copy.base) + f * a.l0_copy.fpitch +
+                                              (long long)(b0.x + r) * a.l0_copy.pitch + 16 * c) = v[u];
             }
         }
     }

@@ -85,6 +85,8 @@ struct ResizeArgs {
 
 struct PyrArgs {
     LevelPtr src;                  // level 0
+    LevelPtr l0_copy;              // base != null: each band also writes its level-0 rows here
+                                   // (src is then the caller's staging copy of the frame)
     LevelPtr dst[kMaxLevels];      // pyramid levels (index = level; 0 unused)
     int nlevels;
     int w[kMaxLevels];             // level widths

@@ -1,0 +1,60 @@
+"""Zero-copy host paths (ORBFE_ZERO_COPY, default on): the single-frame host call
+(ORBextractor::operator(), ORBextractor.cc:1042) reads its frame from the pinned staging buffer
+inside the pyramid kernel and has describe write keypoints / descriptors / count straight into
+the pinned outputs; the host-form matchers scatter their uploads from, and gather their results
+into, the device-mapped staging buffer.  Outputs must be identical to the DMA path
+(ORBFE_ZERO_COPY=0) and to the oracle, call after call (the staging buffers are reused)."""
+import numpy as np
+import pytest
+
+import oracle
+from orbslam_mapsave_amd.synth import synthetic_frame
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("size", [(640, 480), (1920, 1080), (331, 247)])
+def test_single_frame_zero_copy(size, monkeypatch):
+    from orbslam_mapsave_amd.native import ORBextractor
+    w, h = size
+    nf = 2000 if w > 1000 else 1000
+    p = oracle.params(nf, 1.2, 8, 20, 7)
+    imgs = [synthetic_frame(500 + s, w, h) for s in range(3)]
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("ORBFE_ZERO_COPY", flag)
+        e = ORBextractor(nf, 1.2, 8, 20, 7, device=0, max_width=w, max_height=h)
+        try:
+            res[flag] = [tuple(x.copy() for x in e(img)) for img in imgs + imgs[:1]]
+            assert np.array_equal(e.get_level(0), imgs[0])  # level 0 reached the slab
+        finally:
+            e.close()
+    for (k1, d1), (k0, d0) in zip(res["1"], res["0"]):
+        assert k1.tobytes() == k0.tobytes()
+        assert np.array_equal(d1, d0)
+    for img, (k, d) in zip(imgs, res["1"]):
+        ok, od = oracle.extract(p, img)
+        assert k.tobytes() == ok.tobytes()
+        assert np.array_equal(d, od)
+
+
+def test_matcher_zero_copy(monkeypatch):
+    import scenarios as S
+    from orbslam_mapsave_amd.native import ORBmatcher
+    c = S.sbp_keyframe_case(0)
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("ORBFE_ZERO_COPY", flag)
+        m = ORBmatcher(0.9, True, device=0)
+        try:
+            outs[flag] = [m.SearchByProjectionKeyFrame(c["cur"], c["tcw_cur"], c["cam"], c["log_scale"],
+                                                       c["kf_angle"], c["kf_valid"], c["kf_bad"], c["found"],
+                                                       c["kf_xyz"], c["kf_desc"], c["kf_min"], c["kf_max"], 10, 100,
+                                                       frame_mp=c["frame_mp"].copy(), kf_ids=c["kf_ids"])
+                          for _ in range(3)]
+        finally:
+            m.close()
+    rfmp, rnm = oracle.search_by_projection_keyframe(c, 10, 100)
+    for (f1, n1), (f0, n0) in zip(outs["1"], outs["0"]):
+        assert n1 == n0 and np.array_equal(f1, f0)
+    assert outs["1"][0][1] == rnm and np.array_equal(outs["1"][0][0], rfmp)
