@@ -342,6 +342,9 @@ def parse_args():
                          "x86 build (DESIGN.md §2)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--soak-s", type=float, default=2.0,
+                    help="untimed seconds of steps after the warmup (c2/c3/c4), so that an external "
+                         "GPU-utilisation sampler sees the load; 0 = off")
     ap.add_argument("--batch", type=int, default=256, help="frames per rank per step (c3)")
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--per-rank", type=int, default=0,
@@ -484,9 +487,23 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
         acc["bf_match"] = mt.profile_read()
         return acc
 
+    tw = time.perf_counter()
     for _ in range(warmup):
         step()
     barrier()
+    tw = (time.perf_counter() - tw) / max(warmup, 1)
+    # Soak (untimed, --soak-s seconds of the same steps): the timed region of a default run is
+    # tens of milliseconds, too short for an external utilisation sampler (rocm-smi at ~1 Hz) to
+    # see the GPU busy; the soak gives it a window of sustained load before the measurement.
+    # The step count is agreed over the ranks (their collectives must pair up).
+    if args.soak_s > 0:
+        n_soak = torch.tensor([min(int(args.soak_s / max(tw, 1e-4)), 100000)], dtype=torch.int64,
+                              device=dev)
+        if world > 1:
+            dist.all_reduce(n_soak, op=dist.ReduceOp.MAX)
+        for _ in range(int(n_soak.item())):
+            step()
+        barrier()
     # Probe steps (untimed): events on every kernel give the per-stage table and pick the
     # dominant kernel; the timed steps then carry events on that kernel's launches alone, so the
     # instrumentation of the other ~15 launches per call stays out of the timed region.

@@ -243,6 +243,11 @@ struct BowMatchArgs {
     int* nm;                  // [P] nmatches
     int* done;                // [P] workgroups of the pair that finished the node loop
     int* status;              // ORBFE_ERR_UNSUPPORTED / ORBFE_ERR_ARG on bad input
+    // host form (one pair): the pair's last workgroup also copies matches[0, out_n) and
+    // {nm, status} here — the device-mapped pinned staging buffer — so the call needs no
+    // download kernel or copy after the search
+    int* out_host;
+    int out_n;
 };
 
 // One workgroup per pair: vpMapPointMatches = NULL (164), empty histogram, nmatches = 0, the
@@ -413,7 +418,7 @@ __global__ __launch_bounds__(kBowSearchBlock) void bow_search_kernel(BowMatchArg
             }
         }
     }
-    if (!check_ori) return;
+    if (!check_ori && !a.out_host) return;
     // the pair's last workgroup to finish runs the orientation filter: release this
     // workgroup's matches / bins, count it, and the last one acquires everyone's
     __shared__ int last;
@@ -425,7 +430,15 @@ __global__ __launch_bounds__(kBowSearchBlock) void bow_search_kernel(BowMatchArg
     __syncthreads();
     if (!last) return;
     __threadfence();
-    bow_ori_filter(a, p);
+    if (check_ori) bow_ori_filter(a, p);
+    if (a.out_host) {  // host form: results straight into the pinned staging buffer
+        __syncthreads();
+        for (int j = threadIdx.x; j < a.out_n; j += blockDim.x) a.out_host[2 + j] = matches[j];
+        if (threadIdx.x == 0) {
+            a.out_host[0] = atomicAdd(&a.nm[p], 0);
+            a.out_host[1] = atomicAdd(a.status, 0);
+        }
+    }
 }
 
 }  // namespace orbfe
@@ -678,8 +691,8 @@ static int bow_launch(orbfe_vocabulary* v, int nframes, int cap, const uint8_t* 
 }
 
 static int bow_search_launch(orbfe_matcher* m, const BowMatchArgs& a, int n_pairs, int gx,
-                             float nnratio, int check_ori) {
-    hipLaunchKernelGGL(bow_init_kernel, dim3(n_pairs), dim3(256), 0, m->stream, a);
+                             float nnratio, int check_ori, bool init = true) {
+    if (init) hipLaunchKernelGGL(bow_init_kernel, dim3(n_pairs), dim3(256), 0, m->stream, a);
     hipLaunchKernelGGL(bow_search_kernel, dim3(gx, n_pairs), dim3(kBowSearchBlock), 0, m->stream,
                        a, nnratio, check_ori);
     ORBFE_HIP(hipGetLastError());
@@ -731,10 +744,30 @@ int orbfe_search_by_bow(orbfe_matcher* m, float nnratio, int check_ori, int n_kf
         if ((st = m->up(m->fb_ci, f_node_off, (size_t)(f_nn + 1) * 4))) return st;
         if ((st = m->up(m->fb_co, f_feat, (size_t)f_tot * 4))) return st;
         if ((st = m->up(m->nq, nn, sizeof(nn)))) return st;
-        if ((st = m->fa_k.ensure((size_t)f_cap * 4))) return st;
         if ((st = m->s1.ensure((size_t)f_cap * 4))) return st;  // bins per frame feature
-        if ((st = m->scal.ensure(16))) return st;
-        if ((st = m->g_hist.ensure(64 * sizeof(int)))) return st;
+        // bow_init_kernel's work as uploads (the scatter runs anyway): every match NULL (164),
+        // an empty histogram, the finished-workgroup counter, nmatches and status 0
+        const bool zc = m->pin_dev != nullptr;
+        if (zc) {
+            m->init_neg.assign((size_t)f_cap, -1);
+            const int zeros[64] = {};
+            if ((st = m->up(m->fa_k, m->init_neg.data(), (size_t)f_cap * 4))) return st;
+            if ((st = m->up(m->g_hist, zeros, sizeof(zeros)))) return st;
+            if ((st = m->up(m->scal, zeros, 16))) return st;
+        } else {
+            if ((st = m->fa_k.ensure((size_t)f_cap * 4))) return st;
+            if ((st = m->scal.ensure(16))) return st;
+            if ((st = m->g_hist.ensure(64 * sizeof(int)))) return st;
+        }
+        // zero-copy results: {nmatches, status, matches[n_f]} written by the search kernel
+        int* res = nullptr;
+        int* res_dev = nullptr;
+        if (zc) {
+            uint8_t* q = m->stage((size_t)(n_f + 2) * 4);
+            if (!q) return ORBFE_ERR_NOMEM;
+            res = reinterpret_cast<int*>(q);
+            res_dev = reinterpret_cast<int*>(m->pin_dev + (q - m->pin));
+        }
         BowMatchArgs a{};
         a.kf_cap = kf_cap;
         a.f_cap = f_cap;
@@ -757,12 +790,21 @@ int orbfe_search_by_bow(orbfe_matcher* m, float nnratio, int check_ori, int n_kf
         a.nm = m->scal.as<int>();
         a.status = m->scal.as<int>() + 1;
         a.done = m->g_hist.as<int>() + 32;
+        a.out_host = res_dev;
+        a.out_n = n_f;
         if ((st = m->flush())) return st;
-        if ((st = bow_search_launch(m, a, 1, (kf_nn + 3) / 4, nnratio, check_ori))) return st;
-        if ((st = m->down(matches, m->fa_k, (size_t)n_f * 4))) return st;
+        if ((st = bow_search_launch(m, a, 1, (kf_nn + 3) / 4, nnratio, check_ori, !zc))) return st;
         int cnt[2] = {0, 0};
-        if ((st = m->down(cnt, m->scal, sizeof(cnt)))) return st;
-        if ((st = m->sync())) return st;
+        if (zc) {
+            if ((st = m->sync())) return st;
+            std::memcpy(matches, res + 2, (size_t)n_f * 4);
+            cnt[0] = res[0];
+            cnt[1] = res[1];
+        } else {
+            if ((st = m->down(matches, m->fa_k, (size_t)n_f * 4))) return st;
+            if ((st = m->down(cnt, m->scal, sizeof(cnt)))) return st;
+            if ((st = m->sync())) return st;
+        }
         *nmatches = cnt[0];
         return cnt[1];  // ORBFE_ERR_UNSUPPORTED: a node held more than 256 frame features
     });

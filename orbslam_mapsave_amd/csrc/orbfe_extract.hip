@@ -1153,7 +1153,7 @@ __device__ __forceinline__ void child_box(int box, int boy, int q, int& cbx, int
 // every (frame, level) tree: [0] start, [1] counted, [2] compacted, [3] initial nodes,
 // [4 + p] phase-1 pass p, [12 + r] phase-2 round r, [30] passes | rounds << 8, [31] end.
 #ifdef ORBFE_OCT_TIMING
-__device__ long long g_oct_t[256 * 16 * 32];
+__device__ long long g_oct_t[256 * 16 * 64];
 #define OCT_MARK(tm, i) do { if (threadIdx.x == 0 && (tm)) (tm)[(i)] = clock64(); } while (0)
 #else
 #define OCT_MARK(tm, i) do { } while (0)
@@ -1161,7 +1161,10 @@ __device__ long long g_oct_t[256 * 16 * 32];
 
 // Sweep over the live keys (NODE >= 0): body(k, packed key, node) for each.  A thread loads
 // kOctU keys and their nodes before using any, so their LDS round trips overlap.
-constexpr int kOctU = 4;
+#ifndef ORBFE_OCT_U
+#define ORBFE_OCT_U 4
+#endif
+constexpr int kOctU = ORBFE_OCT_U;
 template <class KT, class NT, class F>
 __device__ __forceinline__ void oct_sweep(const KT* K, const NT* NODE, int nkeys, F&& body) {
     for (int k0 = threadIdx.x; k0 < nkeys; k0 += kOctU * kOctBlock) {
@@ -1176,6 +1179,35 @@ __device__ __forceinline__ void oct_sweep(const KT* K, const NT* NODE, int nkeys
 #pragma unroll
         for (int u = 0; u < kOctU; ++u)
             if (node[u] >= 0) body(k0 + u * kOctBlock, kk[u], node[u]);
+    }
+}
+// The same sweep in stages, each stage's LDS lookups for all kOctU keys issued together (a
+// body per key under its own exec mask would wait on each key's lookups in turn): the keys'
+// quadrants in their nodes' boxes, then body(k[], node[], q[]) for the kOctU keys at once
+// (node < 0: not a live key; its lookups read node 0 and are discarded).
+template <class KT, class NT, class F>
+__device__ __forceinline__ void oct_sweep_q(const KT* K, const NT* NODE, int nkeys, const int* bx,
+                                            const int* by, F&& body) {
+    for (int k0 = threadIdx.x; k0 < nkeys; k0 += kOctU * kOctBlock) {
+        int node[kOctU], q[kOctU], kx[kOctU];
+        uint32_t kk[kOctU];
+#pragma unroll
+        for (int u = 0; u < kOctU; ++u) {
+            const int k = k0 + u * kOctBlock;
+            kx[u] = k;
+            node[u] = k < nkeys ? (int)NODE[k] : -1;
+            kk[u] = k < nkeys ? K[k] : 0u;
+        }
+        int bxv[kOctU], byv[kOctU];
+#pragma unroll
+        for (int u = 0; u < kOctU; ++u) {
+            const int nd = max(node[u], 0);
+            bxv[u] = bx[nd];
+            byv[u] = by[nd];
+        }
+#pragma unroll
+        for (int u = 0; u < kOctU; ++u) q[u] = quadrant(bxv[u], byv[u], key_x(kk[u]), key_y(kk[u]));
+        body(kx, node, q);
     }
 }
 
@@ -1199,12 +1231,21 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
         s.qk[i] = (IT)-1;
     }
     __syncthreads();
-    for (int k = tid; k < nkeys; k += kOctBlock) {
-        const int node = min((int)((float)key_x(K[k]) / hX), nini - 1);  // vpIniNodes[kp.pt.x/hX] (568)
-        atomicAdd(&s.qc[node], 1u);
-        s.qk[node] = (IT)k;
+    OCT_MARK(tm, 56);
+    if (nini == 1) {  // every key in node 0: its count, and any key (read only if it is alone)
+        if (tid == 0) {
+            s.qc[0] = (uint32_t)nkeys;
+            s.qk[0] = (IT)(nkeys - 1);
+        }
+    } else {
+        for (int k = tid; k < nkeys; k += kOctBlock) {
+            const int node = min((int)((float)key_x(K[k]) / hX), nini - 1);  // vpIniNodes[kp.pt.x/hX] (568)
+            atomicAdd(&s.qc[node], 1u);
+            s.qk[node] = (IT)k;
+        }
     }
     __syncthreads();
+    OCT_MARK(tm, 57);
     int size;
     {   // list = non-empty initial nodes in index order; single-key nodes are closed
         int total = 0;
@@ -1228,9 +1269,15 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
         size = total;
     }
     __syncthreads();
-    for (int k = tid; k < nkeys; k += kOctBlock) {
-        const int node = s.aux[min((int)((float)key_x(K[k]) / hX), nini - 1)];
-        NODE[k] = (int)s.cnt(0)[node] >= 2 ? node : -1;
+    OCT_MARK(tm, 58);
+    if (nini == 1) {
+        const int nd = (int)s.cnt(0)[0] >= 2 ? 0 : -1;
+        for (int k = tid; k < nkeys; k += kOctBlock) NODE[k] = nd;
+    } else {
+        for (int k = tid; k < nkeys; k += kOctBlock) {
+            const int node = s.aux[min((int)((float)key_x(K[k]) / hX), nini - 1)];
+            NODE[k] = (int)s.cnt(0)[node] >= 2 ? node : -1;
+        }
     }
     __syncthreads();
     OCT_MARK(tm, 3);
@@ -1246,16 +1293,20 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
         const int nxt = cur ^ 1;
         for (int i = tid; i < OctLds<IT>::kQcWords * size; i += kOctBlock) s.qc[i] = 0u;
         __syncthreads();
+        if (pass == 1) OCT_MARK(tm, 32);
         {
-            const int *bx = s.box(cur), *by = s.boy(cur);
             const OctLds<IT> ss = s;
-            oct_sweep(K, NODE, nkeys, [=](int k, uint32_t kk, int node) {
-                const int q = quadrant(bx[node], by[node], key_x(kk), key_y(kk));
-                ss.qinc(node, q);
-                ss.qk[node * 4 + q] = (IT)k;
+            oct_sweep_q(K, NODE, nkeys, s.box(cur), s.boy(cur), [=](const int* k, const int* node, const int* q) {
+#pragma unroll
+                for (int u = 0; u < kOctU; ++u)
+                    if (node[u] >= 0) {
+                        ss.qinc(node[u], q[u]);
+                        ss.qk[node[u] * 4 + q[u]] = (IT)k[u];
+                    }
             });
         }
         __syncthreads();
+        if (pass == 1) OCT_MARK(tm, 33);
         // per node: children (divided) or kept (single); aux = child offset, aux2 = kept offset
         int csize = 0, ksize = 0, nexp = 0;
         for (int base = 0; base < size; base += kOctBlock) {
@@ -1288,6 +1339,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
             nexp += t >> 20;
         }
         const int nsize = csize + ksize;
+        if (pass == 1) OCT_MARK(tm, 34);
         if (nsize > ncap) {  // cannot happen for ncap >= max(N + 3, 4 * nIni)
             if (tid == 0) *out_cnt = -1;
             return;
@@ -1321,12 +1373,18 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
             }
         }
         __syncthreads();
+        if (pass == 1) OCT_MARK(tm, 35);
         {
-            const int *bx = s.box(cur), *by = s.boy(cur);
             const IT *qk = s.qk, *ncnt = s.cnt(nxt);
-            oct_sweep(K, NODE, nkeys, [=](int k, uint32_t kk, int node) {
-                const int np = (int)qk[node * 4 + quadrant(bx[node], by[node], key_x(kk), key_y(kk))];
-                NODE[k] = (int)ncnt[np] >= 2 ? np : -1;
+            oct_sweep_q(K, NODE, nkeys, s.box(cur), s.boy(cur), [=](const int* k, const int* node, const int* q) {
+                int np[kOctU], c[kOctU];
+#pragma unroll
+                for (int u = 0; u < kOctU; ++u) np[u] = node[u] >= 0 ? (int)qk[max(node[u], 0) * 4 + q[u]] : 0;
+#pragma unroll
+                for (int u = 0; u < kOctU; ++u) c[u] = (int)ncnt[np[u]];
+#pragma unroll
+                for (int u = 0; u < kOctU; ++u)
+                    if (node[u] >= 0) NODE[k[u]] = c[u] >= 2 ? np[u] : -1;
             });
         }
         __syncthreads();
@@ -1346,6 +1404,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
         // expandable nodes -> sort keys (size desc, seq desc); carries the list position
         if (tid == 0) { flag_sh[0] = 0; *rmin_sh = 0x7fffffff; }
         __syncthreads();
+        if (round == 0) OCT_MARK(tm, 40);
         for (int i = tid; i < size; i += kOctBlock)
             if ((int)s.cnt(cur)[i] >= 2) {
                 const int slot = atomicAdd(&flag_sh[0], 1);
@@ -1353,10 +1412,13 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
                               ((unsigned long long)(unsigned)s.seq(cur)[i] << 14) | (unsigned)i;
             }
         __syncthreads();
+        if (round == 0) OCT_MARK(tm, 41);
         const int m = flag_sh[0];
         int P = 1;
         while (P < m) P <<= 1;
         if (P <= 64) {  // one wave sorts in registers: no barrier per step
+            // (measured against one-wave rank sorts over v_readlane broadcasts or LDS broadcast
+            // reads: 5.0 K vs 5.9 K / 7.2 K shader cycles at the level-0 tree's ~60 nodes)
             if (tid < 64) {
                 unsigned long long v = tid < m ? s.s64[tid] : 0ull;
                 for (int k = 2; k <= P; k <<= 1)  // bitonic sort, descending
@@ -1389,16 +1451,20 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
         }
         for (int i = tid; i < OctLds<IT>::kQcWords * size; i += kOctBlock) s.qc[i] = 0u;
         __syncthreads();
+        if (round == 0) OCT_MARK(tm, 43);
         {
-            const int *bx = s.box(cur), *by = s.boy(cur);
             const OctLds<IT> ss = s;
-            oct_sweep(K, NODE, nkeys, [=](int k, uint32_t kk, int node) {
-                const int q = quadrant(bx[node], by[node], key_x(kk), key_y(kk));
-                ss.qinc(node, q);
-                ss.qk[node * 4 + q] = (IT)k;
+            oct_sweep_q(K, NODE, nkeys, s.box(cur), s.boy(cur), [=](const int* k, const int* node, const int* q) {
+#pragma unroll
+                for (int u = 0; u < kOctU; ++u)
+                    if (node[u] >= 0) {
+                        ss.qinc(node[u], q[u]);
+                        ss.qk[node[u] * 4 + q[u]] = (IT)k[u];
+                    }
             });
         }
         __syncthreads();
+        if (round == 0) OCT_MARK(tm, 44);
         // cut: first j in sorted order with size + sum_{<=j}(nch-1) >= N (else all m)
         {
             int run = 0;
@@ -1418,9 +1484,11 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
             __syncthreads();
         }
         const int r = min(*rmin_sh, m - 1);
+        if (round == 0) OCT_MARK(tm, 45);
         // processed flags + children offsets (processing order), kept offsets (list order)
         for (int i = tid; i < size; i += kOctBlock) s.aux2[i] = 0;
         __syncthreads();
+        if (round == 0) OCT_MARK(tm, 46);
         int csize = 0;
         for (int base = 0; base <= r; base += kOctBlock) {
             const int j = base + tid;
@@ -1438,6 +1506,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
             csize += t;
         }
         __syncthreads();
+        if (round == 0) OCT_MARK(tm, 47);
         int ksize = 0;
         for (int base = 0; base < size; base += kOctBlock) {
             const int i = base + tid;
@@ -1448,6 +1517,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
             ksize += t;
         }
         const int nsize = csize + ksize;
+        if (round == 0) OCT_MARK(tm, 48);
         if (nsize > ncap) {
             if (tid == 0) *out_cnt = -1;
             return;
@@ -1482,14 +1552,26 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
             }
         }
         __syncthreads();
+        if (round == 0) OCT_MARK(tm, 49);
         {
-            const int *bx = s.box(cur), *by = s.boy(cur), *aux = s.aux, *aux2 = s.aux2;
+            const int *aux = s.aux, *aux2 = s.aux2;
             const IT *qk = s.qk, *ncnt = s.cnt(nxt);
-            oct_sweep(K, NODE, nkeys, [=](int k, uint32_t kk, int node) {
-                const int np = aux2[node] > 0
-                                   ? (int)qk[node * 4 + quadrant(bx[node], by[node], key_x(kk), key_y(kk))]
-                                   : aux[node];
-                NODE[k] = (int)ncnt[np] >= 2 ? np : -1;
+            oct_sweep_q(K, NODE, nkeys, s.box(cur), s.boy(cur), [=](const int* k, const int* node, const int* q) {
+                int a2[kOctU], ca[kOctU], cq[kOctU], np[kOctU], c[kOctU];
+#pragma unroll
+                for (int u = 0; u < kOctU; ++u) {
+                    const int nd = max(node[u], 0);
+                    a2[u] = aux2[nd];
+                    ca[u] = aux[nd];
+                    cq[u] = (int)qk[nd * 4 + q[u]];
+                }
+#pragma unroll
+                for (int u = 0; u < kOctU; ++u) np[u] = node[u] < 0 ? 0 : a2[u] > 0 ? cq[u] : ca[u];
+#pragma unroll
+                for (int u = 0; u < kOctU; ++u) c[u] = (int)ncnt[np[u]];
+#pragma unroll
+                for (int u = 0; u < kOctU; ++u)
+                    if (node[u] >= 0) NODE[k[u]] = c[u] >= 2 ? np[u] : -1;
             });
         }
         __syncthreads();
@@ -1504,6 +1586,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
     // ---- retain the best key per node (740-759), emit in list order
     for (int i = tid; i < size; i += kOctBlock) s.s64[i] = 0ull;
     __syncthreads();
+    OCT_MARK(tm, 52);
     {
         unsigned long long* best = s.s64;
         oct_sweep(K, NODE, nkeys, [=](int k, uint32_t kk, int node) {
@@ -1511,6 +1594,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
         });
     }
     __syncthreads();
+    OCT_MARK(tm, 53);
     for (int i = tid; i < size; i += kOctBlock) {
         const int k = (int)s.cnt(cur)[i] == 1 ? (int)s.key(cur)[i]
                                           : (int)(0xffffffffu - (unsigned)(s.s64[i] & 0xffffffffu));
@@ -1558,7 +1642,7 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
     int* out_cnt = a.oct_cnt + f * a.geo.nlevels + level;
     long long* tm = nullptr;
 #ifdef ORBFE_OCT_TIMING
-    if (f < 256) tm = g_oct_t + (f * 16 + level) * 32;
+    if (f < 256) tm = g_oct_t + (f * 16 + level) * 64;
 #endif
     OCT_MARK(tm, 0);
 
@@ -1573,60 +1657,65 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
         return;
     }
     OCT_MARK(tm, 1);
-    // ---- 2. compact the cell outputs into original key order (LDS when they fit): a thread
-    // per cell copies the cell's keys to its scanned offset, loads batched 8 at a time
+    // ---- 2. compact the cell outputs into original key order (LDS when they fit).  A thread
+    // takes a cell of each of two 256-cell chunks: their counts and slots in one global round
+    // trip, the first 8 keys of both cells in a second (their addresses do not depend on the
+    // scans, which run meanwhile), then the stores at the scanned offsets; cells with more than
+    // 8 keys copy the rest in a loop.
     const bool in_lds = total <= a.lds_keys;
     uint32_t* lkeys = reinterpret_cast<uint32_t*>(region);  // LDS form: keys, node positions
     short* lnode = reinterpret_cast<short*>(lkeys + a.lds_keys);
     uint32_t* K = in_lds ? lkeys : a.keys + f * a.geo.key_total + L.key_off;
     const uint32_t* src = a.cell_keys + f * a.cell_cap_total;
     int nkeys = 0;
-    // the first two chunks' counts and slots are loaded together (one global round trip for
-    // the <= 2 * kOctBlock cells of most levels)
-    int n_next = 0;
-    long long slot_next = 0;
-    {
-        const int c = L.cell_begin + kOctBlock + tid;
-        if (c < L.cell_end) {
-            n_next = a.cell_cnt[f * a.ncells + c];
-            slot_next = a.cells[c].slot;
+    for (int base = L.cell_begin; base < L.cell_end; base += 2 * kOctBlock) {
+        int n[2];
+        long long slot[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int c = base + j * kOctBlock + tid;
+            n[j] = c < L.cell_end ? a.cell_cnt[f * a.ncells + c] : 0;
+            slot[j] = c < L.cell_end ? a.cells[c].slot : 0;
         }
-    }
-    for (int base = L.cell_begin; base < L.cell_end; base += kOctBlock) {
-        const int c = base + tid;
-        int n = 0;
-        long long slot = 0;
-        if (base == L.cell_begin) {
-            if (c < L.cell_end) {
-                n = a.cell_cnt[f * a.ncells + c];
-                slot = a.cells[c].slot;
-            }
-        } else if (base == L.cell_begin + kOctBlock) {
-            n = n_next;
-            slot = slot_next;
-        } else if (c < L.cell_end) {
-            n = a.cell_cnt[f * a.ncells + c];
-            slot = a.cells[c].slot;
-        }
-        int chunk_total;
-        const int off = nkeys + block_exclusive_scan<kOctBlock>(n, tmp, chunk_total);
-        for (int i0 = 0; i0 < n; i0 += 8) {
-            uint32_t v[8];
+        uint32_t v[2][8];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int i = 0; i < 8; ++i)
-                if (i0 + i < n) v[i] = src[slot + i0 + i];
-            // (uniform branch: a store through the selected pointer would be a flat store)
+                if (i < n[j]) v[j][i] = src[slot[j] + i];
+        int t0, t1;
+        const int o0 = nkeys + block_exclusive_scan<kOctBlock>(n[0], tmp, t0);
+        const int o1 = nkeys + t0 + block_exclusive_scan<kOctBlock>(n[1], tmp, t1);
+        const int off[2] = {o0, o1};
+        // (uniform branch: a store through the selected pointer would be a flat store)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
             if (in_lds) {
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
-                    if (i0 + i < n) lkeys[off + i0 + i] = v[i];
+                    if (i < n[j]) lkeys[off[j] + i] = v[j][i];
             } else {
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
-                    if (i0 + i < n) K[off + i0 + i] = v[i];
+                    if (i < n[j]) K[off[j] + i] = v[j][i];
+            }
+            for (int i0 = 8; i0 < n[j]; i0 += 8) {
+                uint32_t w[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    if (i0 + i < n[j]) w[i] = src[slot[j] + i0 + i];
+                if (in_lds) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        if (i0 + i < n[j]) lkeys[off[j] + i0 + i] = w[i];
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        if (i0 + i < n[j]) K[off[j] + i0 + i] = w[i];
+                }
             }
         }
-        nkeys += chunk_total;
+        nkeys += t0 + t1;
     }
     __syncthreads();
     OCT_MARK(tm, 2);
@@ -2591,7 +2680,7 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
 
 #ifdef ORBFE_OCT_TIMING
 extern "C" int orbfe_debug_oct_timing(long long* out, int n) {
-    n = n < 256 * 16 * 32 ? n : 256 * 16 * 32;
+    n = n < 256 * 16 * 64 ? n : 256 * 16 * 64;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(orbfe::g_oct_t), (size_t)n * sizeof(long long)) == hipSuccess ? 0 : -3;
 }
 #endif

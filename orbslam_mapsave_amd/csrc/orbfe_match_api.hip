@@ -97,6 +97,7 @@ struct orbfe_matcher {
     size_t pin_cap = 0, pin_used = 0;
     struct DnSeg { const uint8_t* src; uint8_t* dst; size_t bytes; };
     std::vector<DnSeg> dnq;  // downloads not yet gathered (zero-copy path)
+    std::vector<int32_t> init_neg;  // host-side -1 fill staged as an upload (SearchByBoW)
     std::vector<uint8_t*> pin_retired;  // outgrown buffers, freed once the stream is idle
     struct Pending { void* dst; const uint8_t* src; size_t bytes; };
     std::vector<Pending> pend;

@@ -44,9 +44,9 @@ def run():
                                desc.data_ptr(), n.data_ptr())
     e.synchronize()
     L = native.lib()
-    buf = np.zeros(256 * 16 * 32, np.int64)
+    buf = np.zeros(256 * 16 * 64, np.int64)
     assert L.orbfe_debug_oct_timing(C.c_void_p(buf.ctypes.data), len(buf)) == 0
-    t = buf.reshape(256, 16, 32)[:B, :8]
+    t = buf.reshape(256, 16, 64)[:B, :8]
     start = t[:, :, 0].min()
     res = {}
     for l in range(8):
@@ -61,6 +61,18 @@ def run():
                   "phase2+final": float(np.mean(x[:, 31] - p1_end)),
                   "total": d(0, 31),
                   "start_offset": float(np.mean(x[:, 0] - start)), "end_max": float(x[:, 31].max() - start)}
+        # fine marks (pass 1 of phase 1, round 0 of phase 2, init, final): mean step durations
+        def step(a, b):
+            ok = (x[:, a] > 0) & (x[:, b] > 0)
+            return float(np.mean(x[ok, b] - x[ok, a])) if ok.any() else None
+        res[l]["fine"] = {"init_clear": step(2, 56), "init_keys": step(56, 57), "init_scan": step(57, 58),
+                          "init_node": step(58, 3),
+                          "p1_clear": step(4, 32), "p1_sweep": step(32, 33), "p1_scan": step(33, 34),
+                          "p1_children": step(34, 35), "p1_sweep2": step(35, 5),
+                          "p2_flag": step(40, 41), "p2_sort": step(41, 43), "p2_sweep": step(43, 44),
+                          "p2_cut": step(44, 45), "p2_clear": step(45, 46), "p2_proc_scan": step(46, 47),
+                          "p2_kept_scan": step(47, 48), "p2_children": step(48, 49), "p2_sweep2": step(49, 12),
+                          "final_best": step(52, 53), "final_out": step(53, 31)}
     print(json.dumps(res, indent=1))
 
 
