@@ -203,6 +203,8 @@ struct orbfe_extractor {
         return plan.pyr_ok && (plan.pyr_use[which] || force_pyr) && use_pyr &&
                !(fused_blur && resize_blur) && plan.geo.nlevels >= 2;
     }
+    // ORBFE_RESIZE_TABLE=0: resize_kernel's horizontal pass by byte gathers (A/B)
+    bool table_off = std::getenv("ORBFE_RESIZE_TABLE") && std::strcmp(std::getenv("ORBFE_RESIZE_TABLE"), "0") == 0;
     bool graph_broken = std::getenv("ORBFE_NO_GRAPH") != nullptr;  // capture failed once (or
                                  // disabled for A/B runs): keep to the launch path
 
@@ -413,6 +415,7 @@ struct orbfe_extractor {
             ra.xt = xtab.as<int>() + g.xoff[l];
             ra.yt = ytab.as<int>() + g.yoff[l];
             ra.simd_xb = x86() ? sse2_body_resize(ra.dw) : 0;
+            ra.gtab = g.pyr_ok && !table_off ? ptab.as<uint4>() + g.gtab_off[l] : nullptr;
             if (rb) {  // the level and its blur (describe reads this level's blurred windows)
                 ra.lds_pitch = g.rb_pitch[l];
                 ra.lds_e = g.rb_lds_e[l];

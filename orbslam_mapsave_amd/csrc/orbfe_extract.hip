@@ -222,6 +222,47 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
     const int x = ox + 4 * tx;
     if (x >= a.dw) return;
     const int n = min(4, a.dw - x);
+    uint8_t* dst = const_cast<uint8_t*>(a.dst.base) + f * a.dst.fpitch;
+    if (a.gtab) {
+        // pyramid_kernel's horizontal pass (the level's column-group table): 3 dword LDS reads
+        // per source row, an 8-byte window by v_alignbyte, v_perm + v_dot2 per pixel, instead of
+        // 4 byte gathers, 4 multiplies and 2 adds per pixel
+        typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+        const uint4* gp = a.gtab + 3 * (x >> 2);
+        const uint4 g0 = gp[0], g1 = gp[1], g2 = gp[2];
+        const int base = (int)g0.x - sx0, wofs = base & ~3, sh = base & 3;
+        const uint32_t sel[4] = {g0.y, g0.z, g0.w, g1.x};
+        const us2 cf[4] = {__builtin_bit_cast(us2, g1.y), __builtin_bit_cast(us2, g1.z),
+                           __builtin_bit_cast(us2, g1.w), __builtin_bit_cast(us2, g2.x)};
+        auto hsum = [&](int r, uint32_t (&t)[4]) {
+            const uint32_t* row = reinterpret_cast<const uint32_t*>(rs_lds + r * P + wofs);
+            const uint32_t w0 = row[0], w1 = row[1], w2 = row[2];
+            const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh), hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                t[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(hi, lo, sel[k])), cf[k], 0u, false);
+        };
+#pragma unroll
+        for (int j = 0; j < kRsRPT; ++j) {
+            const int y = oy + kRsRPT * ty + j;
+            if (y >= a.dh) break;
+            const int ry0 = a.yt[3 * y] - sy0, ry1 = a.yt[3 * y + 1] - sy0, bb = a.yt[3 * y + 2];
+            const uint32_t b0 = (uint32_t)bb & 0xffffu, b1 = (uint32_t)bb >> 16;
+            uint32_t t0[4], t1[4];
+            hsum(ry0, t0);
+            hsum(ry1, t1);
+            uint32_t packed = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) packed |= resize_px<kX86>(t0[k], t1[k], b0, b1, x + k < a.simd_xb) << (8 * k);
+            uint8_t* d = dst + (long long)y * a.dst.pitch + x;
+            if (n == 4) {
+                *reinterpret_cast<uint32_t*>(d) = packed;
+            } else {
+                for (int k = 0; k < n; ++k) d[k] = (uint8_t)(packed >> (8 * k));
+            }
+        }
+        return;
+    }
     int x0[4], x1[4], a0[4], a1[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -232,7 +273,6 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
         a0[k] = aa & 0xffff;
         a1[k] = (int)((unsigned)aa >> 16);
     }
-    uint8_t* dst = const_cast<uint8_t*>(a.dst.base) + f * a.dst.fpitch;
 #pragma unroll
     for (int j = 0; j < kRsRPT; ++j) {
         const int y = oy + kRsRPT * ty + j;
@@ -1950,6 +1990,14 @@ constexpr int kDescBlock = kDescBlockSize;
 #define ORBFE_DESC_SKIP 0  // attribution experiments only (wrong descriptors): 1 blur passes,
 #endif                     // 2 IC, 4 samples, 8 window loads, 16 trig
 constexpr int kDescSkip = ORBFE_DESC_SKIP;
+// ORBFE_DESC_PIPE: the blur passes' LDS reads issued ahead of their arithmetic (1 row pass,
+// 2 column pass).  Measured no faster: 72 -> 85-93 VGPRs, 7 -> 5 waves per SIMD, describe
+// 0.2813 (off) / 0.2878 / 0.2915 / 0.283 ms (profiles/r03/experiments/describe_pipe.json)
+#ifndef ORBFE_DESC_PIPE
+#define ORBFE_DESC_PIPE 0
+#endif
+constexpr bool kDescPipe = (ORBFE_DESC_PIPE & 1) != 0;
+constexpr bool kDescPipeCol = (ORBFE_DESC_PIPE & 2) != 0;
 constexpr int kDescGroupSmall = 2;  // small batches (single-frame latency): 4x the waves
 // the group's slot -> level lookup assumes a group spans at most two levels, which holds while
 // a group is no larger than the smallest per-level slot capacity (ncap >= 20)
@@ -2226,16 +2274,14 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
             const int pr0 = lane / kBlurQ, q0 = lane - pr0 * kBlurQ;
             int q = q0;
             int ro = 2 * pr0 * kRawP + 4 * q0;  // byte offset of (row 2pr, quad q) in raw
-            for (int it = lane; it < kPairs * kBlurQ; it += 64) {
+            auto row_item = [&](const uint32_t (&w)[2][3], int it) {
                 uint32_t hh[2][4];
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
-                    const uint32_t* row = reinterpret_cast<const uint32_t*>(raw + ro + e * kRawP);
-                    const uint32_t w0 = row[0], w1 = row[1], w2 = row[2];
 #pragma unroll
                     for (int jj = 0; jj < 4; ++jj) {
-                        const uint32_t lo = jj < 3 ? __builtin_amdgcn_alignbyte(w1, w0, jj + 1) : w1;
-                        const uint32_t hi = jj < 3 ? __builtin_amdgcn_alignbyte(w2, w1, jj + 1) : w2;
+                        const uint32_t lo = jj < 3 ? __builtin_amdgcn_alignbyte(w[e][1], w[e][0], jj + 1) : w[e][1];
+                        const uint32_t hi = jj < 3 ? __builtin_amdgcn_alignbyte(w[e][2], w[e][1], jj + 1) : w[e][2];
                         hh[e][jj] = __builtin_amdgcn_udot4(hi, KHI, __builtin_amdgcn_udot4(lo, KLO, 0u, false), false);
                     }
                 }
@@ -2245,9 +2291,45 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
                                __builtin_amdgcn_perm(hh[1][1], hh[0][1], 0x05040100u),
                                __builtin_amdgcn_perm(hh[1][2], hh[0][2], 0x05040100u),
                                __builtin_amdgcn_perm(hh[1][3], hh[0][3], 0x05040100u));
-                const bool wrap = q >= kBlurQ - 4;
-                q += wrap ? 4 - kBlurQ : 4;
-                ro += wrap ? 7 * 2 * kRawP + 4 * (4 - kBlurQ) : 6 * 2 * kRawP + 16;
+            };
+            if constexpr (kDescPipe) {
+                // every item's six raw dwords are read before the first is used: one LDS round
+                // trip for the pass instead of one per 64 items
+                constexpr int kRowIt = (kPairs * kBlurQ + 63) / 64;  // 4
+                uint32_t w[kRowIt][2][3];
+#pragma unroll
+                for (int u = 0; u < kRowIt; ++u) {
+                    if (lane + 64 * u < kPairs * kBlurQ) {
+#pragma unroll
+                        for (int e = 0; e < 2; ++e) {
+                            const uint32_t* row = reinterpret_cast<const uint32_t*>(raw + ro + e * kRawP);
+                            w[u][e][0] = row[0];
+                            w[u][e][1] = row[1];
+                            w[u][e][2] = row[2];
+                        }
+                    }
+                    const bool wrap = q >= kBlurQ - 4;
+                    q += wrap ? 4 - kBlurQ : 4;
+                    ro += wrap ? 7 * 2 * kRawP + 4 * (4 - kBlurQ) : 6 * 2 * kRawP + 16;
+                }
+#pragma unroll
+                for (int u = 0; u < kRowIt; ++u)
+                    if (lane + 64 * u < kPairs * kBlurQ) row_item(w[u], lane + 64 * u);
+            } else {
+                for (int it = lane; it < kPairs * kBlurQ; it += 64) {
+                    uint32_t w[2][3];
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const uint32_t* row = reinterpret_cast<const uint32_t*>(raw + ro + e * kRawP);
+                        w[e][0] = row[0];
+                        w[e][1] = row[1];
+                        w[e][2] = row[2];
+                    }
+                    row_item(w, it);
+                    const bool wrap = q >= kBlurQ - 4;
+                    q += wrap ? 4 - kBlurQ : 4;
+                    ro += wrap ? 7 * 2 * kRawP + 4 * (4 - kBlurQ) : 6 * 2 * kRawP + 16;
+                }
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -2261,11 +2343,8 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
         const int xq = kX86 ? (int)__builtin_amdgcn_readlane(my_x0, j) - a.simd_xb[(int)__builtin_amdgcn_readlane(my_l, j)] : 0;
         // the sums carry 0x7fff (x86: + the half-to-even bit on the SIMD body) or 2^15
         constexpr uint32_t kRnd = kX86 ? 0x7fffu : 0x8000u;
-        for (int it = lane; it < ((kDescWinRows + 1) / 2) * kBlurQ; it += 64) {
-            const bool even = xq + 4 * cq < 0;
-            uint4 P4[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) P4[i] = *reinterpret_cast<const uint4*>(rowp + 4 * it + i * kRowpP);
+        auto col_item = [&](const uint4 (&P4)[4], int cq_, int wq_) {
+            const bool even = xq + 4 * cq_ < 0;
             uint32_t ev[4], od[4];
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
@@ -2283,14 +2362,50 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
                 if constexpr (kX86) u += blur_round_bit(u, even);
                 od[c] = min(u, 0xffffffu);
             }
-            *reinterpret_cast<uint32_t*>(wb + wq) =
+            *reinterpret_cast<uint32_t*>(wb + wq_) =
                 __builtin_amdgcn_perm(ev[1], ev[0], 0x0c0c0602u) | __builtin_amdgcn_perm(ev[3], ev[2], 0x06020c0cu);
-            if (wq < (kDescWinRows - 1) * kDescWinP)  // row 2jp + 1 exists: jp < 18
-                *reinterpret_cast<uint32_t*>(wb + wq + kDescWinP) =
+            if (wq_ < (kDescWinRows - 1) * kDescWinP)  // row 2jp + 1 exists: jp < 18
+                *reinterpret_cast<uint32_t*>(wb + wq_ + kDescWinP) =
                     __builtin_amdgcn_perm(od[1], od[0], 0x0c0c0602u) | __builtin_amdgcn_perm(od[3], od[2], 0x06020c0cu);
-            const bool wrap = cq >= kBlurQ - 4;
-            cq += wrap ? 4 - kBlurQ : 4;
-            wq += wrap ? 7 * 2 * kDescWinP + 4 * (4 - kBlurQ) : 6 * 2 * kDescWinP + 16;
+        };
+        constexpr int kColItems = ((kDescWinRows + 1) / 2) * kBlurQ;  // 190
+        if constexpr (kDescPipeCol) {
+            // two items' row pairs in flight: the next item's four b128 reads are issued before
+            // the current item's arithmetic
+            constexpr int kColIt = (kColItems + 63) / 64;  // 3
+            int cqs[kColIt], wqs[kColIt];
+#pragma unroll
+            for (int u = 0; u < kColIt; ++u) {
+                cqs[u] = cq;
+                wqs[u] = wq;
+                const bool wrap = cq >= kBlurQ - 4;
+                cq += wrap ? 4 - kBlurQ : 4;
+                wq += wrap ? 7 * 2 * kDescWinP + 4 * (4 - kBlurQ) : 6 * 2 * kDescWinP + 16;
+            }
+            uint4 Pc[4], Pn[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) Pc[i] = *reinterpret_cast<const uint4*>(rowp + 4 * lane + i * kRowpP);
+#pragma unroll
+            for (int u = 0; u < kColIt; ++u) {
+                const int itn = lane + 64 * (u + 1);
+                if (u + 1 < kColIt && itn < kColItems) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) Pn[i] = *reinterpret_cast<const uint4*>(rowp + 4 * itn + i * kRowpP);
+                }
+                if (lane + 64 * u < kColItems) col_item(Pc, cqs[u], wqs[u]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) Pc[i] = Pn[i];
+            }
+        } else {
+            for (int it = lane; it < kColItems; it += 64) {
+                uint4 P4[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) P4[i] = *reinterpret_cast<const uint4*>(rowp + 4 * it + i * kRowpP);
+                col_item(P4, cq, wq);
+                const bool wrap = cq >= kBlurQ - 4;
+                cq += wrap ? 4 - kBlurQ : 4;
+                wq += wrap ? 7 * 2 * kDescWinP + 4 * (4 - kBlurQ) : 6 * 2 * kDescWinP + 16;
+            }
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -2516,7 +2631,8 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
                 for (int ox = 0; ox < dw; ox += kRsTW) {
                     const int ex = std::min(ox + kRsTW, dw) - 1;
                     const int a0 = g.xtab[xb + 3 * ox] & ~3, a1 = g.xtab[xb + 3 * ex + 1];
-                    need_w = std::max(need_w, ((a1 - a0) >> 2) + 1);
+                    // + 2 dwords: the table path reads 3 dwords from a group's first source dword
+                    need_w = std::max(need_w, ((a1 - a0) >> 2) + 1 + 2);
                 }
                 {   // resize_blur_kernel: the source of the rows / columns 3 beyond the tile
                     int rb_rows = 0, rb_w = 0;

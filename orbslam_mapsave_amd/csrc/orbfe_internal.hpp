@@ -76,6 +76,7 @@ struct ResizeArgs {
     const int* xt;
     const int* yt;
     int simd_xb;           // x86 arithmetic: columns [0, simd_xb) use the SSE2 rounding (H5)
+    const uint4* gtab;     // resize_kernel: the level's pyramid_kernel column-group table, or null
     // resize_blur_kernel: the blurred level, its x86 SIMD-body bound (H6), taps, LDS offset of E
     LevelPtr bdst;
     int blur_xb;

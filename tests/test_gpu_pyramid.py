@@ -101,3 +101,30 @@ def test_per_level_path_identical(monkeypatch):
         n = outs[0][2][f]
         assert outs[0][0][f, :n].tobytes() == outs[1][0][f, :n].tobytes()
         assert np.array_equal(outs[0][1][f, :n], outs[1][1][f, :n])
+
+
+@pytest.mark.parametrize("size", [(640, 480), (1920, 1080), (643, 481), (97, 73)])
+@pytest.mark.parametrize("arith", ["scalar", "x86"])
+@pytest.mark.parametrize("table", ["1", "0"])
+def test_per_level_kernels_exact(size, arith, table, monkeypatch):
+    """The per-level path (ORBFE_PYR=0; the default at 1920x1080): resize_kernel's horizontal
+    pass from the column-group table (default) or by byte gathers (ORBFE_RESIZE_TABLE=0), and
+    the one-workgroup tail for batches, every level byte-exact in both readings."""
+    from orbslam_mapsave_amd.native import ORBextractor
+    monkeypatch.setenv("ORBFE_PYR", "0")
+    monkeypatch.setenv("ORBFE_RESIZE_TABLE", table)
+    w, h = size
+    nf = 2000 if w > 1000 else 1000
+    p = oracle.params(nf, 1.2, 8, 20, 7)
+    e = ORBextractor(nf, 1.2, 8, 20, 7, device=0, max_width=w, max_height=h)
+    var = oracle.VAR_H5_SSE2 if arith == "x86" else 0
+    if arith == "x86":
+        e.set_arithmetic(e.ARITH_X86_SIMD)
+    try:
+        imgs = np.stack([synthetic_frame(7 * w + s, w, h) for s in range(9)])
+        e.extract_batch(imgs)
+        _levels_exact(e, p, imgs[:3], var)
+        e(imgs[4])
+        _levels_exact(e, p, imgs[4:5], var)
+    finally:
+        e.close()
