@@ -292,6 +292,13 @@ __global__ __launch_bounds__(kBfBlock) void bf_match_kernel(
 // permutation common to A and B leaves the product unchanged): bit 8 q + b -> dword q, byte b,
 // low nibble; bit 8 q + 4 + b -> the high nibble.  Ranking as above, on f32 keys (min / med3 of
 // exact integers), converted to the 32-bit keys when a tile closes.
+// ORBFE_BF_WAVES: minimum waves per SIMD the FP4 kernel is compiled for.  At 3 it takes 135
+// VGPRs; 4 (<= 128 VGPRs, 3 spilled, all 1,024 blocks of a 256-frame step resident at once
+// instead of in 1.33 rounds) measured the same 103.2-103.9 us per launch
+// (profiles/r03/experiments/bf_waves.json)
+#ifndef ORBFE_BF_WAVES
+#define ORBFE_BF_WAVES 3
+#endif
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr float kBfNoneF = 32767.f;
@@ -326,7 +333,7 @@ struct BfLaneF {
         tb = ts = kBfNoneF;
     }
 };
-__global__ __launch_bounds__(kBfBlock) void bf_match_fp4_kernel(
+__global__ __launch_bounds__(kBfBlock, ORBFE_BF_WAVES) void bf_match_fp4_kernel(
     const uint8_t* q, long long q_pitch, const int* nq_arr, int nq_cap, const uint8_t* r,
     long long r_pitch, const int* nr_arr, int* out) {
     __shared__ i32x4 tile[2][8][kBfRefs];  // [buffer][descriptor dword][row]
