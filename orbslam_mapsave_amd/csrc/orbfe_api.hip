@@ -205,6 +205,8 @@ struct orbfe_extractor {
     }
     // ORBFE_RESIZE_TABLE=0: resize_kernel's horizontal pass by byte gathers (A/B)
     bool table_off = std::getenv("ORBFE_RESIZE_TABLE") && std::strcmp(std::getenv("ORBFE_RESIZE_TABLE"), "0") == 0;
+    // ORBFE_DESC_MFMA=0: describe blurs its raw windows on the VALU instead of the matrix cores
+    bool desc_mfma = !(std::getenv("ORBFE_DESC_MFMA") && std::strcmp(std::getenv("ORBFE_DESC_MFMA"), "0") == 0);
     bool graph_broken = std::getenv("ORBFE_NO_GRAPH") != nullptr;  // capture failed once (or
                                  // disabled for A/B runs): keep to the launch path
 
@@ -549,18 +551,26 @@ struct orbfe_extractor {
         const int group = n >= kDescSmallBatch ? kDescGroupSize : kDescGroupSmall;
         const int per_block = (kDescBlockSize / 64) * group;  // slots per workgroup
         const dim3 dgrid((g.geo.out_total + per_block - 1) / per_block, n);
-        const int variant = (group == kDescGroupSize ? 4 : 0) | (x86() ? 2 : 0) | (all_pre ? 1 : 0);
+        // window source: every level pre-blurred, some levels pre-blurred (VALU blur for the
+        // rest), or none (the matrix-core blur unless ORBFE_DESC_MFMA=0)
+        const int win = all_pre ? kWinPre : (da.pre_mask == 0u && desc_mfma ? kWinMfma : kWinValu);
+        da.frags = bslot.as<uint4>() + kDescFragOff;
+        const int variant = (group == kDescGroupSize ? 6 : 0) + (x86() ? 3 : 0) + win;
         switch (variant) {
-#define ORBFE_DESC_CASE(V, G, X, P) \
-            case V: ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, (describe_kernel<G, X, P>), dgrid, dim3(kDescBlockSize), 0, stream, da); break;
-            ORBFE_DESC_CASE(0, kDescGroupSmall, false, false)
-            ORBFE_DESC_CASE(1, kDescGroupSmall, false, true)
-            ORBFE_DESC_CASE(2, kDescGroupSmall, true, false)
-            ORBFE_DESC_CASE(3, kDescGroupSmall, true, true)
-            ORBFE_DESC_CASE(4, kDescGroupSize, false, false)
-            ORBFE_DESC_CASE(5, kDescGroupSize, false, true)
-            ORBFE_DESC_CASE(6, kDescGroupSize, true, false)
-            ORBFE_DESC_CASE(7, kDescGroupSize, true, true)
+#define ORBFE_DESC_CASE(V, G, X, W) \
+            case V: ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, (describe_kernel<G, X, W>), dgrid, dim3(kDescBlockSize), 0, stream, da); break;
+            ORBFE_DESC_CASE(0, kDescGroupSmall, false, kWinValu)
+            ORBFE_DESC_CASE(1, kDescGroupSmall, false, kWinPre)
+            ORBFE_DESC_CASE(2, kDescGroupSmall, false, kWinMfma)
+            ORBFE_DESC_CASE(3, kDescGroupSmall, true, kWinValu)
+            ORBFE_DESC_CASE(4, kDescGroupSmall, true, kWinPre)
+            ORBFE_DESC_CASE(5, kDescGroupSmall, true, kWinMfma)
+            ORBFE_DESC_CASE(6, kDescGroupSize, false, kWinValu)
+            ORBFE_DESC_CASE(7, kDescGroupSize, false, kWinPre)
+            ORBFE_DESC_CASE(8, kDescGroupSize, false, kWinMfma)
+            ORBFE_DESC_CASE(9, kDescGroupSize, true, kWinValu)
+            ORBFE_DESC_CASE(10, kDescGroupSize, true, kWinPre)
+            ORBFE_DESC_CASE(11, kDescGroupSize, true, kWinMfma)
 #undef ORBFE_DESC_CASE
         }
         ORBFE_HIP(hipGetLastError());

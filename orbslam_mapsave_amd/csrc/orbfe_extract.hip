@@ -1962,7 +1962,14 @@ void blur_items(const Geo& geo, std::vector<uint32_t>& s) {
 // [0, 64)  T[k = 16 hh + j][x = col]  = tap(k - 3 - x)          (row pass)
 // [64,128) V^T[slot 16 hh + j][y = col] = tap(rho - 3 - y), rho = (j & 3) + 8 (j >> 2) + 4 hh
 //          (the row pass's accumulator row held in register j of lane half hh)
-void blur_frags(const int taps[4], uint8_t out[128 * 16]) {
+// [128, 512): describe's window blur (v_mfma_i32_16x16x64_i8), lane l = n + 16 g, byte j:
+// [128 + 64 s, ...) s < 3: H_s[k = raw column 16 g + j][window column 16 s + n]
+//                          = tap(16 g + j - 16 s - n - 4)   (raw column = window column + 4)
+// [320 + 64 u, ...) u < 3: V_u[window row 16 u + n][k = R row 16 t + 4 g + i], j = 4 t + i
+//                          = tap(16 t + 4 g + i - 16 u - n - 3) for t < 3, 0 for j >= 12
+//                          (R row = window row + 3; the R rows are the row pass's accumulator
+//                          rows held in register i of tile t, in that K order)
+void blur_frags(const int taps[4], uint8_t out[512 * 16]) {
     auto tap = [&](int d) { return d < -3 || d > 3 ? 0 : taps[3 - (d < 0 ? -d : d)]; };
     for (int l = 0; l < 64; ++l) {
         const int col = l & 31, hh = l >> 5;
@@ -1971,6 +1978,16 @@ void blur_frags(const int taps[4], uint8_t out[128 * 16]) {
             const int rho = (j & 3) + 8 * (j >> 2) + 4 * hh;
             out[16 * (64 + l) + j] = (uint8_t)tap(rho - 3 - col);
         }
+    }
+    for (int l = 0; l < 64; ++l) {
+        const int n = l & 15, g = l >> 4;
+        for (int q = 0; q < 3; ++q)
+            for (int j = 0; j < 16; ++j) {
+                const int t = j >> 2, i = j & 3;
+                out[16 * (kDescFragOff + 64 * q + l) + j] = (uint8_t)tap(16 * g + j - 16 * q - n - 4);
+                out[16 * (kDescFragOff + 192 + 64 * q + l) + j] =
+                    (uint8_t)(t < 3 ? tap(16 * t + 4 * g + i - 16 * q - n - 3) : 0);
+            }
     }
 }
 
@@ -1998,6 +2015,18 @@ constexpr int kDescSkip = ORBFE_DESC_SKIP;
 #endif
 constexpr bool kDescPipe = (ORBFE_DESC_PIPE & 1) != 0;
 constexpr bool kDescPipeCol = (ORBFE_DESC_PIPE & 2) != 0;
+// ORBFE_DESC_FRAG_LDS: the matrix-core blur's constant fragments read from LDS at each use
+// instead of held in registers (1 H, 2 V at each use, 4 V once per N-tile).  With
+// ORBFE_DESC_WAVES (the register budget: waves per SIMD) the default pair measured best:
+// describe 0.2572 ms (in registers, 90 VGPRs, 5 waves) -> 0.2446 (both from LDS, 72 VGPRs,
+// 7 waves); 8 waves spill (profiles/r03/experiments/describe_mfma.json)
+#ifndef ORBFE_DESC_FRAG_LDS
+#define ORBFE_DESC_FRAG_LDS 3
+#endif
+constexpr int kFragLds = ORBFE_DESC_FRAG_LDS;
+#ifndef ORBFE_DESC_WAVES
+#define ORBFE_DESC_WAVES 7
+#endif
 constexpr int kDescGroupSmall = 2;  // small batches (single-frame latency): 4x the waves
 // the group's slot -> level lookup assumes a group spans at most two levels, which holds while
 // a group is no larger than the smallest per-level slot capacity (ncap >= 20)
@@ -2007,11 +2036,16 @@ constexpr int kDescWinR = 18;                        // rotated pattern radius b
 constexpr int kDescWinRows = 2 * kDescWinR + 1;      // 37
 constexpr int kDescWinP = 48;                        // bytes per window row (3 x 16)
 constexpr int kDescWinBytes = kDescWinRows * kDescWinP;
+constexpr int kMwP = 40;            // kWinMfma window: bytes per column (window rows 0..39)
 typedef float float2v __attribute__((ext_vector_type(2)));
-// kPre: the levels were blurred by K4 (a.blur); the wave copies each keypoint's 37-row
-// blurred window straight into LDS instead of blurring a raw window.
-template <int kDescGroup, bool kX86, bool kPre>
-__global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
+// kWin (window source): kWinPre — the levels were blurred by K4 (a.blur); the wave copies each
+// keypoint's 37-row blurred window straight into LDS instead of blurring a raw window.
+// kWinValu — the raw window is staged in LDS and blurred by v_dot4 / v_dot2 passes (levels in
+// pre_mask read blurred windows).  kWinMfma — the raw window goes from its global loads
+// straight into i8 MFMA A fragments and both passes run on the matrix cores (below).
+template <int kDescGroup, bool kX86, int kWin>
+__global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? ORBFE_DESC_WAVES : 1) void describe_kernel(DescArgs a) {
+    constexpr bool kPre = kWin == kWinPre, kMfma = kWin == kWinMfma;
     int bx, f;
     xcd_block(bx, f);
     const int lane = threadIdx.x & 63;
@@ -2021,6 +2055,12 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
         for (int l = 0; l < a.nlevels; ++l) n += max(cnt[l], 0);
         a.n_out[f] = n;  // the true count: entries past kps_cap are not written (truncation
                          // is visible to the caller as n_out > kps_cap)
+    }
+    typedef int i32x4m __attribute__((ext_vector_type(4)));
+    __shared__ uint4 frag_lds[kMfma && kFragLds ? 384 : 1];
+    if constexpr (kMfma && kFragLds != 0) {  // before any wave leaves
+        for (int i = threadIdx.x; i < 384; i += kDescBlock) frag_lds[i] = a.frags[i];
+        __syncthreads();
     }
     const int s0 = (bx * (kDescBlock / 64) + (threadIdx.x >> 6)) * kDescGroup;
     if (s0 >= a.out_total) return;
@@ -2151,7 +2191,9 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
         const int x = key_x((uint32_t)my_key);
         const int x0 = (x - kDescWinR) & ~3;
         my_x0 = x0;
-        my_kc = (uint32_t)(kDescWinR * kDescWinP + (x - x0)) - 0x400000u * kDescWinP - 0x4b400000u;
+        // (kMfma: the window is stored column-major, column (x - x0) + rx at byte 40 (x - x0 + rx))
+        my_kc = kMfma ? (uint32_t)(kDescWinR + (x - x0) * kMwP) - 0x400000u * kMwP - 0x4b400000u
+                      : (uint32_t)(kDescWinR * kDescWinP + (x - x0)) - 0x400000u * kDescWinP - 0x4b400000u;
     }
     // Pattern pairs lane + 64 q as 4 packed int8 (x1, y1, x2, y2), widened to float per
     // keypoint: 4 VGPRs held across the loop instead of 16 (and the compiler's hoisted products
@@ -2168,11 +2210,14 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
     constexpr int kBlurQ = 10;
     // The raw window is dead once the row pass has read it and the blurred window is written
     // after that (same wave, LDS ops in order), so the two share one buffer.
-    constexpr int kRawWinBytes = kPre ? kDescWinBytes
-                                      : kRawRows * kRawP > kDescWinBytes ? kRawRows * kRawP : kDescWinBytes;
+    // kMfma: the blurred window's columns 0..39, rows 0..39 column-major (the tiles' rows 40..
+    // and columns 40.. are not stored)
+    constexpr int kRawWinBytes = kMfma ? kMwP * kMwP
+                                : kPre ? kDescWinBytes
+                                       : kRawRows * kRawP > kDescWinBytes ? kRawRows * kRawP : kDescWinBytes;
     __shared__ __attribute__((aligned(16))) uint8_t raw_all[kDescBlock / 64][kRawWinBytes];
     constexpr int kRowpP = 4 * kBlurQ;                 // u16 row-pair pitch: window cols 0..39
-    __shared__ __attribute__((aligned(16))) uint32_t rowp_all[kDescBlock / 64][kPre ? 4 : kPairs * kRowpP];
+    __shared__ __attribute__((aligned(16))) uint32_t rowp_all[kDescBlock / 64][kPre || kMfma ? 4 : kPairs * kRowpP];
     uint8_t* raw = raw_all[threadIdx.x >> 6];
     uint32_t* rowp = rowp_all[threadIdx.x >> 6];
     uint8_t* wb = raw;
@@ -2185,7 +2230,7 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
               T0H = us2{0, k0}, T12 = us2{k1, k2}, T32 = us2{k3, k2}, T10 = us2{k1, k0};
     // raw chunk c = lane + 64 i (i < 3, c < 43 * 3): row c / 3, 16-byte part c % 3
     uint4 rv[3];
-    auto load_raw = [&](int j) {
+    auto load_raw = [&](int j) __attribute__((always_inline)) {
         const int kl = __builtin_amdgcn_readlane(my_l, j);
         const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane(my_key, j);
         const int x = key_x(kk), y = key_y(kk), x0 = (x - kDescWinR) & ~3;
@@ -2215,7 +2260,7 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
     // part c % 3, at LDS byte 16 c.  Keypoints lie >= 19 px inside their level, so rows
     // y - 18 .. y + 18 are level rows; the bytes of a row past the level width (< 16, never
     // sampled) stay inside the slab (the last row read is h - 2).
-    auto load_win = [&](int j) {
+    auto load_win = [&](int j) __attribute__((always_inline)) {
         const int kl = __builtin_amdgcn_readlane(my_l, j);
         const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane(my_key, j);
         const int x = key_x(kk), y = key_y(kk), x0 = (x - kDescWinR) & ~3;
@@ -2231,21 +2276,143 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
     // a keypoint of a level whose bit is set in pre_mask reads its blurred window (the level
     // was blurred by the pyramid kernels); the others blur a raw window here.  The choice is
     // wave-uniform per keypoint.
-    auto is_pre = [&](int j) {
-        return kPre || ((a.pre_mask >> __builtin_amdgcn_readlane(my_l, j)) & 1u) != 0u;
+    // kMfma: A fragment t of the row pass = raw row 16 t + (lane & 15), raw columns 16 g .. 16 g
+    // + 15 (g = lane >> 4 < 3; the g = 3 K slots meet zero weights for every sampled column,
+    // rows 43.. feed only window rows >= 37): one 16-byte load per tile straight into registers
+    // (staging them in LDS with global_load_lds instead measured no faster: describe 0.2488 vs
+    // 0.2467 ms, profiles/r03/experiments/describe_mfma.json)
+    auto load_frag = [&](int j) __attribute__((always_inline)) {
+        const int kl = __builtin_amdgcn_readlane(my_l, j);
+        const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane(my_key, j);
+        const int x = key_x(kk), y = key_y(kk), x0 = (x - kDescWinR) & ~3;
+        const LevelPtr pp = a.pyr[kl];
+        const int lw = a.w[kl], lh = a.h[kl];
+        const uint8_t* fb = pp.base + f * pp.fpitch;
+        const bool fast = x0 - 4 >= 0 && x0 + 44 <= pp.pitch && x - 21 >= 0 && x + 21 < lw &&
+                          y - 21 >= 0 && y + 21 < lh;
+        const int g = lane >> 4;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const int r = 16 * t + (lane & 15);
+            rv[t] = make_uint4(0u, 0u, 0u, 0u);
+            if (r >= kRawRows - 1 || g == 3 || (kDescSkip & 8)) continue;
+            if (fast) {
+                rv[t] = load16_a4(fb + (long long)(y - 21 + r) * pp.pitch + x0 - 4 + 16 * g);
+            } else {
+                const uint8_t* row = fb + (long long)reflect101(y - 21 + r, lh) * pp.pitch;
+                uint32_t bb[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    bb[k >> 2] |= (uint32_t)row[reflect101(x0 - 4 + 16 * g + k, lw)] << (8 * (k & 3));
+                rv[t] = make_uint4(bb[0], bb[1], bb[2], bb[3]);
+            }
+        }
     };
-    auto load_kp = [&](int j) {
-        if (is_pre(j)) {
+    auto is_pre = [&](int j) __attribute__((always_inline)) {
+        return kPre || (!kMfma && ((a.pre_mask >> __builtin_amdgcn_readlane(my_l, j)) & 1u) != 0u);
+    };
+    auto load_kp = [&](int j) __attribute__((always_inline)) {
+        if constexpr (kMfma) {
+            load_frag(j);
+        } else if (is_pre(j)) {
             load_win(j);
             rv[2] = make_uint4(0u, 0u, 0u, 0u);
         } else {
             load_raw(j);
         }
     };
+    // kMfma constants: the row pass's B fragments H_s (window columns 16 s ..) and the column
+    // pass's A fragments V_u (window rows 16 u ..), built on the host (blur_frags)
+    i32x4m Hf[3], Vf[3];
+    if constexpr (kMfma) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const uint4 h = a.frags[64 * q + lane], v = a.frags[192 + 64 * q + lane];
+            Hf[q] = i32x4m{(int)h.x, (int)h.y, (int)h.z, (int)h.w};
+            Vf[q] = i32x4m{(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+        }
+    }
+    // (the LDS offset made opaque per use, so the reads are not hoisted back into registers)
+    auto frag = [&](int q, const i32x4m& held, bool from_lds) __attribute__((always_inline)) {
+        if (!from_lds) return held;
+        int o = 64 * q + lane;
+        asm volatile("" : "+v"(o));
+        const uint4 h = frag_lds[o];
+        return i32x4m{(int)h.x, (int)h.y, (int)h.z, (int)h.w};
+    };
     load_kp(__ffsll((long long)vmask) - 1);
     for (unsigned long long m = vmask; m; m &= m - 1) {
         const int j = __ffsll((long long)m) - 1;
         const bool pre_j = is_pre(j);
+        if constexpr (kMfma) {
+            // Both passes as banded i8 GEMMs (v_mfma_i32_16x16x64_i8), every sum exact in i32
+            // (K4's integer passes, App. A.2; S = the taps' sum):
+            //   row pass     R_t,s = (raw - 128) . H_s + 128 S + 2^15     (M = raw rows 16 t ..)
+            //   column pass  O_u,s = (V_u . (lo - 128) + 128 * 257 S + rnd) + ((V_u . (hi - 128)) << 8)
+            // where lo / hi are the bytes of R (<= 255 S < 2^16) and the + 2^15 makes byte 1 of
+            // the accumulator hi ^ 0x80 already.  R_t,s has window column 16 s + (lane & 15) on
+            // the lane and raw rows 16 t + 4 g + i in its registers, so packing its low / high
+            // bytes gives the column pass's B operand with no lane movement (the K order V_u
+            // follows).  O_u,s has the same shape: its 4 window rows of one column are one
+            // dword of the column-major window.
+            const int S = 2 * (a.taps[0] + a.taps[1] + a.taps[2]) + a.taps[3];
+            constexpr uint32_t kRndM = kX86 ? 0x7fffu : 0x8000u;
+            const int ci = 128 * S + 0x8000;
+            const uint32_t kC2 = 128u * 257u * (uint32_t)S + kRndM;
+            const i32x4m Ci = i32x4m{ci, ci, ci, ci}, Z = i32x4m{0, 0, 0, 0};
+            const i32x4m Kc = i32x4m{(int)kC2, (int)kC2, (int)kC2, (int)kC2};
+            i32x4m A[3];
+            const int n = lane & 15, g = lane >> 4;
+#pragma unroll
+            for (int t = 0; t < 3; ++t)
+                A[t] = i32x4m{(int)(rv[t].x ^ 0x80808080u), (int)(rv[t].y ^ 0x80808080u),
+                              (int)(rv[t].z ^ 0x80808080u), (int)(rv[t].w ^ 0x80808080u)};
+            const unsigned long long rest = m & (m - 1);
+            if (rest) load_kp(__ffsll((long long)rest) - 1);  // next keypoint's window in flight
+            const int xs = kX86 ? (int)__builtin_amdgcn_readlane(my_x0, j) + (lane & 15) -
+                                      a.simd_xb[(int)__builtin_amdgcn_readlane(my_l, j)]
+                                : 0;
+#pragma unroll
+            for (int s = 0; s < 3; ++s) {
+                i32x4m Blo, Bhi;
+                const i32x4m Hs = frag(s, Hf[s], (kFragLds & 1) != 0);
+#pragma unroll
+                for (int t = 0; t < 3; ++t) {
+                    const i32x4m R = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[t], Hs, Ci, 0, 0, 0);
+                    const uint32_t x01 = __builtin_amdgcn_perm((uint32_t)R[1], (uint32_t)R[0], 0x05010400u);
+                    const uint32_t x23 = __builtin_amdgcn_perm((uint32_t)R[3], (uint32_t)R[2], 0x05010400u);
+                    Blo[t] = (int)(__builtin_amdgcn_perm(x23, x01, 0x05040100u) ^ 0x80808080u);
+                    Bhi[t] = (int)__builtin_amdgcn_perm(x23, x01, 0x07060302u);
+                }
+                Blo[3] = 0;
+                Bhi[3] = 0;
+                const bool even = xs + 16 * s < 0;  // x86: column in the SIMD body
+                i32x4m Vs[3];  // (kFragLds & 4: the three V fragments read once per N-tile)
+                if constexpr ((kFragLds & 4) != 0) {
+#pragma unroll
+                    for (int u = 0; u < 3; ++u) Vs[u] = frag(3 + u, Vf[u], true);
+                }
+#pragma unroll
+                for (int u = 0; u < 3; ++u) {
+                    const i32x4m Vu = (kFragLds & 4) ? Vs[u] : frag(3 + u, Vf[u], (kFragLds & 2) != 0);
+                    // the two planes' products are independent; the hi one shifted in after
+                    const i32x4m Dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(Vu, Bhi, Z, 0, 0, 0);
+                    const i32x4m Dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(Vu, Blo, Kc, 0, 0, 0);
+                    uint32_t s4[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        uint32_t sm = ((uint32_t)Dh[i] << 8) + (uint32_t)Dl[i];
+                        if constexpr (kX86) sm += blur_round_bit(sm, even);
+                        s4[i] = min(sm, 0xffffffu);  // byte 2 = min(sum >> 16, 255)
+                    }
+                    if ((s < 2 || n < 8) && (u < 2 || g < 2))  // window columns / rows < 40
+                        *reinterpret_cast<uint32_t*>(wb + (16 * s + n) * kMwP + 16 * u + 4 * g) =
+                            __builtin_amdgcn_perm(s4[1], s4[0], 0x0c0c0602u) | __builtin_amdgcn_perm(s4[3], s4[2], 0x06020c0cu);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        } else {
         if (pre_j) {
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
@@ -2410,6 +2577,7 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         }  // !kPre
+        }  // !kMfma
         const float cj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ca), j));
         const float sj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, sa), j));
         const uint32_t kc = (uint32_t)__builtin_amdgcn_readlane((int)my_kc, j);
@@ -2439,8 +2607,13 @@ __global__ __launch_bounds__(kDescBlock) void describe_kernel(DescArgs a) {
                 i0[q] = (int)(__float_as_uint(r0y) ^ __float_as_uint(r1x));
                 i1[q] = (int)(__float_as_uint(r1y) + kc);
             } else {
+            if constexpr (kMfma) {  // column-major window
+            i0[q] = wb[__umul24(__float_as_uint(r0x), (uint32_t)kMwP) + __float_as_uint(r0y) + kc];
+            i1[q] = wb[__umul24(__float_as_uint(r1x), (uint32_t)kMwP) + __float_as_uint(r1y) + kc];
+            } else {
             i0[q] = wb[__umul24(__float_as_uint(r0y), (uint32_t)kDescWinP) + __float_as_uint(r0x) + kc];
             i1[q] = wb[__umul24(__float_as_uint(r1y), (uint32_t)kDescWinP) + __float_as_uint(r1x) + kc];
+            }
             }
         }
         unsigned long long words[4];

@@ -168,6 +168,7 @@ struct DescArgs {
     int simd_xb[kMaxLevels];  // as BlurArgs::simd_xb, for the fused per-keypoint blur
     LevelPtr blur[kMaxLevels];  // blurred levels (K4 output), read by the pre-blurred variant
     uint32_t pre_mask;          // levels whose blurred plane exists (bit l): windows read from it
+    const uint4* frags;         // the matrix-core window blur: H / V fragments (blur_frags, 128..)
 };
 
 // Pixels [0, n) of a w-pixel row that OpenCV 3.3's x86 SSE2 vertical kernels produce (the rest
@@ -242,9 +243,14 @@ constexpr int kFastPitch = 48;  // fast_kernel<kFastPitch>: ROI pitch known at c
 __global__ void octree_kernel(OctArgs);
 template <bool kX86> __global__ void blur_mfma_kernel(BlurArgs);
 void blur_items(const Geo& geo, std::vector<uint32_t>& s);
-void blur_frags(const int taps[4], uint8_t out[128 * 16]);
-constexpr size_t kBlurFragBytes = 128 * 16;
-template <int kDescGroup, bool kX86> __global__ void describe_kernel(DescArgs);
+// constant MFMA fragments: [0, 128) blur_mfma_kernel's, [128, 512) describe's window blur
+void blur_frags(const int taps[4], uint8_t out[512 * 16]);
+constexpr size_t kBlurFragBytes = 512 * 16;
+constexpr int kDescFragOff = 128;  // uint4 index of describe's fragments
+// describe window source: raw window blurred on the VALU (pre_mask levels read blurred
+// windows), every level pre-blurred, or the raw window blurred on the matrix cores
+enum { kWinValu = 0, kWinPre = 1, kWinMfma = 2 };
+template <int kDescGroup, bool kX86, int kWin> __global__ void describe_kernel(DescArgs);
 extern __constant__ int c_umax[16];
 
 // pyramid_kernel band plans: LDS per workgroup for large batches (80 KB: two 1024-thread
