@@ -2024,6 +2024,10 @@ constexpr bool kDescPipeCol = (ORBFE_DESC_PIPE & 2) != 0;
 #define ORBFE_DESC_FRAG_LDS 3
 #endif
 constexpr int kFragLds = ORBFE_DESC_FRAG_LDS;
+#ifndef ORBFE_DESC_LATE_STORE
+#define ORBFE_DESC_LATE_STORE 1  // descriptor words stored once per wave, after the keypoint loop
+#endif
+constexpr bool kDescLateStore = ORBFE_DESC_LATE_STORE != 0;
 #ifndef ORBFE_DESC_WAVES
 #define ORBFE_DESC_WAVES 7
 #endif
@@ -2046,6 +2050,7 @@ typedef float float2v __attribute__((ext_vector_type(2)));
 template <int kDescGroup, bool kX86, int kWin>
 __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? ORBFE_DESC_WAVES : 1) void describe_kernel(DescArgs a) {
     constexpr bool kPre = kWin == kWinPre, kMfma = kWin == kWinMfma;
+    constexpr bool kLate = kDescLateStore && kMfma;
     int bx, f;
     xcd_block(bx, f);
     const int lane = threadIdx.x & 63;
@@ -2095,73 +2100,6 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? ORBFE_DESC_WAVES : 1
     }
     const unsigned long long vmask = __ballot(valid);
     if (!vmask) return;
-
-    // 1. IC moments.  Lane (r = lane >> 1, hh = lane & 1): row v = r - 15, columns
-    //    u = -15 + 16 hh .. +15 (u = 16 never lies in the disc).
-    const int r = lane >> 1, hh = lane & 1, v = r - 15;
-    const int av = v < 0 ? -v : v;
-    const int ulim = r < 31 ? c_umax[min(av, 15)] : -1;
-    uint32_t wu[4], w1[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        uint32_t x = 0, y = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int u = -15 + 16 * hh + 4 * d + b;
-            const bool in = (u < 0 ? -u : u) <= ulim;
-            x |= (in ? (uint32_t)(u + 16) : 0u) << (8 * b);
-            y |= (in ? 1u : 0u) << (8 * b);
-        }
-        wu[d] = x;
-        w1[d] = y;
-    }
-    // the 16-byte row loads of kIcBatch keypoints are issued before their first reduction
-    // (4 at a time: 16 VGPRs of loads in flight, not 32)
-    constexpr int kIcBatch = kDescGroup < 4 ? kDescGroup : 4;
-    int M10 = 0, M01 = 0;
-#pragma unroll
-    for (int j0 = 0; j0 < kDescGroup; j0 += kIcBatch) {
-        uint4 px[kIcBatch];
-#pragma unroll
-        for (int jb = 0; jb < kIcBatch; ++jb) {
-            const int j = j0 + jb;
-            px[jb] = make_uint4(0u, 0u, 0u, 0u);
-            if (!(kDescSkip & 2) && ((vmask >> j) & 1) && r < 31) {
-                const int kl = __builtin_amdgcn_readlane(my_l, j);
-                const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane(my_key, j);
-                const LevelPtr pp = a.pyr[kl];
-                const uint8_t* row = pp.base + f * pp.fpitch + (long long)(key_y(kk) + v) * pp.pitch +
-                                     key_x(kk) - 15 + 16 * hh;
-                px[jb] = load16_a1(row);
-            }
-        }
-#pragma unroll
-        for (int jb = 0; jb < kIcBatch; ++jb) {
-            const int j = j0 + jb;
-            const uint4 p4 = px[jb];
-            const int su = (int)__builtin_amdgcn_udot4(p4.x, wu[0], __builtin_amdgcn_udot4(p4.y, wu[1],
-                           __builtin_amdgcn_udot4(p4.z, wu[2], __builtin_amdgcn_udot4(p4.w, wu[3], 0u, false), false), false), false);
-            const int s = (int)__builtin_amdgcn_udot4(p4.x, w1[0], __builtin_amdgcn_udot4(p4.y, w1[1],
-                          __builtin_amdgcn_udot4(p4.z, w1[2], __builtin_amdgcn_udot4(p4.w, w1[3], 0u, false), false), false), false);
-            const int m10 = wave_sum(su - 16 * s), m01 = wave_sum(v * s);
-            if (lane == j) {
-                M10 = m10;
-                M01 = m01;
-            }
-        }
-    }
-
-    // 2. angle and its rotation, one keypoint per lane
-    const float angle = fast_atan2((float)M01, (float)M10);
-    const float ang = angle * (float)(3.14159265358979323846 / 180.f);
-    float ca = 1.f, sa = 0.f;
-    if (valid && !(kDescSkip & 16)) {
-        // one shared argument reduction (OCML's sin and cos are the two halves of its sincos)
-        double sd, cd;
-        sincos((double)ang, &sd, &cd);
-        ca = (float)cd;
-        sa = (float)sd;
-    }
 
     // 3. rBRIEF: lane handles pairs lane + 64 q; bit k of byte i = pair 8 i + k (122-143).
     // Rotated pattern points stay within 13 sqrt 2 < 18.5 px of the keypoint, so keypoint j's
@@ -2299,11 +2237,13 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? ORBFE_DESC_WAVES : 1
             if (fast) {
                 rv[t] = load16_a4(fb + (long long)(y - 21 + r) * pp.pitch + x0 - 4 + 16 * g);
             } else {
-                const uint8_t* row = fb + (long long)reflect101(y - 21 + r, lh) * pp.pitch;
+                // keypoints lie >= 19 px inside their level (>= 39 px wide and high), so the
+                // window overshoots an edge by at most 2 rows / 6 columns: one reflection
+                const uint8_t* row = fb + (long long)reflect101_1(y - 21 + r, lh) * pp.pitch;
                 uint32_t bb[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
                 for (int k = 0; k < 16; ++k)
-                    bb[k >> 2] |= (uint32_t)row[reflect101(x0 - 4 + 16 * g + k, lw)] << (8 * (k & 3));
+                    bb[k >> 2] |= (uint32_t)row[reflect101_1(x0 - 4 + 16 * g + k, lw)] << (8 * (k & 3));
                 rv[t] = make_uint4(bb[0], bb[1], bb[2], bb[3]);
             }
         }
@@ -2340,7 +2280,76 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? ORBFE_DESC_WAVES : 1
         const uint4 h = frag_lds[o];
         return i32x4m{(int)h.x, (int)h.y, (int)h.z, (int)h.w};
     };
+    unsigned long long dacc = 0;
     load_kp(__ffsll((long long)vmask) - 1);
+    // (the first window's loads are in flight during the IC moments and the trig)
+    // 1. IC moments.  Lane (r = lane >> 1, hh = lane & 1): row v = r - 15, columns
+    //    u = -15 + 16 hh .. +15 (u = 16 never lies in the disc).
+    const int r = lane >> 1, hh = lane & 1, v = r - 15;
+    const int av = v < 0 ? -v : v;
+    const int ulim = r < 31 ? c_umax[min(av, 15)] : -1;
+    uint32_t wu[4], w1[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        uint32_t x = 0, y = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int u = -15 + 16 * hh + 4 * d + b;
+            const bool in = (u < 0 ? -u : u) <= ulim;
+            x |= (in ? (uint32_t)(u + 16) : 0u) << (8 * b);
+            y |= (in ? 1u : 0u) << (8 * b);
+        }
+        wu[d] = x;
+        w1[d] = y;
+    }
+    // the 16-byte row loads of kIcBatch keypoints are issued before their first reduction
+    // (4 at a time: 16 VGPRs of loads in flight, not 32)
+    constexpr int kIcBatch = kDescGroup < 4 ? kDescGroup : 4;
+    int M10 = 0, M01 = 0;
+#pragma unroll
+    for (int j0 = 0; j0 < kDescGroup; j0 += kIcBatch) {
+        uint4 px[kIcBatch];
+#pragma unroll
+        for (int jb = 0; jb < kIcBatch; ++jb) {
+            const int j = j0 + jb;
+            px[jb] = make_uint4(0u, 0u, 0u, 0u);
+            if (!(kDescSkip & 2) && ((vmask >> j) & 1) && r < 31) {
+                const int kl = __builtin_amdgcn_readlane(my_l, j);
+                const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane(my_key, j);
+                const LevelPtr pp = a.pyr[kl];
+                const uint8_t* row = pp.base + f * pp.fpitch + (long long)(key_y(kk) + v) * pp.pitch +
+                                     key_x(kk) - 15 + 16 * hh;
+                px[jb] = load16_a1(row);
+            }
+        }
+#pragma unroll
+        for (int jb = 0; jb < kIcBatch; ++jb) {
+            const int j = j0 + jb;
+            const uint4 p4 = px[jb];
+            const int su = (int)__builtin_amdgcn_udot4(p4.x, wu[0], __builtin_amdgcn_udot4(p4.y, wu[1],
+                           __builtin_amdgcn_udot4(p4.z, wu[2], __builtin_amdgcn_udot4(p4.w, wu[3], 0u, false), false), false), false);
+            const int s = (int)__builtin_amdgcn_udot4(p4.x, w1[0], __builtin_amdgcn_udot4(p4.y, w1[1],
+                          __builtin_amdgcn_udot4(p4.z, w1[2], __builtin_amdgcn_udot4(p4.w, w1[3], 0u, false), false), false), false);
+            const int m10 = wave_sum(su - 16 * s), m01 = wave_sum(v * s);
+            if (lane == j) {
+                M10 = m10;
+                M01 = m01;
+            }
+        }
+    }
+
+    // 2. angle and its rotation, one keypoint per lane
+    const float angle = fast_atan2((float)M01, (float)M10);
+    const float ang = angle * (float)(3.14159265358979323846 / 180.f);
+    float ca = 1.f, sa = 0.f;
+    if (valid && !(kDescSkip & 16)) {
+        // one shared argument reduction (OCML's sin and cos are the two halves of its sincos)
+        double sd, cd;
+        sincos((double)ang, &sd, &cd);
+        ca = (float)cd;
+        sa = (float)sd;
+    }
+
     for (unsigned long long m = vmask; m; m &= m - 1) {
         const int j = __ffsll((long long)m) - 1;
         const bool pre_j = is_pre(j);
@@ -2619,13 +2628,26 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? ORBFE_DESC_WAVES : 1
         unsigned long long words[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) words[q] = __ballot(i0[q] < i1[q]);
-        const long long outi = (long long)f * a.kps_cap + __builtin_amdgcn_readlane(my_o, j);
-        if (lane < 4) {
-            const unsigned long long wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
-            reinterpret_cast<unsigned long long*>(a.desc + outi * 32)[lane] = wv;
+        if constexpr (kLate) {
+            // lanes 4 j .. 4 j + 3 keep keypoint j's four words for one store after the loop
+            // (no store in flight when the next window's loads are waited for)
+            if ((lane >> 2) == j)
+                dacc = (lane & 3) == 0 ? words[0] : (lane & 3) == 1 ? words[1] : (lane & 3) == 2 ? words[2] : words[3];
+        } else {
+            const long long outi = (long long)f * a.kps_cap + __builtin_amdgcn_readlane(my_o, j);
+            if (lane < 4) {
+                const unsigned long long wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
+                reinterpret_cast<unsigned long long*>(a.desc + outi * 32)[lane] = wv;
+            }
         }
         __builtin_amdgcn_wave_barrier();  // the window is rewritten for the next keypoint
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    }
+    if constexpr (kLate) {
+        const int kj = lane >> 2;
+        const int o = __builtin_amdgcn_ds_bpermute(kj << 2, my_o);  // keypoint kj's output index
+        if (kj < kDescGroup && ((vmask >> kj) & 1))
+            reinterpret_cast<unsigned long long*>(a.desc + ((long long)f * a.kps_cap + o) * 32)[lane & 3] = dacc;
     }
     if (valid) {
         const uint32_t kk = (uint32_t)my_key;
