@@ -810,6 +810,14 @@ __global__ __launch_bounds__(kTailBlock) void resize_tail_kernel(ResizeTailArgs 
 // computed once per pixel and both thresholds of the fallback reuse it.  S ranges over
 // [-256, 254]; only S >= 0 can be a corner, so LDS keeps max(S, -1) + 1 as a byte.
 constexpr int kFastBlock = 64;   // one wave per cell: ballot compaction keeps row-major order
+// The workgroup is one wave, whose LDS operations complete in order: its barriers only keep the
+// compiler from moving LDS accesses across them (__syncthreads() would also drain the wave's
+// outstanding global stores at each one; measured level: fast 0.2429 vs 0.2440 ms).
+__device__ __forceinline__ void fast_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 constexpr int kRoiMax = 72;      // cell ROI <= (59+6) x (59+6): wCell < 2*W for every level size
 
 typedef short short2v __attribute__((ext_vector_type(2)));
@@ -1003,7 +1011,7 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
     }
     const uint32_t* lds32 = reinterpret_cast<const uint32_t*>(roi_base);
     const int P4 = P >> 2;
-    __syncthreads();
+    fast_sync();
     // Pass at iniThFAST: only pixels passing the pre-test at that threshold can have S >= t,
     // and every other pixel counts as 0 in the NMS, so S is computed for those alone.
     uint32_t* out = a.cell_keys + f * a.cell_cap_total + cell.slot;
@@ -1037,9 +1045,9 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
         int cnt = 0, scored = 0, emitted = 0;
         for (int r0 = 0; r0 < nr; r0 += rps) {
             if (cnt + sweep_max > a.cand_max) {  // wave-uniform
-                __syncthreads();
+                fast_sync();
                 score(scored, cnt);
-                __syncthreads();
+                fast_sync();
                 const int lim = (r0 - 1) * P;  // entries of rows <= r0 - 2 lie below
                 int k = 0;
                 for (int i0 = 0; i0 < cnt; i0 += 64)
@@ -1047,7 +1055,7 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
                 emitted += fast_emit(S, list, k, P, inv_p, t, cell, out + emitted, cell.cap - emitted);
                 const int n1 = cnt - k;
                 const int e0 = lane < n1 ? list[k + lane] : 0, e1 = lane + 64 < n1 ? list[k + 64 + lane] : 0;
-                __syncthreads();
+                fast_sync();
                 if (lane < n1) list[lane] = (uint16_t)e0;
                 if (lane + 64 < n1) list[lane + 64] = (uint16_t)e1;
                 cnt = scored = n1;
@@ -1094,11 +1102,11 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
             }
             cnt += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
         }
-        __syncthreads();
+        fast_sync();
         score(scored, cnt);
-        __syncthreads();
+        fast_sync();
         total = emitted + fast_emit(S, list, cnt, P, inv_p, t, cell, out + emitted, cell.cap - emitted);
-        __syncthreads();
+        fast_sync();
     }
     if (lane == 0) {
         const int n = min(total, cell.cap);
