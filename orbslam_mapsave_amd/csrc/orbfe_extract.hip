@@ -2418,13 +2418,16 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? ORBFE_DESC_WAVES : 1
                     uint32_t s4[4];
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
-                        uint32_t sm = ((uint32_t)Dh[i] << 8) + (uint32_t)Dl[i];
-                        if constexpr (kX86) sm += blur_round_bit(sm, even);
-                        s4[i] = min(sm, 0xffffffu);  // byte 2 = min(sum >> 16, 255)
+                        s4[i] = ((uint32_t)Dh[i] << 8) + (uint32_t)Dl[i];
+                        if constexpr (kX86) s4[i] += blur_round_bit(s4[i], even);
                     }
+                    // min(sum >> 16, 255) of two sums at once (sum >> 16 <= 257 < 2^16)
+                    const us2 sat = us2{255, 255};
+                    const us2 h01 = __builtin_elementwise_min(__builtin_bit_cast(us2, __builtin_amdgcn_perm(s4[1], s4[0], 0x07060302u)), sat);
+                    const us2 h23 = __builtin_elementwise_min(__builtin_bit_cast(us2, __builtin_amdgcn_perm(s4[3], s4[2], 0x07060302u)), sat);
                     if ((s < 2 || n < 8) && (u < 2 || g < 2))  // window columns / rows < 40
                         *reinterpret_cast<uint32_t*>(wb + (16 * s + n) * kMwP + 16 * u + 4 * g) =
-                            __builtin_amdgcn_perm(s4[1], s4[0], 0x0c0c0602u) | __builtin_amdgcn_perm(s4[3], s4[2], 0x06020c0cu);
+                            __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, h23), __builtin_bit_cast(uint32_t, h01), 0x06040200u);
                 }
             }
             __builtin_amdgcn_wave_barrier();
