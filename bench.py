@@ -570,8 +570,20 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
     value = world * B * K / dt
     nq = NF if mode != "none" else 0
     e2e = e2e_bytes(W, H, NF, nq, NREF if mode == "ref" else (NF if mode == "pred" else 0))
+    # every stage against the same HBM peak, from the probe steps' per-launch events (the
+    # roofline object above is the dominant kernel's, timed live in the timed region)
+    stage_roof = {}
+    for s_ in STAGES:
+        ms = per_step[s_]
+        ab = algorithmic_bytes(s_, W, H, nkp, nref) * B
+        if ms > 0 and ab > 0:
+            gbs = ab / (ms / 1e3) / 1e9
+            stage_roof[f"{s_}_kernel" if s_ != "resize" else "pyramid_kernel"] = {
+                "ms_per_step": round(ms, 4), "bytes_per_step": round(ab),
+                "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
     return {"value": value, "dt": dt, "K": K, "B": B, "S": S, "J": J, "nkp": nkp,
             "roofline": roof, "per_step": per_step, "probe_steps": probe_steps,
+            "stage_roofline": stage_roof,
             "ref_kp": len(ref_desc_np) if ref_desc_np is not None else None,
             "frames_np": frames_np, "ref_desc_np": ref_desc_np,
             "end_to_end": {"bytes_per_frame": e2e, "achieved": round(e2e * value / 1e9, 2),
@@ -803,6 +815,7 @@ def main() -> None:
             "end_to_end": r["end_to_end"],
             "cpu_baseline": cpu,
             "stage_ms_per_step": {k: round(v, 4) for k, v in r["per_step"].items()},
+            "stage_roofline": r.get("stage_roofline"),
             "stage_note": (f"summed kernel durations per step over {r['probe_steps']} untimed "
                            "probe steps (events on every launch); the timed steps carry events "
                            "on the roofline kernel only" + ("; sub-batch streams overlap, so the "
