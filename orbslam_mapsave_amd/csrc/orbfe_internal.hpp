@@ -281,9 +281,12 @@ constexpr int kOctLdsKeys = 4096;  // max oct-tree keys of one level held in LDS
 // 4 keypoints per describe wave: a frame spreads over twice the waves, so ~3.5 frames are in
 // flight per XCD instead of ~7 and each frame's level windows stay in that XCD's 4 MB L2 —
 // describe traffic 1.70x -> 0.69x of its algorithmic bytes for +2 % kernel time
-// (profiles/r02/experiments/describe_group.json)
+// (profiles/r02/experiments/describe_group.json).  With the matrix-core window blur the
+// per-wave setup (slot lookup, IC batches, trig, fragment loads) weighs more: 8 per wave measured
+// best (describe 0.2408 / 0.2357 / 0.246 / 0.253 ms at 4 / 8 / 10 / 12-16;
+// profiles/r03/experiments/describe_mfma.json)
 #ifndef ORBFE_DESC_GROUP
-#define ORBFE_DESC_GROUP 4
+#define ORBFE_DESC_GROUP 8
 #endif
 constexpr int kDescBlockSize = ORBFE_DESC_BLOCK;
 constexpr int kDescSmallBatch = 8;  // batches below this use kDescGroupSmall keypoints per wave
