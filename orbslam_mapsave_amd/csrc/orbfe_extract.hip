@@ -2039,6 +2039,12 @@ constexpr bool kDescLateStore = ORBFE_DESC_LATE_STORE != 0;
 #ifndef ORBFE_DESC_WAVES
 #define ORBFE_DESC_WAVES 7
 #endif
+// ORBFE_DESC_PAT_LDS: the pattern pairs read as floats from LDS per keypoint (one b128 per 64
+// pairs) instead of widened from packed bytes held in registers (four v_cvt per 64 pairs)
+#ifndef ORBFE_DESC_PAT_LDS
+#define ORBFE_DESC_PAT_LDS 1
+#endif
+constexpr bool kPatLds = ORBFE_DESC_PAT_LDS != 0;
 constexpr int kDescGroupSmall = 2;  // small batches (single-frame latency): 4x the waves
 // the group's slot -> level lookup assumes a group spans at most two levels, which holds while
 // a group is no larger than the smallest per-level slot capacity (ncap >= 20)
@@ -2071,8 +2077,15 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? ORBFE_DESC_WAVES : 1
     }
     typedef int i32x4m __attribute__((ext_vector_type(4)));
     __shared__ uint4 frag_lds[kMfma && kFragLds ? 384 : 1];
-    if constexpr (kMfma && kFragLds != 0) {  // before any wave leaves
-        for (int i = threadIdx.x; i < 384; i += kDescBlock) frag_lds[i] = a.frags[i];
+    // kPatLds: the pattern pairs as floats, pat_lds[q][lane] = pair lane + 64 q (x1, y1, x2, y2)
+    __shared__ float4 pat_lds[kPatLds ? 256 : 1];
+    if constexpr ((kMfma && kFragLds != 0) || kPatLds) {  // before any wave leaves
+        if constexpr (kMfma && kFragLds != 0)
+            for (int i = threadIdx.x; i < 384; i += kDescBlock) frag_lds[i] = a.frags[i];
+        if constexpr (kPatLds)
+            for (int i = threadIdx.x; i < 256; i += kDescBlock)
+                pat_lds[i] = make_float4((float)c_pattern[4 * i], (float)c_pattern[4 * i + 1],
+                                         (float)c_pattern[4 * i + 2], (float)c_pattern[4 * i + 3]);
         __syncthreads();
     }
     const int s0 = (bx * (kDescBlock / 64) + (threadIdx.x >> 6)) * kDescGroup;
@@ -2606,10 +2619,18 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? ORBFE_DESC_WAVES : 1
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             float pat[16];
-            asm volatile("" : "+v"(patw[q]));  // keeps the widening inside the loop
+            if constexpr (kPatLds) {
+                const float4 p4 = pat_lds[64 * q + lane];
+                pat[4 * q] = p4.x;
+                pat[4 * q + 1] = p4.y;
+                pat[4 * q + 2] = p4.z;
+                pat[4 * q + 3] = p4.w;
+            } else {
+                asm volatile("" : "+v"(patw[q]));  // keeps the widening inside the loop
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
-                pat[4 * q + c] = (float)(int)(int8_t)(uint8_t)((uint32_t)patw[q] >> (8 * c));
+                for (int c = 0; c < 4; ++c)
+                    pat[4 * q + c] = (float)(int)(int8_t)(uint8_t)((uint32_t)patw[q] >> (8 * c));
+            }
             // x86 arithmetic (H4): x*b + y*a as a GCC -O3 build on an FMA host contracts
             // it, fma(x, b, y*a) and fma(x, a, -(y*b)) (oracle/variant_rot.cpp)
             float2v r0, r1;
