@@ -2041,6 +2041,12 @@ constexpr bool kDescLateStore = ORBFE_DESC_LATE_STORE != 0;
 #endif
 // ORBFE_DESC_PAT_LDS: the pattern pairs read as floats from LDS per keypoint (one b128 per 64
 // pairs) instead of widened from packed bytes held in registers (four v_cvt per 64 pairs)
+// ORBFE_DESC_IC_T: the IC moments of 4 keypoints reduced together (10 lane exchanges) instead
+// of 8 separate wave reductions
+#ifndef ORBFE_DESC_IC_T
+#define ORBFE_DESC_IC_T 1
+#endif
+constexpr bool kIcT = ORBFE_DESC_IC_T != 0;
 #ifndef ORBFE_DESC_PAT_LDS
 #define ORBFE_DESC_PAT_LDS 1
 #endif
@@ -2343,18 +2349,48 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? ORBFE_DESC_WAVES : 1
                 px[jb] = load16_a1(row);
             }
         }
+        int part[2 * kIcBatch];  // lane's partial (m10, m01) of each keypoint of the batch
 #pragma unroll
         for (int jb = 0; jb < kIcBatch; ++jb) {
-            const int j = j0 + jb;
             const uint4 p4 = px[jb];
             const int su = (int)__builtin_amdgcn_udot4(p4.x, wu[0], __builtin_amdgcn_udot4(p4.y, wu[1],
                            __builtin_amdgcn_udot4(p4.z, wu[2], __builtin_amdgcn_udot4(p4.w, wu[3], 0u, false), false), false), false);
             const int s = (int)__builtin_amdgcn_udot4(p4.x, w1[0], __builtin_amdgcn_udot4(p4.y, w1[1],
                           __builtin_amdgcn_udot4(p4.z, w1[2], __builtin_amdgcn_udot4(p4.w, w1[3], 0u, false), false), false), false);
-            const int m10 = wave_sum(su - 16 * s), m01 = wave_sum(v * s);
-            if (lane == j) {
+            part[2 * jb] = su - 16 * s;
+            part[2 * jb + 1] = v * s;
+        }
+        if constexpr (kIcBatch == 4 && kIcT) {
+            // the batch's 8 sums reduced together, halving the values at each exchange (xor 32,
+            // 16, 8) and then summing the last one over 8 lanes: lane L ends with the total of
+            // value 4 b5 + 2 b4 + b3 (bits of L), i.e. keypoint 2 b5 + b4, m01 if b3
+            const bool h32 = (lane & 32) != 0, h16 = (lane & 16) != 0, h8 = (lane & 8) != 0;
+            int a4[4], a2[2];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                a4[k] = (h32 ? part[4 + k] : part[k]) + __shfl_xor(h32 ? part[k] : part[4 + k], 32);
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                a2[k] = (h16 ? a4[2 + k] : a4[k]) + __shfl_xor(h16 ? a4[k] : a4[2 + k], 16);
+            int a1 = (h8 ? a2[1] : a2[0]) + __shfl_xor(h8 ? a2[0] : a2[1], 8);
+            a1 += __shfl_xor(a1, 4);
+            a1 += __shfl_xor(a1, 2);
+            a1 += __shfl_xor(a1, 1);
+            const int jb = (lane - j0) & 3;
+            const int src = ((jb >> 1) << 5) | ((jb & 1) << 4);
+            const int m10 = __shfl(a1, src), m01 = __shfl(a1, src + 8);
+            if (lane >= j0 && lane < j0 + kIcBatch) {
                 M10 = m10;
                 M01 = m01;
+            }
+        } else {
+#pragma unroll
+            for (int jb = 0; jb < kIcBatch; ++jb) {
+                const int m10 = wave_sum(part[2 * jb]), m01 = wave_sum(part[2 * jb + 1]);
+                if (lane == j0 + jb) {
+                    M10 = m10;
+                    M01 = m01;
+                }
             }
         }
     }
