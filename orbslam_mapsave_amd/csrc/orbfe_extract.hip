@@ -2028,6 +2028,9 @@ constexpr bool kDescPipeCol = (ORBFE_DESC_PIPE & 2) != 0;
 // ORBFE_DESC_WAVES (the register budget: waves per SIMD) the default pair measured best:
 // describe 0.2572 ms (in registers, 90 VGPRs, 5 waves) -> 0.2446 (both from LDS, 72 VGPRs,
 // 7 waves); 8 waves spill (profiles/r03/experiments/describe_mfma.json)
+#ifndef ORBFE_DESC_FRAG_OPAQUE
+#define ORBFE_DESC_FRAG_OPAQUE 2
+#endif
 #ifndef ORBFE_DESC_FRAG_LDS
 #define ORBFE_DESC_FRAG_LDS 3
 #endif
@@ -2037,7 +2040,10 @@ constexpr int kFragLds = ORBFE_DESC_FRAG_LDS;
 #endif
 constexpr bool kDescLateStore = ORBFE_DESC_LATE_STORE != 0;
 #ifndef ORBFE_DESC_WAVES
-#define ORBFE_DESC_WAVES 7
+#define ORBFE_DESC_WAVES 6
+#endif
+#ifndef ORBFE_DESC_WAVES_B
+#define ORBFE_DESC_WAVES_B 5  // the x86 reading and the small-batch groups (spill at 6)
 #endif
 // ORBFE_DESC_PAT_LDS: the pattern pairs read as floats from LDS per keypoint (one b128 per 64
 // pairs) instead of widened from packed bytes held in registers (four v_cvt per 64 pairs)
@@ -2068,7 +2074,7 @@ typedef float float2v __attribute__((ext_vector_type(2)));
 // pre_mask read blurred windows).  kWinMfma — the raw window goes from its global loads
 // straight into i8 MFMA A fragments and both passes run on the matrix cores (below).
 template <int kDescGroup, bool kX86, int kWin>
-__global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? ORBFE_DESC_WAVES : 1) void describe_kernel(DescArgs a) {
+__global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kX86 || kDescGroup < 8 ? ORBFE_DESC_WAVES_B : ORBFE_DESC_WAVES) : 1) void describe_kernel(DescArgs a) {
     constexpr bool kPre = kWin == kWinPre, kMfma = kWin == kWinMfma;
     constexpr bool kLate = kDescLateStore && kMfma;
     int bx, f;
@@ -2300,10 +2306,12 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? ORBFE_DESC_WAVES : 1
         }
     }
     // (the LDS offset made opaque per use, so the reads are not hoisted back into registers)
+    // ORBFE_DESC_FRAG_OPAQUE 2: one opaque base per keypoint (the reads free to move within it)
+    int fbase = lane;
     auto frag = [&](int q, const i32x4m& held, bool from_lds) __attribute__((always_inline)) {
         if (!from_lds) return held;
-        int o = 64 * q + lane;
-        asm volatile("" : "+v"(o));
+        int o = 64 * q + fbase;
+        if (ORBFE_DESC_FRAG_OPAQUE == 1) asm volatile("" : "+v"(o));
         const uint4 h = frag_lds[o];
         return i32x4m{(int)h.x, (int)h.y, (int)h.z, (int)h.w};
     };
@@ -2421,6 +2429,10 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? ORBFE_DESC_WAVES : 1
             // bytes gives the column pass's B operand with no lane movement (the K order V_u
             // follows).  O_u,s has the same shape: its 4 window rows of one column are one
             // dword of the column-major window.
+            if (ORBFE_DESC_FRAG_OPAQUE == 2) {
+                fbase = lane;
+                asm volatile("" : "+v"(fbase));
+            }
             const int S = 2 * (a.taps[0] + a.taps[1] + a.taps[2]) + a.taps[3];
             constexpr uint32_t kRndM = kX86 ? 0x7fffu : 0x8000u;
             const int ci = 128 * S + 0x8000;
