@@ -287,8 +287,9 @@ def run_c5(args) -> None:
                "ms_per_call": round(dt_a14 / K * 1e3, 4), "nmatches": out["a14"],
                "same_assignment_as_fused": same_a14,
                "note": "orbfe_search_by_projection_local_device: isInFrustum outputs resident in "
-                       "HBM (computed once, untimed); grid + candidates (count/scan/fill) + "
-                       "greedy rounds + one synchronisation per batch of rounds"}
+                       "HBM (computed once, untimed); grid + one kernel for the candidates "
+                       "(fixed per-point slots) and the greedy initialisation + blind greedy "
+                       "rounds + accept, one synchronisation (CSR path on overflow)"}
         line = {
             "metric": C5_METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),

@@ -512,6 +512,10 @@ __device__ __forceinline__ int sub_scan(int x, int& total) {
     total = __shfl(inc, kSbpLpp - 1, kSbpLpp);
     return inc - x;
 }
+// kPre: the isInFrustum outputs are already resident (orbfe_search_by_projection_local_device:
+// a.mp's track_in_view / is_bad / projection / level / viewing cosine), so the point reads them
+// instead of evaluating the frustum test and fa.fr is unused.
+template <bool kPre>
 __global__ __launch_bounds__(1024) void sbp_local_fused_kernel(SbpFusedArgs fa) {
     const SbpLocalArgs& a = fa.s;
     __shared__ int cs[kGridCells + 1];
@@ -604,12 +608,25 @@ __global__ __launch_bounds__(1024) void sbp_local_fused_kernel(SbpFusedArgs fa) 
     __syncthreads();
     int in = 0, ovf = 0, bad_level = 0;
     if (i < a.mp.m) {  // every lane of the point evaluates the (cheap, uniform) frustum test
-        if (sub == 0) fa.fr.in_view[i] = 0;  // isInFrustum starts with mbTrackInView = false (Frame.cc:389)
+        if (!kPre && sub == 0) fa.fr.in_view[i] = 0;  // isInFrustum starts with mbTrackInView = false (Frame.cc:389)
         FrustumOut o;
         int n = 0;
-        if (frustum_eval(fa.fr, i, o)) {
+        bool ok;
+        if constexpr (kPre) {  // SearchByProjection's mbTrackInView / isBad skips (ORBmatcher.cc:56-60)
+            ok = a.mp.in_view[i] && !a.mp.bad[i];
+            if (ok) {
+                o.u = a.mp.px[i];
+                o.v = a.mp.py[i];
+                o.ur = a.mp.pxr[i];
+                o.lvl = a.mp.lvl[i];
+                o.vc = a.mp.vcos[i];
+            }
+        } else {
+            ok = frustum_eval(fa.fr, i, o);
+        }
+        if (ok) {
             if (sub == 0) {
-                fa.fr.in_view[i] = 1;
+                if (!kPre) fa.fr.in_view[i] = 1;
                 in = 1;
             }
             const int pl = o.lvl;
@@ -681,5 +698,7 @@ __global__ __launch_bounds__(1024) void sbp_local_fused_kernel(SbpFusedArgs fa) 
     __syncthreads();
     if (tid < 3) fa.blk[3 * blockIdx.x + tid] = tally[tid];
 }
+template __global__ void sbp_local_fused_kernel<false>(SbpFusedArgs);
+template __global__ void sbp_local_fused_kernel<true>(SbpFusedArgs);
 
 }  // namespace orbfe

@@ -452,6 +452,97 @@ int guarded(orbfe_matcher* m, F&& f) {
         return ORBFE_ERR_HIP;
     }
 }
+// SearchLocalPoints' fast path (frames of <= kSbpFixKp keypoints): the grid, ONE kernel for
+// isInFrustum (kPre: its outputs already resident) + candidates (fixed per-point slots) + the
+// greedy initialisation, kBlindRounds rounds launched without looking (a round after a change-free
+// one is a no-op), the acceptances whose last workgroup writes the slots and the tallies, and ONE
+// synchronisation reading host[0..5] = {nmatches, nToMatch, status, overflow, last round's
+// changes, rounds}.  A point with more than kSbpFix candidates or a map that needs more rounds
+// (rare: host[3] or host[4] set) has the slots saved by the fused kernel restored, and the caller
+// reruns the call through the CSR path.
+template <bool kPre>
+int sbp_local_fast(orbfe_matcher* m, const orbfe_frame_view* frame, const FrustumArgs& fr,
+                   const SbpMps& mp, float nnratio, float th, const int32_t* d_nobs,
+                   const int32_t* d_mp_ids, int32_t* d_frame_mp, int32_t* d_frame_mp_obs,
+                   int host[6]) {
+    int st;
+    const int M = mp.m, N = frame->n;
+    constexpr int kBlindRounds = 6;
+    const int fblocks = (std::max(std::max(M, N), kBlindRounds + 1) + kSbpPts - 1) / kSbpPts;
+    if ((st = m->cand.ensure((size_t)M * kSbpFix * sizeof(int2)))) return st;
+    if ((st = m->cnt.ensure((size_t)M * sizeof(int)))) return st;
+    if ((st = m->s1.ensure(std::max(N, 1) * sizeof(int)))) return st;
+    if ((st = m->s2.ensure(std::max(N, 1) * sizeof(int)))) return st;
+    if ((st = m->s3.ensure((size_t)3 * fblocks * sizeof(int)))) return st;
+    if ((st = m->g_t0.ensure(std::max(N, 1) * sizeof(int)))) return st;
+    if ((st = m->g_t1.ensure(std::max(N, 1) * sizeof(int)))) return st;
+    if ((st = m->g_t2.ensure(std::max(N, 1) * sizeof(int)))) return st;
+    if ((st = m->g_last.ensure(std::max(N, 1) * sizeof(int)))) return st;
+    if ((st = m->g_dec.ensure((size_t)M * sizeof(int)))) return st;
+    if ((st = m->g_chg.ensure((size_t)std::max(M + 2, kBlindRounds + 2) * sizeof(int)))) return st;
+    // the accept kernel's counter (zeroed by sbp_local_fused_kernel on every call)
+    if ((st = m->done_ctr.ensure(64))) return st;
+    SbpFusedArgs fu{};
+    fu.fr = fr;
+    SbpLocalArgs& a = fu.s;
+    if ((st = m->frame_device(frame, a.f))) return st;  // AssignFeaturesToGrid
+    a.mp = mp;
+    a.th = th;
+    a.nlevels = frame->nlevels;
+    a.cnt = m->cnt.as<int>();
+    a.cand = m->cand.as<int2>();
+    for (int l = 0; l < frame->nlevels; ++l) fu.scalev[l] = frame->scale_factors[l];
+    fu.blk = m->s3.as<int>();
+    fu.rounds = kBlindRounds;
+    GreedyArgs& g = fu.g;
+    g.m = M;
+    g.nkp = N;
+    g.mode = kGreedyLocal;
+    g.nnratio = nnratio;
+    g.kfix = kSbpFix;
+    g.fcnt = m->cnt.as<int>();
+    g.cand = m->cand.as<int2>();
+    g.cand_cap = LLONG_MAX;
+    g.nobs = d_nobs;
+    g.fmp0 = g.fmp = d_frame_mp;
+    g.fobs0 = g.fobs = d_frame_mp_obs;
+    g.ids = d_mp_ids;
+    g.T[0] = m->g_t0.as<int>();
+    g.T[1] = m->g_t1.as<int>();
+    g.T[2] = m->g_t2.as<int>();
+    g.dec = m->g_dec.as<int>();
+    g.chg = m->g_chg.as<int>();
+    g.last = m->g_last.as<int>();
+    g.nm = m->scal.as<int>();
+    g.save_fmp = m->s1.as<int>();
+    g.save_fobs = m->s2.as<int>();
+    g.done = m->done_ctr.as<int>();
+    g.blk = m->s3.as<int>();
+    g.nblk = fblocks;
+    g.stats = m->scal.as<int>();
+    g.conv_round = kBlindRounds - 1;
+    hipLaunchKernelGGL(sbp_local_fused_kernel<kPre>, dim3(fblocks), dim3(1024), (size_t)N * 32, m->stream, fu);
+    const int rblocks = std::max(1, (std::max(std::max(M, N), 32) + kGreedyBlock - 1) / kGreedyBlock);
+    for (int r = 0; r < kBlindRounds - 1; ++r)
+        hipLaunchKernelGGL(greedy_round_kernel, dim3(rblocks), dim3(kGreedyBlock), 0, m->stream, g, r);
+    // the last blind round and the acceptances in one launch
+    hipLaunchKernelGGL(greedy_accept_kernel<true>, dim3((M + kGreedyBlock - 1) / kGreedyBlock),
+                       dim3(kGreedyBlock), 0, m->stream, g, kBlindRounds - 1);
+    ORBFE_HIP(hipGetLastError());
+    m->rounds_on_device = false;
+    for (int k = 0; k < 6; ++k) host[k] = 0;
+    ORBFE_HIP(hipMemcpyAsync(host, m->scal.p, 6 * sizeof(int), hipMemcpyDeviceToHost, m->stream));
+    ORBFE_HIP(hipStreamSynchronize(m->stream));
+    if (!host[3] && host[4] == 0) {  // no overflow, converged
+        m->last_rounds = host[5];
+        return ORBFE_OK;
+    }
+    // restore the frame's slots; the caller takes the CSR path
+    ORBFE_HIP(hipMemcpyAsync(d_frame_mp, m->s1.p, (size_t)N * 4, hipMemcpyDeviceToDevice, m->stream));
+    ORBFE_HIP(hipMemcpyAsync(d_frame_mp_obs, m->s2.p, (size_t)N * 4, hipMemcpyDeviceToDevice, m->stream));
+    ++m->capacity_retries;
+    return ORBFE_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -1004,31 +1095,9 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
             if ((st = b->ensure(std::max<size_t>(16, (size_t)M * 4)))) return st;
         int* d_cnt = m->scal.as<int>() + 1;     // nToMatch
         int* d_status = m->scal.as<int>() + 2;  // UB level
-        // Fast path (frames of <= kSbpFixKp keypoints): the grid, ONE kernel for isInFrustum +
-        // candidates (fixed per-point slots) + the greedy initialisation, kBlindRounds rounds
-        // launched without looking (a round after a change-free one is a no-op), the
-        // acceptances whose last workgroup writes the slots and the tallies, and ONE
-        // synchronisation reading {nmatches, nToMatch, status, overflow, last round's
-        // changes, rounds}.  A point with more than kSbpFix candidates or a map that needs more
-        // rounds (rare) restores the slots saved by the fused kernel and takes the CSR path.
+        // fast path (sbp_local_fast), else / on its fallback the CSR path below
         if (N <= kSbpFixKp && frame->nlevels <= kMaxLevels && M > 0) {
-            constexpr int kBlindRounds = 6;
-            const int fblocks = (std::max(std::max(M, N), kBlindRounds + 1) + kSbpPts - 1) / kSbpPts;
-            if ((st = m->cand.ensure((size_t)M * kSbpFix * sizeof(int2)))) return st;
-            if ((st = m->cnt.ensure((size_t)M * sizeof(int)))) return st;
-            if ((st = m->s1.ensure(std::max(N, 1) * sizeof(int)))) return st;
-            if ((st = m->s2.ensure(std::max(N, 1) * sizeof(int)))) return st;
-            if ((st = m->s3.ensure((size_t)3 * fblocks * sizeof(int)))) return st;
-            if ((st = m->g_t0.ensure(std::max(N, 1) * sizeof(int)))) return st;
-            if ((st = m->g_t1.ensure(std::max(N, 1) * sizeof(int)))) return st;
-            if ((st = m->g_t2.ensure(std::max(N, 1) * sizeof(int)))) return st;
-            if ((st = m->g_last.ensure(std::max(N, 1) * sizeof(int)))) return st;
-            if ((st = m->g_dec.ensure((size_t)M * sizeof(int)))) return st;
-            if ((st = m->g_chg.ensure((size_t)std::max(M + 2, kBlindRounds + 2) * sizeof(int)))) return st;
-            // the accept kernel's counter (zeroed by sbp_local_fused_kernel on every call)
-            if ((st = m->done_ctr.ensure(64))) return st;
-            SbpFusedArgs fu{};
-            FrustumArgs& fa = fu.fr;
+            FrustumArgs fa{};
             fa.n = M;
             fa.xyz = d_xyz;
             fa.normal = d_normal;
@@ -1050,66 +1119,18 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
             fa.in_view = d_in_view;
             fa.skip = d_skip;
             fa.bad = d_bad;
-            SbpLocalArgs& a = fu.s;
-            if ((st = m->frame_device(frame, a.f))) return st;  // AssignFeaturesToGrid
-            a.mp.m = M;
-            a.mp.desc = reinterpret_cast<const uint4*>(d_desc);
-            a.th = th;
-            a.nlevels = frame->nlevels;
-            a.cnt = m->cnt.as<int>();
-            a.cand = m->cand.as<int2>();
-            for (int l = 0; l < frame->nlevels; ++l) fu.scalev[l] = frame->scale_factors[l];
-            fu.blk = m->s3.as<int>();
-            fu.rounds = kBlindRounds;
-            GreedyArgs& g = fu.g;
-            g.m = M;
-            g.nkp = N;
-            g.mode = kGreedyLocal;
-            g.nnratio = nnratio;
-            g.kfix = kSbpFix;
-            g.fcnt = m->cnt.as<int>();
-            g.cand = m->cand.as<int2>();
-            g.cand_cap = LLONG_MAX;
-            g.nobs = d_nobs;
-            g.fmp0 = g.fmp = d_frame_mp;
-            g.fobs0 = g.fobs = d_frame_mp_obs;
-            g.ids = d_mp_ids;
-            g.T[0] = m->g_t0.as<int>();
-            g.T[1] = m->g_t1.as<int>();
-            g.T[2] = m->g_t2.as<int>();
-            g.dec = m->g_dec.as<int>();
-            g.chg = m->g_chg.as<int>();
-            g.last = m->g_last.as<int>();
-            g.nm = m->scal.as<int>();
-            g.save_fmp = m->s1.as<int>();
-            g.save_fobs = m->s2.as<int>();
-            g.done = m->done_ctr.as<int>();
-            g.blk = m->s3.as<int>();
-            g.nblk = fblocks;
-            g.stats = m->scal.as<int>();
-            g.conv_round = kBlindRounds - 1;
-            hipLaunchKernelGGL(sbp_local_fused_kernel, dim3(fblocks), dim3(1024), (size_t)N * 32, m->stream, fu);
-            const int rblocks = std::max(1, (std::max(std::max(M, N), 32) + kGreedyBlock - 1) / kGreedyBlock);
-            for (int r = 0; r < kBlindRounds - 1; ++r)
-                hipLaunchKernelGGL(greedy_round_kernel, dim3(rblocks), dim3(kGreedyBlock), 0, m->stream, g, r);
-            // the last blind round and the acceptances in one launch
-            hipLaunchKernelGGL(greedy_accept_kernel<true>, dim3((M + kGreedyBlock - 1) / kGreedyBlock),
-                               dim3(kGreedyBlock), 0, m->stream, g, kBlindRounds - 1);
-            ORBFE_HIP(hipGetLastError());
-            m->rounds_on_device = false;
-            int host[6] = {0, 0, 0, 0, 0, 0};
-            ORBFE_HIP(hipMemcpyAsync(host, m->scal.p, sizeof(host), hipMemcpyDeviceToHost, m->stream));
-            ORBFE_HIP(hipStreamSynchronize(m->stream));
+            SbpMps mp{};
+            mp.m = M;
+            mp.desc = reinterpret_cast<const uint4*>(d_desc);
+            int host[6];
+            if ((st = sbp_local_fast<false>(m, frame, fa, mp, nnratio, th, d_nobs, d_mp_ids, d_frame_mp,
+                                            d_frame_mp_obs, host)))
+                return st;
             if (!host[3] && host[4] == 0) {  // no overflow, converged
-                m->last_rounds = host[5];
                 counts[0] = host[0];
                 counts[1] = host[1];
                 return host[2] ? host[2] : ORBFE_OK;
             }
-            // restore the frame's slots and take the CSR path
-            ORBFE_HIP(hipMemcpyAsync(d_frame_mp, m->s1.p, (size_t)N * 4, hipMemcpyDeviceToDevice, m->stream));
-            ORBFE_HIP(hipMemcpyAsync(d_frame_mp_obs, m->s2.p, (size_t)N * 4, hipMemcpyDeviceToDevice, m->stream));
-            ++m->capacity_retries;
         }
         bool retried = false;
         // (the fast path above passes mvScaleFactors in its kernel arguments)
@@ -1226,6 +1247,22 @@ int orbfe_search_by_projection_local_device(orbfe_matcher* m, float nnratio,
         if ((st = m->m_f4.ensure(std::max<size_t>(16, (size_t)frame->nlevels * 4)))) return st;
         ORBFE_HIP(hipMemcpyAsync(m->m_f4.p, frame->scale_factors, (size_t)frame->nlevels * 4,
                                  hipMemcpyHostToDevice, m->stream));
+        // fast path (sbp_local_fast on the resident isInFrustum outputs), else / on its
+        // fallback the CSR path below
+        if (N <= kSbpFixKp && frame->nlevels <= kMaxLevels && M > 0 &&
+            !std::getenv("ORBFE_SBP_DEVICE_CSR")) {
+            const SbpMps mp{M, d_mps->track_in_view, d_mps->is_bad, d_mps->proj_x, d_mps->proj_y,
+                            d_mps->proj_xr, d_mps->pred_level, d_mps->view_cos,
+                            reinterpret_cast<const uint4*>(d_mps->desc), d_mps->n_obs};
+            int host[6];
+            if ((st = sbp_local_fast<true>(m, frame, FrustumArgs{}, mp, nnratio, th, d_mps->n_obs,
+                                           d_mp_ids, d_frame_mp, d_frame_mp_obs, host)))
+                return st;
+            if (!host[3] && host[4] == 0) {  // no overflow, converged
+                *nmatches = host[0];
+                return host[2] ? host[2] : ORBFE_OK;
+            }
+        }
         bool retried = false;
         std::function<int()> attempt = [&]() -> int {
             ORBFE_HIP(hipMemsetAsync(m->scal.p, 0, 16, m->stream));

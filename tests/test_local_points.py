@@ -73,11 +73,18 @@ def test_gpu_search_local_points(seed, m, th, stereo):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed,m,th,stereo", [(0, 50000, 1.0, False), (2, 20000, 1.0, True),
-                                              (3, 1000, 5.0, False)])
-def test_gpu_search_by_projection_local_device(seed, m, th, stereo):
+                                              (3, 1000, 5.0, False), (3, 1000, 12.0, False)])
+@pytest.mark.parametrize("path", ["fused", "csr"])
+def test_gpu_search_by_projection_local_device(seed, m, th, stereo, path, monkeypatch):
     """A14 alone on device-resident isInFrustum outputs (orbfe_search_by_projection_local_device,
-    config 5's "A14 alone" leg): slots, Observations and nmatches exact vs the oracle."""
+    config 5's "A14 alone" leg): slots, Observations and nmatches exact vs the oracle, on the
+    fused fixed-slot path (th = 12: points past its 16 candidates, so the CSR fallback) and with
+    the CSR path forced (ORBFE_SBP_DEVICE_CSR)."""
     import torch
+    if path == "csr":
+        monkeypatch.setenv("ORBFE_SBP_DEVICE_CSR", "1")
+    else:
+        monkeypatch.delenv("ORBFE_SBP_DEVICE_CSR", raising=False)
     from orbslam_mapsave_amd.native import ORBmatcher
     f = S.extract_frame(seed, 1000, u_right=stereo)
     lm = synthetic_local_map(f.keys, f.desc, m, seed=seed)
@@ -109,4 +116,6 @@ def test_gpu_search_by_projection_local_device(seed, m, th, stereo):
     assert gnm == nm
     assert np.array_equal(D["fmp"].cpu().numpy(), fmp)
     assert np.array_equal(D["fobs"].cpu().numpy(), fobs)
+    if path == "fused" and th == 12.0:
+        assert mt.capacity_retries() >= 1
     mt.close()
