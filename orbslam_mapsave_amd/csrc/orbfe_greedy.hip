@@ -47,6 +47,8 @@ struct GreedyArgs {
     const int* blk;       //   per-workgroup tallies of sbp_local_fused_kernel (3 each, nblk)
     int nblk;
     int* stats;           //   [1] nToMatch [2] status [3] overflow [4] chg[conv_round] [5] rounds
+    int* hstats;          //   non-NULL: [0..5] also written here (device-mapped pinned host
+                          //   memory: the host reads them after the synchronisation, no D2H copy)
     int conv_round;
     const int* nobs;      // per point; NULL: every point blocks (keyframe overload)
     const int* fmp0;      // slot contents before the call (-1 = NULL)
@@ -323,6 +325,14 @@ __global__ __launch_bounds__(kGreedyBlock) void greedy_accept_kernel(GreedyArgs 
             int r = 0;
             while (r < a.conv_round && a.chg[r] != 0) ++r;
             a.stats[5] = r + 1;                            // rounds to the fixed point
+            if (a.hstats) {
+                a.hstats[0] = __hip_atomic_load(a.nm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                a.hstats[1] = in;
+                a.hstats[2] = a.stats[2];
+                a.hstats[3] = ovf;
+                a.hstats[4] = a.stats[4];
+                a.hstats[5] = r + 1;
+            }
             *a.done = 0;
         }
     }

@@ -86,12 +86,17 @@ struct orbfe_matcher {
             b->release();
         prof.release();
         if (own) hipStreamDestroy(own);
+        if (stat_host) hipHostFree(stat_host);
     }
 
     // Host transfers go through a pinned staging buffer: the copy into it is a CPU memcpy and
     // the DMA is asynchronous (pageable hipMemcpyAsync stages and blocks per call).  Every
     // host-form entry point starts with begin() and ends with sync(), which completes the
     // deferred downloads; the staging memory is reused from call to call.
+    // SearchLocalPoints' fast-path tallies: 6 ints of device-mapped pinned memory written by the
+    // accept kernel's last workgroup (null: read back by a D2H copy)
+    int* stat_host = nullptr;
+    int* stat_dev = nullptr;
     uint8_t* pin = nullptr;
     uint8_t* pin_dev = nullptr;  // the staging buffer's device-mapped address (null: DMA path)
     size_t pin_cap = 0, pin_used = 0;
@@ -521,6 +526,21 @@ int sbp_local_fast(orbfe_matcher* m, const orbfe_frame_view* frame, const Frustu
     g.nblk = fblocks;
     g.stats = m->scal.as<int>();
     g.conv_round = kBlindRounds - 1;
+    if (!m->stat_host && !m->zero_copy_off) {
+        void* q = nullptr;
+        void* dq = nullptr;
+        if (hipHostMalloc(&q, 64, hipHostMallocDefault) == hipSuccess) {
+            if (hipHostGetDevicePointer(&dq, q, 0) == hipSuccess) {
+                m->stat_host = static_cast<int*>(q);
+                m->stat_dev = static_cast<int*>(dq);
+            } else {
+                hipHostFree(q);
+            }
+        }
+    }
+    g.hstats = m->stat_dev;
+    if (m->stat_host)  // "not converged" until the last workgroup writes it
+        for (int k = 0; k < 6; ++k) m->stat_host[k] = k == 4 ? -1 : 0;
     hipLaunchKernelGGL(sbp_local_fused_kernel<kPre>, dim3(fblocks), dim3(1024), (size_t)N * 32, m->stream, fu);
     const int rblocks = std::max(1, (std::max(std::max(M, N), 32) + kGreedyBlock - 1) / kGreedyBlock);
     for (int r = 0; r < kBlindRounds - 1; ++r)
@@ -531,8 +551,11 @@ int sbp_local_fast(orbfe_matcher* m, const orbfe_frame_view* frame, const Frustu
     ORBFE_HIP(hipGetLastError());
     m->rounds_on_device = false;
     for (int k = 0; k < 6; ++k) host[k] = 0;
-    ORBFE_HIP(hipMemcpyAsync(host, m->scal.p, 6 * sizeof(int), hipMemcpyDeviceToHost, m->stream));
+    if (!m->stat_host)
+        ORBFE_HIP(hipMemcpyAsync(host, m->scal.p, 6 * sizeof(int), hipMemcpyDeviceToHost, m->stream));
     ORBFE_HIP(hipStreamSynchronize(m->stream));
+    if (m->stat_host)
+        for (int k = 0; k < 6; ++k) host[k] = __atomic_load_n(&m->stat_host[k], __ATOMIC_ACQUIRE);
     if (!host[3] && host[4] == 0) {  // no overflow, converged
         m->last_rounds = host[5];
         return ORBFE_OK;
