@@ -533,6 +533,7 @@ __global__ __launch_bounds__(1024) void sbp_local_fused_kernel(SbpFusedArgs fa) 
     __shared__ float2 kxy[kSbpFixKp];
     __shared__ int8_t koct[kSbpFixKp];
     __shared__ int tally[3];
+    __shared__ int scan_tmp[1024 / 64 + 1];
     // the frame's descriptors (2 x uint4 per keypoint, F.n of them: dynamic LDS sized by the
     // host), so a candidate's Hamming distance reads LDS instead of waiting on a global load
     extern __shared__ uint4 fdesc[];
@@ -564,41 +565,36 @@ __global__ __launch_bounds__(1024) void sbp_local_fused_kernel(SbpFusedArgs fa) 
     }
     if (tid < 3) tally[tid] = 0;
     // Staging: every load of a batch is issued before its LDS stores (one global latency per
-    // batch, not one per element).  The grid items are read up to F.n (total <= F.n).
+    // batch, not one per element).
+    for (int c = tid; c <= kGridCells; c += 1024) cs[c] = 0;
+    static_assert(kSbpFixKp == 2 * 1024, "two keypoints per thread");
+    int mine[2] = {-1, -1};  // AssignFeaturesToGrid's cell of keypoints tid, tid + 1024
     {
-        constexpr int kCsIt = (kGridCells + 1 + 1023) / 1024;
-        int v[kCsIt];
-#pragma unroll
-        for (int k = 0; k < kCsIt; ++k) {
-            const int c = tid + 1024 * k;
-            v[k] = c <= kGridCells ? F.cstart[c] : 0;
-        }
-#pragma unroll
-        for (int k = 0; k < kCsIt; ++k) {
-            const int c = tid + 1024 * k;
-            if (c <= kGridCells) cs[c] = v[k];
-        }
-    }
-    for (int k0 = 0; k0 < F.n; k0 += 2 * 1024) {
         float kx[2], ky[2];
-        int ko[2], it[2];
+        int ko[2];
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
-            const int k = k0 + tid + 1024 * b;
+            const int k = tid + 1024 * b;
             if (k < F.n) {
                 kx[b] = F.k[k].x;
                 ky[b] = F.k[k].y;
                 ko[b] = F.k[k].octave;
-                it[b] = F.citems[k];
             }
         }
+        __syncthreads();  // cs cleared
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
-            const int k = k0 + tid + 1024 * b;
+            const int k = tid + 1024 * b;
             if (k < F.n) {
                 kxy[k] = make_float2(kx[b], ky[b]);
                 koct[k] = (int8_t)min(max(ko[b], -128), 127);
-                ci[k] = it[b];
+                // PosInGrid (Frame.cc:500-510), as grid_lds_kernel
+                const int gx = (int)roundf((kx[b] - F.minx) * F.gwi);
+                const int gy = (int)roundf((ky[b] - F.miny) * F.ghi);
+                if (gx >= 0 && gx < kGridCols && gy >= 0 && gy < kGridRows) {
+                    mine[b] = gx * kGridRows + gy;
+                    atomicAdd(&cs[mine[b]], 1);
+                }
             }
         }
     }
@@ -614,6 +610,59 @@ __global__ __launch_bounds__(1024) void sbp_local_fused_kernel(SbpFusedArgs fa) 
             const int q = q0 + tid + 1024 * b;
             if (q < 2 * F.n) fdesc[q] = d[b];
         }
+    }
+    // The frame's grid built in this workgroup's LDS (grid_lds_kernel's counting sort): cs[c]
+    // the start of cell c, ci its keypoints in index (insertion) order.
+    __syncthreads();
+    {
+        constexpr int PER = (kGridCells + 1023) / 1024;
+        int local[PER], sum = 0;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int c = tid * PER + j;
+            local[j] = c < kGridCells ? cs[c] : 0;
+            sum += local[j];
+        }
+        int total;
+        int off = block_exclusive_scan<1024>(sum, scan_tmp, total);
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int c = tid * PER + j;
+            if (c < kGridCells) cs[c] = off;  // cursor
+            off += local[j];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+            if (mine[b] >= 0) ci[atomicAdd(&cs[mine[b]], 1)] = tid + 1024 * b;
+        __syncthreads();
+        // cs[c] is now the end of cell c: sort each cell (index order), then shift to starts
+        int endp[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int c = tid * PER + j;
+            endp[j] = 0;
+            if (c < kGridCells) {
+                const int e = cs[c], s0 = c ? cs[c - 1] : 0;
+                for (int q = s0 + 1; q < e; ++q) {
+                    const int v = ci[q];
+                    int b = q - 1;
+                    while (b >= s0 && ci[b] > v) {
+                        ci[b + 1] = ci[b];
+                        --b;
+                    }
+                    ci[b + 1] = v;
+                }
+                endp[j] = c ? cs[c - 1] : 0;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int c = tid * PER + j;
+            if (c < kGridCells) cs[c] = endp[j];
+        }
+        if (tid == 0) cs[kGridCells] = total;
     }
     __syncthreads();
     int in = 0, ovf = 0, bad_level = 0;

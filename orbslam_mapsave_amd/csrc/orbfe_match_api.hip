@@ -277,13 +277,14 @@ struct orbfe_matcher {
     }
 
     // Device-resident frame view (keys_un / desc / u_right are device pointers): builds the grid.
-    int frame_device(const orbfe_frame_view* v, DevFrame& F) {
+    // grid = false: F's grid arrays are not built (a kernel that builds the grid itself)
+    int frame_device(const orbfe_frame_view* v, DevFrame& F, bool grid = true) {
         const int n = v->n;
         int st;
         if ((st = fa_cs.ensure((kGridCells + 1) * sizeof(int)))) return st;
         if ((st = fa_ci.ensure(std::max(n, 1) * sizeof(int)))) return st;
         if ((st = fa_co.ensure(std::max(n, 1) * sizeof(int)))) return st;
-        launch_grid(v->keys_un, n, v, fa_co.as<int>(), fa_cs.as<int>(), fa_ci.as<int>());
+        if (grid) launch_grid(v->keys_un, n, v, fa_co.as<int>(), fa_cs.as<int>(), fa_ci.as<int>());
         F.k = v->keys_un;
         F.desc = reinterpret_cast<const uint4*>(v->desc);
         F.ur = v->u_right;
@@ -490,7 +491,8 @@ int sbp_local_fast(orbfe_matcher* m, const orbfe_frame_view* frame, const Frustu
     SbpFusedArgs fu{};
     fu.fr = fr;
     SbpLocalArgs& a = fu.s;
-    if ((st = m->frame_device(frame, a.f))) return st;  // AssignFeaturesToGrid
+    // AssignFeaturesToGrid: built by every workgroup of the fused kernel in its LDS
+    if ((st = m->frame_device(frame, a.f, false))) return st;
     a.mp = mp;
     a.th = th;
     a.nlevels = frame->nlevels;
