@@ -33,6 +33,12 @@ ARITH = {"scalar": 0, "x86": 1}  # orbfe_set_arithmetic: ORBFE_ARITH_SCALAR / OR
 METRIC = "frames/sec ORB extract+match, 640×480 @1000 kp, 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md "HBM3E peak BW 8.0 TB/s spec"
 STAGES = ("mask", "resize", "fast", "octree", "blur", "describe", "bf_match")
+# ORBextractor.{scaleFactor,nLevels,iniThFAST,minThFAST} of Examples/ORB_RGB640x480.yaml:38-48
+# (its nFeatures, 2000, is config 4's; configs 2/3/5 extract the metric's 1000).  Pinned against
+# the reference text by tests/test_constants.py (tests/golden/constants_fixture.json).
+ORB_SCALE, ORB_LEVELS, ORB_INI_TH, ORB_MIN_TH = 1.2, 8, 32, 7
+ORB_YAML_NFEATURES = 2000
+ORB = (ORB_SCALE, ORB_LEVELS, ORB_INI_TH, ORB_MIN_TH)
 
 
 def level_sizes(w, h, nlevels=8, scale=1.2):
@@ -99,7 +105,7 @@ def cpu_baseline(frames: np.ndarray, ref_desc: np.ndarray | None, budget_s: floa
     import oracle  # test infrastructure: the cpu_baseline leg is allowed to load it
     oracle.set_variant(0 if arith == "scalar" else
                        oracle.VAR_H4_FMA | oracle.VAR_H5_SSE2 | oracle.VAR_H6_SIMD)
-    p = oracle.params(nfeatures, 1.2, 8, 32, 7)
+    p = oracle.params(nfeatures, *ORB)
     host = host_cpu()
 
     def one(i, prev):
@@ -173,7 +179,7 @@ def run_c5(args) -> None:
     dev = torch.device("cuda", local)
     W, H, M = 640, 480, 50_000
     img = synthetic_frame(2024 + rank, W, H)
-    ex = ORBextractor(1000, 1.2, 8, 32, 7, device=local, max_width=W, max_height=H)
+    ex = ORBextractor(1000, *ORB, device=local, max_width=W, max_height=H)
     keys, desc = ex(img)
     scale = ex.GetScaleFactors()
     ex.close()
@@ -343,9 +349,9 @@ def parse_args():
                          "x86 build (DESIGN.md §2)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--soak-s", type=float, default=2.0,
-                    help="untimed seconds of steps after the warmup (c2/c3/c4), so that an external "
-                         "GPU-utilisation sampler sees the load; 0 = off")
+    ap.add_argument("--soak-s", type=float, default=8.0,
+                    help="untimed wall-clock seconds of steps after the warmup (c2/c3/c4), so "
+                         "that an external GPU-utilisation sampler sees the load; 0 = off")
     ap.add_argument("--batch", type=int, default=256, help="frames per rank per step (c3)")
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--per-rank", type=int, default=0,
@@ -353,10 +359,10 @@ def parse_args():
                          "per-rank shape on one GPU)")
     ap.add_argument("--distinct", type=int, default=32, help="distinct synthetic seeds (cycled)")
     ap.add_argument("--streams", type=int, default=0,
-                    help="sub-batches per rank, each on its own HIP stream and extractor handle "
-                         "(2 overlaps the sub-batches' kernels: more frames/s, but per-launch "
-                         "durations then measure a shared chip); 0 = 1 for c2/c3, 2 for c4 "
-                         "(sub-batch A's all-gather runs while B is extracted)")
+                    help="sub-batches per rank in the timed steps, each on its own HIP stream and "
+                         "extractor handle (their latency-bound kernels overlap; c4: sub-batch "
+                         "A's all-gather runs while B is extracted); 0 = 2.  The probe and "
+                         "roofline legs always run the whole batch on one stream")
     ap.add_argument("--probe-steps", type=int, default=2,
                     help="steps after the warmup with events on every kernel, for the per-stage "
                          "table and the choice of the dominant kernel")
@@ -386,15 +392,18 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
 
     frames_np = synthetic_batch(B, W, H, first_seed=1000 * rank, distinct=args.distinct)
     frames = torch.from_numpy(frames_np).to(dev)
-    S = max(1, min(args.streams or (2 if mode == "pred" else 1), B))
+    S = max(1, min(args.streams or 2, B))
     while B % S:
         S -= 1
     C = B // S  # frames per sub-batch
     streams = [torch.cuda.Stream(dev) for _ in range(S)]
 
+    # handle 0 also serves the single-stream legs (probe and roofline steps: the whole batch in
+    # one call), so it is planned for B frames; the other sub-batch handles for C
     exs = []
     for k in range(S):
-        e = ORBextractor(NF, 1.2, 8, 32, 7, device=local, max_width=W, max_height=H, max_batch=C)
+        e = ORBextractor(NF, *ORB, device=local, max_width=W, max_height=H,
+                         max_batch=B if k == 0 else C)
         e.set_arithmetic(ARITH[args.arith])
         e.set_stream(streams[k].cuda_stream)
         exs.append(e)
@@ -408,7 +417,7 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
     ref_desc_np = None
     if mode == "ref":  # reference frame (config 3): the 2x-feature extractor, once on the GPU
         ref_np = synthetic_frame(999_999, W, H)
-        ex_ref = ORBextractor(NREF, 1.2, 8, 32, 7, device=local, max_width=W, max_height=H)
+        ex_ref = ORBextractor(NREF, *ORB, device=local, max_width=W, max_height=H)
         ex_ref.set_arithmetic(ARITH[args.arith])
         ref_kps, ref_desc_np = ex_ref(ref_np)
         ex_ref.close()
@@ -441,7 +450,24 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
 
     skew_next = [False]
 
+    def step_single():
+        """The whole batch in one extraction call (+ one match launch) on stream 0: the probe
+        and roofline legs, where a kernel's launch has the chip to itself."""
+        exs[0].extract_batch_device(frames[0].data_ptr(), B, W, H, W, W * H, d_kps[0].data_ptr(),
+                                    cap, d_desc[0].data_ptr(), d_n.data_ptr())
+        mt.set_stream(streams[0].cuda_stream)
+        if mode == "ref":
+            mt.bf_match_batch_device(d_desc[0].data_ptr(), cap * 32, d_n.data_ptr(), cap,
+                                     ref_desc.data_ptr(), 0, d_nr.data_ptr(), B,
+                                     d_out[0].data_ptr())
+        elif mode == "pred":  # the local predecessor stands in for the gathered one (leg only)
+            mt.bf_match_batch_device(d_desc[0].data_ptr(), cap * 32, d_n.data_ptr(), cap,
+                                     d_desc[0].data_ptr(), cap * 32, d_n.data_ptr(), B,
+                                     d_out[0].data_ptr())
+
     def step():
+        if S == 1 and mode != "pred":
+            return step_single()
         if mode != "pred":  # sub-batch k: extract (+ match) on stream k, no cross-stream deps
             ev = {}
             for j in range(J):
@@ -488,26 +514,48 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
         acc["bf_match"] = mt.profile_read()
         return acc
 
-    tw = time.perf_counter()
+    def agreed(flag: bool) -> bool:
+        """True once every rank reports flag (a MIN over ranks: collective counts pair up)."""
+        if world == 1:
+            return flag
+        t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
     for _ in range(warmup):
         step()
     barrier()
-    tw = (time.perf_counter() - tw) / max(warmup, 1)
-    # Soak (untimed, --soak-s seconds of the same steps): the timed region of a default run is
-    # tens of milliseconds, too short for an external utilisation sampler (rocm-smi at ~1 Hz) to
-    # see the GPU busy; the soak gives it a window of sustained load before the measurement.
-    # The step count is agreed over the ranks (their collectives must pair up).
+    # Soak (untimed, >= --soak-s seconds of wall clock of the same steps): the timed region of a
+    # default run is tens of milliseconds, too short for an external utilisation sampler (rocm-smi
+    # every few seconds) to see the GPU busy; the soak gives it a window of sustained load before
+    # the measurement and settles the clocks.  Steady-state step time from 10 steps after the
+    # warmup (the warmup's first calls include plan, workspace and graph setup); the soak then
+    # runs in chunks of ~0.5 s and stops when every rank has passed --soak-s (collective counts
+    # stay paired).
+    soak = {"seconds": 0.0, "steps": 0}
     if args.soak_s > 0:
-        n_soak = torch.tensor([min(int(args.soak_s / max(tw, 1e-4)), 100000)], dtype=torch.int64,
-                              device=dev)
-        if world > 1:
-            dist.all_reduce(n_soak, op=dist.ReduceOp.MAX)
-        for _ in range(int(n_soak.item())):
+        ta = time.perf_counter()
+        for _ in range(10):
             step()
         barrier()
-    # Probe steps (untimed): events on every kernel give the per-stage table and pick the
-    # dominant kernel; the timed steps then carry events on that kernel's launches alone, so the
-    # instrumentation of the other ~15 launches per call stays out of the timed region.
+        tw = (time.perf_counter() - ta) / 10
+        chunk = max(1, min(int(0.5 / max(tw, 1e-5)), 20000))
+        if world > 1:
+            c = torch.tensor([chunk], dtype=torch.int64, device=dev)
+            dist.all_reduce(c, op=dist.ReduceOp.MIN)
+            chunk = int(c.item())
+        ts = time.perf_counter()
+        while True:
+            for _ in range(chunk):
+                step()
+            barrier()
+            soak["steps"] += chunk
+            if agreed(time.perf_counter() - ts >= args.soak_s):
+                break
+        soak["seconds"] = round(time.perf_counter() - ts, 2)
+        soak["steady_ms_per_step"] = round(tw * 1e3, 4)
+    # Probe steps (untimed, single-stream): events on every kernel give the per-stage table and
+    # pick the dominant kernel.
     probe_steps = max(args.probe_steps, 1) if args.profile else 0
     for e in exs:
         e.profile(bool(probe_steps))
@@ -515,21 +563,31 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
     mt.profile(bool(probe_steps))
     mt.profile_read()
     for _ in range(probe_steps):
-        step()
+        step_single()
     barrier()
     probe = read_stages()
     dom = max(STAGES, key=lambda st: probe[st][0]) if probe_steps else None
     for e in exs:
-        e.profile(dom is not None and dom != "bf_match", stages=(dom,))
-        e.profile_read()
-    mt.profile(dom == "bf_match")
-    mt.profile_read()
+        e.profile(False)
+    mt.profile(False)
+    # Timed steps: the workload as it runs best (S sub-batch streams), no instrumentation.
     skew_next[0] = bool(args.skew) and S > 1 and J >= S
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     barrier()
     dt = time.perf_counter() - t0
+    # Roofline leg (untimed for `value`): the same number of steps single-stream with HIP events
+    # on the dominant kernel's launches alone, so each event pair times that kernel with the chip
+    # to itself (with S streams a launch shares the chip with the other sub-batch's kernels).
+    if dom is not None:
+        exs[0].profile(dom != "bf_match", stages=(dom,))
+        exs[0].profile_read()
+        mt.profile(dom == "bf_match")
+        mt.profile_read()
+        for _ in range(steps):
+            step_single()
+        barrier()
     stages = read_stages()
     for e in exs:
         e.profile(False)
@@ -567,7 +625,10 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "traffic_source": tsrc,
             "bytes_per_launch": round(bytes_per_step * K / max(dom_launches, 1)),
-            "avg_launch_ms": round(dom_ms / max(dom_launches, 1), 4)}
+            "avg_launch_ms": round(dom_ms / max(dom_launches, 1), 4), "launches": dom_launches,
+            "leg": (f"{K} single-stream steps of {B} frames after the timed region, HIP events on "
+                    f"the {dom} launches only (the timed steps run {S} sub-batch streams, "
+                    "uninstrumented)")}
     value = world * B * K / dt
     nq = NF if mode != "none" else 0
     e2e = e2e_bytes(W, H, NF, nq, NREF if mode == "ref" else (NF if mode == "pred" else 0))
@@ -582,7 +643,7 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
             stage_roof[f"{s_}_kernel" if s_ != "resize" else "pyramid_kernel"] = {
                 "ms_per_step": round(ms, 4), "bytes_per_step": round(ab),
                 "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
-    return {"value": value, "dt": dt, "K": K, "B": B, "S": S, "J": J, "nkp": nkp,
+    return {"value": value, "dt": dt, "K": K, "B": B, "S": S, "J": J, "nkp": nkp, "soak": soak,
             "roofline": roof, "per_step": per_step, "probe_steps": probe_steps,
             "stage_roofline": stage_roof,
             "ref_kp": len(ref_desc_np) if ref_desc_np is not None else None,
@@ -773,7 +834,7 @@ def main() -> None:
                         args.warmup)
         parallelism = f"frame-sharded x{world}, no data-path collective"
     else:
-        W, H, NF, NREF = 1920, 1080, 2000, 2000
+        W, H, NF, NREF = 1920, 1080, ORB_YAML_NFEATURES, ORB_YAML_NFEATURES
         B = args.per_rank if args.per_rank > 0 else max(1, 256 // world)
         metric = C4_METRIC
         workload = (f"configs[3]: 1920x1080 @2000 kp, global batch {B * world} sharded "
@@ -818,9 +879,11 @@ def main() -> None:
             "stage_ms_per_step": {k: round(v, 4) for k, v in r["per_step"].items()},
             "stage_roofline": r.get("stage_roofline"),
             "stage_note": (f"summed kernel durations per step over {r['probe_steps']} untimed "
-                           "probe steps (events on every launch); the timed steps carry events "
-                           "on the roofline kernel only" + ("; sub-batch streams overlap, so the "
-                           "sum can exceed ms_per_step" if S > 1 else "")),
+                           "single-stream probe steps (events on every launch, the whole batch "
+                           "in one call); the timed steps are uninstrumented" +
+                           (f" and overlap {S} sub-batch streams, so ms_per_step is below the "
+                            "sum" if S > 1 else "")),
+            "soak": r["soak"],
         }
         if sweep is not None:
             line["batch_sweep"] = sweep

@@ -101,6 +101,16 @@ void orbfe_destroy(orbfe_extractor* h);
 int orbfe_set_arithmetic(orbfe_extractor* h, int mode);
 int orbfe_get_arithmetic(const orbfe_extractor* h);
 
+/* The reference's compile-time constants as this library's kernels use them: PATCH_SIZE,
+ * HALF_PATCH_SIZE, EDGE_THRESHOLD (ORBextractor.cc:71-73) and ORBmatcher::TH_HIGH, TH_LOW,
+ * HISTO_LENGTH (ORBmatcher.cc:37-39).  Needs no device; for the known-answer check against the
+ * reference text (tests/golden/constants_fixture.json). */
+typedef struct orbfe_reference_constants {
+    int32_t patch_size, half_patch_size, edge_threshold;
+    int32_t th_high, th_low, histo_length;
+} orbfe_reference_constants;
+int orbfe_get_reference_constants(orbfe_reference_constants* out);
+
 /* Getters — ORBextractor::GetLevels / GetScaleFactor / GetScaleFactors /
  * GetInverseScaleFactors / GetScaleSigmaSquares / GetInverseScaleSigmaSquares
  * (ORBextractor.h:68-88).  Table outputs hold nlevels floats each; any may be NULL. */

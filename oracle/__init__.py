@@ -65,6 +65,18 @@ class variant:
         return False
 
 
+def reference_constants() -> dict:
+    """PATCH_SIZE, HALF_PATCH_SIZE, EDGE_THRESHOLD, TH_HIGH, TH_LOW, HISTO_LENGTH as the
+    restatement uses them (oracle_reference_constants)."""
+    out = (C.c_int32 * 6)()
+    _check("oracle_reference_constants", lib().oracle_reference_constants(out))
+    return dict(zip(CONSTANT_NAMES, list(out)))
+
+
+CONSTANT_NAMES = ("PATCH_SIZE", "HALF_PATCH_SIZE", "EDGE_THRESHOLD", "TH_HIGH", "TH_LOW",
+                  "HISTO_LENGTH")
+
+
 def params(nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7) -> Params:
     return Params(nfeatures, scale_factor, nlevels, ini_th, min_th)
 

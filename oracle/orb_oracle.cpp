@@ -1805,3 +1805,10 @@ int oracle_is_in_frustum(int n, const float* xyz, const float* normal, const flo
 }
 
 }  // extern "C"
+
+extern "C" int oracle_reference_constants(int32_t out[6]) {
+    if (!out) return -1;
+    const int32_t v[6] = {kPatchSize, kHalfPatch, kEdge, kThHigh, kThLow, kHistLen};
+    for (int i = 0; i < 6; ++i) out[i] = v[i];
+    return 0;
+}

@@ -23,6 +23,9 @@ extern "C" {
 /* A1 tables: scale, inv_scale, sigma2, inv_sigma2, features per level, umax[16]. */
 int oracle_tables(const orbfe_params* p, float* scale, float* inv_scale, float* sigma2,
                   float* inv_sigma2, int32_t* nfeat, int32_t* umax);
+/* The constants the restatement uses, in the order PATCH_SIZE, HALF_PATCH_SIZE, EDGE_THRESHOLD
+ * (ORBextractor.cc:71-73), TH_HIGH, TH_LOW, HISTO_LENGTH (ORBmatcher.cc:37-39). */
+int oracle_reference_constants(int32_t out[6]);
 /* Level sizes of the pyramid for a w x h input (ORBextractor.cc:1114-1115). */
 int oracle_level_sizes(const orbfe_params* p, int w, int h, int32_t* lw, int32_t* lh);
 

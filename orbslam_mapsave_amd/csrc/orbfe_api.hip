@@ -763,6 +763,13 @@ int orbfe_set_arithmetic(orbfe_extractor* h, int mode) {
 
 int orbfe_get_arithmetic(const orbfe_extractor* h) { return h ? h->arith : ORBFE_ERR_ARG; }
 
+int orbfe_get_reference_constants(orbfe_reference_constants* out) {
+    if (!out) return ORBFE_ERR_ARG;
+    *out = orbfe_reference_constants{kPatchSize, kHalfPatchSize, kEdgeThreshold,
+                                     kThHigh, kThLow, kHistoLength};
+    return ORBFE_OK;
+}
+
 int orbfe_get_levels(const orbfe_extractor* h) { return h ? h->tab.p.nlevels : ORBFE_ERR_ARG; }
 float orbfe_get_scale_factor(const orbfe_extractor* h) { return h ? h->tab.p.scale_factor : 0.f; }
 

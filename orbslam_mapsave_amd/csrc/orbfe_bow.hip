@@ -400,7 +400,7 @@ __global__ __launch_bounds__(kBowSearchBlock) void bow_search_kernel(BowMatchArg
                 for (int j = 0; j < 4; ++j)
                     if (j < nj && free_[j] && lane + 64 * j != brank) sec = min(sec, dist[j]);
                 sec = __ockl_wfred_min_i32(sec);
-                if (b1 <= 50 && (float)b1 < nnratio * (float)sec) {  // TH_LOW, ratio (233-237)
+                if (b1 <= kThLow && (float)b1 < nnratio * (float)sec) {  // TH_LOW, ratio (233-237)
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         if (lane + 64 * j == brank) {

@@ -9,6 +9,17 @@
 
 namespace orbfe {
 
+// The reference's compile-time constants, as every kernel and host plan here uses them:
+// PATCH_SIZE / HALF_PATCH_SIZE / EDGE_THRESHOLD (ORBextractor.cc:71-73) and ORBmatcher::TH_HIGH /
+// TH_LOW / HISTO_LENGTH (ORBmatcher.cc:37-39).  Exported by orbfe_get_reference_constants and
+// pinned against the reference text (tests/golden/constants_fixture.json).
+constexpr int kPatchSize = 31;
+constexpr int kHalfPatchSize = 15;
+constexpr int kEdgeThreshold = 19;
+constexpr int kThHigh = 100;
+constexpr int kThLow = 50;
+constexpr int kHistoLength = 30;
+
 // XCD-aware block remap (cdna_hip_programming.md T1): blocks are dealt round-robin over the 8
 // XCDs (blocks b and b + 8 share one), so give each XCD a contiguous range of the linear
 // (x fastest, then y) grid: the tiles, cells and keypoints of one frame then share one XCD's

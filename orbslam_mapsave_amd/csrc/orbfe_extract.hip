@@ -38,8 +38,8 @@ __constant__ int8_t c_pattern[1024] = {
 };
 __constant__ int c_umax[16];
 
-constexpr int kEdge = 19;       // EDGE_THRESHOLD (ORBextractor.cc:73)
-constexpr int kMinBorder = 16;  // EDGE_THRESHOLD - 3 (772)
+constexpr int kEdge = kEdgeThreshold;   // EDGE_THRESHOLD (ORBextractor.cc:73)
+constexpr int kMinBorder = kEdge - 3;    // EDGE_THRESHOLD - 3 (772)
 constexpr int kCellW = 30;      // W (768)
 // 16-byte global loads from addresses aligned to 4 bytes (FAST ROI rows) or to 1 byte (the
 // describe kernel's disc rows); memcpy lets the compiler pick dwordx4 with that alignment.
@@ -2784,10 +2784,11 @@ int make_tables(const orbfe_params& p, HostTables& t) {
         per *= factor;
     }
     t.nfeat[p.nlevels - 1] = std::max(p.nfeatures - sum, 0);
-    const int vmax = (int)std::floor(15 * std::sqrt(2.f) / 2 + 1);  // 453-468
-    const int vmin = (int)std::ceil(15 * std::sqrt(2.f) / 2);
-    for (int v = 0; v <= vmax; ++v) t.umax[v] = (int)std::lrint(std::sqrt(225.0 - v * v));
-    for (int v = 15, v0 = 0; v >= vmin; --v) {
+    const int vmax = (int)std::floor(kHalfPatchSize * std::sqrt(2.f) / 2 + 1);  // 453-468
+    const int vmin = (int)std::ceil(kHalfPatchSize * std::sqrt(2.f) / 2);
+    for (int v = 0; v <= vmax; ++v)
+        t.umax[v] = (int)std::lrint(std::sqrt((double)kHalfPatchSize * kHalfPatchSize - v * v));
+    for (int v = kHalfPatchSize, v0 = 0; v >= vmin; --v) {
         while (t.umax[v0] == t.umax[v0 + 1]) ++v0;
         t.umax[v] = v0;
         ++v0;

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(kGreedyBlock) void greedy_init_kernel(GreedyArgs a)
         a.last[t] = -1;
     }
     if (t < a.m) a.dec[t] = -2;
-    if (t < 30 && a.hist) a.hist[t] = 0;
+    if (t < kHistoLength && a.hist) a.hist[t] = 0;
     if (t == 0) *a.nm = 0;
 }
 
@@ -106,7 +106,7 @@ struct GreedyAcc {
     }
     __device__ __forceinline__ int result(const GreedyArgs& a) const {
         if (a.mode == kGreedyLocal) {
-            if (best > 100) return -1;  // TH_HIGH
+            if (best > kThHigh) return -1;  // TH_HIGH
             if (bl == sl && best > a.nnratio * second) return -1;
             return bi;
         }
@@ -350,9 +350,9 @@ __global__ __launch_bounds__(kGreedyBlock) void greedy_slots_kernel(GreedyArgs a
 
 // G4: orientation filter over the acceptances (every block recomputes the three maxima).
 __global__ __launch_bounds__(kGreedyBlock) void greedy_ori_kernel(GreedyArgs a) {
-    __shared__ int h[30];
+    __shared__ int h[kHistoLength];
     __shared__ int top[3];
-    if (threadIdx.x < 30) h[threadIdx.x] = a.hist[threadIdx.x];
+    if (threadIdx.x < kHistoLength) h[threadIdx.x] = a.hist[threadIdx.x];
     __syncthreads();
     if (threadIdx.x == 0) three_maxima(h, top[0], top[1], top[2]);
     __syncthreads();
@@ -383,7 +383,7 @@ constexpr int kGreedySmallSlots = 5000;    // slots (keypoints): 4 x 4 B each wi
 __global__ __launch_bounds__(kGreedySmallBlock) void greedy_small_kernel(GreedyArgs a) {
     extern __shared__ int lds[];
     __shared__ int changed, nm;
-    __shared__ int h[30];
+    __shared__ int h[kHistoLength];
     __shared__ int top[3];
     const int tid = threadIdx.x;
     int* T[2] = {lds, lds + a.nkp};
@@ -404,7 +404,7 @@ __global__ __launch_bounds__(kGreedySmallBlock) void greedy_small_kernel(GreedyA
     else cc.e0 = cc.e1 = 0;
     int my_dec = -2;
     const bool my_blocks = tid < a.m && (!a.nobs || a.nobs[tid] > 0);
-    if (tid < 30) h[tid] = 0;
+    if (tid < kHistoLength) h[tid] = 0;
     if (tid == 0) nm = 0;
     __syncthreads();
     int cur = 0, r = 0;

@@ -26,7 +26,7 @@ namespace orbfe {
 
 constexpr int kGridCols = 64, kGridRows = 48;  // FRAME_GRID_COLS/ROWS (Frame.h:37-38)
 constexpr int kGridCells = kGridCols * kGridRows;
-constexpr int kThHigh = 100, kThLow = 50, kHistLen = 30;  // ORBmatcher.cc:37-39
+constexpr int kHistLen = kHistoLength;  // ORBmatcher.cc:39 (kThHigh / kThLow: orbfe_device.hpp)
 
 struct DevFrame {
     const orbfe_keypoint* k;

@@ -26,7 +26,7 @@
 
 namespace orbfe {
 
-constexpr int kStereoThHigh = 100;  // ORBmatcher::TH_HIGH (ORBmatcher.cc:37)
+constexpr int kStereoThHigh = kThHigh;  // ORBmatcher::TH_HIGH (ORBmatcher.cc:37)
 constexpr int kStereoW = 5;         // window half size w (Frame.cc:672)
 constexpr int kStereoL = 5;         // search half range L (Frame.cc:680)
 constexpr int kStereoRowsBlock = 1024;

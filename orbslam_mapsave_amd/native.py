@@ -30,6 +30,7 @@ EXPORTED = [
     "orbfe_create", "orbfe_destroy", "orbfe_get_levels", "orbfe_get_scale_factor",
     "orbfe_get_scale_tables", "orbfe_get_features_per_level", "orbfe_keypoint_capacity",
     "orbfe_keypoint_capacity_for", "orbfe_set_arithmetic", "orbfe_get_arithmetic",
+    "orbfe_get_reference_constants",
     "orbfe_extract", "orbfe_extract_color", "orbfe_human_mask_rect", "orbfe_extract_batch",
     "orbfe_extract_batch_device", "orbfe_extract_color_batch_device", "orbfe_set_stream",
     "orbfe_synchronize", "orbfe_compute_stereo_matches", "orbfe_compute_stereo_matches_device",
@@ -88,6 +89,15 @@ def lib() -> C.CDLL:
 def _check(fn: str, st: int) -> None:
     if st != ORBFE_OK:
         raise OrbfeError(fn, st)
+
+
+def reference_constants() -> dict:
+    """The reference's compile-time constants as the HIP library uses them
+    (orbfe_get_reference_constants: ORBextractor.cc:71-73, ORBmatcher.cc:37-39); no device."""
+    out = (C.c_int32 * 6)()
+    _check("orbfe_get_reference_constants", lib().orbfe_get_reference_constants(out))
+    return dict(zip(("PATCH_SIZE", "HALF_PATCH_SIZE", "EDGE_THRESHOLD", "TH_HIGH", "TH_LOW",
+                     "HISTO_LENGTH"), list(out)))
 
 
 # ORBFE_PIX_* (include/orbfe.h): the cvtColor codes of Tracking::GrabImage*
