@@ -174,7 +174,7 @@ struct orbfe_extractor {
     // Every buffer the capture embeds is either in g1_key (outputs, pinned staging) or is a
     // plan / workspace buffer: set_plan and a growing ensure_frames drop the graph.
     hipGraphExec_t g1 = nullptr;
-    const void* g1_key[8] = {};  // the buffers and plan the graph was captured with
+    const void* g1_key[11] = {};  // the buffers, plan and staging mode the graph was captured with
     // K4 fused into K5 per keypoint window (default), or its own pass over every level with
     // K5 reading the blurred levels (ORBFE_PREBLUR=1: describe 0.30 -> 0.20 ms per 256 frames,
     // but the pass costs 0.19 ms; profiles/r02/experiments/preblur.json)
@@ -230,9 +230,13 @@ struct orbfe_extractor {
         if ((st = pin_kps.ensure((size_t)cap * sizeof(orbfe_keypoint)))) return st;
         if ((st = pin_desc.ensure((size_t)cap * 32))) return st;
         if ((st = pin_n.ensure(sizeof(int32_t)))) return st;
-        const void* key[8] = {pyr.p, out_kps.p, out_desc.p, out_n.p, pin_in.p, pin_kps.p,
-                              reinterpret_cast<const void*>((uintptr_t)w << 32 | (uint32_t)h),
-                              reinterpret_cast<const void*>((uintptr_t)frames_cap)};
+        // every buffer the capture can embed (the zero-copy outputs write pin_kps / pin_desc /
+        // pin_n through their device mappings) and the staging mode
+        const void* key[11] = {pyr.p, out_kps.p, out_desc.p, out_n.p, pin_in.p, pin_kps.p,
+                               pin_desc.p, pin_n.p,
+                               reinterpret_cast<const void*>((uintptr_t)w << 32 | (uint32_t)h),
+                               reinterpret_cast<const void*>((uintptr_t)frames_cap),
+                               reinterpret_cast<const void*>((uintptr_t)zero_copy)};
         if (g1 && std::memcmp(key, g1_key, sizeof(key)) != 0) drop_graph();
         const Plan& g = plan;
         const LevelGeo& l0 = g.geo.lv[0];
@@ -418,7 +422,7 @@ struct orbfe_extractor {
             ra.yt = ytab.as<int>() + g.yoff[l];
             ra.simd_xb = x86() ? sse2_body_resize(ra.dw) : 0;
             ra.gtab = g.pyr_ok && !table_off ? ptab.as<uint4>() + g.gtab_off[l] : nullptr;
-            if (rb) {  // the level and its blur (describe reads this level's blurred windows)
+            if (rb && g.rb_lds[l]) {  // the level and its blur (describe reads this level's blurred windows)
                 ra.lds_pitch = g.rb_pitch[l];
                 ra.lds_e = g.rb_lds_e[l];
                 ra.bdst = bp[l];

@@ -2931,7 +2931,9 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
                     const size_t stage = std::max((size_t)rb_rows * g.rb_pitch[l], (size_t)kRbRowpBytes);
                     g.rb_lds_e[l] = (int)((stage + 15) & ~(size_t)15);
                     g.rb_lds[l] = (size_t)g.rb_lds_e[l] + (size_t)kRbERows * kRbEP + 3 * (kRsTH + 6) * sizeof(int);
-                    if (g.rb_lds[l] > 64 * 1024) return ORBFE_ERR_UNSUPPORTED;
+                    // over 64 KB (scale factors around 3.3 and up) the opt-in fused kernel is
+                    // unavailable for this level: resize_kernel makes it (rb_lds = 0)
+                    if (g.rb_lds[l] > 64 * 1024) g.rb_lds[l] = 0;
                 }
                 g.rs_tiles_x[l] = (dw + kRsTW - 1) / kRsTW;
                 g.rs_tiles[l] = g.rs_tiles_x[l] * ((dh + kRsTH - 1) / kRsTH);

@@ -1269,11 +1269,8 @@ int orbfe_search_by_projection_local_device(orbfe_matcher* m, float nnratio,
         int st;
         const int N = frame->n;
         if ((st = m->scal.ensure(64))) return st;
-        if ((st = m->m_f4.ensure(std::max<size_t>(16, (size_t)frame->nlevels * 4)))) return st;
-        ORBFE_HIP(hipMemcpyAsync(m->m_f4.p, frame->scale_factors, (size_t)frame->nlevels * 4,
-                                 hipMemcpyHostToDevice, m->stream));
-        // fast path (sbp_local_fast on the resident isInFrustum outputs), else / on its
-        // fallback the CSR path below
+        // fast path (sbp_local_fast on the resident isInFrustum outputs; the scale factors go
+        // as kernel arguments), else / on its fallback the CSR path below
         if (N <= kSbpFixKp && frame->nlevels <= kMaxLevels && M > 0 &&
             !std::getenv("ORBFE_SBP_DEVICE_CSR")) {
             const SbpMps mp{M, d_mps->track_in_view, d_mps->is_bad, d_mps->proj_x, d_mps->proj_y,
@@ -1288,6 +1285,10 @@ int orbfe_search_by_projection_local_device(orbfe_matcher* m, float nnratio,
                 return host[2] ? host[2] : ORBFE_OK;
             }
         }
+        // the CSR path reads the scale factors from device memory
+        if ((st = m->m_f4.ensure(std::max<size_t>(16, (size_t)frame->nlevels * 4)))) return st;
+        ORBFE_HIP(hipMemcpyAsync(m->m_f4.p, frame->scale_factors, (size_t)frame->nlevels * 4,
+                                 hipMemcpyHostToDevice, m->stream));
         bool retried = false;
         std::function<int()> attempt = [&]() -> int {
             ORBFE_HIP(hipMemsetAsync(m->scal.p, 0, 16, m->stream));

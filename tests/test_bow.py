@@ -274,14 +274,21 @@ def test_gpu_bow_transform_batch(vocab_paths):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("ori,ratio", [(True, 0.75), (False, 0.7), (True, 0.9)])
-def test_gpu_search_by_bow(ori, ratio, vocab_paths, frames):
+@pytest.mark.parametrize("zc", ["1", "0"])
+def test_gpu_search_by_bow(ori, ratio, zc, vocab_paths, frames, monkeypatch):
+    """Host SearchByBoW with the pair's last workgroup writing the results into device-mapped
+    pinned memory (ORBFE_ZERO_COPY=1) and through bow_init_kernel + D2H copies (0); three calls
+    on one matcher (the done counter and staging reused)."""
+    monkeypatch.setenv("ORBFE_ZERO_COPY", zc)
     from orbslam_mapsave_amd.native import ORBmatcher
     kf, f, kf_ok, kf_fv, f_fv = bow_case(vocab_paths["k10L4_l1_tfidf"], frames, seed=int(ori))
     mt = ORBmatcher(ratio, ori, device=0)
-    m, nm = mt.SearchByBoW(kf.desc, kf.keys["angle"], kf_ok, kf_fv, f.desc, f.keys["angle"], f_fv)
     om, onm = oracle.search_by_bow(kf.desc, kf.keys["angle"], kf_ok, kf_fv, f.desc,
                                    f.keys["angle"], f_fv, ratio, ori)
-    assert nm == onm and np.array_equal(m, om)
+    for _ in range(3):
+        m, nm = mt.SearchByBoW(kf.desc, kf.keys["angle"], kf_ok, kf_fv, f.desc, f.keys["angle"],
+                               f_fv)
+        assert nm == onm and np.array_equal(m, om)
     mt.close()
 
 
