@@ -144,6 +144,27 @@ int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int w, int hgt, size_t
                   const uint8_t* mask, size_t mask_stride, orbfe_keypoint* kps, int kps_cap,
                   uint8_t* desc, int* n_out);
 
+/* Zero-copy form of the same call for the tracking loop.  Frame::ExtractORB
+ * (Frame.cc:358-364) hands operator() the cv::Mat that GrabImageMonocular's cvtColor just
+ * produced (Tracking.cc:409-422); orbfe_extract copies it into the handle's pinned staging
+ * buffer first.  Instead:
+ *   orbfe_input_buffer   : the handle's pinned, device-mapped w x h u8 staging buffer (*buf,
+ *                          row stride *stride bytes) — wrap it as cv::Mat(h, w, CV_8UC1, buf,
+ *                          stride) and let cvtColor write the gray frame straight into it.
+ *                          Valid until the next orbfe_input_buffer / orbfe_destroy on h.
+ *   orbfe_extract_staged : operator() on that buffer (the GPU reads it in place).  With
+ *                          kps_cap == 0 (kps, desc NULL) the outputs stay in the handle's pinned
+ *                          output buffers and orbfe_staged_outputs returns them (*n_out is set).
+ *   orbfe_staged_outputs : the last single-frame call's keypoints / descriptors (n of them), in
+ *                          handle-owned memory valid until the next call on h.
+ * Errors and capacity rules as orbfe_extract; orbfe_extract_staged without a buffer handed out
+ * for at least w x h returns ORBFE_ERR_ARG. */
+int orbfe_input_buffer(orbfe_extractor* h, int w, int hgt, uint8_t** buf, size_t* stride);
+int orbfe_extract_staged(orbfe_extractor* h, int w, int hgt, orbfe_keypoint* kps, int kps_cap,
+                         uint8_t* desc, int* n_out);
+int orbfe_staged_outputs(const orbfe_extractor* h, const orbfe_keypoint** kps,
+                         const uint8_t** desc, int* n);
+
 /* Colour front-end: cvtColor(img, gray, CV_*2GRAY) of Tracking::GrabImage* (Tracking.cc:409-422
  * and the stereo / RGB-D twins) fused with Frame::ExtractORBMask -> operator()(gray, mask)
  * (Frame.cc:366-371, ORBextractor.cc:1053).  `pix` is an ORBFE_PIX_* format, `stride` the row

@@ -142,6 +142,10 @@ struct orbfe_extractor {
     Profiler prof;
     std::vector<orbfe_keypoint> h_kps;
     std::vector<uint8_t> h_desc;
+    // the last single-frame host call's outputs where the call left them (orbfe_staged_outputs)
+    const orbfe_keypoint* staged_kps = nullptr;
+    const uint8_t* staged_desc = nullptr;
+    int staged_n = 0;
     std::vector<int32_t> h_n;
 
     // Single-frame host path (Frame::ExtractORB's per-frame call): pinned staging and the whole
@@ -286,7 +290,9 @@ struct orbfe_extractor {
             }
             std::memcpy(g1_key, key, sizeof(key));
         }
-        if (stride == (size_t)w) {
+        if (img == pin_in.p) {
+            // staged (orbfe_input_buffer): the caller wrote the frame into pin_in already
+        } else if (stride == (size_t)w) {
             std::memcpy(pin_in.p, img, (size_t)w * h);
         } else {
             for (int r = 0; r < h; ++r) std::memcpy(pin_in.p + (size_t)r * w, img + r * stride, w);
@@ -826,6 +832,9 @@ static int extract_host_common(orbfe_extractor* h, const uint8_t* const* imgs, i
                                size_t mask_stride, const orbfe_rect* rects, orbfe_keypoint* kps,
                                int kps_cap, uint8_t* desc, int32_t* n_out) {
     DeviceGuard dg(h->device);
+    h->staged_kps = nullptr;
+    h->staged_desc = nullptr;
+    h->staged_n = 0;
     if (n == 1 && pix == ORBFE_PIX_GRAY && !(masks && masks[0]) && !rects) {
         bool done = false;
         int st = h->run_single_graph(imgs[0], w, hgt, stride, &done);
@@ -833,6 +842,10 @@ static int extract_host_common(orbfe_extractor* h, const uint8_t* const* imgs, i
         if (done) {
             const int cnt = *reinterpret_cast<const int32_t*>(h->pin_n.p);
             n_out[0] = cnt;
+            h->staged_kps = reinterpret_cast<const orbfe_keypoint*>(h->pin_kps.p);
+            h->staged_desc = h->pin_desc.p;
+            h->staged_n = std::min(cnt, h->kp_capacity());
+            if (!kps) return ORBFE_OK;  // orbfe_extract_staged: outputs stay in the staging
             if (cnt > kps_cap) return ORBFE_ERR_CAPACITY;
             std::memcpy(kps, h->pin_kps.p, (size_t)cnt * sizeof(orbfe_keypoint));
             if (desc) std::memcpy(desc, h->pin_desc.p, (size_t)cnt * 32);
@@ -842,6 +855,15 @@ static int extract_host_common(orbfe_extractor* h, const uint8_t* const* imgs, i
     int st = h->run_host(imgs, n, w, hgt, stride, pix, masks, mask_stride, rects);
     if (st != ORBFE_OK) return st;
     const int cap = h->kp_capacity();
+    if (n == 1) {
+        h->staged_kps = h->h_kps.data();
+        h->staged_desc = h->h_desc.data();
+        h->staged_n = std::min(h->h_n[0], cap);
+        if (!kps) {
+            n_out[0] = h->h_n[0];
+            return ORBFE_OK;
+        }
+    }
     int worst = ORBFE_OK;
     for (int f = 0; f < n; ++f) {
         const int cnt = h->h_n[f];
@@ -891,6 +913,50 @@ int orbfe_extract_color(orbfe_extractor* h, const uint8_t* img, int pix, int w, 
     } catch (...) {
         return ORBFE_ERR_HIP;
     }
+}
+
+int orbfe_input_buffer(orbfe_extractor* h, int w, int hgt, uint8_t** buf, size_t* stride) {
+    if (!h || w <= 0 || hgt <= 0 || !buf || !stride) return ORBFE_ERR_ARG;
+    try {
+        DeviceGuard dg(h->device);
+        int st;
+        if ((st = h->set_plan(w, hgt))) return st;  // the size must be one the plan supports
+        if ((st = h->pin_in.ensure((size_t)w * hgt))) return st;
+        *buf = h->pin_in.p;
+        *stride = (size_t)w;
+        return ORBFE_OK;
+    } catch (const std::bad_alloc&) {
+        return ORBFE_ERR_NOMEM;
+    } catch (...) {
+        return ORBFE_ERR_HIP;
+    }
+}
+
+int orbfe_extract_staged(orbfe_extractor* h, int w, int hgt, orbfe_keypoint* kps, int kps_cap,
+                         uint8_t* desc, int* n_out) {
+    if (!h || w <= 0 || hgt <= 0 || !n_out || kps_cap < 0 || (kps_cap > 0 && !kps)) return ORBFE_ERR_ARG;
+    if (!h->pin_in.p || h->pin_in.bytes < (size_t)w * hgt) return ORBFE_ERR_ARG;  // no buffer handed out
+    try {
+        const uint8_t* img = h->pin_in.p;
+        int32_t cnt = 0;
+        const int st = extract_host_common(h, &img, 1, w, hgt, (size_t)w, ORBFE_PIX_GRAY, nullptr, 0,
+                                           nullptr, kps_cap ? kps : nullptr, kps_cap, desc, &cnt);
+        *n_out = cnt;
+        return st;
+    } catch (const std::bad_alloc&) {
+        return ORBFE_ERR_NOMEM;
+    } catch (...) {
+        return ORBFE_ERR_HIP;
+    }
+}
+
+int orbfe_staged_outputs(const orbfe_extractor* h, const orbfe_keypoint** kps, const uint8_t** desc,
+                         int* n) {
+    if (!h || !kps || !desc || !n) return ORBFE_ERR_ARG;
+    *kps = h->staged_kps;
+    *desc = h->staged_desc;
+    *n = h->staged_kps ? h->staged_n : 0;
+    return ORBFE_OK;
 }
 
 int orbfe_extract_batch(orbfe_extractor* h, const uint8_t* const* imgs, int n, int w, int hgt,

@@ -31,7 +31,8 @@ EXPORTED = [
     "orbfe_get_scale_tables", "orbfe_get_features_per_level", "orbfe_keypoint_capacity",
     "orbfe_keypoint_capacity_for", "orbfe_set_arithmetic", "orbfe_get_arithmetic",
     "orbfe_get_reference_constants",
-    "orbfe_extract", "orbfe_extract_color", "orbfe_human_mask_rect", "orbfe_extract_batch",
+    "orbfe_extract", "orbfe_input_buffer", "orbfe_extract_staged", "orbfe_staged_outputs",
+    "orbfe_extract_color", "orbfe_human_mask_rect", "orbfe_extract_batch",
     "orbfe_extract_batch_device", "orbfe_extract_color_batch_device", "orbfe_set_stream",
     "orbfe_synchronize", "orbfe_compute_stereo_matches", "orbfe_compute_stereo_matches_device",
     "orbfe_stereo_status", "orbfe_profile", "orbfe_profile_read", "orbfe_get_level", "orbfe_get_blurred_level", "orbfe_get_fast_keys",
@@ -209,6 +210,47 @@ class ORBextractor:
             self._h, C.c_void_p(image.ctypes.data), w, h, C.c_size_t(stride), ptr(m),
             C.c_size_t(w), ptr(kps), cap, ptr(desc), C.byref(n)))
         return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def input_buffer(self, w: int, h: int) -> np.ndarray:
+        """The handle's pinned staging buffer as a writable (h, w) uint8 view
+        (orbfe_input_buffer): write the gray frame into it (as GrabImageMonocular's cvtColor
+        would), then call :meth:`extract_staged`."""
+        buf = C.POINTER(C.c_uint8)()
+        stride = C.c_size_t(0)
+        _check("orbfe_input_buffer", lib().orbfe_input_buffer(self._h, w, h, C.byref(buf),
+                                                              C.byref(stride)))
+        flat = np.ctypeslib.as_array(buf, shape=(h * stride.value,))
+        return np.lib.stride_tricks.as_strided(flat, (h, w), (stride.value, 1))
+
+    def extract_staged(self, w: int, h: int, copy_out: bool = True):
+        """operator() on the staged frame (orbfe_extract_staged).  copy_out=False leaves the
+        outputs in the handle's pinned buffers (kps_cap 0) and returns views of them
+        (orbfe_staged_outputs), valid until the next call."""
+        n = C.c_int(0)
+        if copy_out:
+            cap = self.capacity(w, h)
+            kps = np.zeros(cap, KEYPOINT_DTYPE)
+            desc = np.zeros((cap, 32), np.uint8)
+            _check("orbfe_extract_staged", lib().orbfe_extract_staged(
+                self._h, w, h, ptr(kps), cap, ptr(desc), C.byref(n)))
+            return kps[:n.value].copy(), desc[:n.value].copy()
+        _check("orbfe_extract_staged", lib().orbfe_extract_staged(self._h, w, h, None, 0, None,
+                                                                  C.byref(n)))
+        return self.staged_outputs()
+
+    def staged_outputs(self):
+        """Views of the last single-frame call's outputs in handle-owned memory."""
+        k = C.c_void_p()
+        d = C.c_void_p()
+        n = C.c_int(0)
+        _check("orbfe_staged_outputs", lib().orbfe_staged_outputs(self._h, C.byref(k), C.byref(d),
+                                                                  C.byref(n)))
+        if not k.value or n.value == 0:
+            return np.zeros(0, KEYPOINT_DTYPE), np.zeros((0, 32), np.uint8)
+        kb = (C.c_uint8 * (n.value * KEYPOINT_DTYPE.itemsize)).from_address(k.value)
+        db = (C.c_uint8 * (n.value * 32)).from_address(d.value)
+        return (np.frombuffer(kb, KEYPOINT_DTYPE, n.value),
+                np.frombuffer(db, np.uint8).reshape(n.value, 32))
 
     def extract_color(self, image: np.ndarray, pix: int, mask: np.ndarray | None = None,
                       rect: tuple[int, int, int, int] | None = None):

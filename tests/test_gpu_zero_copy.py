@@ -58,3 +58,51 @@ def test_matcher_zero_copy(monkeypatch):
     for (f1, n1), (f0, n0) in zip(outs["1"], outs["0"]):
         assert n1 == n0 and np.array_equal(f1, f0)
     assert outs["1"][0][1] == rnm and np.array_equal(outs["1"][0][0], rfmp)
+
+
+@pytest.mark.parametrize("size", [(640, 480), (1920, 1080), (331, 247)])
+def test_staged_input_buffer(size):
+    """orbfe_input_buffer / orbfe_extract_staged / orbfe_staged_outputs (the zero-copy form of
+    Frame::ExtractORB, Frame.cc:358-364): the caller writes each frame into the handle's pinned
+    staging buffer (as GrabImageMonocular's cvtColor would, Tracking.cc:409-422); results are
+    identical to orbfe_extract and to the oracle, call after call, copied out or left in the
+    handle's pinned outputs."""
+    from orbslam_mapsave_amd.native import ORBextractor
+    w, h = size
+    nf = 2000 if w > 1000 else 1000
+    p = oracle.params(nf, 1.2, 8, 20, 7)
+    imgs = [synthetic_frame(700 + s, w, h) for s in range(3)]
+    e = ORBextractor(nf, 1.2, 8, 20, 7, device=0, max_width=w, max_height=h)
+    try:
+        for i, img in enumerate(imgs + imgs[:1]):
+            buf = e.input_buffer(w, h)
+            assert buf.shape == (h, w) and buf.flags["WRITEABLE"]
+            buf[:] = img
+            ok, od = oracle.extract(p, img)
+            if i % 2 == 0:
+                k, d = e.extract_staged(w, h)
+            else:  # outputs left in the pinned buffers
+                kv, dv = e.extract_staged(w, h, copy_out=False)
+                k, d = kv.copy(), dv.copy()
+            assert k.tobytes() == ok.tobytes()
+            assert np.array_equal(d, od)
+            k2, d2 = e(img)  # the copying form agrees
+            assert k2.tobytes() == k.tobytes() and np.array_equal(d2, d)
+            ks, ds = e.staged_outputs()  # the last single-frame call's outputs
+            assert ks.tobytes() == k.tobytes() and np.array_equal(ds, d)
+    finally:
+        e.close()
+
+
+def test_staged_requires_buffer():
+    from orbslam_mapsave_amd.abi import OrbfeError
+    from orbslam_mapsave_amd.native import ORBextractor
+    e = ORBextractor(1000, 1.2, 8, 20, 7, device=0)
+    try:
+        with pytest.raises(OrbfeError):
+            e.extract_staged(640, 480)  # no staging buffer handed out yet
+        e.input_buffer(320, 240)
+        with pytest.raises(OrbfeError):
+            e.extract_staged(640, 480)  # the buffer handed out is smaller than the frame
+    finally:
+        e.close()
