@@ -211,6 +211,8 @@ struct orbfe_extractor {
     bool table_off = std::getenv("ORBFE_RESIZE_TABLE") && std::strcmp(std::getenv("ORBFE_RESIZE_TABLE"), "0") == 0;
     // ORBFE_DESC_MFMA=0: describe blurs its raw windows on the VALU instead of the matrix cores
     bool desc_mfma = !(std::getenv("ORBFE_DESC_MFMA") && std::strcmp(std::getenv("ORBFE_DESC_MFMA"), "0") == 0);
+    // ORBFE_OCT_SMALL=0: small batches keep the 256-thread oct-tree (A/B)
+    bool oct_small = !(std::getenv("ORBFE_OCT_SMALL") && std::strcmp(std::getenv("ORBFE_OCT_SMALL"), "0") == 0);
     bool graph_broken = std::getenv("ORBFE_NO_GRAPH") != nullptr;  // capture failed once (or
                                  // disabled for A/B runs): keep to the launch path
 
@@ -510,7 +512,12 @@ struct orbfe_extractor {
         oa.ncap_max = g.ncap_max;
         oa.sort_cap = g.sort_cap;
         oa.lds_keys = g.oct_keys;
-        ORBFE_LAUNCH(prof, ORBFE_STAGE_OCTREE, octree_kernel, dim3(n, L), dim3(kOctBlockSize), g.oct_lds, stream, oa);
+        // batches of a few frames (the single-frame call): 1024-thread trees (one per CU at
+        // most, the level-0 tree's sweeps over 16 waves); else 256-thread trees, six per CU
+        if (n < kTailMinFrames && oct_small)
+            ORBFE_LAUNCH(prof, ORBFE_STAGE_OCTREE, octree_kernel<1024>, dim3(n, L), dim3(1024), g.oct_lds, stream, oa);
+        else
+            ORBFE_LAUNCH(prof, ORBFE_STAGE_OCTREE, octree_kernel<kOctBlockSize>, dim3(n, L), dim3(kOctBlockSize), g.oct_lds, stream, oa);
         // K4 blur: fused into K5, where each keypoint's window is blurred in LDS, or (PREBLUR)
         // every level of every frame, read by the pre-blurred describe
         if (!fused_blur) {

@@ -683,6 +683,155 @@ __global__ __launch_bounds__(kPyrBlock) void pyramid_kernel(PyrArgs a) {
 template __global__ void pyramid_kernel<false>(PyrArgs);
 template __global__ void pyramid_kernel<true>(PyrArgs);
 
+// K1 as one launch for any frame size — the band streams down its rows.  pyramid_kernel holds
+// a band's computed rows of two levels in LDS at once, so 1920 x 1080 needs ~90 thin bands
+// (twice the pyramid's pixels in seam rows) and takes the per-level kernels instead.  Here a
+// band (a few per frame) advances in steps of about `chunk` level-0 rows: each step stages
+// its new level-0 rows in an LDS ring, then makes, level by level, every row whose two source
+// rows are now in the ring below (sched, from the host's simulation of the same rule), into the
+// level's own ring (and to the pyramid for the band's own rows).  A ring keeps the rows its
+// next level still needs plus those of the step (the host sizes it), so each level makes its
+// rows once and the seams are only between the few bands.  The next step's level-0 chunks are
+// loaded into registers while this step's levels are made.  Arithmetic as pyramid_kernel's.
+template <bool kX86>
+__global__ __launch_bounds__(kPyrBlock) void pyramid_roll_kernel(PyrArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char pr_lds[];
+    const int band = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    const int L = a.nlevels;
+    const int4* bt = a.bands + band * L;
+    const int* sc = a.sched + (size_t)band * a.nsteps * L;
+    const int w0 = a.w[0], P0 = a.lp[0], R0 = a.ring_rows[0], cpr = (w0 + 15) >> 4;
+    const uint8_t* src = a.src.base + f * a.src.fpitch;
+    const int4 b0 = bt[0];
+    int4* yd = reinterpret_cast<int4*>(pr_lds + a.ydesc);
+    constexpr int kPre = 4;  // level-0 chunks in flight per thread (the host bounds a step)
+    uint4 v[kPre];
+    auto load_rows = [&](int r0, int r1) __attribute__((always_inline)) {
+        const int total = (r1 - r0) * cpr;
+#pragma unroll
+        for (int u = 0; u < kPre; ++u) {
+            const int i = kPyrBlock * u + tid;
+            if (i >= total) continue;
+            const int r = r0 + i / cpr, c = i - (i / cpr) * cpr;
+            const uint8_t* row = src + (long long)r * a.src.pitch;
+            const int x = 16 * c;
+            if (x + 16 <= w0) {
+                v[u] = load16_a4(row + x);
+            } else {
+                uint32_t wd[4];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const int xd = x + 4 * d;
+                    wd[d] = 0;
+                    if (xd + 4 <= w0) wd[d] = *reinterpret_cast<const uint32_t*>(row + xd);
+                    else
+                        for (int q = 0; q < 4 && xd + q < w0; ++q) wd[d] |= (uint32_t)row[xd + q] << (8 * q);
+                }
+                v[u] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+            }
+        }
+    };
+    auto store_rows = [&](int r0, int r1) __attribute__((always_inline)) {
+        const int total = (r1 - r0) * cpr;
+        const int slot0 = r0 % R0;
+#pragma unroll
+        for (int u = 0; u < kPre; ++u) {
+            const int i = kPyrBlock * u + tid;
+            if (i >= total) continue;
+            const int j = i / cpr, c = i - j * cpr;
+            int slot = slot0 + j;
+            if (slot >= R0) slot -= R0;
+            *reinterpret_cast<uint4*>(pr_lds + a.ring_off[0] + slot * P0 + 16 * c) = v[u];
+            const int r = r0 + j;
+            if (a.l0_copy.base && r >= b0.z && r < b0.w)
+                *reinterpret_cast<uint4*>(const_cast<uint8_t*>(a.l0_copy.base) + f * a.l0_copy.fpitch +
+                                          (long long)r * a.l0_copy.pitch + 16 * c) = v[u];
+        }
+    };
+    int e0 = b0.x;
+    load_rows(e0, sc[0]);
+    for (int s = 0; s < a.nsteps; ++s) {
+        const int* cur = sc + s * L;
+        const int* prv = s ? cur - L : nullptr;
+        // this step's row descriptors: per level l >= 1, rows [prv[l], cur[l]) of its table as
+        // {source row 0 LDS offset, source row 1 LDS offset, b0 | b1 << 16, own ring offset}
+        {
+            int base = 0;
+            for (int l = 1; l < L; ++l) {
+                const int r0 = prv ? prv[l] : bt[l].x, n = cur[l] - r0;
+                if (n <= 0) continue;
+                const int Rs = a.ring_rows[l - 1], Rd = a.ring_rows[l];
+                for (int i = tid; i < n; i += kPyrBlock) {
+                    const int r = r0 + i;
+                    const int* yy = a.yt[l] + 3 * r;
+                    const int so = a.ring_off[l - 1], ps = a.lp[l - 1];
+                    yd[base + i] = make_int4(so + (yy[0] % Rs) * ps, so + (yy[1] % Rs) * ps, yy[2],
+                                             l + 1 < L ? a.ring_off[l] + (r % Rd) * a.lp[l] : 0);
+                }
+                base += n;
+            }
+        }
+        store_rows(e0, cur[0]);
+        e0 = cur[0];
+        if (s + 1 < a.nsteps) load_rows(e0, cur[L]);  // next step's level-0 rows, in flight
+        __syncthreads();
+        int base = 0;
+        for (int l = 1; l < L; ++l) {
+            const int r0 = prv ? prv[l] : bt[l].x, nrows = cur[l] - r0;
+            if (nrows <= 0) continue;  // uniform: nothing made, nothing to order
+            const int4 bl = bt[l];
+            const int w = a.w[l], gpr = (w + 3) >> 2, rps = kPyrBlock / gpr;
+            const int gx = tid % gpr, ry = tid / gpr;
+            if (ry < rps) {
+                const uint4* gp = a.gtab[l] + 3 * gx;
+                const uint4 g0 = gp[0], g1 = gp[1], g2 = gp[2];
+                const int xbase = (int)g0.x, wofs = (xbase >> 2) << 2, sh = xbase & 3;
+                const uint32_t sel[4] = {g0.y, g0.z, g0.w, g1.x};
+                typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+                const us2 cf[4] = {__builtin_bit_cast(us2, g1.y), __builtin_bit_cast(us2, g1.z),
+                                   __builtin_bit_cast(us2, g1.w), __builtin_bit_cast(us2, g2.x)};
+                const int x = 4 * gx, n = min(4, w - x);
+                const int xb = a.simd_xb[l];
+                const LevelPtr dp = a.dst[l];
+                uint8_t* dst = const_cast<uint8_t*>(dp.base) + f * dp.fpitch;
+                const bool ring = l + 1 < L;
+                auto hsum = [&](int off, uint32_t (&t)[4]) {
+                    const uint32_t* row = reinterpret_cast<const uint32_t*>(pr_lds + off + wofs);
+                    const uint32_t q0 = row[0], q1 = row[1], q2 = row[2];
+                    const uint32_t lo = __builtin_amdgcn_alignbyte(q1, q0, sh), hi = __builtin_amdgcn_alignbyte(q2, q1, sh);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        t[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(hi, lo, sel[k])), cf[k], 0u, false);
+                };
+                for (int j = ry; j < nrows; j += rps) {
+                    const int4 d = yd[base + j];
+                    const uint32_t bb0 = (uint32_t)d.z & 0xffffu, bb1 = (uint32_t)d.z >> 16;
+                    uint32_t t0[4], t1[4];
+                    hsum(d.x, t0);
+                    hsum(d.y, t1);
+                    uint32_t packed = 0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) packed |= resize_px<kX86>(t0[k], t1[k], bb0, bb1, x + k < xb) << (8 * k);
+                    if (ring) *reinterpret_cast<uint32_t*>(pr_lds + d.w + x) = packed;
+                    const int r = r0 + j;
+                    if (r >= bl.z && r < bl.w) {
+                        uint8_t* o = dst + (long long)r * dp.pitch + x;
+                        if (n == 4) {
+                            *reinterpret_cast<uint32_t*>(o) = packed;
+                        } else {
+                            for (int k = 0; k < n; ++k) o[k] = (uint8_t)(packed >> (8 * k));
+                        }
+                    }
+                }
+            }
+            base += nrows;
+            __syncthreads();
+        }
+    }
+}
+template __global__ void pyramid_roll_kernel<false>(PyrArgs);
+template __global__ void pyramid_roll_kernel<true>(PyrArgs);
+
 // Host: pyramid_kernel's per-level column-group tables (3 uint4 per group of 4 output columns:
 // x0[0], the 4 perm selectors pairing bytes x0[k] - x0[0], x1[k] - x0[0] as u16 (0x0c = zero),
 // the 4 (a0 | a1 << 16) coefficient pairs).  False when a group's source bytes do not fit 8
@@ -1139,6 +1288,9 @@ template __global__ void fast_kernel<kFastPitch>(FastArgs);
 // a level with more keys runs the same code on global arrays.  Final: per node the max
 // response, first (lowest original index) on ties (741-759).
 constexpr int kOctBlock = kOctBlockSize;
+// small batches (the single-frame call): one tree per CU at most, so the level-0 tree's sweeps
+// spread over 16 waves instead of 4
+constexpr int kOctBlockSmall = 1024;
 
 // Carve of the dynamic LDS region (sizes in elements).  IT is the type of the per-node key
 // counts, single-key indices and quadrant keys / child positions: u16 when the level's keys
@@ -1217,35 +1369,35 @@ __device__ long long g_oct_t[256 * 16 * 64];
 #define ORBFE_OCT_U 4
 #endif
 constexpr int kOctU = ORBFE_OCT_U;
-template <class KT, class NT, class F>
+template <int BLK, class KT, class NT, class F>
 __device__ __forceinline__ void oct_sweep(const KT* K, const NT* NODE, int nkeys, F&& body) {
-    for (int k0 = threadIdx.x; k0 < nkeys; k0 += kOctU * kOctBlock) {
+    for (int k0 = threadIdx.x; k0 < nkeys; k0 += kOctU * BLK) {
         int node[kOctU];
         uint32_t kk[kOctU];
 #pragma unroll
         for (int u = 0; u < kOctU; ++u) {
-            const int k = k0 + u * kOctBlock;
+            const int k = k0 + u * BLK;
             node[u] = k < nkeys ? (int)NODE[k] : -1;
             kk[u] = k < nkeys ? K[k] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < kOctU; ++u)
-            if (node[u] >= 0) body(k0 + u * kOctBlock, kk[u], node[u]);
+            if (node[u] >= 0) body(k0 + u * BLK, kk[u], node[u]);
     }
 }
 // The same sweep in stages, each stage's LDS lookups for all kOctU keys issued together (a
 // body per key under its own exec mask would wait on each key's lookups in turn): the keys'
 // quadrants in their nodes' boxes, then body(k[], node[], q[]) for the kOctU keys at once
 // (node < 0: not a live key; its lookups read node 0 and are discarded).
-template <class KT, class NT, class F>
+template <int BLK, class KT, class NT, class F>
 __device__ __forceinline__ void oct_sweep_q(const KT* K, const NT* NODE, int nkeys, const int* bx,
                                             const int* by, F&& body) {
-    for (int k0 = threadIdx.x; k0 < nkeys; k0 += kOctU * kOctBlock) {
+    for (int k0 = threadIdx.x; k0 < nkeys; k0 += kOctU * BLK) {
         int node[kOctU], q[kOctU], kx[kOctU];
         uint32_t kk[kOctU];
 #pragma unroll
         for (int u = 0; u < kOctU; ++u) {
-            const int k = k0 + u * kOctBlock;
+            const int k = k0 + u * BLK;
             kx[u] = k;
             node[u] = k < nkeys ? (int)NODE[k] : -1;
             kk[u] = k < nkeys ? K[k] : 0u;
@@ -1264,7 +1416,7 @@ __device__ __forceinline__ void oct_sweep_q(const KT* K, const NT* NODE, int nke
 }
 
 // The tree of one (frame, level) after its keys are in K (nkeys, original order).
-template <class IT, class KT, class NT>
+template <int BLK, class IT, class KT, class NT>
 __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>& s, const LevelGeo& L, KT* K,
                              NT* NODE, int nkeys, uint32_t* out, int* out_cnt,
                                               long long* tm) {
@@ -1273,12 +1425,13 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
     const int N = L.nfeat;
     int* flag_sh = s.scal + 2;    // scal[2]: counters
     int* rmin_sh = s.scal + 3;    // scal[3]: phase-2 cut index
+    int* nexp_sh = s.scal + 4;    // scal[4]: phase-1 expandable children
 
     // ---- initial nodes (542-584)
     const int nini = L.nini;
     const float hX = L.hx;
     const int H = L.bh;
-    for (int i = tid; i < nini; i += kOctBlock) {
+    for (int i = tid; i < nini; i += BLK) {
         s.qc[i] = 0u;  // per initial node here (nini <= NC / 4 entries)
         s.qk[i] = (IT)-1;
     }
@@ -1290,7 +1443,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
             s.qk[0] = (IT)(nkeys - 1);
         }
     } else {
-        for (int k = tid; k < nkeys; k += kOctBlock) {
+        for (int k = tid; k < nkeys; k += BLK) {
             const int node = min((int)((float)key_x(K[k]) / hX), nini - 1);  // vpIniNodes[kp.pt.x/hX] (568)
             atomicAdd(&s.qc[node], 1u);
             s.qk[node] = (IT)k;
@@ -1301,11 +1454,11 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
     int size;
     {   // list = non-empty initial nodes in index order; single-key nodes are closed
         int total = 0;
-        for (int base = 0; base < nini; base += kOctBlock) {
+        for (int base = 0; base < nini; base += BLK) {
             const int i = base + tid;
             const int ne = i < nini && s.qc[i] > 0u;
             int chunk_total;
-            const int off = block_exclusive_scan<kOctBlock>(ne, s.tmp, chunk_total);
+            const int off = block_exclusive_scan<BLK>(ne, s.tmp, chunk_total);
             if (ne) {
                 const int pos = total + off;
                 const int x0 = (int)(hX * (float)i), x1 = (int)(hX * (float)(i + 1));
@@ -1324,9 +1477,9 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
     OCT_MARK(tm, 58);
     if (nini == 1) {
         const int nd = (int)s.cnt(0)[0] >= 2 ? 0 : -1;
-        for (int k = tid; k < nkeys; k += kOctBlock) NODE[k] = nd;
+        for (int k = tid; k < nkeys; k += BLK) NODE[k] = nd;
     } else {
-        for (int k = tid; k < nkeys; k += kOctBlock) {
+        for (int k = tid; k < nkeys; k += BLK) {
             const int node = s.aux[min((int)((float)key_x(K[k]) / hX), nini - 1)];
             NODE[k] = (int)s.cnt(0)[node] >= 2 ? node : -1;
         }
@@ -1343,12 +1496,12 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
     for (int pass = 0; pass < 64 && !finished && !phase2; ++pass) {
         const int prev = size;
         const int nxt = cur ^ 1;
-        for (int i = tid; i < OctLds<IT>::kQcWords * size; i += kOctBlock) s.qc[i] = 0u;
+        for (int i = tid; i < OctLds<IT>::kQcWords * size; i += BLK) s.qc[i] = 0u;
         __syncthreads();
         if (pass == 1) OCT_MARK(tm, 32);
         {
             const OctLds<IT> ss = s;
-            oct_sweep_q(K, NODE, nkeys, s.box(cur), s.boy(cur), [=](const int* k, const int* node, const int* q) {
+            oct_sweep_q<BLK>(K, NODE, nkeys, s.box(cur), s.boy(cur), [=](const int* k, const int* node, const int* q) {
 #pragma unroll
                 for (int u = 0; u < kOctU; ++u)
                     if (node[u] >= 0) {
@@ -1360,8 +1513,10 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
         __syncthreads();
         if (pass == 1) OCT_MARK(tm, 33);
         // per node: children (divided) or kept (single); aux = child offset, aux2 = kept offset
-        int csize = 0, ksize = 0, nexp = 0;
-        for (int base = 0; base < size; base += kOctBlock) {
+        // (nexp_sh: zeroed here, after the sweep's barrier; summed after the first scan barrier)
+        if (tid == 0) *nexp_sh = 0;
+        int csize = 0, ksize = 0;
+        for (int base = 0; base < size; base += BLK) {
             const int i = base + tid;
             int nch = 0, keep = 0, ne = 0;
             if (i < size) {
@@ -1376,19 +1531,20 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
                     keep = 1;
                 }
             }
-            // one scan for all three: children (bits 0-10), kept (11-19), expandable (20-30);
-            // a chunk of kOctBlock <= 256 nodes sums to <= 1024 / 256 / 1024, so no field
-            // carries into the next or into the sign bit
-            static_assert(kOctBlock <= 256, "scan packing assumes <= 256 threads");
+            // one scan for both: children (bits 0-12), kept (13-23); a chunk of BLK <= 1024
+            // nodes sums to <= 4096 / 1024, so no field carries into the next.  The expandable
+            // count needs only its total: a wave sum and one LDS atomic per wave
+            static_assert(BLK <= 1024, "scan packing assumes <= 1024 threads");
             int t;
-            const int o = block_exclusive_scan<kOctBlock>(nch | (keep << 11) | (ne << 20), s.tmp, t);
+            const int o = block_exclusive_scan<BLK>(nch | (keep << 13), s.tmp, t);
             if (i < size) {
-                s.aux[i] = csize + (o & 0x7ff);
-                s.aux2[i] = ksize + ((o >> 11) & 0x1ff);
+                s.aux[i] = csize + (o & 0x1fff);
+                s.aux2[i] = ksize + ((o >> 13) & 0x7ff);
             }
-            csize += t & 0x7ff;
-            ksize += (t >> 11) & 0x1ff;
-            nexp += t >> 20;
+            const int wne = wave_sum(ne);
+            if ((tid & 63) == 0 && wne) atomicAdd(nexp_sh, wne);
+            csize += t & 0x1fff;
+            ksize += (t >> 13) & 0x7ff;
         }
         const int nsize = csize + ksize;
         if (pass == 1) OCT_MARK(tm, 34);
@@ -1397,7 +1553,8 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
             return;
         }
         __syncthreads();
-        for (int i = tid; i < size; i += kOctBlock) {
+        const int nexp = *nexp_sh;
+        for (int i = tid; i < size; i += BLK) {
             if ((int)s.cnt(cur)[i] >= 2) {
                 int cp = s.aux[i];
 #pragma unroll
@@ -1428,7 +1585,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
         if (pass == 1) OCT_MARK(tm, 35);
         {
             const IT *qk = s.qk, *ncnt = s.cnt(nxt);
-            oct_sweep_q(K, NODE, nkeys, s.box(cur), s.boy(cur), [=](const int* k, const int* node, const int* q) {
+            oct_sweep_q<BLK>(K, NODE, nkeys, s.box(cur), s.boy(cur), [=](const int* k, const int* node, const int* q) {
                 int np[kOctU], c[kOctU];
 #pragma unroll
                 for (int u = 0; u < kOctU; ++u) np[u] = node[u] >= 0 ? (int)qk[max(node[u], 0) * 4 + q[u]] : 0;
@@ -1457,7 +1614,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
         if (tid == 0) { flag_sh[0] = 0; *rmin_sh = 0x7fffffff; }
         __syncthreads();
         if (round == 0) OCT_MARK(tm, 40);
-        for (int i = tid; i < size; i += kOctBlock)
+        for (int i = tid; i < size; i += BLK)
             if ((int)s.cnt(cur)[i] >= 2) {
                 const int slot = atomicAdd(&flag_sh[0], 1);
                 s.s64[slot] = ((unsigned long long)(unsigned)s.cnt(cur)[i] << 40) |
@@ -1491,22 +1648,33 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
             // instead of a bitonic network's log2(P)(log2(P)+1)/2.  qc (>= 8 NC bytes, 8-byte
             // aligned) holds the sorted copy until it is cleared below.
             unsigned long long* srt = reinterpret_cast<unsigned long long*>(s.qc);
-            for (int j = tid; j < m; j += kOctBlock) {
+            // (8 broadcast reads in flight per step, two keys per ds_read_b128: the rolled loop
+            // waited on each read — 13.5 K cycles at the 1080p level-0 tree's ~300 nodes)
+            const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(s.s64);
+            const int m8 = m & ~7;
+            for (int j = tid; j < m; j += BLK) {
                 const unsigned long long v = s.s64[j];
                 int rank = 0;
-                for (int i = 0; i < m; ++i) rank += s.s64[i] > v;
+                for (int i = 0; i < m8; i += 8) {
+                    ulonglong2 w[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) w[u] = s2[(i >> 1) + u];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) rank += (w[u].x > v) + (w[u].y > v);
+                }
+                for (int i = m8; i < m; ++i) rank += s.s64[i] > v;
                 srt[rank] = v;
             }
             __syncthreads();
-            for (int j = tid; j < m; j += kOctBlock) s.s64[j] = srt[j];
+            for (int j = tid; j < m; j += BLK) s.s64[j] = srt[j];
             __syncthreads();
         }
-        for (int i = tid; i < OctLds<IT>::kQcWords * size; i += kOctBlock) s.qc[i] = 0u;
+        for (int i = tid; i < OctLds<IT>::kQcWords * size; i += BLK) s.qc[i] = 0u;
         __syncthreads();
         if (round == 0) OCT_MARK(tm, 43);
         {
             const OctLds<IT> ss = s;
-            oct_sweep_q(K, NODE, nkeys, s.box(cur), s.boy(cur), [=](const int* k, const int* node, const int* q) {
+            oct_sweep_q<BLK>(K, NODE, nkeys, s.box(cur), s.boy(cur), [=](const int* k, const int* node, const int* q) {
 #pragma unroll
                 for (int u = 0; u < kOctU; ++u)
                     if (node[u] >= 0) {
@@ -1520,7 +1688,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
         // cut: first j in sorted order with size + sum_{<=j}(nch-1) >= N (else all m)
         {
             int run = 0;
-            for (int base = 0; base < m; base += kOctBlock) {
+            for (int base = 0; base < m; base += BLK) {
                 const int j = base + tid;
                 int delta = 0;
                 if (j < m) {
@@ -1529,7 +1697,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
                     delta -= 1;
                 }
                 int t;
-                const int ex = block_exclusive_scan<kOctBlock>(delta, s.tmp, t);
+                const int ex = block_exclusive_scan<BLK>(delta, s.tmp, t);
                 if (j < m && size + run + ex + delta >= N) atomicMin(rmin_sh, j);
                 run += t;
             }
@@ -1538,11 +1706,11 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
         const int r = min(*rmin_sh, m - 1);
         if (round == 0) OCT_MARK(tm, 45);
         // processed flags + children offsets (processing order), kept offsets (list order)
-        for (int i = tid; i < size; i += kOctBlock) s.aux2[i] = 0;
+        for (int i = tid; i < size; i += BLK) s.aux2[i] = 0;
         __syncthreads();
         if (round == 0) OCT_MARK(tm, 46);
         int csize = 0;
-        for (int base = 0; base <= r; base += kOctBlock) {
+        for (int base = 0; base <= r; base += BLK) {
             const int j = base + tid;
             int nch = 0, i = -1;
             if (j <= r) {
@@ -1550,7 +1718,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
                 for (int q = 0; q < 4; ++q) nch += s.qcount(i, q) > 0;
             }
             int t;
-            const int o = block_exclusive_scan<kOctBlock>(nch, s.tmp, t);
+            const int o = block_exclusive_scan<BLK>(nch, s.tmp, t);
             if (j <= r) {
                 s.aux[i] = csize + o;
                 s.aux2[i] = 1;
@@ -1560,11 +1728,11 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
         __syncthreads();
         if (round == 0) OCT_MARK(tm, 47);
         int ksize = 0;
-        for (int base = 0; base < size; base += kOctBlock) {
+        for (int base = 0; base < size; base += BLK) {
             const int i = base + tid;
             const int keep = i < size && !s.aux2[i];
             int t;
-            const int o = block_exclusive_scan<kOctBlock>(keep, s.tmp, t);
+            const int o = block_exclusive_scan<BLK>(keep, s.tmp, t);
             if (keep) s.aux2[i] = -(1 + ksize + o);  // kept: encoded new offset
             ksize += t;
         }
@@ -1575,7 +1743,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
             return;
         }
         __syncthreads();
-        for (int i = tid; i < size; i += kOctBlock) {
+        for (int i = tid; i < size; i += BLK) {
             if (s.aux2[i] > 0) {  // processed: children
                 int cp = s.aux[i];
 #pragma unroll
@@ -1608,7 +1776,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
         {
             const int *aux = s.aux, *aux2 = s.aux2;
             const IT *qk = s.qk, *ncnt = s.cnt(nxt);
-            oct_sweep_q(K, NODE, nkeys, s.box(cur), s.boy(cur), [=](const int* k, const int* node, const int* q) {
+            oct_sweep_q<BLK>(K, NODE, nkeys, s.box(cur), s.boy(cur), [=](const int* k, const int* node, const int* q) {
                 int a2[kOctU], ca[kOctU], cq[kOctU], np[kOctU], c[kOctU];
 #pragma unroll
                 for (int u = 0; u < kOctU; ++u) {
@@ -1636,18 +1804,18 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
     }
 
     // ---- retain the best key per node (740-759), emit in list order
-    for (int i = tid; i < size; i += kOctBlock) s.s64[i] = 0ull;
+    for (int i = tid; i < size; i += BLK) s.s64[i] = 0ull;
     __syncthreads();
     OCT_MARK(tm, 52);
     {
         unsigned long long* best = s.s64;
-        oct_sweep(K, NODE, nkeys, [=](int k, uint32_t kk, int node) {
+        oct_sweep<BLK>(K, NODE, nkeys, [=](int k, uint32_t kk, int node) {
             atomicMax(&best[node], ((unsigned long long)key_score(kk) << 32) | (0xffffffffu - (unsigned)k));
         });
     }
     __syncthreads();
     OCT_MARK(tm, 53);
-    for (int i = tid; i < size; i += kOctBlock) {
+    for (int i = tid; i < size; i += BLK) {
         const int k = (int)s.cnt(cur)[i] == 1 ? (int)s.key(cur)[i]
                                           : (int)(0xffffffffu - (unsigned)(s.s64[i] & 0xffffffffu));
         const uint32_t kk = K[k];
@@ -1660,7 +1828,8 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
     OCT_MARK(tm, 31);
 }
 
-__global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
+template <int BLK>
+__global__ __launch_bounds__(BLK) void octree_kernel(OctArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     // level-major block order: every frame's level-0 tree (the longest) is dispatched first,
     // the small levels fill the remaining slots
@@ -1720,12 +1889,12 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
     uint32_t* K = in_lds ? lkeys : a.keys + f * a.geo.key_total + L.key_off;
     const uint32_t* src = a.cell_keys + f * a.cell_cap_total;
     int nkeys = 0;
-    for (int base = L.cell_begin; base < L.cell_end; base += 2 * kOctBlock) {
+    for (int base = L.cell_begin; base < L.cell_end; base += 2 * BLK) {
         int n[2];
         long long slot[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const int c = base + j * kOctBlock + tid;
+            const int c = base + j * BLK + tid;
             n[j] = c < L.cell_end ? a.cell_cnt[f * a.ncells + c] : 0;
             slot[j] = c < L.cell_end ? a.cells[c].slot : 0;
         }
@@ -1736,8 +1905,8 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
             for (int i = 0; i < 8; ++i)
                 if (i < n[j]) v[j][i] = src[slot[j] + i];
         int t0, t1;
-        const int o0 = nkeys + block_exclusive_scan<kOctBlock>(n[0], tmp, t0);
-        const int o1 = nkeys + t0 + block_exclusive_scan<kOctBlock>(n[1], tmp, t1);
+        const int o0 = nkeys + block_exclusive_scan<BLK>(n[0], tmp, t0);
+        const int o1 = nkeys + t0 + block_exclusive_scan<BLK>(n[1], tmp, t1);
         const int off[2] = {o0, o1};
         // (uniform branch: a store through the selected pointer would be a flat store)
 #pragma unroll
@@ -1774,14 +1943,18 @@ __global__ __launch_bounds__(kOctBlock) void octree_kernel(OctArgs a) {
     if (in_lds) {
         OctLds<uint16_t> s;
         carve(s, reinterpret_cast<unsigned char*>(lnode + a.lds_keys));
-        octree_level(a, s, L, lkeys, lnode, nkeys, out, out_cnt, tm);
+        octree_level<BLK>(a, s, L, lkeys, lnode, nkeys, out, out_cnt, tm);
     } else {  // more keys than LDS holds: the same passes over global arrays
         OctLds<int> s;
         carve(s, region);
         int* node = reinterpret_cast<int*>(a.act) + (f * a.geo.key_total + L.key_off);
-        octree_level(a, s, L, K, node, nkeys, out, out_cnt, tm);
+        octree_level<BLK>(a, s, L, K, node, nkeys, out, out_cnt, tm);
     }
 }
+
+// ---------------------------------------------------------------------------------------------
+template __global__ void octree_kernel<kOctBlock>(OctArgs);
+template __global__ void octree_kernel<kOctBlockSmall>(OctArgs);
 
 // ---------------------------------------------------------------------------------------------
 // K4 — GaussianBlur(7x7, sigma 2, REFLECT_101), integer path (App. A.2): row pass R = sum k_i I

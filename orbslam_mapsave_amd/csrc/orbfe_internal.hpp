@@ -97,6 +97,13 @@ struct PyrArgs {
     const uint4* gtab[kMaxLevels]; // per level >= 1: 3 uint4 per column group
     const int* yt[kMaxLevels];     // per level >= 1: the resize y table
     int simd_xb[kMaxLevels];
+    // pyramid_roll_kernel: the band streams down its rows in steps (about `chunk` level-0 rows
+    // each); level l < L-1 keeps its rows in an LDS ring of ring_rows[l] rows at ring_off[l];
+    // sched[(band * nsteps + step) * L + l] = the level's rows made once the step is done
+    // (exclusive end row); row descriptors of a step at ydesc (4 ints per row)
+    const int* sched;
+    int nsteps, ydesc;
+    int ring_rows[kMaxLevels], ring_off[kMaxLevels];
 };
 
 struct ResizeTailArgs {
@@ -227,6 +234,11 @@ struct Plan {
     int band_off[2] = {}, nbands[2] = {}, pyr_bufb[2] = {}, pyr_ybuf[2] = {}, pyr_ymax[2] = {};
     int pyr_lp[kMaxLevels] = {};
     size_t pyr_lds[2] = {};
+    // pyramid_roll_kernel plans (same two batch classes): bands, steps, rings, LDS bytes
+    bool roll_ok[2] = {false, false};
+    int roll_bands[2] = {}, roll_steps[2] = {}, roll_band_off[2] = {}, roll_sched_off[2] = {};
+    int roll_ring_rows[2][kMaxLevels] = {}, roll_ring_off[2][kMaxLevels] = {}, roll_ydesc[2] = {};
+    size_t roll_lds[2] = {};
 };
 
 int make_tables(const orbfe_params& p, HostTables& t);
@@ -238,9 +250,10 @@ template <bool kX86> __global__ void resize_kernel(ResizeArgs);
 template <bool kX86> __global__ void resize_tail_kernel(ResizeTailArgs);
 template <bool kX86> __global__ void resize_blur_kernel(ResizeArgs);
 template <bool kX86> __global__ void pyramid_kernel(PyrArgs);
+template <bool kX86> __global__ void pyramid_roll_kernel(PyrArgs);
 template <int kP> __global__ void fast_kernel(FastArgs);
 constexpr int kFastPitch = 48;  // fast_kernel<kFastPitch>: ROI pitch known at compile time
-__global__ void octree_kernel(OctArgs);
+template <int BLK> __global__ void octree_kernel(OctArgs);
 template <bool kX86> __global__ void blur_mfma_kernel(BlurArgs);
 void blur_items(const Geo& geo, std::vector<uint32_t>& s);
 // constant MFMA fragments: [0, 128) blur_mfma_kernel's, [128, 512) describe's window blur

@@ -32,9 +32,10 @@ def run():
     from orbslam_mapsave_amd import native
     from orbslam_mapsave_amd.synth import synthetic_batch
     torch.zeros(1, device="cuda:0")
-    W, H, B = 640, 480, int(os.environ.get("OCT_B", "256"))
+    W, H, B = int(os.environ.get("OCT_W", "640")), int(os.environ.get("OCT_H", "480")), int(os.environ.get("OCT_B", "256"))
+    NF = int(os.environ.get("OCT_NF", "1000"))
     frames = torch.from_numpy(synthetic_batch(B, W, H, distinct=32)).cuda()
-    e = native.ORBextractor(1000, 1.2, 8, 32, 7, device=0, max_width=W, max_height=H, max_batch=B)
+    e = native.ORBextractor(NF, 1.2, 8, 32, 7, device=0, max_width=W, max_height=H, max_batch=B)
     cap = e.capacity(W, H)
     kps = torch.empty((B, cap * 28), dtype=torch.uint8, device="cuda")
     desc = torch.empty((B, cap, 32), dtype=torch.uint8, device="cuda")
