@@ -202,11 +202,24 @@ struct orbfe_extractor {
     // run(): the pyramid kernel reads level 0 from l0_stage and writes it to the slab level 0
     LevelPtr l0_stage{};
     bool l0_from_stage = false;
-    bool pyr_path(int n) const {  // run() makes the pyramid with pyramid_kernel for n frames
+    // ORBFE_PYR=3: the rolling-band kernel wherever it plans (measured slower than the band
+    // kernel at 640 x 480 and no faster than the per-level kernels at 1920 x 1080, DESIGN.md
+    // §5c; off by default); ORBFE_ROLL=1: where the band plan is not the faster path
+    bool force_roll = std::getenv("ORBFE_PYR") && std::strcmp(std::getenv("ORBFE_PYR"), "3") == 0;
+    bool use_roll = force_roll || (std::getenv("ORBFE_ROLL") && std::strcmp(std::getenv("ORBFE_ROLL"), "1") == 0);
+    bool band_path(int n) const {  // run() makes the pyramid with pyramid_kernel for n frames
         const int which = n >= kTailMinFrames ? 0 : 1;
-        return plan.pyr_ok && (plan.pyr_use[which] || force_pyr) && use_pyr &&
+        return plan.pyr_ok && (plan.pyr_use[which] || force_pyr) && use_pyr && !force_roll &&
                !(fused_blur && resize_blur) && plan.geo.nlevels >= 2;
     }
+    // ... or with pyramid_roll_kernel: where the band plan is not the faster path (1920 x 1080)
+    bool roll_path(int n) const {
+        const int which = n >= kTailMinFrames ? 0 : 1;
+        return plan.roll_ok[which] && use_pyr && use_roll && !force_pyr &&
+               !(fused_blur && resize_blur) && plan.geo.nlevels >= 2 &&
+               (force_roll || !band_path(n));
+    }
+    bool pyr_path(int n) const { return band_path(n) || roll_path(n); }  // one launch
     // ORBFE_RESIZE_TABLE=0: resize_kernel's horizontal pass by byte gathers (A/B)
     bool table_off = std::getenv("ORBFE_RESIZE_TABLE") && std::strcmp(std::getenv("ORBFE_RESIZE_TABLE"), "0") == 0;
     // ORBFE_DESC_MFMA=0: describe blurs its raw windows on the VALU instead of the matrix cores
@@ -319,6 +332,13 @@ struct orbfe_extractor {
         if (!g.ptab.empty())
             ORBFE_HIP(hipMemcpyAsync(ptab.p, g.ptab.data(), g.ptab.size() * sizeof(uint32_t),
                                      hipMemcpyHostToDevice, stream));
+        if (g.roll_ok[0] || g.roll_ok[1]) {
+            const int mx = (int)std::max(g.roll_ok[0] ? g.roll_lds[0] : 0, g.roll_ok[1] ? g.roll_lds[1] : 0);
+            hipFuncSetAttribute(reinterpret_cast<const void*>(&pyramid_roll_kernel<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+            hipFuncSetAttribute(reinterpret_cast<const void*>(&pyramid_roll_kernel<true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        }
         if (g.pyr_ok) {  // dynamic LDS above 64 KB must be allowed per kernel
             const int mx = (int)std::max(g.pyr_lds[0], g.pyr_lds[1]);
             hipFuncSetAttribute(reinterpret_cast<const void*>(&pyramid_kernel<false>),
@@ -390,7 +410,7 @@ struct orbfe_extractor {
         uint32_t pre_mask = 0;
         // K1 as one launch (pyramid_kernel): every level of a band of every frame in LDS
         const int which = n >= kTailMinFrames ? 0 : 1;
-        const bool one_pyr = pyr_path(n);
+        const bool one_pyr = pyr_path(n), roll = roll_path(n);
         if (l0_from_stage && !one_pyr) return ORBFE_ERR_ARG;  // callers check pyr_path first
         if (one_pyr) {
             PyrArgs pa;
@@ -409,7 +429,24 @@ struct orbfe_extractor {
             pa.ybuf = g.pyr_ybuf[which];
             pa.ymax = g.pyr_ymax[which];
             pa.bands = reinterpret_cast<const int4*>(ptab.as<uint4>() + g.band_off[which]);
-            if (x86())
+            if (roll) {
+                pa.bands = reinterpret_cast<const int4*>(ptab.as<uint4>() + g.roll_band_off[which]);
+                pa.sched = reinterpret_cast<const int*>(ptab.as<uint32_t>() + g.roll_sched_off[which]);
+                pa.nsteps = g.roll_steps[which];
+                pa.ydoff = reinterpret_cast<const int*>(ptab.as<uint32_t>() + g.roll_ydoff_off[which]);
+                pa.ydtab = reinterpret_cast<const int4*>(ptab.as<uint4>() + g.roll_ydtab_off[which]);
+                pa.ydesc = g.roll_ydesc[which];
+                for (int l = 0; l < L; ++l) {
+                    pa.ring_rows[l] = g.roll_ring_rows[which][l];
+                    pa.ring_off[l] = g.roll_ring_off[which][l];
+                }
+                if (x86())
+                    ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, pyramid_roll_kernel<true>, dim3(g.roll_bands[which], n),
+                                 dim3(kPyrBlockSize), g.roll_lds[which], stream, pa);
+                else
+                    ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, pyramid_roll_kernel<false>, dim3(g.roll_bands[which], n),
+                                 dim3(kPyrBlockSize), g.roll_lds[which], stream, pa);
+            } else if (x86())
                 ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, pyramid_kernel<true>, dim3(g.nbands[which], n),
                              dim3(kPyrBlockSize), g.pyr_lds[which], stream, pa);
             else

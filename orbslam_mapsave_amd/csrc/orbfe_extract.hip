@@ -704,7 +704,7 @@ __global__ __launch_bounds__(kPyrBlock) void pyramid_roll_kernel(PyrArgs a) {
     const uint8_t* src = a.src.base + f * a.src.fpitch;
     const int4 b0 = bt[0];
     int4* yd = reinterpret_cast<int4*>(pr_lds + a.ydesc);
-    constexpr int kPre = 4;  // level-0 chunks in flight per thread (the host bounds a step)
+    constexpr int kPre = kPyrRollPre;  // level-0 chunks in flight per thread (host-bounded)
     uint4 v[kPre];
     auto load_rows = [&](int r0, int r1) __attribute__((always_inline)) {
         const int total = (r1 - r0) * cpr;
@@ -748,43 +748,52 @@ __global__ __launch_bounds__(kPyrBlock) void pyramid_roll_kernel(PyrArgs a) {
                                           (long long)r * a.l0_copy.pitch + 16 * c) = v[u];
         }
     };
+    // row descriptors of every step (host-made): per level l >= 1 in order, the rows the step
+    // makes as {source row 0 LDS offset, source row 1 LDS offset, b0 | b1 << 16, own ring row
+    // offset}; step s's are [yo[s], yo[s + 1]) (<= kPyrBlock), one per thread, loaded a step
+    // ahead.  The thread's column-group table of the next level to make is loaded a level ahead
+    // (they sit behind this level's work and barrier instead of in front of the next one's).
+    const int* yo = a.ydoff + (size_t)band * (a.nsteps + 1);
+    int4 ydn = make_int4(0, 0, 0, 0);
+    auto yload = [&](int s) __attribute__((always_inline)) {
+        const int i0 = yo[s], n = yo[s + 1] - i0;
+        if (tid < n) ydn = a.ydtab[i0 + tid];
+    };
+    uint4 gn0 = make_uint4(0u, 0u, 0u, 0u), gn1 = gn0, gn2 = gn0;
+    auto gload = [&](int l) __attribute__((always_inline)) {
+        const int gpr = (a.w[l] + 3) >> 2;
+        if (tid / gpr < kPyrBlock / gpr) {
+            const uint4* gp = a.gtab[l] + 3 * (tid % gpr);
+            gn0 = gp[0];
+            gn1 = gp[1];
+            gn2 = gp[2];
+        }
+    };
     int e0 = b0.x;
     load_rows(e0, sc[0]);
+    yload(0);
+    gload(1);
     for (int s = 0; s < a.nsteps; ++s) {
         const int* cur = sc + s * L;
         const int* prv = s ? cur - L : nullptr;
-        // this step's row descriptors: per level l >= 1, rows [prv[l], cur[l]) of its table as
-        // {source row 0 LDS offset, source row 1 LDS offset, b0 | b1 << 16, own ring offset}
-        {
-            int base = 0;
-            for (int l = 1; l < L; ++l) {
-                const int r0 = prv ? prv[l] : bt[l].x, n = cur[l] - r0;
-                if (n <= 0) continue;
-                const int Rs = a.ring_rows[l - 1], Rd = a.ring_rows[l];
-                for (int i = tid; i < n; i += kPyrBlock) {
-                    const int r = r0 + i;
-                    const int* yy = a.yt[l] + 3 * r;
-                    const int so = a.ring_off[l - 1], ps = a.lp[l - 1];
-                    yd[base + i] = make_int4(so + (yy[0] % Rs) * ps, so + (yy[1] % Rs) * ps, yy[2],
-                                             l + 1 < L ? a.ring_off[l] + (r % Rd) * a.lp[l] : 0);
-                }
-                base += n;
-            }
-        }
+        if (tid < yo[s + 1] - yo[s]) yd[tid] = ydn;
         store_rows(e0, cur[0]);
         e0 = cur[0];
-        if (s + 1 < a.nsteps) load_rows(e0, cur[L]);  // next step's level-0 rows, in flight
+        if (s + 1 < a.nsteps) {  // next step's level-0 rows and row descriptors, in flight
+            load_rows(e0, cur[L]);
+            yload(s + 1);
+        }
         __syncthreads();
         int base = 0;
         for (int l = 1; l < L; ++l) {
+            const uint4 g0 = gn0, g1 = gn1, g2 = gn2;
+            gload(l + 1 < L ? l + 1 : 1);
             const int r0 = prv ? prv[l] : bt[l].x, nrows = cur[l] - r0;
             if (nrows <= 0) continue;  // uniform: nothing made, nothing to order
             const int4 bl = bt[l];
             const int w = a.w[l], gpr = (w + 3) >> 2, rps = kPyrBlock / gpr;
             const int gx = tid % gpr, ry = tid / gpr;
             if (ry < rps) {
-                const uint4* gp = a.gtab[l] + 3 * gx;
-                const uint4 g0 = gp[0], g1 = gp[1], g2 = gp[2];
                 const int xbase = (int)g0.x, wofs = (xbase >> 2) << 2, sh = xbase & 3;
                 const uint32_t sel[4] = {g0.y, g0.z, g0.w, g1.x};
                 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
@@ -3149,6 +3158,7 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
             g.gtab_off[l] = (int)(g.ptab.size() / 4);
             g.pyr_ok = pyramid_group_table(g.xtab, g.xoff[l], g.geo.lv[l].w, g.ptab);
         }
+        const bool groups_ok = g.pyr_ok;  // every level's column groups fit 8 source bytes
         for (int l = 0; l < L; ++l) g.pyr_lp[l] = ((g.geo.lv[l].w + 15) & ~15) + 16;
         double work = 0, own = 0;  // pixels computed by the bands vs the pyramid's
         for (int l = 1; l < L; ++l) own += (double)g.geo.lv[l].w * g.geo.lv[l].h;
@@ -3211,6 +3221,104 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
                 while (g.ptab.size() % 4) g.ptab.push_back(0u);
                 g.band_off[which] = (int)(g.ptab.size() / 4);  // int4 units
                 for (int v : bt[which]) g.ptab.push_back((uint32_t)v);
+            }
+        }
+        // pyramid_roll_kernel plans: the same band rows (plan_bands), streamed in steps of
+        // `chunk` level-0 rows.  The host runs the kernel's rule — a level's row is made in the
+        // first step after which both its source rows exist — to get every step's row ranges
+        // and each ring's size (the rows its next level still needs when the step starts, plus
+        // the rows the step makes).  Large batches: a few bands per frame (2 or 3 workgroups
+        // per CU by LDS); small ones: thin bands for latency.
+        for (int which = 0; which < 2 && groups_ok; ++which) {
+            const char* be = std::getenv(which == 0 ? "ORBFE_ROLL_BANDS" : "ORBFE_ROLL_BANDS_SMALL");
+            const char* ce = std::getenv(which == 0 ? "ORBFE_ROLL_CHUNK" : "ORBFE_ROLL_CHUNK_SMALL");
+            int nb = be ? std::atoi(be) : (which == 0 ? std::max(1, std::min(8, (h0 + 359) / 360))
+                                                      : std::max(1, std::min(std::min(64, htop), h0 / 24)));
+            nb = std::max(1, std::min(nb, htop));
+            const int cpr0 = (g.geo.lv[0].w + 15) >> 4;
+            int C0 = ce ? std::atoi(ce) : (which == 0 ? 16 : 8);
+            C0 = std::max(2, std::min(C0, (kPyrRollPre * kPyrBlockSize) / cpr0));
+            std::vector<int> rbt;
+            size_t lds_unused;
+            int u1, u2, u3;
+            plan_bands(nb, rbt, lds_unused, u1, u2, u3);
+            auto B4 = [&](int b, int l, int k) { return rbt[((size_t)b * L + l) * 4 + k]; };
+            int S = 1;
+            for (int b = 0; b < nb; ++b)
+                S = std::max(S, (B4(b, 0, 1) - B4(b, 0, 0) + 1 + C0 - 1) / C0);
+            std::vector<int> sched((size_t)nb * S * L);
+            int R[kMaxLevels] = {};
+            int ymax = 1;
+            bool ok = C0 * cpr0 <= kPyrRollPre * kPyrBlockSize;
+            auto y0 = [&](int l, int r) { return g.ytab[g.yoff[l] + 3 * r]; };
+            auto y1 = [&](int l, int r) { return g.ytab[g.yoff[l] + 3 * r + 1]; };
+            for (int b = 0; b < nb && ok; ++b) {
+                int e[kMaxLevels], ep[kMaxLevels];
+                for (int l = 0; l < L; ++l) e[l] = B4(b, l, 0);
+                for (int s = 0; s < S; ++s) {
+                    for (int l = 0; l < L; ++l) ep[l] = e[l];
+                    e[0] = std::min(B4(b, 0, 0) + (s + 1) * C0, B4(b, 0, 1) + 1);
+                    int made = 0;
+                    for (int l = 1; l < L; ++l) {
+                        int r = e[l];
+                        while (r <= B4(b, l, 1) && y1(l, r) < e[l - 1]) ++r;
+                        e[l] = r;
+                        made += e[l] - ep[l];
+                    }
+                    ymax = std::max(ymax, made);
+                    for (int l = 0; l + 1 < L; ++l) {
+                        // rows of level l the ring must hold during the step
+                        const int need = ep[l + 1] <= B4(b, l + 1, 1) ? y0(l + 1, ep[l + 1]) : e[l];
+                        R[l] = std::max(R[l], e[l] - std::min(need, ep[l]));
+                    }
+                    for (int l = 0; l < L; ++l) sched[((size_t)b * S + s) * L + l] = e[l];
+                }
+                for (int l = 0; l < L; ++l) ok = ok && e[l] == B4(b, l, 1) + 1;  // every row made
+            }
+            size_t off = 0;
+            for (int l = 0; l + 1 < L; ++l) {
+                R[l] = std::max(R[l], 2);
+                g.roll_ring_rows[which][l] = R[l];
+                g.roll_ring_off[which][l] = (int)off;
+                off += ((size_t)R[l] * g.pyr_lp[l] + 15) & ~(size_t)15;
+            }
+            g.roll_ydesc[which] = (int)off;
+            g.roll_lds[which] = off + (size_t)ymax * 16;
+            g.roll_ok[which] = ok && ymax <= kPyrBlockSize && g.roll_lds[which] <= 160 * 1024;
+            // every step's row descriptors (the kernel's LDS offsets of the two source rows in
+            // the ring below, the coefficients, the row's own ring offset)
+            std::vector<int> ydoff((size_t)nb * (S + 1)), ydtab;
+            for (int b = 0; b < nb && g.roll_ok[which]; ++b) {
+                for (int s = 0; s < S; ++s) {
+                    ydoff[(size_t)b * (S + 1) + s] = (int)(ydtab.size() / 4);
+                    for (int l = 1; l < L; ++l) {
+                        const int r0 = s ? sched[((size_t)b * S + s - 1) * L + l] : B4(b, l, 0);
+                        const int r1 = sched[((size_t)b * S + s) * L + l];
+                        const int so = g.roll_ring_off[which][l - 1], ps = g.pyr_lp[l - 1];
+                        for (int r = r0; r < r1; ++r) {
+                            const int* yy = &g.ytab[g.yoff[l] + 3 * r];
+                            ydtab.push_back(so + (yy[0] % R[l - 1]) * ps);
+                            ydtab.push_back(so + (yy[1] % R[l - 1]) * ps);
+                            ydtab.push_back(yy[2]);
+                            ydtab.push_back(l + 1 < L ? g.roll_ring_off[which][l] + (r % R[l]) * g.pyr_lp[l] : 0);
+                        }
+                    }
+                }
+                ydoff[(size_t)b * (S + 1) + S] = (int)(ydtab.size() / 4);
+            }
+            g.roll_bands[which] = nb;
+            g.roll_steps[which] = S;
+            if (g.roll_ok[which]) {
+                while (g.ptab.size() % 4) g.ptab.push_back(0u);
+                g.roll_band_off[which] = (int)(g.ptab.size() / 4);
+                for (int v : rbt) g.ptab.push_back((uint32_t)v);
+                g.roll_sched_off[which] = (int)g.ptab.size();
+                for (int v : sched) g.ptab.push_back((uint32_t)v);
+                g.roll_ydoff_off[which] = (int)g.ptab.size();
+                for (int v : ydoff) g.ptab.push_back((uint32_t)v);
+                while (g.ptab.size() % 4) g.ptab.push_back(0u);
+                g.roll_ydtab_off[which] = (int)(g.ptab.size() / 4);
+                for (int v : ydtab) g.ptab.push_back((uint32_t)v);
             }
         }
     }

@@ -102,6 +102,8 @@ struct PyrArgs {
     // sched[(band * nsteps + step) * L + l] = the level's rows made once the step is done
     // (exclusive end row); row descriptors of a step at ydesc (4 ints per row)
     const int* sched;
+    const int* ydoff;              // [band][step 0 .. nsteps]: start of the step's descriptors
+    const int4* ydtab;
     int nsteps, ydesc;
     int ring_rows[kMaxLevels], ring_off[kMaxLevels];
 };
@@ -237,6 +239,7 @@ struct Plan {
     // pyramid_roll_kernel plans (same two batch classes): bands, steps, rings, LDS bytes
     bool roll_ok[2] = {false, false};
     int roll_bands[2] = {}, roll_steps[2] = {}, roll_band_off[2] = {}, roll_sched_off[2] = {};
+    int roll_ydoff_off[2] = {}, roll_ydtab_off[2] = {};
     int roll_ring_rows[2][kMaxLevels] = {}, roll_ring_off[2][kMaxLevels] = {}, roll_ydesc[2] = {};
     size_t roll_lds[2] = {};
 };
@@ -271,6 +274,7 @@ extern __constant__ int c_umax[16];
 constexpr int kPyrLdsCapKB = 80;
 constexpr int kPyrBlockSize = 1024;
 constexpr int kPyrSmallRows = 12;
+constexpr int kPyrRollPre = 4;  // pyramid_roll_kernel: level-0 chunks in flight per thread
 // band plans whose rows computed exceed the pyramid's by more than this use the per-level
 // kernels instead (large batches: throughput; small ones: latency)
 constexpr double kPyrMaxWork = 1.25, kPyrMaxWorkSmall = 3.0;

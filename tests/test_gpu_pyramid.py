@@ -128,3 +128,51 @@ def test_per_level_kernels_exact(size, arith, table, monkeypatch):
         _levels_exact(e, p, imgs[4:5], var)
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("size", [(1920, 1080), (640, 480), (643, 481), (331, 247), (97, 73), (1281, 722)])
+@pytest.mark.parametrize("batch", [1, 9])
+@pytest.mark.parametrize("arith", ["scalar", "x86"])
+def test_roll_levels_bit_exact(size, batch, arith, monkeypatch):
+    """pyramid_roll_kernel (the one-launch pyramid where the band kernel's seams cost too much:
+    the default at 1920x1080; ORBFE_PYR=3 forces it everywhere): every level of every frame
+    byte-exact against the oracle in both readings, single frames (thin bands) and batches."""
+    from orbslam_mapsave_amd.native import ORBextractor
+    monkeypatch.setenv("ORBFE_PYR", "3")
+    w, h = size
+    nf = 2000 if w > 1000 else 1000
+    p = oracle.params(nf, 1.2, 8, 20, 7)
+    e = ORBextractor(nf, 1.2, 8, 20, 7, device=0, max_width=w, max_height=h)
+    var = oracle.VAR_H5_SSE2 if arith == "x86" else 0
+    if arith == "x86":
+        e.set_arithmetic(e.ARITH_X86_SIMD)
+    try:
+        imgs = np.stack([synthetic_frame(5 * w + s, w, h) for s in range(batch)])
+        if batch == 1:
+            e(imgs[0])
+        else:
+            e.extract_batch(imgs)
+        _levels_exact(e, p, imgs[:3], var)
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("bands,chunk", [("1", "2"), ("3", "5"), ("7", "16"), ("2", "33")])
+def test_roll_plans(bands, chunk, monkeypatch):
+    """Other rolling plans (band counts, level-0 rows per step: ring sizes, step counts and the
+    per-thread chunk bound change) give the same levels and keypoints."""
+    from orbslam_mapsave_amd.native import ORBextractor
+    monkeypatch.setenv("ORBFE_PYR", "3")
+    monkeypatch.setenv("ORBFE_ROLL_BANDS", bands)
+    monkeypatch.setenv("ORBFE_ROLL_CHUNK", chunk)
+    p = oracle.params(2000, 1.2, 8, 20, 7)
+    e = ORBextractor(2000, 1.2, 8, 20, 7, device=0, max_width=1920, max_height=1080)
+    try:
+        imgs = np.stack([synthetic_frame(170 + s, 1920, 1080) for s in range(8)])
+        kps, desc, cnt = e.extract_batch(imgs)
+        _levels_exact(e, p, imgs[:2], 0)
+        okps, odesc = oracle.extract(p, imgs[1])
+        assert kps[1, :cnt[1]].tobytes() == okps.tobytes()
+        assert np.array_equal(desc[1, :cnt[1]], odesc)
+    finally:
+        e.close()

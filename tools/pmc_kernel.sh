@@ -8,5 +8,5 @@ OUT=gpurun_out/pmc_$1
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-trace --kernel-include-regex "$RX" -d $OUT -o run \
-    --output-format csv -- python3 bench.py --cpu-budget 0 --steps 3 --warmup 1 --streams 1 \
+    --output-format csv -- python3 bench.py --cpu-budget 0 --steps 3 --warmup 1 --streams 1 --soak-s 0 $PMC_ARGS \
     > $OUT/stdout.txt 2>&1
