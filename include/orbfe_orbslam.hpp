@@ -61,6 +61,25 @@ public:
         descriptors.resize((size_t)n * 32);
     }
 
+    // Zero-copy form (orbfe_input_buffer / orbfe_extract_staged): the caller writes the gray
+    // frame into InputBuffer (GrabImageMonocular's cvtColor target, Tracking.cc:409-422), then
+    // ExtractStaged runs operator() on it in place (Frame::ExtractORB, Frame.cc:358-364).
+    uint8_t* InputBuffer(int cols, int rows, size_t* step) {
+        uint8_t* buf = nullptr;
+        check("orbfe_input_buffer", orbfe_input_buffer(h_, cols, rows, &buf, step));
+        return buf;
+    }
+    void ExtractStaged(int cols, int rows, std::vector<orbfe_keypoint>& keypoints,
+                       std::vector<uint8_t>& descriptors) {
+        int n = 0;
+        check("orbfe_extract_staged", orbfe_extract_staged(h_, cols, rows, nullptr, 0, nullptr, &n));
+        const orbfe_keypoint* k = nullptr;
+        const uint8_t* d = nullptr;
+        check("orbfe_staged_outputs", orbfe_staged_outputs(h_, &k, &d, &n));
+        keypoints.assign(k, k + n);
+        descriptors.assign(d, d + (size_t)n * 32);
+    }
+
     int GetLevels() { return orbfe_get_levels(h_); }
     float GetScaleFactor() { return orbfe_get_scale_factor(h_); }
     std::vector<float> GetScaleFactors() { return table(0); }

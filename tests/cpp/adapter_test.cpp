@@ -43,6 +43,17 @@ int main() {
                           !std::memcmp(desc.data(), odesc.data(), (size_t)n * 32);
         std::printf("seed %u: %zu keypoints (oracle %d) %s\n", seed, kps.size(), n, same ? "bit-exact" : "MISMATCH");
         fails += !same;
+        // the zero-copy form: the frame written into the staging buffer, outputs read in place
+        size_t step = 0;
+        uint8_t* buf = ex.InputBuffer(W, H, &step);
+        for (int y = 0; y < H; ++y) std::memcpy(buf + (size_t)y * step, img.data() + (size_t)y * W, W);
+        std::vector<orbfe_keypoint> skps;
+        std::vector<uint8_t> sdesc;
+        ex.ExtractStaged(W, H, skps, sdesc);
+        const bool same_staged = (int)skps.size() == n && !std::memcmp(skps.data(), okps.data(), n * sizeof(orbfe_keypoint)) &&
+                                 !std::memcmp(sdesc.data(), odesc.data(), (size_t)n * 32);
+        std::printf("seed %u staged: %zu keypoints %s\n", seed, skps.size(), same_staged ? "bit-exact" : "MISMATCH");
+        fails += !same_staged;
     }
     // scale tables through the getters
     std::vector<float> sf = ex.GetScaleFactors(), osf(8);
