@@ -163,6 +163,25 @@ __device__ __forceinline__ uint32_t resize_px(uint32_t t0, uint32_t t1, uint32_t
     return min(sse2 ? sv : sc, 255u);
 }
 
+// Four pixels of a row (columns x .. x + 3) from their horizontal sums.  x86: a group entirely
+// inside the SSE2 body (x + 3 < xb, nearly every group) takes the body formula alone instead of
+// computing both and selecting per pixel.
+template <bool kX86>
+__device__ __forceinline__ uint32_t resize4(const uint32_t (&t0)[4], const uint32_t (&t1)[4],
+                                            uint32_t b0, uint32_t b1, int x, int xb) {
+    uint32_t packed = 0;
+    if (kX86 && x + 3 < xb) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            packed |= min((((uint32_t)__umul24(t0[k] >> 4, b0) >> 16) +
+                           ((uint32_t)__umul24(t1[k] >> 4, b1) >> 16) + 2u) >> 2, 255u) << (8 * k);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) packed |= resize_px<kX86>(t0[k], t1[k], b0, b1, x + k < xb) << (8 * k);
+    }
+    return packed;
+}
+
 #ifndef ORBFE_RS_TH
 #define ORBFE_RS_TH 32
 #endif
@@ -251,9 +270,7 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
             uint32_t t0[4], t1[4];
             hsum(ry0, t0);
             hsum(ry1, t1);
-            uint32_t packed = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) packed |= resize_px<kX86>(t0[k], t1[k], b0, b1, x + k < a.simd_xb) << (8 * k);
+            const uint32_t packed = resize4<kX86>(t0, t1, b0, b1, x, a.simd_xb);
             uint8_t* d = dst + (long long)y * a.dst.pitch + x;
             if (n == 4) {
                 *reinterpret_cast<uint32_t*>(d) = packed;
@@ -281,15 +298,15 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
         const int b0 = bb & 0xffff, b1 = (int)((unsigned)bb >> 16);
         const uint8_t* s0 = rs_lds + ry0 * P;
         const uint8_t* s1 = rs_lds + ry1 * P;
-        uint32_t packed = 0;
+        uint32_t t0[4], t1[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             // coefficients sum to 2048 (INTER_RESIZE_COEF_SCALE): t < 2^19, t * b < 2^30, so
             // every product is a full-rate v_mul_u32_u24 (not the quarter-rate v_mul_lo_u32)
-            const uint32_t t0 = __umul24(s0[x0[k]], a0[k]) + __umul24(s0[x1[k]], a1[k]);
-            const uint32_t t1 = __umul24(s1[x0[k]], a0[k]) + __umul24(s1[x1[k]], a1[k]);
-            packed |= resize_px<kX86>(t0, t1, b0, b1, x + k < a.simd_xb) << (8 * k);
+            t0[k] = __umul24(s0[x0[k]], a0[k]) + __umul24(s0[x1[k]], a1[k]);
+            t1[k] = __umul24(s1[x0[k]], a0[k]) + __umul24(s1[x1[k]], a1[k]);
         }
+        const uint32_t packed = resize4<kX86>(t0, t1, b0, b1, x, a.simd_xb);
         uint8_t* d = dst + (long long)y * a.dst.pitch + x;
         if (n == 4) {
             *reinterpret_cast<uint32_t*>(d) = packed;
@@ -658,9 +675,7 @@ __global__ __launch_bounds__(kPyrBlock) void pyramid_kernel(PyrArgs a) {
             uint32_t t0[4], t1[4];
             hsum(yy[0] - bs.x, t0);
             hsum(yy[1] - bs.x, t1);
-            uint32_t packed = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) packed |= resize_px<kX86>(t0[k], t1[k], b0, b1, x + k < xb) << (8 * k);
+            const uint32_t packed = resize4<kX86>(t0, t1, b0, b1, x, xb);
             *reinterpret_cast<uint32_t*>(d + (r - bl.x) * dpitch + x) = packed;
             if (r >= bl.z && r < bl.w) {
                 uint8_t* o = dst + (long long)r * dp.pitch + x;
@@ -818,9 +833,7 @@ __global__ __launch_bounds__(kPyrBlock) void pyramid_roll_kernel(PyrArgs a) {
                     uint32_t t0[4], t1[4];
                     hsum(d.x, t0);
                     hsum(d.y, t1);
-                    uint32_t packed = 0;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) packed |= resize_px<kX86>(t0[k], t1[k], bb0, bb1, x + k < xb) << (8 * k);
+                    const uint32_t packed = resize4<kX86>(t0, t1, bb0, bb1, x, xb);
                     if (ring) *reinterpret_cast<uint32_t*>(pr_lds + d.w + x) = packed;
                     const int r = r0 + j;
                     if (r >= bl.z && r < bl.w) {
@@ -941,13 +954,13 @@ __global__ __launch_bounds__(kTailBlock) void resize_tail_kernel(ResizeTailArgs 
                 const int b0 = bb & 0xffff, b1 = (int)((unsigned)bb >> 16);
                 const uint8_t* s0 = s + yt[3 * y] * sp_l;
                 const uint8_t* s1 = s + yt[3 * y + 1] * sp_l;
-                uint32_t packed = 0;
+                uint32_t t0[4], t1[4];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const uint32_t t0 = __umul24(s0[x0[q]], a0[q]) + __umul24(s0[x1[q]], a1[q]);
-                    const uint32_t t1 = __umul24(s1[x0[q]], a0[q]) + __umul24(s1[x1[q]], a1[q]);
-                    packed |= resize_px<kX86>(t0, t1, b0, b1, x + q < xb) << (8 * q);
+                    t0[q] = __umul24(s0[x0[q]], a0[q]) + __umul24(s0[x1[q]], a1[q]);
+                    t1[q] = __umul24(s1[x0[q]], a0[q]) + __umul24(s1[x1[q]], a1[q]);
                 }
+                const uint32_t packed = resize4<kX86>(t0, t1, b0, b1, x, xb);
                 *reinterpret_cast<uint32_t*>(d + y * dp_l + x) = packed;  // LDS pitch % 4 == 0
                 uint8_t* o = dst + (long long)y * dp.pitch + x;
                 if (n == 4) {
@@ -2229,7 +2242,10 @@ constexpr bool kDescLateStore = ORBFE_DESC_LATE_STORE != 0;
 #define ORBFE_DESC_WAVES 6
 #endif
 #ifndef ORBFE_DESC_WAVES_B
-#define ORBFE_DESC_WAVES_B 5  // the x86 reading and the small-batch groups (spill at 6)
+#define ORBFE_DESC_WAVES_B 5  // the small-batch groups (spill at 6)
+#endif
+#ifndef ORBFE_DESC_WAVES_X86
+#define ORBFE_DESC_WAVES_X86 6  // the x86 reading (4 dwords of scratch at 6)
 #endif
 // ORBFE_DESC_PAT_LDS: the pattern pairs read as floats from LDS per keypoint (one b128 per 64
 // pairs) instead of widened from packed bytes held in registers (four v_cvt per 64 pairs)
@@ -2260,7 +2276,7 @@ typedef float float2v __attribute__((ext_vector_type(2)));
 // pre_mask read blurred windows).  kWinMfma — the raw window goes from its global loads
 // straight into i8 MFMA A fragments and both passes run on the matrix cores (below).
 template <int kDescGroup, bool kX86, int kWin>
-__global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kX86 || kDescGroup < 8 ? ORBFE_DESC_WAVES_B : ORBFE_DESC_WAVES) : 1) void describe_kernel(DescArgs a) {
+__global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? ORBFE_DESC_WAVES_B : kX86 ? ORBFE_DESC_WAVES_X86 : ORBFE_DESC_WAVES) : 1) void describe_kernel(DescArgs a) {
     constexpr bool kPre = kWin == kWinPre, kMfma = kWin == kWinMfma;
     constexpr bool kLate = kDescLateStore && kMfma;
     int bx, f;
@@ -2650,7 +2666,8 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kX86 || kDescGroup 
                 }
                 Blo[3] = 0;
                 Bhi[3] = 0;
-                const bool even = xs + 16 * s < 0;  // x86: column in the SIMD body
+                // x86: 1 where the column is in the SIMD body (round half to even), else 0
+                const uint32_t em = xs + 16 * s < 0 ? 1u : 0u;
                 i32x4m Vs[3];  // (kFragLds & 4: the three V fragments read once per N-tile)
                 if constexpr ((kFragLds & 4) != 0) {
 #pragma unroll
@@ -2666,7 +2683,11 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kX86 || kDescGroup 
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         s4[i] = ((uint32_t)Dh[i] << 8) + (uint32_t)Dl[i];
-                        if constexpr (kX86) s4[i] += blur_round_bit(s4[i], even);
+                        // x86 (kRndM = 0x7fff): + bit 16 of the sum in the SIMD body, + 1 past
+                        // it.  The bit of sum + 0x7fff equals the true sum's bit 16 in the only
+                        // case it matters (a tie, low half 0x8000), and adding it elsewhere
+                        // changes no carry: (em & (s4 >> 16)) | (~em & 1) in one v_bfi
+                        if constexpr (kX86) s4[i] += (em & (s4[i] >> 16)) | (~em & 1u);
                     }
                     // min(sum >> 16, 255) of two sums at once (sum >> 16 <= 257 < 2^16)
                     const us2 sat = us2{255, 255};
