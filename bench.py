@@ -343,10 +343,11 @@ def parse_args():
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the multi-rank launch: gloo backend, no GPU, the "
                          "config-4 exchange step on small random descriptor slabs")
-    ap.add_argument("--arith", default="scalar", choices=["scalar", "x86"],
-                    help="arithmetic reading of the extractor (orbfe_set_arithmetic): OpenCV's "
-                         "scalar paths, or the SSE2 resize / blur bodies + FMA rotation of an "
-                         "x86 build (DESIGN.md §2)")
+    ap.add_argument("--arith", default="x86", choices=["scalar", "x86"],
+                    help="arithmetic reading of the extractor (orbfe_set_arithmetic): the SSE2 "
+                         "resize / blur bodies + FMA rotation of the reference's x86-64 build "
+                         "(the default, as the library's), or OpenCV's portable scalar paths "
+                         "(DESIGN.md §2)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--soak-s", type=float, default=8.0,

@@ -87,9 +87,10 @@ orbfe_extractor* orbfe_create(const orbfe_params* params, int device, int max_wi
 void orbfe_destroy(orbfe_extractor* h);
 
 /* Which build of the reference's OpenCV 3.3 primitives the pixel arithmetic reproduces
- * (tests/golden/README.md).  ORBFE_ARITH_SCALAR (the default): OpenCV's scalar
+ * (tests/golden/README.md).  ORBFE_ARITH_SCALAR: OpenCV's portable scalar
  * paths — resize FixedPtCast<int,uchar,22>, blur FixedPtCastEx, uncontracted rotation products.
- * ORBFE_ARITH_X86_SIMD: what an x86-64 build of the reference computes — the SSE2 bodies of
+ * ORBFE_ARITH_X86_SIMD (the default, what the reference's build.sh Release build computes on
+ * x86-64, where SSE2 is always on): the SSE2 bodies of
  * VResizeLinearVec_32s8u (ORBextractor.cc:1123; ~18 % of the pixels of levels >= 1 differ
  * by 1 from the scalar path) and SymmColumnVec_32s8u (1089; ties rounded to even) with the
  * scalar tails past them, and the descriptor rotation FMA-contracted as GCC -O3 on an FMA host

@@ -40,9 +40,13 @@ def _check(fn: str, st: int) -> None:
         raise OrbfeError(fn, st)
 
 
-# Build-dependent readings of the reference for the residual study (orb_oracle.h,
-# oracle/residuals.py); 0 is the pinned oracle every GPU test compares against.
+# Build-dependent readings of the reference (orb_oracle.h, oracle/residuals.py): the default is
+# the x86-64 build's (H4 FMA + H5 SSE2 + H6 SIMD), matched by the GPU's default arithmetic;
+# VAR_SCALAR is OpenCV's portable reading (ORBFE_ARITH_SCALAR).
 VAR_H2_ADDR, VAR_H4_COSF, VAR_H4_FMA, VAR_H5_SSE2, VAR_H6_SIMD = 1, 2, 4, 8, 16
+VAR_SCALAR = 0                                    # OpenCV's portable scalar reading
+VAR_X86 = VAR_H4_FMA | VAR_H5_SSE2 | VAR_H6_SIMD  # the reference's x86-64 build (the default)
+DEFAULT_VARIANT = VAR_X86
 
 
 def set_variant(flags: int) -> None:

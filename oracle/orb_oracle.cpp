@@ -58,7 +58,9 @@ enum {
     kVarH5Sse2 = 8,   // resize vertical pass: OpenCV's SSE2 VResizeLinearVec_32s8u body
     kVarH6Simd = 16,  // blur column pass: OpenCV's SSE2 SymmColumnVec_32s8u (float) body
 };
-int g_variant = 0;
+// The default reading is the reference's x86-64 build: SSE2 resize / blur bodies
+// and the FMA-contracted rotation; 0 is OpenCV's portable scalar reading.
+int g_variant = kVarH4Fma | kVarH5Sse2 | kVarH6Simd;
 
 // Pixels [0, n) of a row that OpenCV 3.3's SSE2 vertical kernels produce (the rest goes to
 // the scalar tail): VResizeLinearVec_32s8u runs 16-pixel steps while x <= w - 16, then 4-pixel

@@ -29,10 +29,11 @@ int oracle_reference_constants(int32_t out[6]);
 /* Level sizes of the pyramid for a w x h input (ORBextractor.cc:1114-1115). */
 int oracle_level_sizes(const orbfe_params* p, int w, int h, int32_t* lw, int32_t* lh);
 
-/* Residual study only (oracle/residuals.py): switch to other build-dependent readings of the
- * reference.  Bits: 1 H2 oct-tree ties by real heap address, 2 H4 glibc cosf/sinf, 4 H4 FMA
- * contraction, 8 H5 SSE2 resize rounding, 16 H6 SIMD blur rounding; 0 = the pinned oracle the
- * GPU is checked against.  Process-global, not thread-safe. */
+/* The build-dependent reading of the reference the oracle computes.  Bits: 1 H2 oct-tree ties
+ * by real heap address (residual study only), 2 H4 glibc cosf/sinf, 4 H4 FMA contraction, 8 H5
+ * SSE2 resize rounding, 16 H6 SIMD blur rounding.  Default 4 | 8 | 16: the reference's x86-64
+ * build, which the GPU's default (ORBFE_ARITH_X86_SIMD) is checked against; 0 = OpenCV's
+ * portable scalar reading (ORBFE_ARITH_SCALAR).  Process-global, not thread-safe. */
 int oracle_set_variant(int flags);
 int oracle_get_variant(void);
 

@@ -113,6 +113,12 @@ def frame_set(quick: bool = False):
 
 
 def measure(quick: bool = False, variants=None) -> dict:
+    """Every variant against the portable scalar reading (variant 0)."""
+    with oracle.variant(oracle.VAR_SCALAR):
+        return _measure(quick, variants)
+
+
+def _measure(quick: bool = False, variants=None) -> dict:
     variants = variants or VARIANTS
     res = {"variants": {}, "frames": {}}
     for name, p, frames in frame_set(quick):
@@ -161,6 +167,11 @@ def host_info() -> dict:
 def h2_repeats(n: int = 4) -> list[int]:
     """H2 depends on the heap history: the 32-frame pass repeated in one process (the heap
     state each pass starts from is what the previous pass left), keypoints changed per pass."""
+    with oracle.variant(oracle.VAR_SCALAR):
+        return _h2_repeats(n)
+
+
+def _h2_repeats(n: int) -> list[int]:
     p = oracle.params(1000, 1.2, 8, 32, 7)
     frames = [synthetic_frame(s, 640, 480) for s in range(32)]
     canon = [oracle.extract(p, img) for img in frames]

@@ -124,7 +124,7 @@ struct orbfe_extractor {
     int device = 0;
     hipStream_t own = nullptr, stream = nullptr;
     HostTables tab{};
-    int arith = ORBFE_ARITH_SCALAR;  // orbfe_set_arithmetic
+    int arith = ORBFE_ARITH_X86_SIMD;  // orbfe_set_arithmetic (default: the reference's x86-64 build)
     bool x86() const { return arith == ORBFE_ARITH_X86_SIMD; }
     Plan plan;
     bool planned = false;
@@ -224,6 +224,8 @@ struct orbfe_extractor {
     bool table_off = std::getenv("ORBFE_RESIZE_TABLE") && std::strcmp(std::getenv("ORBFE_RESIZE_TABLE"), "0") == 0;
     // ORBFE_DESC_MFMA=0: describe blurs its raw windows on the VALU instead of the matrix cores
     bool desc_mfma = !(std::getenv("ORBFE_DESC_MFMA") && std::strcmp(std::getenv("ORBFE_DESC_MFMA"), "0") == 0);
+    // ORBFE_DESC_STRIDE=0: describe waves take consecutive slots in batches too (A/B)
+    bool desc_stride = !(std::getenv("ORBFE_DESC_STRIDE") && std::strcmp(std::getenv("ORBFE_DESC_STRIDE"), "0") == 0);
     // ORBFE_OCT_SMALL=0: small batches keep the 256-thread oct-tree (A/B)
     bool oct_small = !(std::getenv("ORBFE_OCT_SMALL") && std::strcmp(std::getenv("ORBFE_OCT_SMALL"), "0") == 0);
     bool graph_broken = std::getenv("ORBFE_NO_GRAPH") != nullptr;  // capture failed once (or
@@ -605,6 +607,9 @@ struct orbfe_extractor {
         const int group = n >= kDescSmallBatch ? kDescGroupSize : kDescGroupSmall;
         const int per_block = (kDescBlockSize / 64) * group;  // slots per workgroup
         const dim3 dgrid((g.geo.out_total + per_block - 1) / per_block, n);
+        // batches: strided slots (a frame's waves sweep its oct-tree output in runs of W
+        // consecutive slots, sharing window lines in L2); ORBFE_DESC_STRIDE=0: grouped slots
+        da.wave_stride = group == kDescGroupSize && desc_stride ? (int)dgrid.x * (kDescBlockSize / 64) : 0;
         // window source: every level pre-blurred, some levels pre-blurred (VALU blur for the
         // rest), or none (the matrix-core blur unless ORBFE_DESC_MFMA=0)
         const int win = all_pre ? kWinPre : (da.pre_mask == 0u && desc_mfma ? kWinMfma : kWinValu);

@@ -2302,24 +2302,50 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
                                          (float)c_pattern[4 * i + 2], (float)c_pattern[4 * i + 3]);
         __syncthreads();
     }
-    const int s0 = (bx * (kDescBlock / 64) + (threadIdx.x >> 6)) * kDescGroup;
+    // the frame's waves: wave wv takes slots wv * G .. wv * G + G - 1 (grouped), or with
+    // a.wave_stride = W (the waves of a frame) slots wv, wv + W, wv + 2 W, ... (strided): then at
+    // any moment the frame's waves work on one run of W consecutive oct-tree slots — one level,
+    // clustered by the node list's quadrant order — so the 128-byte lines their windows share
+    // are fetched while they are still in the XCD's L2 (1080p: the frames in flight per XCD
+    // overflow it otherwise)
+    const int wv = bx * (kDescBlock / 64) + (threadIdx.x >> 6);
+    const int stride = a.wave_stride;
+    const int s0 = stride ? wv : wv * kDescGroup;
     if (s0 >= a.out_total) return;
 
-    // lane j < kDescGroup: slot s0 + j -> level, key, output index.  The level key counts are
-    // one load (lane q holds level q's) and their exclusive prefix a wave scan, so a wave's
-    // start is one global round trip, not a chain of dependent loads.  The group's slots lie in
-    // the level of s0 or the next one (every level has >= 20 slots).
+    // lane j < kDescGroup: slot s0 + j (grouped) or s0 + j W (strided) -> level, key, output
+    // index.  The level key counts are one load (lane q holds level q's) and their exclusive
+    // prefix a wave scan, so a wave's start is one global round trip, not a chain of dependent
+    // loads.  Grouped, the group's slots lie in the level of s0 or the next one (every level
+    // has >= 20 slots); strided, each lane finds its level.
     const int cq = lane < a.nlevels ? max(cnt[lane], 0) : 0;
     const int pre = wave_inclusive_sum(cq) - cq;
+    int my_l = 0, my_key = 0, my_o = 0;
+    bool valid = false;
+    if (stride) {
+        const int slot = min(s0 + min(lane, kDescGroup - 1) * stride, a.out_total - 1);
+        int lv = 0, off = 0;
+        for (int k = 1; k < a.nlevels; ++k) {
+            const bool ge = slot >= a.out_off[k];
+            lv = ge ? k : lv;
+            off = ge ? a.out_off[k] : off;
+        }
+        const int c = __shfl(cq, lv, 64), pr = __shfl(pre, lv, 64);  // every lane active
+        const int idx = slot - off;
+        if (lane < kDescGroup && s0 + lane * stride < a.out_total && idx < c && idx + pr < a.kps_cap) {
+            valid = true;
+            my_l = lv;
+            my_o = idx + pr;
+            my_key = (int)a.oct_out[f * a.out_total + slot];
+        }
+    }
     int l0 = 0;
-    while (l0 + 1 < a.nlevels && s0 >= a.out_off[l0 + 1]) ++l0;  // uniform: scalar loads
+    while (!stride && l0 + 1 < a.nlevels && s0 >= a.out_off[l0 + 1]) ++l0;  // uniform: scalar loads
     const int l1 = min(l0 + 1, a.nlevels - 1);
     const int off0 = a.out_off[l0], off1 = l1 > l0 ? a.out_off[l1] : a.out_total;
     const int c0 = __builtin_amdgcn_readlane(cq, l0), c1 = __builtin_amdgcn_readlane(cq, l1);
     const int p0 = __builtin_amdgcn_readlane(pre, l0), p1 = __builtin_amdgcn_readlane(pre, l1);
-    int my_l = 0, my_key = 0, my_o = 0;
-    bool valid = false;
-    if (lane < kDescGroup && s0 + lane < a.out_total) {
+    if (!stride && lane < kDescGroup && s0 + lane < a.out_total) {
         const int slot = s0 + lane;
         const bool nx = slot >= off1;
         const int idx = slot - (nx ? off1 : off0);

@@ -164,6 +164,7 @@ struct BlurArgs {
 
 struct DescArgs {
     int nlevels, out_total, kps_cap;
+    int wave_stride;  // 0: a wave takes G consecutive slots; W > 0: slots wv, wv + W, ... (W = waves per frame)
     int out_off[kMaxLevels];
     float scale[kMaxLevels], size[kMaxLevels];
     int w[kMaxLevels], h[kMaxLevels];

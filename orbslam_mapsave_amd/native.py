@@ -174,9 +174,9 @@ class ORBextractor:
     ARITH_SCALAR, ARITH_X86_SIMD = 0, 1
 
     def set_arithmetic(self, mode: int) -> None:
-        """orbfe_set_arithmetic: ARITH_SCALAR (OpenCV's scalar paths, the default) or
-        ARITH_X86_SIMD (the SSE2 resize / blur bodies and FMA-contracted rotation of an x86
-        build of the reference)."""
+        """orbfe_set_arithmetic: ARITH_X86_SIMD (the default: the SSE2 resize / blur bodies and
+        FMA-contracted rotation of the reference's x86-64 build) or ARITH_SCALAR (OpenCV's
+        portable scalar paths)."""
         _check("orbfe_set_arithmetic", lib().orbfe_set_arithmetic(self._h, int(mode)))
 
     def capacity(self, w: int | None = None, h: int | None = None) -> int:

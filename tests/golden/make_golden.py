@@ -84,7 +84,10 @@ def match_fixture():
 
 
 if __name__ == "__main__":
-    np.savez_compressed(os.path.join(OUT, "extract_golden.npz"), **extract_fixture())
-    np.savez_compressed(os.path.join(OUT, "match_golden.npz"), **match_fixture())
+    # the fixtures are in OpenCV's portable scalar reading (the oracle's default is the x86-64
+    # build's; tests/test_oracle_cpu.py checks these under oracle.variant(VAR_SCALAR))
+    with oracle.variant(oracle.VAR_SCALAR):
+        np.savez_compressed(os.path.join(OUT, "extract_golden.npz"), **extract_fixture())
+        np.savez_compressed(os.path.join(OUT, "match_golden.npz"), **match_fixture())
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))

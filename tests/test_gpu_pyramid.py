@@ -37,8 +37,7 @@ def test_levels_bit_exact(size, batch, arith, monkeypatch):
     p = oracle.params(nf, 1.2, 8, 20, 7)
     e = ORBextractor(nf, 1.2, 8, 20, 7, device=0, max_width=w, max_height=h)
     var = oracle.VAR_H5_SSE2 if arith == "x86" else 0
-    if arith == "x86":
-        e.set_arithmetic(e.ARITH_X86_SIMD)
+    e.set_arithmetic(e.ARITH_X86_SIMD if arith == "x86" else e.ARITH_SCALAR)
     try:
         imgs = np.stack([synthetic_frame(3 * w + s, w, h) for s in range(batch)])
         if batch == 1:
@@ -61,7 +60,7 @@ def test_band_plans(lds_kb, monkeypatch):
     try:
         imgs = np.stack([synthetic_frame(90 + s, 640, 480) for s in range(8)])
         kps, desc, cnt = e.extract_batch(imgs)
-        _levels_exact(e, p, imgs, 0)
+        _levels_exact(e, p, imgs, oracle.DEFAULT_VARIANT)
         okps, odesc = oracle.extract(p, imgs[3])
         assert kps[3, :cnt[3]].tobytes() == okps.tobytes()
         assert np.array_equal(desc[3, :cnt[3]], odesc)
@@ -79,7 +78,7 @@ def test_other_scale_factors(sf, nl, monkeypatch):
     try:
         imgs = np.stack([synthetic_frame(120 + s, 640, 480) for s in range(8)])
         e.extract_batch(imgs)
-        _levels_exact(e, p, imgs[:2], 0)
+        _levels_exact(e, p, imgs[:2], oracle.DEFAULT_VARIANT)
     finally:
         e.close()
 
@@ -118,8 +117,7 @@ def test_per_level_kernels_exact(size, arith, table, monkeypatch):
     p = oracle.params(nf, 1.2, 8, 20, 7)
     e = ORBextractor(nf, 1.2, 8, 20, 7, device=0, max_width=w, max_height=h)
     var = oracle.VAR_H5_SSE2 if arith == "x86" else 0
-    if arith == "x86":
-        e.set_arithmetic(e.ARITH_X86_SIMD)
+    e.set_arithmetic(e.ARITH_X86_SIMD if arith == "x86" else e.ARITH_SCALAR)
     try:
         imgs = np.stack([synthetic_frame(7 * w + s, w, h) for s in range(9)])
         e.extract_batch(imgs)
@@ -144,8 +142,7 @@ def test_roll_levels_bit_exact(size, batch, arith, monkeypatch):
     p = oracle.params(nf, 1.2, 8, 20, 7)
     e = ORBextractor(nf, 1.2, 8, 20, 7, device=0, max_width=w, max_height=h)
     var = oracle.VAR_H5_SSE2 if arith == "x86" else 0
-    if arith == "x86":
-        e.set_arithmetic(e.ARITH_X86_SIMD)
+    e.set_arithmetic(e.ARITH_X86_SIMD if arith == "x86" else e.ARITH_SCALAR)
     try:
         imgs = np.stack([synthetic_frame(5 * w + s, w, h) for s in range(batch)])
         if batch == 1:
@@ -170,7 +167,7 @@ def test_roll_plans(bands, chunk, monkeypatch):
     try:
         imgs = np.stack([synthetic_frame(170 + s, 1920, 1080) for s in range(8)])
         kps, desc, cnt = e.extract_batch(imgs)
-        _levels_exact(e, p, imgs[:2], 0)
+        _levels_exact(e, p, imgs[:2], oracle.DEFAULT_VARIANT)
         okps, odesc = oracle.extract(p, imgs[1])
         assert kps[1, :cnt[1]].tobytes() == okps.tobytes()
         assert np.array_equal(desc[1, :cnt[1]], odesc)

@@ -41,8 +41,7 @@ def test_single_frame_levels(size, arith, monkeypatch):
     p = oracle.params(nf, 1.2, 8, 20, 7)
     e = ORBextractor(nf, 1.2, 8, 20, 7, device=0, max_width=w, max_height=h)
     var = X86 if arith == "x86" else 0
-    if arith == "x86":
-        e.set_arithmetic(e.ARITH_X86_SIMD)
+    e.set_arithmetic(e.ARITH_X86_SIMD if arith == "x86" else e.ARITH_SCALAR)
     try:
         img = synthetic_frame(w + h, w, h)
         kps, desc = e(img)
@@ -63,8 +62,7 @@ def test_batch_levels(arith, monkeypatch):
     p = oracle.params(1000, 1.2, 8, 20, 7)
     e = ORBextractor(1000, 1.2, 8, 20, 7, device=0, max_width=640, max_height=480)
     var = X86 if arith == "x86" else 0
-    if arith == "x86":
-        e.set_arithmetic(e.ARITH_X86_SIMD)
+    e.set_arithmetic(e.ARITH_X86_SIMD if arith == "x86" else e.ARITH_SCALAR)
     try:
         imgs = np.stack([synthetic_frame(40 + s, 640, 480) for s in range(9)])
         kps, desc, cnt = e.extract_batch(imgs)

@@ -22,6 +22,15 @@ GOLD = os.path.join(os.path.dirname(__file__), "golden")
 P = oracle.params(1000, 1.2, 8, 32, 7)
 
 
+@pytest.fixture(autouse=True)
+def _scalar_reading():
+    """The restatements below follow OpenCV's portable scalar formulas, and the golden fixtures
+    were made in that reading (make_golden.py): the module runs the oracle in it (its default is
+    the x86 build's reading, tested against the GPU in test_gpu_x86_arith / the GPU suite)."""
+    with oracle.variant(oracle.VAR_SCALAR):
+        yield
+
+
 # ---- (a) known answers ------------------------------------------------------------------
 def test_tables_match_survey():
     t = oracle.tables(P)

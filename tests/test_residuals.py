@@ -51,4 +51,4 @@ def test_recorded_summary():
     assert t5["pyramid_px_diff"] > 0.05 * (t5["pyramid_px"] - 32 * 640 * 480)
     assert v["H4_glibc_cosf"]["640x480@1000"]["total"]["desc_byte_diff"] == 0
     assert v["H6_simd_blur"]["640x480@1000"]["total"]["desc_byte_diff"] == 0
-    assert oracle.lib().oracle_get_variant() == 0  # nothing left switched
+    assert oracle.lib().oracle_get_variant() == oracle.DEFAULT_VARIANT  # nothing left switched
