@@ -1334,20 +1334,25 @@ struct OctLds {
     __device__ __forceinline__ IT* key(int b) const { return ilists + (b * 2 + 1) * nc; }
     static constexpr bool kPacked = sizeof(IT) == 2;
     static constexpr int kQcWords = kPacked ? 2 : 4;  // u32 words of quadrant counters per node
-    uint32_t* qc;   // keys per quadrant (kPacked: quadrants 2w, 2w + 1 in the halves of word w)
-    IT* qk;         // 4 per node: a key of the quadrant, then the child's new list position
+    // keys per quadrant of list b's nodes (kPacked: quadrants 2w, 2w + 1 in the halves of word
+    // w), kQcWords * nc words per list
+    uint32_t* qc;
+    IT* qk;         // 4 per node: the child's new list position (initial nodes: a key)
     int* aux;       // per node: scan offsets / kept position / processed flag
     int* aux2;
     unsigned long long* s64;  // sort keys (phase 2) / best response (final)
     int* tmp;
     int* scal;      // scalars
-    __device__ __forceinline__ int qcount(int node, int q) const {
-        if constexpr (kPacked) return (int)((qc[node * 2 + (q >> 1)] >> (16 * (q & 1))) & 0xffffu);
-        else return (int)qc[node * 4 + q];
+    __device__ __forceinline__ uint32_t* qcb(int b) const { return qc + b * kQcWords * nc; }
+    __device__ __forceinline__ int qcount(int b, int node, int q) const {
+        const uint32_t* c = qcb(b);
+        if constexpr (kPacked) return (int)((c[node * 2 + (q >> 1)] >> (16 * (q & 1))) & 0xffffu);
+        else return (int)c[node * 4 + q];
     }
-    __device__ __forceinline__ void qinc(int node, int q) const {
-        if constexpr (kPacked) atomicAdd(&qc[node * 2 + (q >> 1)], 1u << (16 * (q & 1)));
-        else atomicAdd(&qc[node * 4 + q], 1u);
+    __device__ __forceinline__ void qinc(int b, int node, int q) const {
+        uint32_t* c = qcb(b);
+        if constexpr (kPacked) atomicAdd(&c[node * 2 + (q >> 1)], 1u << (16 * (q & 1)));
+        else atomicAdd(&c[node * 4 + q], 1u);
     }
 };
 
@@ -1356,7 +1361,7 @@ struct OctLds {
 constexpr size_t oct_lds_bytes(bool in_lds, int ncap, int sort_cap, int lds_keys) {
     const size_t it = in_lds ? 2 : 4;
     return (size_t)sort_cap * 8 + (in_lds ? (size_t)lds_keys * 6 : 0) +
-           (size_t)ncap * (6 * 4 + 4 * it + (in_lds ? 8 : 16) + 4 * it + 8) + (64 + 16) * 4 + 16;
+           (size_t)ncap * (6 * 4 + 4 * it + 2 * (in_lds ? 8 : 16) + 4 * it + 8) + (64 + 16) * 4 + 16;
 }
 
 __device__ __forceinline__ int quadrant(int box, int boy, int x, int y) {
@@ -1433,11 +1438,17 @@ __device__ __forceinline__ void oct_sweep_q(const KT* K, const NT* NODE, int nke
         }
 #pragma unroll
         for (int u = 0; u < kOctU; ++u) q[u] = quadrant(bxv[u], byv[u], key_x(kk[u]), key_y(kk[u]));
-        body(kx, node, q);
+        body(kx, node, q, kk);
     }
 }
 
 // The tree of one (frame, level) after its keys are in K (nkeys, original order).
+//
+// Quadrant counts are double-buffered with the node lists (qcb(b) belongs to list b), so each
+// pass / round needs a single sweep over the keys: a key moves to its node's child (or keeps
+// its node) in the list being built and at once counts its quadrant in that node for the next
+// pass; a key left alone in its node records itself as the node's key.  Per pass: the node
+// scan, the node rewrite (which also clears the next list's counters) and the fused sweep.
 template <int BLK, class IT, class KT, class NT>
 __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>& s, const LevelGeo& L, KT* K,
                              NT* NODE, int nkeys, uint32_t* out, int* out_cnt,
@@ -1448,26 +1459,30 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
     int* flag_sh = s.scal + 2;    // scal[2]: counters
     int* rmin_sh = s.scal + 3;    // scal[3]: phase-2 cut index
     int* nexp_sh = s.scal + 4;    // scal[4]: phase-1 expandable children
+    constexpr int QW = OctLds<IT>::kQcWords;
 
-    // ---- initial nodes (542-584)
+    // ---- initial nodes (542-584): per-node key counts in list 1's quadrant buffer (free now),
+    // list 0's quadrant counters cleared for the first pass
     const int nini = L.nini;
     const float hX = L.hx;
     const int H = L.bh;
+    uint32_t* icnt = s.qcb(1);  // nini <= NC / 4 entries
     for (int i = tid; i < nini; i += BLK) {
-        s.qc[i] = 0u;  // per initial node here (nini <= NC / 4 entries)
+        icnt[i] = 0u;
         s.qk[i] = (IT)-1;
     }
+    for (int i = tid; i < QW * nini; i += BLK) s.qcb(0)[i] = 0u;
     __syncthreads();
     OCT_MARK(tm, 56);
     if (nini == 1) {  // every key in node 0: its count, and any key (read only if it is alone)
         if (tid == 0) {
-            s.qc[0] = (uint32_t)nkeys;
+            icnt[0] = (uint32_t)nkeys;
             s.qk[0] = (IT)(nkeys - 1);
         }
     } else {
         for (int k = tid; k < nkeys; k += BLK) {
             const int node = min((int)((float)key_x(K[k]) / hX), nini - 1);  // vpIniNodes[kp.pt.x/hX] (568)
-            atomicAdd(&s.qc[node], 1u);
+            atomicAdd(&icnt[node], 1u);
             s.qk[node] = (IT)k;
         }
     }
@@ -1478,7 +1493,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
         int total = 0;
         for (int base = 0; base < nini; base += BLK) {
             const int i = base + tid;
-            const int ne = i < nini && s.qc[i] > 0u;
+            const int ne = i < nini && icnt[i] > 0u;
             int chunk_total;
             const int off = block_exclusive_scan<BLK>(ne, s.tmp, chunk_total);
             if (ne) {
@@ -1486,9 +1501,9 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
                 const int x0 = (int)(hX * (float)i), x1 = (int)(hX * (float)(i + 1));
                 s.box(0)[pos] = x0 | (x1 << 16);
                 s.boy(0)[pos] = 0 | (H << 16);
-                s.cnt(0)[pos] = (IT)s.qc[i];
+                s.cnt(0)[pos] = (IT)icnt[i];
                 s.seq(0)[pos] = i;
-                s.key(0)[pos] = s.qc[i] == 1u ? s.qk[i] : (IT)-1;
+                s.key(0)[pos] = icnt[i] == 1u ? s.qk[i] : (IT)-1;
                 s.aux[i] = pos;
             }
             total += chunk_total;
@@ -1497,13 +1512,41 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
     }
     __syncthreads();
     OCT_MARK(tm, 58);
+    // keys -> list-0 nodes, each live key's quadrant counted for the first pass
     if (nini == 1) {
-        const int nd = (int)s.cnt(0)[0] >= 2 ? 0 : -1;
-        for (int k = tid; k < nkeys; k += BLK) NODE[k] = nd;
+        const bool live = (int)s.cnt(0)[0] >= 2;
+        const int bx0 = s.box(0)[0], by0 = s.boy(0)[0];
+        uint32_t w01 = 0u, w23 = 0u;  // this thread's quadrant counts, one atomic pair per wave
+        for (int k = tid; k < nkeys; k += BLK) {
+            NODE[k] = live ? 0 : -1;
+            if (live) {
+                const uint32_t kk = K[k];
+                const int q = quadrant(bx0, by0, key_x(kk), key_y(kk));
+                const uint32_t inc = 1u << (16 * (q & 1));
+                if (q < 2) w01 += inc; else w23 += inc;
+            }
+        }
+        if (live) {
+            uint32_t c[4] = {w01 & 0xffffu, w01 >> 16, w23 & 0xffffu, w23 >> 16};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) c[q] = (uint32_t)wave_sum((int)c[q]);
+            if ((tid & 63) == 0) {
+                if constexpr (OctLds<IT>::kPacked) {
+                    atomicAdd(&s.qcb(0)[0], c[0] | (c[1] << 16));
+                    atomicAdd(&s.qcb(0)[1], c[2] | (c[3] << 16));
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) atomicAdd(&s.qcb(0)[q], c[q]);
+                }
+            }
+        }
     } else {
         for (int k = tid; k < nkeys; k += BLK) {
-            const int node = s.aux[min((int)((float)key_x(K[k]) / hX), nini - 1)];
-            NODE[k] = (int)s.cnt(0)[node] >= 2 ? node : -1;
+            const uint32_t kk = K[k];
+            const int node = s.aux[min((int)((float)key_x(kk) / hX), nini - 1)];
+            const bool live = (int)s.cnt(0)[node] >= 2;
+            NODE[k] = live ? node : -1;
+            if (live) s.qinc(0, node, quadrant(s.box(0)[node], s.boy(0)[node], key_x(kk), key_y(kk)));
         }
     }
     __syncthreads();
@@ -1514,28 +1557,14 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
     bool phase2 = false;
     [[maybe_unused]] int npass = 0, nround = 0;  // read by the ORBFE_OCT_TIMING build
 
-    // ---- phase 1: split every open node per pass (593-671)
+    // ---- phase 1: split every open node per pass (593-671); the current nodes' quadrant
+    // counts are in qcb(cur)
     for (int pass = 0; pass < 64 && !finished && !phase2; ++pass) {
         const int prev = size;
         const int nxt = cur ^ 1;
-        for (int i = tid; i < OctLds<IT>::kQcWords * size; i += BLK) s.qc[i] = 0u;
-        __syncthreads();
-        if (pass == 1) OCT_MARK(tm, 32);
-        {
-            const OctLds<IT> ss = s;
-            oct_sweep_q<BLK>(K, NODE, nkeys, s.box(cur), s.boy(cur), [=](const int* k, const int* node, const int* q) {
-#pragma unroll
-                for (int u = 0; u < kOctU; ++u)
-                    if (node[u] >= 0) {
-                        ss.qinc(node[u], q[u]);
-                        ss.qk[node[u] * 4 + q[u]] = (IT)k[u];
-                    }
-            });
-        }
-        __syncthreads();
         if (pass == 1) OCT_MARK(tm, 33);
         // per node: children (divided) or kept (single); aux = child offset, aux2 = kept offset
-        // (nexp_sh: zeroed here, after the sweep's barrier; summed after the first scan barrier)
+        // (nexp_sh: zeroed here, after the previous barrier; summed after the first scan barrier)
         if (tid == 0) *nexp_sh = 0;
         int csize = 0, ksize = 0;
         for (int base = 0; base < size; base += BLK) {
@@ -1545,7 +1574,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
                 if ((int)s.cnt(cur)[i] >= 2) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const int qn = s.qcount(i, q);
+                        const int qn = s.qcount(cur, i, q);
                         nch += qn > 0;
                         ne += qn > 1;
                     }
@@ -1581,7 +1610,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
                 int cp = s.aux[i];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const int qn = s.qcount(i, q);
+                    const int qn = s.qcount(cur, i, q);
                     if (!qn) continue;
                     const int np = csize - 1 - cp;
                     int cbx, cby;
@@ -1590,7 +1619,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
                     s.boy(nxt)[np] = cby;
                     s.cnt(nxt)[np] = (IT)qn;
                     s.seq(nxt)[np] = seq_base + cp;
-                    s.key(nxt)[np] = qn == 1 ? s.qk[i * 4 + q] : (IT)-1;
+                    s.key(nxt)[np] = (IT)-1;  // a single-key child's key: set by that key below
                     s.qk[i * 4 + q] = (IT)np;
                     ++cp;
                 }
@@ -1603,19 +1632,32 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
                 s.key(nxt)[np] = s.key(cur)[i];
             }
         }
+        for (int i = tid; i < QW * nsize; i += BLK) s.qcb(nxt)[i] = 0u;
         __syncthreads();
         if (pass == 1) OCT_MARK(tm, 35);
         {
-            const IT *qk = s.qk, *ncnt = s.cnt(nxt);
-            oct_sweep_q<BLK>(K, NODE, nkeys, s.box(cur), s.boy(cur), [=](const int* k, const int* node, const int* q) {
-                int np[kOctU], c[kOctU];
+            const OctLds<IT> ss = s;
+            oct_sweep_q<BLK>(K, NODE, nkeys, s.box(cur), s.boy(cur), [=](const int* k, const int* node, const int* q, const uint32_t* kk) {
+                int np[kOctU], c[kOctU], nbx[kOctU], nby[kOctU];
 #pragma unroll
-                for (int u = 0; u < kOctU; ++u) np[u] = node[u] >= 0 ? (int)qk[max(node[u], 0) * 4 + q[u]] : 0;
+                for (int u = 0; u < kOctU; ++u) np[u] = node[u] >= 0 ? (int)ss.qk[max(node[u], 0) * 4 + q[u]] : 0;
 #pragma unroll
-                for (int u = 0; u < kOctU; ++u) c[u] = (int)ncnt[np[u]];
+                for (int u = 0; u < kOctU; ++u) {
+                    c[u] = (int)ss.cnt(nxt)[np[u]];
+                    nbx[u] = ss.box(nxt)[np[u]];
+                    nby[u] = ss.boy(nxt)[np[u]];
+                }
 #pragma unroll
-                for (int u = 0; u < kOctU; ++u)
-                    if (node[u] >= 0) NODE[k[u]] = c[u] >= 2 ? np[u] : -1;
+                for (int u = 0; u < kOctU; ++u) {
+                    if (node[u] < 0) continue;
+                    if (c[u] >= 2) {
+                        NODE[k[u]] = np[u];
+                        ss.qinc(nxt, np[u], quadrant(nbx[u], nby[u], key_x(kk[u]), key_y(kk[u])));
+                    } else {
+                        NODE[k[u]] = -1;
+                        ss.key(nxt)[np[u]] = (IT)k[u];
+                    }
+                }
             });
         }
         __syncthreads();
@@ -1667,11 +1709,11 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
         } else {
             // rank sort (the keys are distinct: seq is unique): an entry's rank is the number of
             // larger keys; every thread scans all m keys (LDS broadcast reads), two barriers
-            // instead of a bitonic network's log2(P)(log2(P)+1)/2.  qc (>= 8 NC bytes, 8-byte
-            // aligned) holds the sorted copy until it is cleared below.
-            unsigned long long* srt = reinterpret_cast<unsigned long long*>(s.qc);
+            // instead of a bitonic network's log2(P)(log2(P)+1)/2.  The next list's quadrant
+            // buffer (>= 8 NC bytes, 8-byte aligned, cleared below) holds the sorted copy.
             // (8 broadcast reads in flight per step, two keys per ds_read_b128: the rolled loop
             // waited on each read — 13.5 K cycles at the 1080p level-0 tree's ~300 nodes)
+            unsigned long long* srt = reinterpret_cast<unsigned long long*>(s.qcb(nxt));
             const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(s.s64);
             const int m8 = m & ~7;
             for (int j = tid; j < m; j += BLK) {
@@ -1691,21 +1733,6 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
             for (int j = tid; j < m; j += BLK) s.s64[j] = srt[j];
             __syncthreads();
         }
-        for (int i = tid; i < OctLds<IT>::kQcWords * size; i += BLK) s.qc[i] = 0u;
-        __syncthreads();
-        if (round == 0) OCT_MARK(tm, 43);
-        {
-            const OctLds<IT> ss = s;
-            oct_sweep_q<BLK>(K, NODE, nkeys, s.box(cur), s.boy(cur), [=](const int* k, const int* node, const int* q) {
-#pragma unroll
-                for (int u = 0; u < kOctU; ++u)
-                    if (node[u] >= 0) {
-                        ss.qinc(node[u], q[u]);
-                        ss.qk[node[u] * 4 + q[u]] = (IT)k[u];
-                    }
-            });
-        }
-        __syncthreads();
         if (round == 0) OCT_MARK(tm, 44);
         // cut: first j in sorted order with size + sum_{<=j}(nch-1) >= N (else all m)
         {
@@ -1715,7 +1742,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
                 int delta = 0;
                 if (j < m) {
                     const int i = (int)(s.s64[j] & 0x3fff);
-                    for (int q = 0; q < 4; ++q) delta += s.qcount(i, q) > 0;
+                    for (int q = 0; q < 4; ++q) delta += s.qcount(cur, i, q) > 0;
                     delta -= 1;
                 }
                 int t;
@@ -1737,7 +1764,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
             int nch = 0, i = -1;
             if (j <= r) {
                 i = (int)(s.s64[j] & 0x3fff);
-                for (int q = 0; q < 4; ++q) nch += s.qcount(i, q) > 0;
+                for (int q = 0; q < 4; ++q) nch += s.qcount(cur, i, q) > 0;
             }
             int t;
             const int o = block_exclusive_scan<BLK>(nch, s.tmp, t);
@@ -1770,7 +1797,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
                 int cp = s.aux[i];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const int qn = s.qcount(i, q);
+                    const int qn = s.qcount(cur, i, q);
                     if (!qn) continue;
                     const int np = csize - 1 - cp;
                     int cbx, cby;
@@ -1779,7 +1806,7 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
                     s.boy(nxt)[np] = cby;
                     s.cnt(nxt)[np] = (IT)qn;
                     s.seq(nxt)[np] = seq_base + cp;
-                    s.key(nxt)[np] = qn == 1 ? s.qk[i * 4 + q] : (IT)-1;
+                    s.key(nxt)[np] = (IT)-1;  // a single-key child's key: set by that key below
                     s.qk[i * 4 + q] = (IT)np;
                     ++cp;
                 }
@@ -1793,27 +1820,39 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
                 s.aux[i] = np;
             }
         }
+        for (int i = tid; i < QW * nsize; i += BLK) s.qcb(nxt)[i] = 0u;
         __syncthreads();
         if (round == 0) OCT_MARK(tm, 49);
         {
-            const int *aux = s.aux, *aux2 = s.aux2;
-            const IT *qk = s.qk, *ncnt = s.cnt(nxt);
-            oct_sweep_q<BLK>(K, NODE, nkeys, s.box(cur), s.boy(cur), [=](const int* k, const int* node, const int* q) {
-                int a2[kOctU], ca[kOctU], cq[kOctU], np[kOctU], c[kOctU];
+            const OctLds<IT> ss = s;
+            oct_sweep_q<BLK>(K, NODE, nkeys, s.box(cur), s.boy(cur), [=](const int* k, const int* node, const int* q, const uint32_t* kk) {
+                int a2[kOctU], ca[kOctU], cq[kOctU], np[kOctU], c[kOctU], nbx[kOctU], nby[kOctU];
 #pragma unroll
                 for (int u = 0; u < kOctU; ++u) {
                     const int nd = max(node[u], 0);
-                    a2[u] = aux2[nd];
-                    ca[u] = aux[nd];
-                    cq[u] = (int)qk[nd * 4 + q[u]];
+                    a2[u] = ss.aux2[nd];
+                    ca[u] = ss.aux[nd];
+                    cq[u] = (int)ss.qk[nd * 4 + q[u]];
                 }
 #pragma unroll
                 for (int u = 0; u < kOctU; ++u) np[u] = node[u] < 0 ? 0 : a2[u] > 0 ? cq[u] : ca[u];
 #pragma unroll
-                for (int u = 0; u < kOctU; ++u) c[u] = (int)ncnt[np[u]];
+                for (int u = 0; u < kOctU; ++u) {
+                    c[u] = (int)ss.cnt(nxt)[np[u]];
+                    nbx[u] = ss.box(nxt)[np[u]];
+                    nby[u] = ss.boy(nxt)[np[u]];
+                }
 #pragma unroll
-                for (int u = 0; u < kOctU; ++u)
-                    if (node[u] >= 0) NODE[k[u]] = c[u] >= 2 ? np[u] : -1;
+                for (int u = 0; u < kOctU; ++u) {
+                    if (node[u] < 0) continue;
+                    if (c[u] >= 2) {
+                        NODE[k[u]] = np[u];
+                        ss.qinc(nxt, np[u], quadrant(nbx[u], nby[u], key_x(kk[u]), key_y(kk[u])));
+                    } else {  // alone in a new child (kept nodes hold >= 2 live keys)
+                        NODE[k[u]] = -1;
+                        ss.key(nxt)[np[u]] = (IT)k[u];
+                    }
+                }
             });
         }
         __syncthreads();
@@ -1873,7 +1912,7 @@ __global__ __launch_bounds__(BLK) void octree_kernel(OctArgs a) {
         s.lists = reinterpret_cast<int*>(p);
         p += 6 * 4 * (size_t)NC;
         s.qc = reinterpret_cast<uint32_t*>(p);  // 8-byte aligned: the rank sort's u64 copy
-        p += (size_t)std::remove_reference_t<decltype(s)>::kQcWords * 4 * NC;
+        p += 2 * (size_t)std::remove_reference_t<decltype(s)>::kQcWords * 4 * NC;
         s.ilists = reinterpret_cast<IT*>(p);
         p += 4 * sizeof(IT) * (size_t)NC;
         s.qk = reinterpret_cast<IT*>(p);
