@@ -2732,7 +2732,7 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
                 Blo[3] = 0;
                 Bhi[3] = 0;
                 // x86: 1 where the column is in the SIMD body (round half to even), else 0
-                const uint32_t em = xs + 16 * s < 0 ? 1u : 0u;
+                const uint32_t em = xs + 16 * s < 0 ? 1u : 0u, nem = 1u - em;
                 i32x4m Vs[3];  // (kFragLds & 4: the three V fragments read once per N-tile)
                 if constexpr ((kFragLds & 4) != 0) {
 #pragma unroll
@@ -2751,8 +2751,8 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
                         // x86 (kRndM = 0x7fff): + bit 16 of the sum in the SIMD body, + 1 past
                         // it.  The bit of sum + 0x7fff equals the true sum's bit 16 in the only
                         // case it matters (a tie, low half 0x8000), and adding it elsewhere
-                        // changes no carry: (em & (s4 >> 16)) | (~em & 1) in one v_bfi
-                        if constexpr (kX86) s4[i] += (em & (s4[i] >> 16)) | (~em & 1u);
+                        // changes no carry: v_bfe with width em (0 or 1), then one v_add3
+                        if constexpr (kX86) s4[i] = s4[i] + __builtin_amdgcn_ubfe(s4[i], 16u, em) + nem;
                     }
                     // min(sum >> 16, 255) of two sums at once (sum >> 16 <= 257 < 2^16)
                     const us2 sat = us2{255, 255};
