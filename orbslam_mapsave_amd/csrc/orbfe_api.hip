@@ -202,11 +202,13 @@ struct orbfe_extractor {
     // run(): the pyramid kernel reads level 0 from l0_stage and writes it to the slab level 0
     LevelPtr l0_stage{};
     bool l0_from_stage = false;
-    // ORBFE_PYR=3: the rolling-band kernel wherever it plans (measured slower than the band
-    // kernel at 640 x 480 and no faster than the per-level kernels at 1920 x 1080, DESIGN.md
-    // §5c; off by default); ORBFE_ROLL=1: where the band plan is not the faster path
+    // The rolling-band kernel: for batches where the band plan is not the faster path (1920 x
+    // 1080: one launch instead of the per-level kernels, measured level with them — DESIGN.md
+    // §5c); ORBFE_ROLL=0: never; ORBFE_ROLL=1: also for small batches; ORBFE_PYR=3: wherever
+    // it plans (measured slower than the band kernel at 640 x 480)
     bool force_roll = std::getenv("ORBFE_PYR") && std::strcmp(std::getenv("ORBFE_PYR"), "3") == 0;
-    bool use_roll = force_roll || (std::getenv("ORBFE_ROLL") && std::strcmp(std::getenv("ORBFE_ROLL"), "1") == 0);
+    bool use_roll = !(std::getenv("ORBFE_ROLL") && std::strcmp(std::getenv("ORBFE_ROLL"), "0") == 0);
+    bool roll_small = force_roll || (std::getenv("ORBFE_ROLL") && std::strcmp(std::getenv("ORBFE_ROLL"), "1") == 0);
     bool band_path(int n) const {  // run() makes the pyramid with pyramid_kernel for n frames
         const int which = n >= kTailMinFrames ? 0 : 1;
         return plan.pyr_ok && (plan.pyr_use[which] || force_pyr) && use_pyr && !force_roll &&
@@ -215,7 +217,7 @@ struct orbfe_extractor {
     // ... or with pyramid_roll_kernel: where the band plan is not the faster path (1920 x 1080)
     bool roll_path(int n) const {
         const int which = n >= kTailMinFrames ? 0 : 1;
-        return plan.roll_ok[which] && use_pyr && use_roll && !force_pyr &&
+        return plan.roll_ok[which] && use_pyr && use_roll && !force_pyr && (which == 0 || roll_small) &&
                !(fused_blur && resize_blur) && plan.geo.nlevels >= 2 &&
                (force_roll || !band_path(n));
     }

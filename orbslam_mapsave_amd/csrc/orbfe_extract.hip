@@ -3318,11 +3318,13 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
         for (int which = 0; which < 2 && groups_ok; ++which) {
             const char* be = std::getenv(which == 0 ? "ORBFE_ROLL_BANDS" : "ORBFE_ROLL_BANDS_SMALL");
             const char* ce = std::getenv(which == 0 ? "ORBFE_ROLL_CHUNK" : "ORBFE_ROLL_CHUNK_SMALL");
-            int nb = be ? std::atoi(be) : (which == 0 ? std::max(1, std::min(8, (h0 + 359) / 360))
+            // large batches: ~180 level-0 rows per band, 32 rows per step (1080p: 6 bands,
+            // measured level with the per-level kernels and 8 / 12-band plans, §5c)
+            int nb = be ? std::atoi(be) : (which == 0 ? std::max(1, std::min(16, (h0 + 179) / 180))
                                                       : std::max(1, std::min(std::min(64, htop), h0 / 24)));
             nb = std::max(1, std::min(nb, htop));
             const int cpr0 = (g.geo.lv[0].w + 15) >> 4;
-            int C0 = ce ? std::atoi(ce) : (which == 0 ? 16 : 8);
+            int C0 = ce ? std::atoi(ce) : (which == 0 ? 32 : 8);
             C0 = std::max(2, std::min(C0, (kPyrRollPre * kPyrBlockSize) / cpr0));
             std::vector<int> rbt;
             size_t lds_unused;

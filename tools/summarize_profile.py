@@ -37,8 +37,9 @@ for f in ("bench.json", "trace_bench.json", "bench_args.txt"):
 # trace (kernel, total grid) select the PMC dispatches.  Multi-launch stages (resize: one launch
 # per level) are averaged over all their bench-shape launches, as bench.py's avg_launch_ms is.
 _cfg = json.loads(open(os.path.join(SRC, "bench.json")).read())["config"]
-FRAMES = int(os.environ.get("BENCH_SUBBATCH", 0)) or (
-    _cfg["frames_per_rank_per_step"] // _cfg.get("streams_per_rank", 1) // _cfg.get("chunks_per_stream", 1))
+# round 4: the probe and roofline legs run the rank's whole batch in one call (the timed steps'
+# sub-batch launches are not what roofline.avg_launch_ms times)
+FRAMES = int(os.environ.get("BENCH_SUBBATCH", 0)) or _cfg["frames_per_rank_per_step"]
 trace_rows = list(csv.DictReader(open(os.path.join(SRC, "trace", "run_kernel_trace.csv"))))
 shapes = collections.defaultdict(set)
 
@@ -129,7 +130,7 @@ if k:
     with open(bpath, "w") as fh:
         fh.write(json.dumps(line) + "\n")
     check = {"kernel": k, "frames_per_launch": FRAMES,
-             "bench_avg_launch_ms (HIP events, timed steps)": roof.get("avg_launch_ms"),
+             "bench_avg_launch_ms (HIP events, roofline leg)": roof.get("avg_launch_ms"),
              "rocprofv3_avg_ms (bench-shape launches)": launch.get(k, {}).get("avg_ms"),
              "traffic_bytes_per_launch (2 x FETCH_SIZE + WRITE_SIZE)": roof["traffic"],
              "algorithmic_bytes_per_launch": roof.get("bytes_per_launch")}
