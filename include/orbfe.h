@@ -232,6 +232,15 @@ int orbfe_synchronize(orbfe_extractor* h);
 int orbfe_profile(orbfe_extractor* h, int enable);
 int orbfe_profile_read(orbfe_extractor* h, double* total_ms, int32_t* launches);
 
+/* Which pyramid path an extraction of `nframes` frames at the extractor's current frame size
+ * takes (the last extracted size; a test hook, no reference counterpart): ORBFE_PYR_PER_LEVEL
+ * (resize_kernel per level), ORBFE_PYR_BANDS (pyramid_kernel), ORBFE_PYR_ROLL
+ * (pyramid_roll_kernel); ORBFE_ERR_ARG before any extraction. */
+#define ORBFE_PYR_PER_LEVEL 0
+#define ORBFE_PYR_BANDS     1
+#define ORBFE_PYR_ROLL      2
+int orbfe_pyramid_path(const orbfe_extractor* h, int nframes);
+
 /* Pyramid access — replaces the public member mvImagePyramid (ORBextractor.h:90) read by
  * stereo matching (Frame.cc:589, 679, 696).  Copies level `level` of frame `frame` of the
  * most recent extraction (interior pixels only, rows w bytes apart) into `out`

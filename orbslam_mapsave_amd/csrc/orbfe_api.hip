@@ -130,7 +130,7 @@ struct orbfe_extractor {
     bool planned = false;
     int frames_cap = 0;
     DevBuf cells, xtab, ytab, bslot, ptab;
-    DevBuf pyr, blur, cell_cnt, cell_keys, keys, act, oct_out, oct_cnt, level_keys;
+    DevBuf pyr, blur, cell_cnt, cell_keys, keys, act, oct_out, oct_cnt, oct_ord, level_keys;
     DevBuf out_kps, out_desc, out_n;  // staging for the host-pointer entry points
     DevBuf stage, rects;              // host colour frames / rectangle masks (level-0 inputs)
     DevBuf st_off, st_items, st_sad, st_status;           // stereo workspaces (left handle)
@@ -202,21 +202,23 @@ struct orbfe_extractor {
     // run(): the pyramid kernel reads level 0 from l0_stage and writes it to the slab level 0
     LevelPtr l0_stage{};
     bool l0_from_stage = false;
-    // The rolling-band kernel: for batches where the band plan is not the faster path (1920 x
-    // 1080: one launch instead of the per-level kernels, measured level with them — DESIGN.md
-    // §5c); ORBFE_ROLL=0: never; ORBFE_ROLL=1: also for small batches; ORBFE_PYR=3: wherever
-    // it plans (measured slower than the band kernel at 640 x 480)
+    // The rolling-band kernel, opt-in: one launch where the band plan is not the faster path
+    // (1920 x 1080), measured slower there than the per-level kernels;
+    // ORBFE_ROLL=1: batches, ORBFE_ROLL=2: also small batches; ORBFE_PYR=3: wherever it plans
+    // (measured slower than the band kernel at 640 x 480 too)
     bool force_roll = std::getenv("ORBFE_PYR") && std::strcmp(std::getenv("ORBFE_PYR"), "3") == 0;
-    bool use_roll = !(std::getenv("ORBFE_ROLL") && std::strcmp(std::getenv("ORBFE_ROLL"), "0") == 0);
-    bool roll_small = force_roll || (std::getenv("ORBFE_ROLL") && std::strcmp(std::getenv("ORBFE_ROLL"), "1") == 0);
+    bool use_roll = force_roll || (std::getenv("ORBFE_ROLL") && std::atoi(std::getenv("ORBFE_ROLL")) >= 1);
+    bool roll_small = force_roll || (std::getenv("ORBFE_ROLL") && std::atoi(std::getenv("ORBFE_ROLL")) >= 2);
+    // ORBFE_PYR_SMALL_BELOW (A/B): batches below it take the small-batch band plans (thin bands)
+    int pyr_small_below = std::getenv("ORBFE_PYR_SMALL_BELOW") ? std::atoi(std::getenv("ORBFE_PYR_SMALL_BELOW")) : kTailMinFrames;
     bool band_path(int n) const {  // run() makes the pyramid with pyramid_kernel for n frames
-        const int which = n >= kTailMinFrames ? 0 : 1;
+        const int which = n >= pyr_small_below ? 0 : 1;
         return plan.pyr_ok && (plan.pyr_use[which] || force_pyr) && use_pyr && !force_roll &&
                !(fused_blur && resize_blur) && plan.geo.nlevels >= 2;
     }
     // ... or with pyramid_roll_kernel: where the band plan is not the faster path (1920 x 1080)
     bool roll_path(int n) const {
-        const int which = n >= kTailMinFrames ? 0 : 1;
+        const int which = n >= pyr_small_below ? 0 : 1;
         return plan.roll_ok[which] && use_pyr && use_roll && !force_pyr && (which == 0 || roll_small) &&
                !(fused_blur && resize_blur) && plan.geo.nlevels >= 2 &&
                (force_roll || !band_path(n));
@@ -228,6 +230,11 @@ struct orbfe_extractor {
     bool desc_mfma = !(std::getenv("ORBFE_DESC_MFMA") && std::strcmp(std::getenv("ORBFE_DESC_MFMA"), "0") == 0);
     // ORBFE_DESC_STRIDE=0: describe waves take consecutive slots in batches too (A/B)
     bool desc_stride = !(std::getenv("ORBFE_DESC_STRIDE") && std::strcmp(std::getenv("ORBFE_DESC_STRIDE"), "0") == 0);
+    // ORBFE_DESC_ORDER=0: strided describe waves take the oct-tree output order (A/B); 2: the
+    // band order at every frame size
+    bool desc_order = !(std::getenv("ORBFE_DESC_ORDER") && std::strcmp(std::getenv("ORBFE_DESC_ORDER"), "0") == 0);
+    bool desc_order_all = std::getenv("ORBFE_DESC_ORDER") && std::strcmp(std::getenv("ORBFE_DESC_ORDER"), "2") == 0;
+    int num_cus = 256;  // compute units of the device (launch-shape choices)
     // ORBFE_OCT_SMALL=0: small batches keep the 256-thread oct-tree (A/B)
     bool oct_small = !(std::getenv("ORBFE_OCT_SMALL") && std::strcmp(std::getenv("ORBFE_OCT_SMALL"), "0") == 0);
     bool graph_broken = std::getenv("ORBFE_NO_GRAPH") != nullptr;  // capture failed once (or
@@ -384,6 +391,7 @@ struct orbfe_extractor {
         if ((st = act.ensure(N * 2 * std::max<long long>(1, g.geo.key_total) * sizeof(int4)))) return st;
         if ((st = oct_out.ensure(N * g.geo.out_total * sizeof(uint32_t)))) return st;
         if ((st = oct_cnt.ensure(N * g.geo.nlevels * sizeof(int)))) return st;
+        if ((st = oct_ord.ensure(N * g.geo.out_total * sizeof(uint16_t)))) return st;
         if ((st = level_keys.ensure(N * kMaxLevels * sizeof(int)))) return st;
         // the FAST kernel adds into these, the oct-tree kernel reads and clears them
         ORBFE_HIP(hipMemsetAsync(level_keys.p, 0, N * kMaxLevels * sizeof(int), stream));
@@ -413,7 +421,7 @@ struct orbfe_extractor {
         const bool rb = fused_blur && resize_blur;
         uint32_t pre_mask = 0;
         // K1 as one launch (pyramid_kernel): every level of a band of every frame in LDS
-        const int which = n >= kTailMinFrames ? 0 : 1;
+        const int which = n >= pyr_small_below ? 0 : 1;
         const bool one_pyr = pyr_path(n), roll = roll_path(n);
         if (l0_from_stage && !one_pyr) return ORBFE_ERR_ARG;  // callers check pyr_path first
         if (one_pyr) {
@@ -443,12 +451,16 @@ struct orbfe_extractor {
                 for (int l = 0; l < L; ++l) {
                     pa.ring_rows[l] = g.roll_ring_rows[which][l];
                     pa.ring_off[l] = g.roll_ring_off[which][l];
+                    pa.lp[l] = g.roll_pitch[which][l];
                 }
+                pa.cols = reinterpret_cast<const int4*>(ptab.as<uint4>() + g.roll_col_off[which]);
+                pa.ncols = g.roll_cols[which];
+                const dim3 rgrid(g.roll_bands[which] * g.roll_cols[which], n);
                 if (x86())
-                    ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, pyramid_roll_kernel<true>, dim3(g.roll_bands[which], n),
+                    ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, pyramid_roll_kernel<true>, rgrid,
                                  dim3(kPyrBlockSize), g.roll_lds[which], stream, pa);
                 else
-                    ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, pyramid_roll_kernel<false>, dim3(g.roll_bands[which], n),
+                    ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, pyramid_roll_kernel<false>, rgrid,
                                  dim3(kPyrBlockSize), g.roll_lds[which], stream, pa);
             } else if (x86())
                 ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, pyramid_kernel<true>, dim3(g.nbands[which], n),
@@ -550,12 +562,20 @@ struct orbfe_extractor {
         oa.act = act.as<int4>();
         oa.oct_out = oct_out.as<uint32_t>();
         oa.oct_cnt = oct_cnt.as<int>();
+        // describe's strided waves (batches) sweep each level in 32-row bands where a frame's
+        // pyramid overflows half an XCD's L2 (level 0 >= 1 Mpx; 1080p: describe traffic -13 %,
+        // 640 x 480: no traffic to save, oct-tree +2.5 %): the oct-tree writes that order beside
+        // its output (ORBFE_DESC_ORDER=0: never, =2: at every size)
+        const bool banded = n >= kDescSmallBatch && desc_stride && desc_order &&
+                            (desc_order_all || (long long)g.geo.lv[0].w * g.geo.lv[0].h >= (1 << 20));
+        oa.oct_ord = banded ? oct_ord.as<uint16_t>() : nullptr;
         oa.ncap_max = g.ncap_max;
         oa.sort_cap = g.sort_cap;
         oa.lds_keys = g.oct_keys;
-        // batches of a few frames (the single-frame call): 1024-thread trees (one per CU at
-        // most, the level-0 tree's sweeps over 16 waves); else 256-thread trees, six per CU
-        if (n < kTailMinFrames && oct_small)
+        // 1024-thread trees while the launch has at most one tree per CU (the single-frame call,
+        // config 4 at 32 frames per rank: each level-0 tree is the launch's long pole); 256-thread
+        // trees, six per CU, for larger batches (throughput)
+        if (n * L <= num_cus && oct_small)
             ORBFE_LAUNCH(prof, ORBFE_STAGE_OCTREE, octree_kernel<1024>, dim3(n, L), dim3(1024), g.oct_lds, stream, oa);
         else
             ORBFE_LAUNCH(prof, ORBFE_STAGE_OCTREE, octree_kernel<kOctBlockSize>, dim3(n, L), dim3(kOctBlockSize), g.oct_lds, stream, oa);
@@ -598,6 +618,7 @@ struct orbfe_extractor {
         for (int i = 0; i < 4; ++i) da.taps[i] = tab.taps[i];
         da.oct_out = oct_out.as<uint32_t>();
         da.oct_cnt = oct_cnt.as<int>();
+        da.oct_ord = banded ? oct_ord.as<uint16_t>() : nullptr;
         da.kps = d_kps;
         da.desc = d_desc;
         da.n_out = d_n;
@@ -745,7 +766,7 @@ struct orbfe_extractor {
 
     ~orbfe_extractor() {
         for (DevBuf* b : {&cells, &xtab, &ytab, &bslot, &ptab, &pyr, &blur, &cell_cnt, &cell_keys, &keys, &act,
-                          &oct_out, &oct_cnt, &level_keys, &out_kps, &out_desc, &out_n, &stage, &rects, &st_off, &st_items,
+                          &oct_out, &oct_cnt, &oct_ord, &level_keys, &out_kps, &out_desc, &out_n, &stage, &rects, &st_off, &st_items,
                           &st_sad, &st_status, &st_kl, &st_dl, &st_kr, &st_dr, &st_n, &st_ur, &st_dp})
             b->release();
         drop_graph();
@@ -783,6 +804,9 @@ orbfe_extractor* orbfe_create(const orbfe_params* params, int device, int max_wi
             DeviceGuard dg(device);
             h = new orbfe_extractor();
             h->device = device;
+            int cus = 0;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+                h->num_cus = cus;
             st = make_tables(*params, h->tab);
             if (st == ORBFE_OK && hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess)
                 st = ORBFE_ERR_HIP;
@@ -1271,6 +1295,11 @@ int orbfe_profile_read(orbfe_extractor* h, double* total_ms, int32_t* launches) 
     }
     h->prof.used = 0;
     return ORBFE_OK;
+}
+
+int orbfe_pyramid_path(const orbfe_extractor* h, int nframes) {
+    if (!h || !h->planned || nframes < 1) return ORBFE_ERR_ARG;
+    return h->band_path(nframes) ? ORBFE_PYR_BANDS : h->roll_path(nframes) ? ORBFE_PYR_ROLL : ORBFE_PYR_PER_LEVEL;
 }
 
 int orbfe_set_stream(orbfe_extractor* h, void* s) {

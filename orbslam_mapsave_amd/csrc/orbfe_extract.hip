@@ -23,6 +23,7 @@
 #include <mutex>
 #include <new>
 #include <type_traits>
+#include <array>
 #include <vector>
 
 #include "../../include/orbfe.h"
@@ -163,21 +164,43 @@ __device__ __forceinline__ uint32_t resize_px(uint32_t t0, uint32_t t1, uint32_t
     return min(sse2 ? sv : sc, 255u);
 }
 
-// Four pixels of a row (columns x .. x + 3) from their horizontal sums.  x86: a group entirely
-// inside the SSE2 body (x + 3 < xb, nearly every group) takes the body formula alone instead of
-// computing both and selecting per pixel.
+// Horizontal coefficient pairs (a0 | a1 << 16) as the horizontal passes feeding resize4 use
+// them: x86 scales both by 16 (a0, a1 <= 2049: each half stays below 2^16), so the sums arrive
+// as h = 16 t (< 2^23).
 template <bool kX86>
-__device__ __forceinline__ uint32_t resize4(const uint32_t (&t0)[4], const uint32_t (&t1)[4],
+__device__ __forceinline__ uint32_t hcoef(uint32_t a01) { return kX86 ? a01 << 4 : a01; }
+
+// Four pixels of a row (columns x .. x + 3) from their horizontal sums h (t, or 16 t in x86
+// mode: hcoef).  x86: every pixel takes the SSE2 body formula, ((t >> 4) * b) >> 16 as
+// v_mul_hi_u32_u24 of (h with its low 8 bits cleared) = (t >> 4) << 8 and b << 8 — one AND and
+// one multiply per term instead of a shift, a multiply and a shift; t >> 4 <= 32,655 and
+// b0 + b1 <= 2049 keep the sum <= 1,022, so no clamp — and only a group reaching the scalar
+// tail (x + 3 >= xb: the last one or two groups of a row) replaces its tail pixels, so the
+// waves holding a row's end run the body once plus the tail's few operations (an if / else
+// per group made those waves run both formulas in full).
+template <bool kX86>
+__device__ __forceinline__ uint32_t resize4(const uint32_t (&h0)[4], const uint32_t (&h1)[4],
                                             uint32_t b0, uint32_t b1, int x, int xb) {
     uint32_t packed = 0;
-    if (kX86 && x + 3 < xb) {
+    if constexpr (!kX86) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) packed |= resize_px<false>(h0[k], h1[k], b0, b1, false) << (8 * k);
+        return packed;
+    }
+    const uint32_t c0 = (b0 & 0xffffu) << 8, c1 = (b1 & 0xffffu) << 8;  // < 2^24
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t p0 = (uint32_t)(((unsigned long long)(h0[k] & 0x7fff00u) * c0) >> 32);
+        const uint32_t p1 = (uint32_t)(((unsigned long long)(h1[k] & 0x7fff00u) * c1) >> 32);
+        packed |= ((p0 + p1 + 2u) >> 2) << (8 * k);
+    }
+    if (x + 3 >= xb) {
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            packed |= min((((uint32_t)__umul24(t0[k] >> 4, b0) >> 16) +
-                           ((uint32_t)__umul24(t1[k] >> 4, b1) >> 16) + 2u) >> 2, 255u) << (8 * k);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) packed |= resize_px<kX86>(t0[k], t1[k], b0, b1, x + k < xb) << (8 * k);
+            if (x + k >= xb) {
+                const uint32_t sc = min((__umul24(h0[k] >> 4, b0) + __umul24(h1[k] >> 4, b1) + (1u << 21)) >> 22, 255u);
+                packed = (packed & ~(0xffu << (8 * k))) | (sc << (8 * k));
+            }
     }
     return packed;
 }
@@ -251,8 +274,8 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
         const uint4 g0 = gp[0], g1 = gp[1], g2 = gp[2];
         const int base = (int)g0.x - sx0, wofs = base & ~3, sh = base & 3;
         const uint32_t sel[4] = {g0.y, g0.z, g0.w, g1.x};
-        const us2 cf[4] = {__builtin_bit_cast(us2, g1.y), __builtin_bit_cast(us2, g1.z),
-                           __builtin_bit_cast(us2, g1.w), __builtin_bit_cast(us2, g2.x)};
+        const us2 cf[4] = {__builtin_bit_cast(us2, hcoef<kX86>(g1.y)), __builtin_bit_cast(us2, hcoef<kX86>(g1.z)),
+                           __builtin_bit_cast(us2, hcoef<kX86>(g1.w)), __builtin_bit_cast(us2, hcoef<kX86>(g2.x))};
         auto hsum = [&](int r, uint32_t (&t)[4]) {
             const uint32_t* row = reinterpret_cast<const uint32_t*>(rs_lds + r * P + wofs);
             const uint32_t w0 = row[0], w1 = row[1], w2 = row[2];
@@ -287,8 +310,8 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
         x0[k] = a.xt[3 * dx] - sx0;
         x1[k] = a.xt[3 * dx + 1] - sx0;
         const int aa = a.xt[3 * dx + 2];
-        a0[k] = aa & 0xffff;
-        a1[k] = (int)((unsigned)aa >> 16);
+        a0[k] = (int)(hcoef<kX86>((uint32_t)aa) & 0xffffu);  // x86: 16 a0, 16 a1 (hcoef)
+        a1[k] = (int)(hcoef<kX86>((uint32_t)aa) >> 16);
     }
 #pragma unroll
     for (int j = 0; j < kRsRPT; ++j) {
@@ -654,8 +677,8 @@ __global__ __launch_bounds__(kPyrBlock) void pyramid_kernel(PyrArgs a) {
         const int xbase = (int)g0.x, wofs = (xbase >> 2) << 2, sh = xbase & 3;
         const uint32_t sel[4] = {g0.y, g0.z, g0.w, g1.x};
         typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-        const us2 cf[4] = {__builtin_bit_cast(us2, g1.y), __builtin_bit_cast(us2, g1.z),
-                           __builtin_bit_cast(us2, g1.w), __builtin_bit_cast(us2, g2.x)};
+        const us2 cf[4] = {__builtin_bit_cast(us2, hcoef<kX86>(g1.y)), __builtin_bit_cast(us2, hcoef<kX86>(g1.z)),
+                           __builtin_bit_cast(us2, hcoef<kX86>(g1.w)), __builtin_bit_cast(us2, hcoef<kX86>(g2.x))};
         const int x = 4 * gx, n = min(4, w - x);
         const int xb = a.simd_xb[l];
         const LevelPtr dp = a.dst[l];
@@ -711,11 +734,15 @@ template __global__ void pyramid_kernel<true>(PyrArgs);
 template <bool kX86>
 __global__ __launch_bounds__(kPyrBlock) void pyramid_roll_kernel(PyrArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char pr_lds[];
-    const int band = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    const int band = (int)blockIdx.x / a.ncols, f = blockIdx.y, tid = threadIdx.x;
     const int L = a.nlevels;
     const int4* bt = a.bands + band * L;
+    // the workgroup's column tile: cc[l] = {first, last computed column, own [z, w)}; rings
+    // hold the computed columns from cc[l].x (a multiple of 4) at pitch lp[l]
+    const int4* cc = a.cols + ((int)blockIdx.x - band * a.ncols) * L;
     const int* sc = a.sched + (size_t)band * a.nsteps * L;
-    const int w0 = a.w[0], P0 = a.lp[0], R0 = a.ring_rows[0], cpr = (w0 + 15) >> 4;
+    const int w0 = a.w[0], P0 = a.lp[0], R0 = a.ring_rows[0];
+    const int x00 = cc[0].x, cpr = (cc[0].y - x00 + 16) >> 4;
     const uint8_t* src = a.src.base + f * a.src.fpitch;
     const int4 b0 = bt[0];
     int4* yd = reinterpret_cast<int4*>(pr_lds + a.ydesc);
@@ -729,7 +756,7 @@ __global__ __launch_bounds__(kPyrBlock) void pyramid_roll_kernel(PyrArgs a) {
             if (i >= total) continue;
             const int r = r0 + i / cpr, c = i - (i / cpr) * cpr;
             const uint8_t* row = src + (long long)r * a.src.pitch;
-            const int x = 16 * c;
+            const int x = x00 + 16 * c;
             if (x + 16 <= w0) {
                 v[u] = load16_a4(row + x);
             } else {
@@ -760,7 +787,7 @@ __global__ __launch_bounds__(kPyrBlock) void pyramid_roll_kernel(PyrArgs a) {
             const int r = r0 + j;
             if (a.l0_copy.base && r >= b0.z && r < b0.w)
                 *reinterpret_cast<uint4*>(const_cast<uint8_t*>(a.l0_copy.base) + f * a.l0_copy.fpitch +
-                                          (long long)r * a.l0_copy.pitch + 16 * c) = v[u];
+                                          (long long)r * a.l0_copy.pitch + x00 + 16 * c) = v[u];
         }
     };
     // row descriptors of every step (host-made): per level l >= 1 in order, the rows the step
@@ -776,9 +803,9 @@ __global__ __launch_bounds__(kPyrBlock) void pyramid_roll_kernel(PyrArgs a) {
     };
     uint4 gn0 = make_uint4(0u, 0u, 0u, 0u), gn1 = gn0, gn2 = gn0;
     auto gload = [&](int l) __attribute__((always_inline)) {
-        const int gpr = (a.w[l] + 3) >> 2;
+        const int gpr = (cc[l].y - cc[l].x + 4) >> 2;
         if (tid / gpr < kPyrBlock / gpr) {
-            const uint4* gp = a.gtab[l] + 3 * (tid % gpr);
+            const uint4* gp = a.gtab[l] + 3 * ((cc[l].x >> 2) + tid % gpr);
             gn0 = gp[0];
             gn1 = gp[1];
             gn2 = gp[2];
@@ -805,16 +832,18 @@ __global__ __launch_bounds__(kPyrBlock) void pyramid_roll_kernel(PyrArgs a) {
             gload(l + 1 < L ? l + 1 : 1);
             const int r0 = prv ? prv[l] : bt[l].x, nrows = cur[l] - r0;
             if (nrows <= 0) continue;  // uniform: nothing made, nothing to order
-            const int4 bl = bt[l];
-            const int w = a.w[l], gpr = (w + 3) >> 2, rps = kPyrBlock / gpr;
+            const int4 bl = bt[l], cl = cc[l];
+            const int w = a.w[l], gpr = (cl.y - cl.x + 4) >> 2, rps = kPyrBlock / gpr;
             const int gx = tid % gpr, ry = tid / gpr;
             if (ry < rps) {
-                const int xbase = (int)g0.x, wofs = (xbase >> 2) << 2, sh = xbase & 3;
+                // the group's source window, relative to the ring row's first column
+                const int xrel = (int)g0.x - cc[l - 1].x, wofs = (xrel >> 2) << 2, sh = xrel & 3;
                 const uint32_t sel[4] = {g0.y, g0.z, g0.w, g1.x};
                 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-                const us2 cf[4] = {__builtin_bit_cast(us2, g1.y), __builtin_bit_cast(us2, g1.z),
-                                   __builtin_bit_cast(us2, g1.w), __builtin_bit_cast(us2, g2.x)};
-                const int x = 4 * gx, n = min(4, w - x);
+                const us2 cf[4] = {__builtin_bit_cast(us2, hcoef<kX86>(g1.y)), __builtin_bit_cast(us2, hcoef<kX86>(g1.z)),
+                                   __builtin_bit_cast(us2, hcoef<kX86>(g1.w)), __builtin_bit_cast(us2, hcoef<kX86>(g2.x))};
+                const int x = cl.x + 4 * gx, n = min(4, w - x);
+                const bool own_x = x >= cl.z && x < cl.w;  // own bounds are multiples of 4
                 const int xb = a.simd_xb[l];
                 const LevelPtr dp = a.dst[l];
                 uint8_t* dst = const_cast<uint8_t*>(dp.base) + f * dp.fpitch;
@@ -834,9 +863,9 @@ __global__ __launch_bounds__(kPyrBlock) void pyramid_roll_kernel(PyrArgs a) {
                     hsum(d.x, t0);
                     hsum(d.y, t1);
                     const uint32_t packed = resize4<kX86>(t0, t1, bb0, bb1, x, xb);
-                    if (ring) *reinterpret_cast<uint32_t*>(pr_lds + d.w + x) = packed;
+                    if (ring) *reinterpret_cast<uint32_t*>(pr_lds + d.w + x - cl.x) = packed;
                     const int r = r0 + j;
-                    if (r >= bl.z && r < bl.w) {
+                    if (own_x && r >= bl.z && r < bl.w) {
                         uint8_t* o = dst + (long long)r * dp.pitch + x;
                         if (n == 4) {
                             *reinterpret_cast<uint32_t*>(o) = packed;
@@ -946,8 +975,8 @@ __global__ __launch_bounds__(kTailBlock) void resize_tail_kernel(ResizeTailArgs 
                 x0[q] = xt[3 * dx];
                 x1[q] = xt[3 * dx + 1];
                 const int aa = xt[3 * dx + 2];
-                a0[q] = aa & 0xffff;
-                a1[q] = (int)((unsigned)aa >> 16);
+                a0[q] = (int)(hcoef<kX86>((uint32_t)aa) & 0xffffu);  // x86: 16 a0, 16 a1 (hcoef)
+                a1[q] = (int)(hcoef<kX86>((uint32_t)aa) >> 16);
             }
             for (int y = ry; y < dh; y += rps) {
                 const int bb = yt[3 * y + 2];
@@ -1355,6 +1384,10 @@ struct OctLds {
         else atomicAdd(&c[node * 4 + q], 1u);
     }
 };
+
+// describe's processing order: 32-row bands per level (the last takes every row below), counted
+// in the node lists' first words (24 * nc bytes, nc >= 20)
+constexpr int kOctBands = 120;
 
 // Bytes of the carve: the LDS form (keys and node positions in LDS, u16 node fields) and the
 // global-array form (wider node fields in place of the keys); the launch takes the larger.
@@ -1866,6 +1899,12 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
 
     // ---- retain the best key per node (740-759), emit in list order
     for (int i = tid; i < size; i += BLK) s.s64[i] = 0ull;
+    // describe's processing order (a.oct_ord): the level's keypoints by 32-row band, counted in
+    // the node boxes' words (dead from here on; >= 24 * nc >= 480 bytes)
+    uint16_t* ord = a.oct_ord ? a.oct_ord + (out - a.oct_out) : nullptr;
+    int* ybin = s.lists;
+    if (ord)
+        for (int i = tid; i < kOctBands; i += BLK) ybin[i] = 0;
     __syncthreads();
     OCT_MARK(tm, 52);
     {
@@ -1881,6 +1920,21 @@ __device__ __forceinline__ void octree_level(const OctArgs& a, const OctLds<IT>&
                                           : (int)(0xffffffffu - (unsigned)(s.s64[i] & 0xffffffffu));
         const uint32_t kk = K[k];
         out[i] = pack_key(key_x(kk) + kMinBorder, key_y(kk) + kMinBorder, key_score(kk));
+        if (ord) {  // band and rank in it (any order inside a band: only the sweep order changes)
+            const int yb = min((int)key_y(kk) >> 5, kOctBands - 1);
+            s.s64[i] = ((unsigned long long)yb << 16) | (unsigned)atomicAdd(&ybin[yb], 1);
+        }
+    }
+    if (ord) {
+        __syncthreads();
+        int t;
+        const int ex = block_exclusive_scan<BLK>(tid < kOctBands ? ybin[tid] : 0, s.tmp, t);
+        if (tid < kOctBands) ybin[tid] = ex;
+        __syncthreads();
+        for (int i = tid; i < size; i += BLK) {
+            const unsigned long long v = s.s64[i];
+            ord[ybin[(int)(v >> 16)] + (int)(v & 0xffffu)] = (uint16_t)i;
+        }
     }
     if (tid == 0) *out_cnt = size;
 #ifdef ORBFE_OCT_TIMING
@@ -2370,12 +2424,17 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
             off = ge ? a.out_off[k] : off;
         }
         const int c = __shfl(cq, lv, 64), pr = __shfl(pre, lv, 64);  // every lane active
-        const int idx = slot - off;
-        if (lane < kDescGroup && s0 + lane * stride < a.out_total && idx < c && idx + pr < a.kps_cap) {
-            valid = true;
-            my_l = lv;
-            my_o = idx + pr;
-            my_key = (int)a.oct_out[f * a.out_total + slot];
+        int idx = slot - off;
+        if (lane < kDescGroup && s0 + lane * stride < a.out_total && idx < c) {
+            // the oct-tree's band order: the frame's waves sweep each level top to bottom, so
+            // the windows of one run share their lines (output order unchanged: my_o)
+            if (a.oct_ord) idx = a.oct_ord[f * a.out_total + slot];
+            if (idx + pr < a.kps_cap) {
+                valid = true;
+                my_l = lv;
+                my_o = idx + pr;
+                my_key = (int)a.oct_out[f * a.out_total + off + idx];
+            }
         }
     }
     int l0 = 0;
@@ -3315,99 +3374,177 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
         // and each ring's size (the rows its next level still needs when the step starts, plus
         // the rows the step makes).  Large batches: a few bands per frame (2 or 3 workgroups
         // per CU by LDS); small ones: thin bands for latency.
+        // Column tiles (batches): a band can also be split into column tiles, each computing
+        // its own columns of every level plus the source columns its next level's columns read
+        // (derived top-down like the rows; whole 4-column groups), so a tile's rings are
+        // narrower and two workgroups fit a CU.  Default: the tallest step (32, 24, 16, 8 rows),
+        // then the fewest tiles, whose LDS fits 80 KB; else the first that fits 160 KB.
+        auto plan_cols = [&](int nct, std::vector<int>& ct, int (&pitch)[kMaxLevels]) {
+            ct.assign((size_t)nct * L * 4, 0);
+            for (int l = 0; l < L; ++l) pitch[l] = 0;
+            for (int t = 0; t < nct; ++t) {
+                auto O = [&](int l, int tt) {  // own column boundaries: multiples of 4, w at the end
+                    return tt >= nct ? g.geo.lv[l].w : (int)(((long long)tt * g.geo.lv[l].w / nct) & ~3LL);
+                };
+                int c0[kMaxLevels], c1[kMaxLevels];
+                for (int l = L - 1; l >= 0; --l) {
+                    const int w = g.geo.lv[l].w;
+                    int a0 = O(l, t), a1 = O(l, t + 1) - 1;
+                    if (l + 1 < L) {  // the source columns of level l + 1's computed groups
+                        const int xo = g.xoff[l + 1], wn = g.geo.lv[l + 1].w;
+                        a0 = std::min(a0, g.xtab[xo + 3 * c0[l + 1]]);
+                        a1 = std::max(a1, g.xtab[xo + 3 * std::min(c1[l + 1] | 3, wn - 1) + 1]);
+                    }
+                    c0[l] = a0 & ~3;
+                    c1[l] = std::min(w - 1, a1 | 3);
+                    int* e = &ct[((size_t)t * L + l) * 4];
+                    e[0] = c0[l];
+                    e[1] = c1[l];
+                    e[2] = O(l, t);
+                    e[3] = O(l, t + 1);
+                    pitch[l] = std::max(pitch[l], ((c1[l] - c0[l] + 1 + 15) & ~15) + 16);
+                }
+            }
+        };
         for (int which = 0; which < 2 && groups_ok; ++which) {
             const char* be = std::getenv(which == 0 ? "ORBFE_ROLL_BANDS" : "ORBFE_ROLL_BANDS_SMALL");
             const char* ce = std::getenv(which == 0 ? "ORBFE_ROLL_CHUNK" : "ORBFE_ROLL_CHUNK_SMALL");
-            // large batches: ~180 level-0 rows per band, 32 rows per step (1080p: 6 bands,
-            // measured level with the per-level kernels and 8 / 12-band plans, §5c)
+            const char* te = std::getenv(which == 0 ? "ORBFE_ROLL_COLS" : "ORBFE_ROLL_COLS_SMALL");
+            // large batches: ~180 level-0 rows per band (1080p: 6 bands); small ones: thin
+            // bands of one column tile for latency
             int nb = be ? std::atoi(be) : (which == 0 ? std::max(1, std::min(16, (h0 + 179) / 180))
                                                       : std::max(1, std::min(std::min(64, htop), h0 / 24)));
             nb = std::max(1, std::min(nb, htop));
-            const int cpr0 = (g.geo.lv[0].w + 15) >> 4;
-            int C0 = ce ? std::atoi(ce) : (which == 0 ? 32 : 8);
-            C0 = std::max(2, std::min(C0, (kPyrRollPre * kPyrBlockSize) / cpr0));
             std::vector<int> rbt;
             size_t lds_unused;
             int u1, u2, u3;
             plan_bands(nb, rbt, lds_unused, u1, u2, u3);
             auto B4 = [&](int b, int l, int k) { return rbt[((size_t)b * L + l) * 4 + k]; };
-            int S = 1;
-            for (int b = 0; b < nb; ++b)
-                S = std::max(S, (B4(b, 0, 1) - B4(b, 0, 0) + 1 + C0 - 1) / C0);
-            std::vector<int> sched((size_t)nb * S * L);
-            int R[kMaxLevels] = {};
-            int ymax = 1;
-            bool ok = C0 * cpr0 <= kPyrRollPre * kPyrBlockSize;
             auto y0 = [&](int l, int r) { return g.ytab[g.yoff[l] + 3 * r]; };
             auto y1 = [&](int l, int r) { return g.ytab[g.yoff[l] + 3 * r + 1]; };
-            for (int b = 0; b < nb && ok; ++b) {
-                int e[kMaxLevels], ep[kMaxLevels];
-                for (int l = 0; l < L; ++l) e[l] = B4(b, l, 0);
-                for (int s = 0; s < S; ++s) {
-                    for (int l = 0; l < L; ++l) ep[l] = e[l];
-                    e[0] = std::min(B4(b, 0, 0) + (s + 1) * C0, B4(b, 0, 1) + 1);
-                    int made = 0;
-                    for (int l = 1; l < L; ++l) {
-                        int r = e[l];
-                        while (r <= B4(b, l, 1) && y1(l, r) < e[l - 1]) ++r;
-                        e[l] = r;
-                        made += e[l] - ep[l];
+            // the kernel's rule for a step of C0 level-0 rows: every step's made rows, each
+            // ring's rows, the rows made per step at most
+            struct Sim {
+                int S = 1, ymax = 1, R[kMaxLevels] = {};
+                std::vector<int> sched;
+                bool ok = true;
+            };
+            auto simulate = [&](int C0) {
+                Sim m;
+                for (int b = 0; b < nb; ++b)
+                    m.S = std::max(m.S, (B4(b, 0, 1) - B4(b, 0, 0) + 1 + C0 - 1) / C0);
+                m.sched.assign((size_t)nb * m.S * L, 0);
+                for (int b = 0; b < nb && m.ok; ++b) {
+                    int e[kMaxLevels], ep[kMaxLevels];
+                    for (int l = 0; l < L; ++l) e[l] = B4(b, l, 0);
+                    for (int st = 0; st < m.S; ++st) {
+                        for (int l = 0; l < L; ++l) ep[l] = e[l];
+                        e[0] = std::min(B4(b, 0, 0) + (st + 1) * C0, B4(b, 0, 1) + 1);
+                        int made = 0;
+                        for (int l = 1; l < L; ++l) {
+                            int r = e[l];
+                            while (r <= B4(b, l, 1) && y1(l, r) < e[l - 1]) ++r;
+                            e[l] = r;
+                            made += e[l] - ep[l];
+                        }
+                        m.ymax = std::max(m.ymax, made);
+                        for (int l = 0; l + 1 < L; ++l) {
+                            // rows of level l the ring must hold during the step
+                            const int need = ep[l + 1] <= B4(b, l + 1, 1) ? y0(l + 1, ep[l + 1]) : e[l];
+                            m.R[l] = std::max(m.R[l], e[l] - std::min(need, ep[l]));
+                        }
+                        for (int l = 0; l < L; ++l) m.sched[((size_t)b * m.S + st) * L + l] = e[l];
                     }
-                    ymax = std::max(ymax, made);
-                    for (int l = 0; l + 1 < L; ++l) {
-                        // rows of level l the ring must hold during the step
-                        const int need = ep[l + 1] <= B4(b, l + 1, 1) ? y0(l + 1, ep[l + 1]) : e[l];
-                        R[l] = std::max(R[l], e[l] - std::min(need, ep[l]));
-                    }
-                    for (int l = 0; l < L; ++l) sched[((size_t)b * S + s) * L + l] = e[l];
+                    for (int l = 0; l < L; ++l) m.ok = m.ok && e[l] == B4(b, l, 1) + 1;  // every row made
                 }
-                for (int l = 0; l < L; ++l) ok = ok && e[l] == B4(b, l, 1) + 1;  // every row made
+                for (int l = 0; l + 1 < L; ++l) m.R[l] = std::max(m.R[l], 2);
+                return m;
+            };
+            auto lds_of = [&](const Sim& m, const int (&pitch)[kMaxLevels]) {
+                size_t off = 0;
+                for (int l = 0; l + 1 < L; ++l) off += ((size_t)m.R[l] * pitch[l] + 15) & ~(size_t)15;
+                return off + (size_t)m.ymax * 16;
+            };
+            std::vector<std::pair<int, int>> cand;  // (column tiles, rows per step)
+            const int nct_max = which == 0 ? 4 : 1;
+            for (int C0 : {32, 24, 16, 8})  // the tallest step first, then the fewest tiles
+                for (int nct = te ? std::atoi(te) : 1; nct <= (te ? std::atoi(te) : nct_max); ++nct)
+                    if (ce ? C0 == 32 : (which == 0 || C0 == 8)) cand.emplace_back(std::max(1, nct), ce ? std::atoi(ce) : C0);
+            int pick = -1, fit = -1;
+            std::vector<Sim> sims(cand.size());
+            std::vector<std::vector<int>> cts(cand.size());
+            std::vector<std::array<int, kMaxLevels>> pitches(cand.size());
+            for (size_t k = 0; k < cand.size() && pick < 0; ++k) {
+                int pitch[kMaxLevels];
+                plan_cols(cand[k].first, cts[k], pitch);
+                for (int l = 0; l < L; ++l) pitches[k][l] = pitch[l];
+                const int cpr0 = (pitch[0] - 16) >> 4;  // level-0 chunks per tile row
+                const int C0 = std::max(2, std::min(cand[k].second, (kPyrRollPre * kPyrBlockSize) / std::max(cpr0, 1)));
+                cand[k].second = C0;
+                sims[k] = simulate(C0);
+                bool groups = true;  // a tile's groups of every level fit one thread each
+                for (int t = 0; t < cand[k].first; ++t)
+                    for (int l = 1; l < L; ++l) {
+                        const int* e = &cts[k][((size_t)t * L + l) * 4];
+                        groups = groups && ((e[1] - e[0] + 4) >> 2) <= kPyrBlockSize;
+                    }
+                const size_t lds = lds_of(sims[k], pitch);
+                const bool ok = sims[k].ok && groups && sims[k].ymax <= kPyrBlockSize && lds <= 160 * 1024 &&
+                                C0 * cpr0 <= kPyrRollPre * kPyrBlockSize;
+                if (ok && fit < 0) fit = (int)k;
+                if (ok && (lds <= 80 * 1024 || te || ce || which == 1)) pick = (int)k;
             }
+            if (pick < 0) pick = fit;
+            g.roll_ok[which] = pick >= 0;
+            if (!g.roll_ok[which]) continue;
+            const Sim& m = sims[pick];
+            const int S = m.S, nct = cand[pick].first;
             size_t off = 0;
+            for (int l = 0; l < L; ++l) g.roll_pitch[which][l] = pitches[pick][l];
             for (int l = 0; l + 1 < L; ++l) {
-                R[l] = std::max(R[l], 2);
-                g.roll_ring_rows[which][l] = R[l];
+                g.roll_ring_rows[which][l] = m.R[l];
                 g.roll_ring_off[which][l] = (int)off;
-                off += ((size_t)R[l] * g.pyr_lp[l] + 15) & ~(size_t)15;
+                off += ((size_t)m.R[l] * g.roll_pitch[which][l] + 15) & ~(size_t)15;
             }
             g.roll_ydesc[which] = (int)off;
-            g.roll_lds[which] = off + (size_t)ymax * 16;
-            g.roll_ok[which] = ok && ymax <= kPyrBlockSize && g.roll_lds[which] <= 160 * 1024;
+            g.roll_lds[which] = off + (size_t)m.ymax * 16;
             // every step's row descriptors (the kernel's LDS offsets of the two source rows in
             // the ring below, the coefficients, the row's own ring offset)
             std::vector<int> ydoff((size_t)nb * (S + 1)), ydtab;
-            for (int b = 0; b < nb && g.roll_ok[which]; ++b) {
-                for (int s = 0; s < S; ++s) {
-                    ydoff[(size_t)b * (S + 1) + s] = (int)(ydtab.size() / 4);
+            for (int b = 0; b < nb; ++b) {
+                for (int st = 0; st < S; ++st) {
+                    ydoff[(size_t)b * (S + 1) + st] = (int)(ydtab.size() / 4);
                     for (int l = 1; l < L; ++l) {
-                        const int r0 = s ? sched[((size_t)b * S + s - 1) * L + l] : B4(b, l, 0);
-                        const int r1 = sched[((size_t)b * S + s) * L + l];
-                        const int so = g.roll_ring_off[which][l - 1], ps = g.pyr_lp[l - 1];
+                        const int r0 = st ? m.sched[((size_t)b * S + st - 1) * L + l] : B4(b, l, 0);
+                        const int r1 = m.sched[((size_t)b * S + st) * L + l];
+                        const int so = g.roll_ring_off[which][l - 1], ps = g.roll_pitch[which][l - 1];
+                        const int R0 = m.R[l - 1];
                         for (int r = r0; r < r1; ++r) {
                             const int* yy = &g.ytab[g.yoff[l] + 3 * r];
-                            ydtab.push_back(so + (yy[0] % R[l - 1]) * ps);
-                            ydtab.push_back(so + (yy[1] % R[l - 1]) * ps);
+                            ydtab.push_back(so + (yy[0] % R0) * ps);
+                            ydtab.push_back(so + (yy[1] % R0) * ps);
                             ydtab.push_back(yy[2]);
-                            ydtab.push_back(l + 1 < L ? g.roll_ring_off[which][l] + (r % R[l]) * g.pyr_lp[l] : 0);
+                            ydtab.push_back(l + 1 < L ? g.roll_ring_off[which][l] + (r % m.R[l]) * g.roll_pitch[which][l] : 0);
                         }
                     }
                 }
                 ydoff[(size_t)b * (S + 1) + S] = (int)(ydtab.size() / 4);
             }
             g.roll_bands[which] = nb;
+            g.roll_cols[which] = nct;
             g.roll_steps[which] = S;
-            if (g.roll_ok[which]) {
-                while (g.ptab.size() % 4) g.ptab.push_back(0u);
-                g.roll_band_off[which] = (int)(g.ptab.size() / 4);
-                for (int v : rbt) g.ptab.push_back((uint32_t)v);
-                g.roll_sched_off[which] = (int)g.ptab.size();
-                for (int v : sched) g.ptab.push_back((uint32_t)v);
-                g.roll_ydoff_off[which] = (int)g.ptab.size();
-                for (int v : ydoff) g.ptab.push_back((uint32_t)v);
-                while (g.ptab.size() % 4) g.ptab.push_back(0u);
-                g.roll_ydtab_off[which] = (int)(g.ptab.size() / 4);
-                for (int v : ydtab) g.ptab.push_back((uint32_t)v);
-            }
+            while (g.ptab.size() % 4) g.ptab.push_back(0u);
+            g.roll_band_off[which] = (int)(g.ptab.size() / 4);
+            for (int v : rbt) g.ptab.push_back((uint32_t)v);
+            g.roll_col_off[which] = (int)(g.ptab.size() / 4);
+            for (int v : cts[pick]) g.ptab.push_back((uint32_t)v);
+            g.roll_sched_off[which] = (int)g.ptab.size();
+            for (int v : m.sched) g.ptab.push_back((uint32_t)v);
+            g.roll_ydoff_off[which] = (int)g.ptab.size();
+            for (int v : ydoff) g.ptab.push_back((uint32_t)v);
+            while (g.ptab.size() % 4) g.ptab.push_back(0u);
+            g.roll_ydtab_off[which] = (int)(g.ptab.size() / 4);
+            for (int v : ydtab) g.ptab.push_back((uint32_t)v);
         }
     }
     int rmax = 7, cmax = 7;

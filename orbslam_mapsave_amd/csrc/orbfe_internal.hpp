@@ -106,6 +106,10 @@ struct PyrArgs {
     const int4* ydtab;
     int nsteps, ydesc;
     int ring_rows[kMaxLevels], ring_off[kMaxLevels];
+    // column tiles: blockIdx.x = band * ncols + tile; cols[tile * nlevels + l] = {first, last
+    // computed column, own columns [z, w)}; lp[] is then the rings' row pitch
+    const int4* cols;
+    int ncols;
 };
 
 struct ResizeTailArgs {
@@ -146,6 +150,8 @@ struct OctArgs {
                            // exceed kOctLdsKeys (int per key)
     uint32_t* oct_out;     // [frame][out_total]
     int* oct_cnt;          // [frame][nlevels]
+    uint16_t* oct_ord;     // [frame][out_total] or null: each level's keypoints in 32-row bands
+                           // (level-local indices; describe's processing order, not the output's)
     int ncap_max, sort_cap;
     int lds_keys;          // keys of a level held in LDS (Plan::oct_keys)
 };
@@ -172,6 +178,7 @@ struct DescArgs {
     LevelPtr pyr[kMaxLevels];
     const uint32_t* oct_out;
     const int* oct_cnt;
+    const uint16_t* oct_ord;  // strided waves: slot -> level-local keypoint (OctArgs::oct_ord), or null
     orbfe_keypoint* kps;
     uint8_t* desc;
     int32_t* n_out;
@@ -242,6 +249,8 @@ struct Plan {
     int roll_bands[2] = {}, roll_steps[2] = {}, roll_band_off[2] = {}, roll_sched_off[2] = {};
     int roll_ydoff_off[2] = {}, roll_ydtab_off[2] = {};
     int roll_ring_rows[2][kMaxLevels] = {}, roll_ring_off[2][kMaxLevels] = {}, roll_ydesc[2] = {};
+    int roll_cols[2] = {1, 1}, roll_col_off[2] = {};   // column tiles per band, their table
+    int roll_pitch[2][kMaxLevels] = {};                // ring row pitch per level
     size_t roll_lds[2] = {};
 };
 

@@ -35,7 +35,7 @@ EXPORTED = [
     "orbfe_extract_color", "orbfe_human_mask_rect", "orbfe_extract_batch",
     "orbfe_extract_batch_device", "orbfe_extract_color_batch_device", "orbfe_set_stream",
     "orbfe_synchronize", "orbfe_compute_stereo_matches", "orbfe_compute_stereo_matches_device",
-    "orbfe_stereo_status", "orbfe_profile", "orbfe_profile_read", "orbfe_get_level", "orbfe_get_blurred_level", "orbfe_get_fast_keys",
+    "orbfe_stereo_status", "orbfe_profile", "orbfe_profile_read", "orbfe_pyramid_path", "orbfe_get_level", "orbfe_get_blurred_level", "orbfe_get_fast_keys",
     "orbfe_matcher_create", "orbfe_matcher_destroy", "orbfe_matcher_set_stream",
     "orbfe_matcher_profile", "orbfe_matcher_profile_read", "orbfe_hamming",
     "orbfe_bf_match", "orbfe_bf_match_batch_device", "orbfe_search_for_initialization",
@@ -67,6 +67,7 @@ def lib() -> C.CDLL:
         for fn in ("orbfe_get_levels", "orbfe_get_scale_factor", "orbfe_keypoint_capacity",
                    "orbfe_synchronize"):
             getattr(L, fn).argtypes = [C.c_void_p]
+        L.orbfe_pyramid_path.argtypes = [C.c_void_p, C.c_int]
         if hasattr(L, "orbfe_matcher_create"):
             L.orbfe_matcher_create.restype = C.c_void_p
             L.orbfe_matcher_create.argtypes = [C.c_int, C.c_void_p]
@@ -369,6 +370,15 @@ class ORBextractor:
         n = np.zeros(len(self.STAGES), np.int32)
         _check("orbfe_profile_read", lib().orbfe_profile_read(self._h, ptr(ms), ptr(n)))
         return {s: (float(ms[i]), int(n[i])) for i, s in enumerate(self.STAGES)}
+
+    PYR_PATHS = ("per_level", "bands", "roll")
+
+    def pyramid_path(self, nframes: int) -> str:
+        """The pyramid kernel an extraction of `nframes` frames at the last extracted size takes
+        (orbfe_pyramid_path): "per_level", "bands" or "roll"."""
+        r = lib().orbfe_pyramid_path(self._h, int(nframes))
+        _check("orbfe_pyramid_path", r if r < 0 else 0)
+        return self.PYR_PATHS[r]
 
     # ---- probes of the last extraction
     def _level(self, fn, frame: int, level: int) -> np.ndarray:

@@ -1,6 +1,7 @@
 // GPU parity check of the C++ adapter (include/orbfe_orbslam.hpp) against the CPU oracle, as
 // C++ host code of the reference would use it.  Built by __graft_entry__.build(); run by
 // tests/test_gpu_cpp.py on the MI355X.  Prints "ADAPTER PASS" on success.
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -54,6 +55,35 @@ int main() {
                                  !std::memcmp(sdesc.data(), odesc.data(), (size_t)n * 32);
         std::printf("seed %u staged: %zu keypoints %s\n", seed, skps.size(), same_staged ? "bit-exact" : "MISMATCH");
         fails += !same_staged;
+    }
+    // single-frame latency from a C++ caller (Frame::ExtractORB's position): the host form
+    // (frame copied into the staging buffer by the call) and the staged form (frame already in
+    // the staging buffer: the caller's cvtColor target; outputs read in place, or copied into
+    // the adapter's vectors as Frame keeps them).  Mean over 2,000 calls after 100 warm-up calls.
+    {
+        std::vector<uint8_t> img = make_image(W, H, 5);
+        std::vector<orbfe_keypoint> kps;
+        std::vector<uint8_t> desc;
+        size_t step = 0;
+        uint8_t* buf = ex.InputBuffer(W, H, &step);
+        for (int y = 0; y < H; ++y) std::memcpy(buf + (size_t)y * step, img.data() + (size_t)y * W, W);
+        auto mean_us = [&](auto&& call) {
+            for (int i = 0; i < 100; ++i) call();
+            const auto t0 = std::chrono::steady_clock::now();
+            for (int i = 0; i < 2000; ++i) call();
+            return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / 2000;
+        };
+        const double host_us = mean_us([&] { ex(img.data(), W, H, W, nullptr, 0, kps, desc); });
+        const double staged_copy_us = mean_us([&] { ex.ExtractStaged(W, H, kps, desc); });
+        const double staged_us = mean_us([&] {
+            int n = 0;
+            const orbfe_keypoint* k = nullptr;
+            const uint8_t* d = nullptr;
+            if (orbfe_extract_staged(ex.handle(), W, H, nullptr, 0, nullptr, &n) ||
+                orbfe_staged_outputs(ex.handle(), &k, &d, &n))
+                ++fails;
+        });
+        std::printf("LATENCY host_us=%.2f staged_copy_us=%.2f staged_us=%.2f\n", host_us, staged_copy_us, staged_us);
     }
     // scale tables through the getters
     std::vector<float> sf = ex.GetScaleFactors(), osf(8);

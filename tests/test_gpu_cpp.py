@@ -15,3 +15,4 @@ def test_cpp_adapter_parity():
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=300)
     print(r.stdout)
     assert r.returncode == 0 and "ADAPTER PASS" in r.stdout, r.stdout + r.stderr
+    assert "LATENCY" in r.stdout  # the C++ caller's single-frame latency (tools/bench_rows.py row)

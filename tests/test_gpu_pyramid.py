@@ -44,6 +44,7 @@ def test_levels_bit_exact(size, batch, arith, monkeypatch):
             e(imgs[0])
         else:
             e.extract_batch(imgs)
+        assert e.pyramid_path(batch) == "bands"
         _levels_exact(e, p, imgs, var)
     finally:
         e.close()
@@ -60,6 +61,7 @@ def test_band_plans(lds_kb, monkeypatch):
     try:
         imgs = np.stack([synthetic_frame(90 + s, 640, 480) for s in range(8)])
         kps, desc, cnt = e.extract_batch(imgs)
+        assert e.pyramid_path(len(imgs)) == "bands"
         _levels_exact(e, p, imgs, oracle.DEFAULT_VARIANT)
         okps, odesc = oracle.extract(p, imgs[3])
         assert kps[3, :cnt[3]].tobytes() == okps.tobytes()
@@ -79,6 +81,24 @@ def test_other_scale_factors(sf, nl, monkeypatch):
         imgs = np.stack([synthetic_frame(120 + s, 640, 480) for s in range(8)])
         e.extract_batch(imgs)
         _levels_exact(e, p, imgs[:2], oracle.DEFAULT_VARIANT)
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("size,batch,path", [((640, 480), 1, "bands"), ((640, 480), 9, "bands"),
+                                             ((1920, 1080), 1, "bands"), ((1920, 1080), 9, "per_level")])
+def test_default_paths(size, batch, path, monkeypatch):
+    """The pyramid path each shape takes by default (the measured choices of DESIGN.md §5e)."""
+    from orbslam_mapsave_amd.native import ORBextractor
+    for v in ("ORBFE_PYR", "ORBFE_ROLL", "ORBFE_ROLL_BANDS", "ORBFE_ROLL_CHUNK"):
+        monkeypatch.delenv(v, raising=False)
+    w, h = size
+    nf = 2000 if w > 1000 else 1000
+    e = ORBextractor(nf, 1.2, 8, 20, 7, device=0, max_width=w, max_height=h)
+    try:
+        imgs = np.stack([synthetic_frame(11 * w + s, w, h) for s in range(batch)])
+        e(imgs[0]) if batch == 1 else e.extract_batch(imgs)
+        assert e.pyramid_path(batch) == path
     finally:
         e.close()
 
@@ -121,6 +141,7 @@ def test_per_level_kernels_exact(size, arith, table, monkeypatch):
     try:
         imgs = np.stack([synthetic_frame(7 * w + s, w, h) for s in range(9)])
         e.extract_batch(imgs)
+        assert e.pyramid_path(len(imgs)) == "per_level"
         _levels_exact(e, p, imgs[:3], var)
         e(imgs[4])
         _levels_exact(e, p, imgs[4:5], var)
@@ -132,9 +153,9 @@ def test_per_level_kernels_exact(size, arith, table, monkeypatch):
 @pytest.mark.parametrize("batch", [1, 9])
 @pytest.mark.parametrize("arith", ["scalar", "x86"])
 def test_roll_levels_bit_exact(size, batch, arith, monkeypatch):
-    """pyramid_roll_kernel (the one-launch pyramid where the band kernel's seams cost too much:
-    the default at 1920x1080; ORBFE_PYR=3 forces it everywhere): every level of every frame
-    byte-exact against the oracle in both readings, single frames (thin bands) and batches."""
+    """pyramid_roll_kernel (the one-launch pyramid at any size; opt-in, ORBFE_PYR=3 forces it
+    everywhere): every level of every frame byte-exact against the oracle in both readings,
+    single frames (thin bands) and batches — and the rolling kernel is the one that ran."""
     from orbslam_mapsave_amd.native import ORBextractor
     monkeypatch.setenv("ORBFE_PYR", "3")
     w, h = size
@@ -149,24 +170,29 @@ def test_roll_levels_bit_exact(size, batch, arith, monkeypatch):
             e(imgs[0])
         else:
             e.extract_batch(imgs)
+        assert e.pyramid_path(batch) == "roll"
         _levels_exact(e, p, imgs[:3], var)
     finally:
         e.close()
 
 
-@pytest.mark.parametrize("bands,chunk", [("1", "2"), ("3", "5"), ("7", "16"), ("2", "33")])
-def test_roll_plans(bands, chunk, monkeypatch):
-    """Other rolling plans (band counts, level-0 rows per step: ring sizes, step counts and the
-    per-thread chunk bound change) give the same levels and keypoints."""
+@pytest.mark.parametrize("bands,chunk,cols", [("1", "2", "1"), ("3", "5", "1"), ("7", "16", "1"), ("2", "24", "1"),
+                                              ("2", "16", "2"), ("5", "8", "3"), ("1", "32", "4")])
+def test_roll_plans(bands, chunk, cols, monkeypatch):
+    """Other rolling plans (band counts, level-0 rows per step, column tiles per band: ring
+    sizes, step counts, tile seams and the per-thread chunk bound change) give the same levels
+    and keypoints."""
     from orbslam_mapsave_amd.native import ORBextractor
     monkeypatch.setenv("ORBFE_PYR", "3")
     monkeypatch.setenv("ORBFE_ROLL_BANDS", bands)
     monkeypatch.setenv("ORBFE_ROLL_CHUNK", chunk)
+    monkeypatch.setenv("ORBFE_ROLL_COLS", cols)
     p = oracle.params(2000, 1.2, 8, 20, 7)
     e = ORBextractor(2000, 1.2, 8, 20, 7, device=0, max_width=1920, max_height=1080)
     try:
         imgs = np.stack([synthetic_frame(170 + s, 1920, 1080) for s in range(8)])
         kps, desc, cnt = e.extract_batch(imgs)
+        assert e.pyramid_path(len(imgs)) == "roll"
         _levels_exact(e, p, imgs[:2], oracle.DEFAULT_VARIANT)
         okps, odesc = oracle.extract(p, imgs[1])
         assert kps[1, :cnt[1]].tobytes() == okps.tobytes()

@@ -127,6 +127,19 @@ def row_single():
          "target), outputs left in pinned memory (orbfe_staged_outputs), one graph launch + one "
          "synchronisation per call", cpu_units=1)
     ex.close()
+    # the same calls from C++ (the adapter program, as Frame::ExtractORB would make them): no
+    # Python / ctypes in the loop
+    import re
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "cpp", "build", "adapter_test")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    m = re.search(r"LATENCY host_us=([0-9.]+) staged_copy_us=([0-9.]+) staged_us=([0-9.]+)", r.stdout)
+    if r.returncode == 0 and m:
+        for us, what in ((float(m.group(1)), "host form (orbfe::ORBextractor::operator(), frame copied in)"),
+                         (float(m.group(3)), "zero-copy staging (orbfe_extract_staged, outputs in place)")):
+            emit(f"single-frame latency from C++, {what} (640x480, 1000 kp)", "frames/s", 1, us * 1e-6, tc,
+                 640 * 480 + 1000 * 60, "tests/cpp/adapter_test: mean of 2,000 calls after 100 warm-up "
+                 "calls, C++ caller through include/orbfe_orbslam.hpp", cpu_units=1)
 
 
 def row_stereo():

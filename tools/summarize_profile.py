@@ -127,6 +127,8 @@ roof = line.get("roofline") or {}
 k = roof.get("kernel")
 if k:
     roof["traffic"] = traffic.get(k.replace("_kernel", ""), roof.get("traffic"))
+    if roof["traffic"] is not None:
+        roof["traffic_source"] = f"profiles/{R}/pmc_summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this command)"
     with open(bpath, "w") as fh:
         fh.write(json.dumps(line) + "\n")
     check = {"kernel": k, "frames_per_launch": FRAMES,
