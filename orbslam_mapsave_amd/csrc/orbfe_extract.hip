@@ -164,43 +164,65 @@ __device__ __forceinline__ uint32_t resize_px(uint32_t t0, uint32_t t1, uint32_t
     return min(sse2 ? sv : sc, 255u);
 }
 
-// Horizontal coefficient pairs (a0 | a1 << 16) as the horizontal passes feeding resize4 use
-// them: x86 scales both by 16 (a0, a1 <= 2049: each half stays below 2^16), so the sums arrive
-// as h = 16 t (< 2^23).
-template <bool kX86>
-__device__ __forceinline__ uint32_t hcoef(uint32_t a01) { return kX86 ? a01 << 4 : a01; }
+// ORBFE_RS_X86 — the x86 (H5) body formula ((t0 >> 4) * b0 >> 16) + ((t1 >> 4) * b1 >> 16) + 2
+// >> 2 (build-time A/B): 0 = shifts, multiplies, shifts and a clamp per pixel; 1 = the
+// horizontal sums scaled by 16 (hcoef) so each term is one AND + v_mul_hi_u32_u24; 2 = the +2
+// folded into the first product (v_mad_u32_u24) and both >> 16 into one SDWA add.
+#ifndef ORBFE_RS_X86
+#define ORBFE_RS_X86 2
+#endif
+constexpr int kRsX86 = ORBFE_RS_X86;
 
-// Four pixels of a row (columns x .. x + 3) from their horizontal sums h (t, or 16 t in x86
-// mode: hcoef).  x86: every pixel takes the SSE2 body formula, ((t >> 4) * b) >> 16 as
-// v_mul_hi_u32_u24 of (h with its low 8 bits cleared) = (t >> 4) << 8 and b << 8 — one AND and
-// one multiply per term instead of a shift, a multiply and a shift; t >> 4 <= 32,655 and
-// b0 + b1 <= 2049 keep the sum <= 1,022, so no clamp — and only a group reaching the scalar
-// tail (x + 3 >= xb: the last one or two groups of a row) replaces its tail pixels, so the
-// waves holding a row's end run the body once plus the tail's few operations (an if / else
-// per group made those waves run both formulas in full).
+// Horizontal coefficient pairs (a0 | a1 << 16) as the horizontal passes feeding resize4 use
+// them: in mode 1 x86 scales both by 16 (a0, a1 <= 2049: each half stays below 2^16), so the
+// sums arrive as h = 16 t (< 2^23).
+template <bool kX86>
+__device__ __forceinline__ uint32_t hcoef(uint32_t a01) { return kX86 && kRsX86 == 1 ? a01 << 4 : a01; }
+
+// (P0 >> 16) + (P1 >> 16) in one VOP2 SDWA add (word 1 of each operand)
+__device__ __forceinline__ uint32_t add_hi16(uint32_t p0, uint32_t p1) {
+    uint32_t r;
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_1"
+        : "=v"(r) : "v"(p0), "v"(p1));
+    return r;
+}
+
+// Four pixels of a row (columns x .. x + 3) from their horizontal sums (16 t in x86 mode 1,
+// else t).  x86: a group entirely inside the SSE2 body (x + 3 < xb, nearly every group) takes
+// the body formula alone; t >> 4 <= 32,655 and b0 + b1 <= 2049 keep the body's sum <= 1,022,
+// so it needs no clamp.  Groups reaching the scalar tail select per pixel.
 template <bool kX86>
 __device__ __forceinline__ uint32_t resize4(const uint32_t (&h0)[4], const uint32_t (&h1)[4],
                                             uint32_t b0, uint32_t b1, int x, int xb) {
+    constexpr int kS = kX86 && kRsX86 == 1 ? 4 : 0;  // h >> kS = t
     uint32_t packed = 0;
-    if constexpr (!kX86) {
+    if (kX86 && x + 3 < xb) {
+        if constexpr (kRsX86 == 1) {
+            const uint32_t c0 = (b0 & 0xffffu) << 8, c1 = (b1 & 0xffffu) << 8;  // < 2^24
 #pragma unroll
-        for (int k = 0; k < 4; ++k) packed |= resize_px<false>(h0[k], h1[k], b0, b1, false) << (8 * k);
-        return packed;
-    }
-    const uint32_t c0 = (b0 & 0xffffu) << 8, c1 = (b1 & 0xffffu) << 8;  // < 2^24
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t p0 = (uint32_t)(((unsigned long long)(h0[k] & 0x7fff00u) * c0) >> 32);
+                const uint32_t p1 = (uint32_t)(((unsigned long long)(h1[k] & 0x7fff00u) * c1) >> 32);
+                packed |= ((p0 + p1 + 2u) >> 2) << (8 * k);
+            }
+        } else if constexpr (kRsX86 == 2) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t p0 = (uint32_t)(((unsigned long long)(h0[k] & 0x7fff00u) * c0) >> 32);
-        const uint32_t p1 = (uint32_t)(((unsigned long long)(h1[k] & 0x7fff00u) * c1) >> 32);
-        packed |= ((p0 + p1 + 2u) >> 2) << (8 * k);
-    }
-    if (x + 3 >= xb) {
+            for (int k = 0; k < 4; ++k) {
+                // (t0 >> 4) b0 + 2^17 < 2^27: its word 1 is ((t0 >> 4) b0 >> 16) + 2
+                const uint32_t p0 = __umul24(h0[k] >> 4, b0) + (2u << 16);
+                const uint32_t p1 = __umul24(h1[k] >> 4, b1);
+                packed |= (add_hi16(p0, p1) >> 2) << (8 * k);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                packed |= min((((uint32_t)__umul24(h0[k] >> 4, b0) >> 16) +
+                               ((uint32_t)__umul24(h1[k] >> 4, b1) >> 16) + 2u) >> 2, 255u) << (8 * k);
+        }
+    } else {
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            if (x + k >= xb) {
-                const uint32_t sc = min((__umul24(h0[k] >> 4, b0) + __umul24(h1[k] >> 4, b1) + (1u << 21)) >> 22, 255u);
-                packed = (packed & ~(0xffu << (8 * k))) | (sc << (8 * k));
-            }
+            packed |= resize_px<kX86>(h0[k] >> kS, h1[k] >> kS, b0, b1, x + k < xb) << (8 * k);
     }
     return packed;
 }
@@ -3374,11 +3396,11 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
         // and each ring's size (the rows its next level still needs when the step starts, plus
         // the rows the step makes).  Large batches: a few bands per frame (2 or 3 workgroups
         // per CU by LDS); small ones: thin bands for latency.
-        // Column tiles (batches): a band can also be split into column tiles, each computing
-        // its own columns of every level plus the source columns its next level's columns read
-        // (derived top-down like the rows; whole 4-column groups), so a tile's rings are
-        // narrower and two workgroups fit a CU.  Default: the tallest step (32, 24, 16, 8 rows),
-        // then the fewest tiles, whose LDS fits 80 KB; else the first that fits 160 KB.
+        // Column tiles (ORBFE_ROLL_COLS): a band can also be split into column tiles, each
+        // computing its own columns of every level plus the source columns its next level's
+        // columns read (derived top-down like the rows; whole 4-column groups), so a tile's
+        // rings are narrower (two workgroups per CU).  Plan: the tallest step (32, 24, 16, 8
+        // rows), then the fewest tiles, whose LDS fits 160 KB.
         auto plan_cols = [&](int nct, std::vector<int>& ct, int (&pitch)[kMaxLevels]) {
             ct.assign((size_t)nct * L * 4, 0);
             for (int l = 0; l < L; ++l) pitch[l] = 0;
@@ -3466,11 +3488,13 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
                 return off + (size_t)m.ymax * 16;
             };
             std::vector<std::pair<int, int>> cand;  // (column tiles, rows per step)
-            const int nct_max = which == 0 ? 4 : 1;
+            // column tiles only on request (ORBFE_ROLL_COLS): at 1080p 2-4 tiles per band
+            // measured 1.76-2.76 ms per 256 frames against one tile's 1.34
+            const int nct_max = 1;
             for (int C0 : {32, 24, 16, 8})  // the tallest step first, then the fewest tiles
                 for (int nct = te ? std::atoi(te) : 1; nct <= (te ? std::atoi(te) : nct_max); ++nct)
                     if (ce ? C0 == 32 : (which == 0 || C0 == 8)) cand.emplace_back(std::max(1, nct), ce ? std::atoi(ce) : C0);
-            int pick = -1, fit = -1;
+            int pick = -1;
             std::vector<Sim> sims(cand.size());
             std::vector<std::vector<int>> cts(cand.size());
             std::vector<std::array<int, kMaxLevels>> pitches(cand.size());
@@ -3491,10 +3515,8 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
                 const size_t lds = lds_of(sims[k], pitch);
                 const bool ok = sims[k].ok && groups && sims[k].ymax <= kPyrBlockSize && lds <= 160 * 1024 &&
                                 C0 * cpr0 <= kPyrRollPre * kPyrBlockSize;
-                if (ok && fit < 0) fit = (int)k;
-                if (ok && (lds <= 80 * 1024 || te || ce || which == 1)) pick = (int)k;
+                if (ok) pick = (int)k;
             }
-            if (pick < 0) pick = fit;
             g.roll_ok[which] = pick >= 0;
             if (!g.roll_ok[which]) continue;
             const Sim& m = sims[pick];
