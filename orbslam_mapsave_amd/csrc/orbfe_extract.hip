@@ -1143,11 +1143,32 @@ __device__ __forceinline__ int lane_prefix(unsigned long long mask) {
 // pre-test ruled a corner out.  cv::FAST's strict 3x3 NMS (H1) keeps s when s >= t and
 // s > nv for every neighbour, nv = (ns >= t ? ns : 0): for s >= max(t, 1) that is exactly
 // max(ns) < s, and for s = t = 0 it never holds — so one byte compare against the neighbour
-// maximum decides it.
-__device__ __forceinline__ int fast_emit(const uint8_t* S, const uint16_t* list, int cnt, int P,
+// maximum decides it.  ORBFE_FAST_EMIT2 (default): the entries whose own score reaches the
+// threshold (about a quarter of the pre-test survivors) are first compacted in order to the
+// front of the list, so the eight neighbour reads run over full waves of corners only.
+#ifndef ORBFE_FAST_EMIT2
+#define ORBFE_FAST_EMIT2 1
+#endif
+__device__ __forceinline__ int fast_emit(const uint8_t* S, uint16_t* list, int cnt, int P,
                                          unsigned inv_p, int t, const CellDesc& cell,
                                          uint32_t* out, int cap) {
     const int tb = max(t, 1) + 1;
+    if (ORBFE_FAST_EMIT2) {
+        int nc = 0;  // in place: chunk k's writes land below its own (already read) entries
+        for (int base = 0; base < cnt; base += 64) {
+            const int i = base + (int)threadIdx.x;
+            int off = 0, sb = 0;
+            if (i < cnt) {
+                off = list[i];
+                sb = S[off + P + 1];
+            }
+            const unsigned long long m = __ballot(sb >= tb);
+            if (sb >= tb) list[nc + lane_prefix(m)] = (uint16_t)off;
+            nc += __popcll(m);
+        }
+        fast_sync();
+        cnt = nc;
+    }
     int o = 0;
     for (int base = 0; base < cnt; base += 64) {
         const int i = base + (int)threadIdx.x;
