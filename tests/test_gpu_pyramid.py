@@ -85,6 +85,26 @@ def test_other_scale_factors(sf, nl, monkeypatch):
         e.close()
 
 
+@pytest.mark.parametrize("size,cols", [((1281, 722), "2"), ((643, 481), "3"), ((331, 247), "2")])
+def test_roll_column_tiles_sizes(size, cols, monkeypatch):
+    """Column tiles of the rolling kernel at odd sizes (tile seams on unaligned level widths,
+    the SSE2 body boundary inside a tile): every level of every frame byte-exact."""
+    from orbslam_mapsave_amd.native import ORBextractor
+    monkeypatch.setenv("ORBFE_PYR", "3")
+    monkeypatch.setenv("ORBFE_ROLL_COLS", cols)
+    w, h = size
+    nf = 1500 if w > 1000 else 1000
+    p = oracle.params(nf, 1.2, 8, 20, 7)
+    e = ORBextractor(nf, 1.2, 8, 20, 7, device=0, max_width=w, max_height=h)
+    try:
+        imgs = np.stack([synthetic_frame(13 * w + s, w, h) for s in range(9)])
+        e.extract_batch(imgs)
+        assert e.pyramid_path(9) == "roll"
+        _levels_exact(e, p, imgs[:3], oracle.DEFAULT_VARIANT)
+    finally:
+        e.close()
+
+
 @pytest.mark.parametrize("size,batch,path", [((640, 480), 1, "bands"), ((640, 480), 9, "bands"),
                                              ((1920, 1080), 1, "bands"), ((1920, 1080), 9, "per_level")])
 def test_default_paths(size, batch, path, monkeypatch):
