@@ -110,6 +110,24 @@ def test_describe_slot_orders(p, order, stride, monkeypatch):
         e.close()
 
 
+def test_describe_band_order_1080p():
+    """The default at >= 1 Mpx: describe's strided waves take the oct-tree's 32-row band order
+    (batches of >= 8 frames) — keypoints and descriptors of a 1920 x 1080 batch identical to the
+    oracle's, in the output order."""
+    from orbslam_mapsave_amd.native import ORBextractor
+    p2 = oracle.params(2000, 1.2, 8, 20, 7)
+    e = ORBextractor(2000, 1.2, 8, 20, 7, device=0, max_width=1920, max_height=1080)
+    try:
+        imgs = np.stack([synthetic_frame(60 + s, 1920, 1080) for s in range(8)])
+        kps, desc, cnt = e.extract_batch(imgs)
+        for f in (0, 7):
+            okps, odesc = oracle.extract(p2, imgs[f])
+            _assert_same_keys(kps[f, :cnt[f]], okps)
+            assert np.array_equal(desc[f, :cnt[f]], odesc)
+    finally:
+        e.close()
+
+
 def test_profile_stage_mask(ex, p):
     """orbfe_profile: events on every launch, or on the masked stages' launches only (bench.py's
     timed steps); results stay bit-exact either way."""
