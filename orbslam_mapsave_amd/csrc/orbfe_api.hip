@@ -224,6 +224,8 @@ struct orbfe_extractor {
                (force_roll || !band_path(n));
     }
     bool pyr_path(int n) const { return band_path(n) || roll_path(n); }  // one launch
+    // ORBFE_RS2=0: one resize launch per level where resize2_kernel would take two (A/B)
+    bool use_rs2 = !(std::getenv("ORBFE_RS2") && std::strcmp(std::getenv("ORBFE_RS2"), "0") == 0);
     // ORBFE_RESIZE_TABLE=0: resize_kernel's horizontal pass by byte gathers (A/B)
     bool table_off = std::getenv("ORBFE_RESIZE_TABLE") && std::strcmp(std::getenv("ORBFE_RESIZE_TABLE"), "0") == 0;
     // ORBFE_DESC_MFMA=0: describe blurs its raw windows on the VALU instead of the matrix cores
@@ -470,6 +472,39 @@ struct orbfe_extractor {
                              dim3(kPyrBlockSize), g.pyr_lds[which], stream, pa);
         }
         for (int l = 1; l < (one_pyr ? 1 : ts); ++l) {
+            // levels l and l + 1 in one launch (resize2_kernel) where planned; ORBFE_RS2=0: one
+            // launch per level
+            if (use_rs2 && l + 1 < ts && g.rs2_ok[l] && !rb && !table_off) {
+                Resize2Args r2;
+                r2.src = lp[l - 1];
+                r2.mid = lp[l];
+                r2.dst = lp[l + 1];
+                r2.sw = g.geo.lv[l - 1].w;
+                r2.mw = g.geo.lv[l].w;
+                r2.dw = g.geo.lv[l + 1].w;
+                r2.dh = g.geo.lv[l + 1].h;
+                r2.tiles_x = g.rs2_tiles_x[l];
+                r2.tiles = reinterpret_cast<const int4*>(ptab.as<uint4>() + g.rs2_off[l]);
+                r2.yt_m = ytab.as<int>() + g.yoff[l];
+                r2.xt_m = xtab.as<int>() + g.xoff[l];
+                r2.yt_d = ytab.as<int>() + g.yoff[l + 1];
+                r2.xt_d = xtab.as<int>() + g.xoff[l + 1];
+                r2.gtab_m = ptab.as<uint4>() + g.gtab_off[l];
+                r2.gtab_d = ptab.as<uint4>() + g.gtab_off[l + 1];
+                r2.pa = g.rs2_pa[l];
+                r2.pb = g.rs2_pb[l];
+                r2.bofs = g.rs2_bofs[l];
+                r2.xb_m = x86() ? sse2_body_resize(r2.mw) : 0;
+                r2.xb_d = x86() ? sse2_body_resize(r2.dw) : 0;
+                if (x86())
+                    ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resize2_kernel<true>, dim3(g.rs2_tiles[l], n),
+                                 dim3(256), g.rs2_lds[l], stream, r2);
+                else
+                    ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resize2_kernel<false>, dim3(g.rs2_tiles[l], n),
+                                 dim3(256), g.rs2_lds[l], stream, r2);
+                ++l;
+                continue;
+            }
             ResizeArgs ra;
             ra.src = lp[l - 1];
             ra.dst = lp[l];

@@ -361,6 +361,142 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
     }
 }
 
+// K1, two levels per launch (1920 x 1080 and other sizes the band kernel leaves to the
+// per-level kernels): a workgroup owns a 128 x 32 tile of level l + 1.  It stages the level
+// l - 1 rows and columns its level-l region reads (16-byte chunks, as resize_kernel), makes that
+// level-l region in LDS (its own part of level l also to the pyramid: the host partitions level
+// l among the tiles by the first source row / column of each tile), then the level l + 1 tile
+// from LDS.  Level l never makes a round trip through HBM between the two launches it used to
+// take (1080p: level 1 is 369 MB per 256 frames written and read back).  The host table gives
+// each tile its computed and own level-l rectangles; both passes are resize_kernel's
+// column-group horizontal pass and resize4.
+template <bool kX86>
+__global__ __launch_bounds__(256) void resize2_kernel(Resize2Args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char r2_lds[];
+    int bx, f;
+    xcd_block(bx, f);
+    const int4 c = a.tiles[2 * bx], own = a.tiles[2 * bx + 1];
+    const int tid = threadIdx.x;
+    // level l - 1 rectangle the level-l region reads
+    const int ay0 = a.yt_m[3 * c.x], ay1 = a.yt_m[3 * c.y + 1];
+    const int ax0 = a.xt_m[3 * c.z] & ~3, ax1 = a.xt_m[3 * c.w + 1];
+    {
+        const int nrow = ay1 - ay0 + 1, cpr = ((ax1 - ax0) >> 4) + 1, total = nrow * cpr;
+        const uint8_t* src = a.src.base + f * a.src.fpitch;
+        for (int base = 0; base < total; base += 4 * 256) {
+            uint4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = base + 256 * u + tid;
+                if (i >= total) continue;
+                const int r = i / cpr, cc = i - r * cpr;
+                const uint8_t* row = src + (long long)(ay0 + r) * a.src.pitch;
+                const int x = ax0 + 16 * cc;
+                if (x + 16 <= a.sw) {
+                    v[u] = load16_a4(row + x);
+                } else {
+                    uint32_t w[4];
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) {
+                        const int xd = x + 4 * d;
+                        w[d] = 0;
+                        if (xd + 4 <= a.sw) w[d] = *reinterpret_cast<const uint32_t*>(row + xd);
+                        else
+                            for (int q = 0; q < 4 && xd + q < a.sw; ++q) w[d] |= (uint32_t)row[xd + q] << (8 * q);
+                    }
+                    v[u] = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = base + 256 * u + tid;
+                if (i >= total) continue;
+                const int r = i / cpr, cc = i - r * cpr;
+                *reinterpret_cast<uint4*>(r2_lds + r * a.pa + 16 * cc) = v[u];
+            }
+        }
+    }
+    __syncthreads();
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    // one thread per (column group, row phase): the group's table entry loaded once
+    auto hsum = [&](const unsigned char* base, int pitch, int r, int wofs, int sh, const uint32_t (&sel)[4],
+                    const us2 (&cf)[4], uint32_t (&t)[4]) {
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(base + r * pitch + wofs);
+        const uint32_t w0 = row[0], w1 = row[1], w2 = row[2];
+        const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh), hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            t[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(hi, lo, sel[k])), cf[k], 0u, false);
+    };
+    unsigned char* B = r2_lds + a.bofs;
+    {   // level l region: rows c.x .. c.y, column groups c.z / 4 .. c.w / 4
+        const int gpr = ((c.w - c.z) >> 2) + 1, rps = 256 / gpr;
+        const int gx = tid % gpr, ry = tid / gpr;
+        if (ry < rps) {
+            const int x = c.z + 4 * gx;
+            const uint4* gp = a.gtab_m + 3 * (x >> 2);
+            const uint4 g0 = gp[0], g1 = gp[1], g2 = gp[2];
+            const int xrel = (int)g0.x - ax0, wofs = (xrel >> 2) << 2, sh = xrel & 3;
+            const uint32_t sel[4] = {g0.y, g0.z, g0.w, g1.x};
+            const us2 cf[4] = {__builtin_bit_cast(us2, hcoef<kX86>(g1.y)), __builtin_bit_cast(us2, hcoef<kX86>(g1.z)),
+                               __builtin_bit_cast(us2, hcoef<kX86>(g1.w)), __builtin_bit_cast(us2, hcoef<kX86>(g2.x))};
+            const int n = min(4, a.mw - x);
+            const bool own_x = x >= own.z && x < own.w;  // own column bounds are multiples of 4
+            uint8_t* mid = const_cast<uint8_t*>(a.mid.base) + f * a.mid.fpitch;
+            for (int r = c.x + ry; r <= c.y; r += rps) {
+                const int* yy = a.yt_m + 3 * r;
+                const uint32_t b0 = (uint32_t)yy[2] & 0xffffu, b1 = (uint32_t)yy[2] >> 16;
+                uint32_t t0[4], t1[4];
+                hsum(r2_lds, a.pa, yy[0] - ay0, wofs, sh, sel, cf, t0);
+                hsum(r2_lds, a.pa, yy[1] - ay0, wofs, sh, sel, cf, t1);
+                const uint32_t packed = resize4<kX86>(t0, t1, b0, b1, x, a.xb_m);
+                *reinterpret_cast<uint32_t*>(B + (r - c.x) * a.pb + (x - c.z)) = packed;
+                if (own_x && r >= own.x && r < own.y) {
+                    uint8_t* o = mid + (long long)r * a.mid.pitch + x;
+                    if (n == 4) {
+                        *reinterpret_cast<uint32_t*>(o) = packed;
+                    } else {
+                        for (int k = 0; k < n; ++k) o[k] = (uint8_t)(packed >> (8 * k));
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    {   // level l + 1 tile from the level-l region (resize_kernel's thread layout)
+        const int tiles_x = a.tiles_x;
+        const int ox = (bx % tiles_x) * kRsTW, oy = (bx / tiles_x) * kRsTH;
+        const int tx = tid & 31, ty = tid >> 5;
+        const int x = ox + 4 * tx;
+        if (x >= a.dw) return;
+        const int n = min(4, a.dw - x);
+        const uint4* gp = a.gtab_d + 3 * (x >> 2);
+        const uint4 g0 = gp[0], g1 = gp[1], g2 = gp[2];
+        const int xrel = (int)g0.x - c.z, wofs = (xrel >> 2) << 2, sh = xrel & 3;
+        const uint32_t sel[4] = {g0.y, g0.z, g0.w, g1.x};
+        const us2 cf[4] = {__builtin_bit_cast(us2, hcoef<kX86>(g1.y)), __builtin_bit_cast(us2, hcoef<kX86>(g1.z)),
+                           __builtin_bit_cast(us2, hcoef<kX86>(g1.w)), __builtin_bit_cast(us2, hcoef<kX86>(g2.x))};
+        uint8_t* dst = const_cast<uint8_t*>(a.dst.base) + f * a.dst.fpitch;
+#pragma unroll
+        for (int j = 0; j < kRsRPT; ++j) {
+            const int y = oy + kRsRPT * ty + j;
+            if (y >= a.dh) break;
+            const int* yy = a.yt_d + 3 * y;
+            const uint32_t b0 = (uint32_t)yy[2] & 0xffffu, b1 = (uint32_t)yy[2] >> 16;
+            uint32_t t0[4], t1[4];
+            hsum(B, a.pb, yy[0] - c.x, wofs, sh, sel, cf, t0);
+            hsum(B, a.pb, yy[1] - c.x, wofs, sh, sel, cf, t1);
+            const uint32_t packed = resize4<kX86>(t0, t1, b0, b1, x, a.xb_d);
+            uint8_t* o = dst + (long long)y * a.dst.pitch + x;
+            if (n == 4) {
+                *reinterpret_cast<uint32_t*>(o) = packed;
+            } else {
+                for (int k = 0; k < n; ++k) o[k] = (uint8_t)(packed >> (8 * k));
+            }
+        }
+    }
+}
+
 // Column-pass rounding.  The sums carry 0x7fff; the scalar FixedPtCastEx (sum + 2^15) >> 16
 // adds one more, the x86 SIMD body (H6: float sum, exact below 2^24, _mm_cvtps_epi32) rounds
 // half to even: (sum + 0x7fff + bit 16 of sum) >> 16.  v = sum + 0x7fff.
@@ -3416,6 +3552,55 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
                 g.band_off[which] = (int)(g.ptab.size() / 4);  // int4 units
                 for (int v : bt[which]) g.ptab.push_back((uint32_t)v);
             }
+        }
+        // resize2_kernel plans: levels (l, l + 1) per launch, tiles of level l + 1.  Level l is
+        // partitioned among the tiles by each tile's first source row / column (columns rounded
+        // down to whole 4-column groups); a tile computes its own part plus what its level l + 1
+        // rows and columns read.
+        for (int l = 1; l + 1 < L && g.pyr_ok; ++l) {
+            const int mw = g.geo.lv[l].w, mh = g.geo.lv[l].h;
+            const int dw = g.geo.lv[l + 1].w, dh = g.geo.lv[l + 1].h;
+            const int* xm = &g.xtab[g.xoff[l]];
+            const int* ym = &g.ytab[g.yoff[l]];
+            const int* xd = &g.xtab[g.xoff[l + 1]];
+            const int* yd = &g.ytab[g.yoff[l + 1]];
+            const int ntx = (dw + kRsTW - 1) / kRsTW, nty = (dh + kRsTH - 1) / kRsTH;
+            std::vector<int> tt;
+            tt.reserve((size_t)ntx * nty * 8);
+            int arows = 0, awid = 0, brows = 0, bwid = 0, gmax = 0;
+            for (int ty = 0; ty < nty; ++ty)
+                for (int tx = 0; tx < ntx; ++tx) {
+                    const int ox = tx * kRsTW, oy = ty * kRsTH;
+                    const int ex = std::min(ox + kRsTW, dw) - 1, ey = std::min(oy + kRsTH, dh) - 1;
+                    const int oy0 = ty ? yd[3 * oy] : 0, oy1 = ty + 1 < nty ? yd[3 * (oy + kRsTH)] : mh;
+                    const int ox0 = tx ? (xd[3 * ox] & ~3) : 0;
+                    const int ox1 = tx + 1 < ntx ? (xd[3 * (ox + kRsTW)] & ~3) : mw;
+                    const int cy0 = std::min(yd[3 * oy], oy0), cy1 = std::max(yd[3 * ey + 1], oy1 - 1);
+                    const int cx0 = std::min(xd[3 * ox] & ~3, ox0);
+                    const int cx1 = std::min(mw - 1, std::max(xd[3 * std::min(ex | 3, dw - 1) + 1], ox1 - 1) | 3);
+                    tt.insert(tt.end(), {cy0, cy1, cx0, cx1, oy0, oy1, ox0, ox1});
+                    const int ay0 = ym[3 * cy0], ay1 = ym[3 * cy1 + 1];
+                    const int ax0 = xm[3 * cx0] & ~3, ax1 = xm[3 * cx1 + 1];
+                    arows = std::max(arows, ay1 - ay0 + 1);
+                    awid = std::max(awid, ax1 - ax0 + 1);
+                    brows = std::max(brows, cy1 - cy0 + 1);
+                    bwid = std::max(bwid, cx1 - cx0 + 1);
+                    gmax = std::max(gmax, ((cx1 - cx0) >> 2) + 1);
+                }
+            const int pa = ((awid + 15) & ~15) + 16, pb = ((bwid + 15) & ~15) + 16;
+            const size_t bofs = ((size_t)arows * pa + 15) & ~(size_t)15;
+            const size_t lds = bofs + (size_t)brows * pb;
+            g.rs2_ok[l] = lds <= 64 * 1024 && gmax <= 256;
+            if (!g.rs2_ok[l]) continue;
+            g.rs2_tiles_x[l] = ntx;
+            g.rs2_tiles[l] = ntx * nty;
+            g.rs2_pa[l] = pa;
+            g.rs2_pb[l] = pb;
+            g.rs2_bofs[l] = (int)bofs;
+            g.rs2_lds[l] = lds;
+            while (g.ptab.size() % 4) g.ptab.push_back(0u);
+            g.rs2_off[l] = (int)(g.ptab.size() / 4);
+            for (int v : tt) g.ptab.push_back((uint32_t)v);
         }
         // pyramid_roll_kernel plans: the same band rows (plan_bands), streamed in steps of
         // `chunk` level-0 rows.  The host runs the kernel's rule — a level's row is made in the

@@ -84,6 +84,24 @@ struct ResizeArgs {
     int lds_e;
 };
 
+// resize2_kernel: levels l and l + 1 in one launch, tiles of level l + 1 (see the kernel)
+struct Resize2Args {
+    LevelPtr src, mid, dst;             // levels l - 1, l, l + 1
+    int sw, mw, dw, dh;                 // widths of l - 1, l, l + 1; rows of l + 1
+    int tiles_x;
+    // per tile: {computed rows first, last, computed columns first, last (4-aligned start)} and
+    // {own rows [y0, y1), own columns [x0, x1)} of level l
+    const int4* tiles;
+    const int* yt_m;                    // level l's y / x tables (rows / columns of l - 1)
+    const int* xt_m;
+    const int* yt_d;                    // level l + 1's (of level l)
+    const int* xt_d;
+    const uint4* gtab_m;                // column-group tables of levels l, l + 1
+    const uint4* gtab_d;
+    int pa, pb, bofs;                   // LDS: level l - 1 rows at 0 (pitch pa), level l at bofs (pb)
+    int xb_m, xb_d;                     // x86 SIMD-body bounds of levels l, l + 1
+};
+
 struct PyrArgs {
     LevelPtr src;                  // level 0
     LevelPtr l0_copy;              // base != null: each band also writes its level-0 rows here
@@ -231,6 +249,11 @@ struct Plan {
     size_t fast_lds = 0;
     int rs_tiles_x[kMaxLevels] = {}, rs_tiles[kMaxLevels] = {}, rs_pitch[kMaxLevels] = {};
     size_t rs_lds[kMaxLevels] = {};
+    // resize2_kernel plans for the level pairs (l, l + 1): tile table offset (int4 units in ptab)
+    bool rs2_ok[kMaxLevels] = {};
+    int rs2_tiles_x[kMaxLevels] = {}, rs2_tiles[kMaxLevels] = {}, rs2_off[kMaxLevels] = {};
+    int rs2_pa[kMaxLevels] = {}, rs2_pb[kMaxLevels] = {}, rs2_bofs[kMaxLevels] = {};
+    size_t rs2_lds[kMaxLevels] = {};
     // resize_blur_kernel: staging pitch / LDS bytes, offset of its E image
     int rb_pitch[kMaxLevels] = {}, rb_lds_e[kMaxLevels] = {};
     size_t rb_lds[kMaxLevels] = {};
@@ -264,6 +287,7 @@ template <bool kX86> __global__ void resize_tail_kernel(ResizeTailArgs);
 template <bool kX86> __global__ void resize_blur_kernel(ResizeArgs);
 template <bool kX86> __global__ void pyramid_kernel(PyrArgs);
 template <bool kX86> __global__ void pyramid_roll_kernel(PyrArgs);
+template <bool kX86> __global__ void resize2_kernel(Resize2Args);
 template <int kP> __global__ void fast_kernel(FastArgs);
 constexpr int kFastPitch = 48;  // fast_kernel<kFastPitch>: ROI pitch known at compile time
 template <int BLK> __global__ void octree_kernel(OctArgs);
