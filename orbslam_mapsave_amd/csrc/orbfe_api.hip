@@ -226,6 +226,10 @@ struct orbfe_extractor {
     bool pyr_path(int n) const { return band_path(n) || roll_path(n); }  // one launch
     // ORBFE_RS2=0: one resize launch per level where resize2_kernel would take two (A/B)
     bool use_rs2 = !(std::getenv("ORBFE_RS2") && std::strcmp(std::getenv("ORBFE_RS2"), "0") == 0);
+    // ORBFE_RSN=1: chains of 3-4 levels per launch (resizeN_kernel) instead of resize2_kernel's
+    // pairs; bit-exact but measured slower at 1920 x 1080 (c4 resize 0.870 ms per 256 frames with
+    // pairs, 1.015 with chains of <= 3, 1.135 with <= 4; profiles/r04/experiments/resize_chain/)
+    bool use_rsn = std::getenv("ORBFE_RSN") && std::strcmp(std::getenv("ORBFE_RSN"), "1") == 0;
     // ORBFE_RESIZE_TABLE=0: resize_kernel's horizontal pass by byte gathers (A/B)
     bool table_off = std::getenv("ORBFE_RESIZE_TABLE") && std::strcmp(std::getenv("ORBFE_RESIZE_TABLE"), "0") == 0;
     // ORBFE_DESC_MFMA=0: describe blurs its raw windows on the VALU instead of the matrix cores
@@ -472,6 +476,36 @@ struct orbfe_extractor {
                              dim3(kPyrBlockSize), g.pyr_lds[which], stream, pa);
         }
         for (int l = 1; l < (one_pyr ? 1 : ts); ++l) {
+            // levels l .. l + n - 1 in one launch (resizeN_kernel, n = 3 or 4) where planned
+            // and ORBFE_RSN=1 (opt-in: slower than the pairs below)
+            if (use_rsn && use_rs2 && g.rsn_n[l] >= 3 && l + g.rsn_n[l] - 1 < ts && !rb && !table_off) {
+                ResizeNArgs rn;
+                const int nl = g.rsn_n[l];
+                rn.src = lp[l - 1];
+                rn.sw = g.geo.lv[l - 1].w;
+                rn.n = nl;
+                for (int k = 0; k < nl; ++k) {
+                    rn.lv[k] = lp[l + k];
+                    rn.w[k] = g.geo.lv[l + k].w;
+                    rn.yt[k] = ytab.as<int>() + g.yoff[l + k];
+                    rn.xt[k] = xtab.as<int>() + g.xoff[l + k];
+                    rn.gtab[k] = ptab.as<uint4>() + g.gtab_off[l + k];
+                    rn.xb[k] = x86() ? sse2_body_resize(rn.w[k]) : 0;
+                    rn.pitch[k] = g.rsn_pitch[l][k];
+                    rn.lofs[k] = g.rsn_lofs[l][k];
+                }
+                rn.dh = g.geo.lv[l + nl - 1].h;
+                rn.tiles_x = g.rsn_tiles_x[l];
+                rn.tiles = reinterpret_cast<const int4*>(ptab.as<uint4>() + g.rsn_off[l]);
+                if (x86())
+                    ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resizeN_kernel<true>, dim3(g.rsn_tiles[l], n),
+                                 dim3(256), g.rsn_lds[l], stream, rn);
+                else
+                    ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resizeN_kernel<false>, dim3(g.rsn_tiles[l], n),
+                                 dim3(256), g.rsn_lds[l], stream, rn);
+                l += nl - 1;
+                continue;
+            }
             // levels l and l + 1 in one launch (resize2_kernel) where planned; ORBFE_RS2=0: one
             // launch per level
             if (use_rs2 && l + 1 < ts && g.rs2_ok[l] && !rb && !table_off) {

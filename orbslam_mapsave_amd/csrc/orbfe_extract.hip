@@ -497,6 +497,154 @@ __global__ __launch_bounds__(256) void resize2_kernel(Resize2Args a) {
     }
 }
 
+// K1, three or four levels per launch (1920 x 1080): resize2_kernel's scheme carried through
+// more levels.  A workgroup owns a 128 x 32 tile of the chain's last level.  It stages the
+// level l - 1 rows and columns its first made level's region reads, makes each intermediate
+// level's region in LDS from the image before it (writing the part of that level it owns: the
+// host partitions every intermediate level among the tiles by the row / column of it that each
+// tile's first row / column reaches first), then the tile.  Two LDS regions alternate (the
+// staged level and odd made levels in one, even ones in the other), so of a chain's levels only
+// level l - 1 is read from HBM: at 1080p the chains (1-4) (5-7) read levels 0 and 4 instead of
+// resize2's 0, 2, 4 and 6.  Bit-exact, but slower than the pairs (a workgroup's phases run
+// one after another behind its barriers, and the larger LDS leaves fewer workgroups per CU to
+// overlap them): opt-in, ORBFE_RSN=1.
+template <bool kX86>
+__global__ __launch_bounds__(256) void resizeN_kernel(ResizeNArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char rn_lds[];
+    int bx, f;
+    xcd_block(bx, f);
+    const int nm = a.n - 1;  // levels made region by region before the tile
+    const int4* tt = a.tiles + (size_t)bx * 2 * nm;
+    const int tid = threadIdx.x;
+    int sy, sx;  // level coordinates of the current source image's first row / column
+    {
+        const int4 c = tt[0];
+        sy = a.yt[0][3 * c.x];
+        sx = a.xt[0][3 * c.z] & ~3;
+        const int ay1 = a.yt[0][3 * c.y + 1], ax1 = a.xt[0][3 * c.w + 1];
+        const int nrow = ay1 - sy + 1, cpr = ((ax1 - sx) >> 4) + 1, total = nrow * cpr;
+        const uint8_t* src = a.src.base + f * a.src.fpitch;
+        unsigned char* img = rn_lds + a.lofs[0];
+        for (int base = 0; base < total; base += 4 * 256) {
+            uint4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = base + 256 * u + tid;
+                if (i >= total) continue;
+                const int r = i / cpr, cc = i - r * cpr;
+                const uint8_t* row = src + (long long)(sy + r) * a.src.pitch;
+                const int x = sx + 16 * cc;
+                if (x + 16 <= a.sw) {
+                    v[u] = load16_a4(row + x);
+                } else {
+                    uint32_t w[4];
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) {
+                        const int xd = x + 4 * d;
+                        w[d] = 0;
+                        if (xd + 4 <= a.sw) w[d] = *reinterpret_cast<const uint32_t*>(row + xd);
+                        else
+                            for (int q = 0; q < 4 && xd + q < a.sw; ++q) w[d] |= (uint32_t)row[xd + q] << (8 * q);
+                    }
+                    v[u] = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = base + 256 * u + tid;
+                if (i >= total) continue;
+                const int r = i / cpr, cc = i - r * cpr;
+                *reinterpret_cast<uint4*>(img + r * a.pitch[0] + 16 * cc) = v[u];
+            }
+        }
+    }
+    __syncthreads();
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    auto hsum = [&](const unsigned char* base, int pitch, int r, int wofs, int sh, const uint32_t (&sel)[4],
+                    const us2 (&cf)[4], uint32_t (&t)[4]) {
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(base + r * pitch + wofs);
+        const uint32_t w0 = row[0], w1 = row[1], w2 = row[2];
+        const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh), hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            t[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(hi, lo, sel[k])), cf[k], 0u, false);
+    };
+    for (int k = 0; k < nm; ++k) {  // level k's region: rows c.x .. c.y, column groups c.z / 4 .. c.w / 4
+        const int4 c = tt[2 * k], own = tt[2 * k + 1];
+        const unsigned char* S = rn_lds + a.lofs[k];
+        unsigned char* D = rn_lds + a.lofs[k + 1];
+        const int sp = a.pitch[k], dp = a.pitch[k + 1];
+        const int gpr = ((c.w - c.z) >> 2) + 1, rps = 256 / gpr;
+        const int gx = tid % gpr, ry = tid / gpr;
+        if (ry < rps) {
+            const int x = c.z + 4 * gx;
+            const uint4* gp = a.gtab[k] + 3 * (x >> 2);
+            const uint4 g0 = gp[0], g1 = gp[1], g2 = gp[2];
+            const int xrel = (int)g0.x - sx, wofs = (xrel >> 2) << 2, sh = xrel & 3;
+            const uint32_t sel[4] = {g0.y, g0.z, g0.w, g1.x};
+            const us2 cf[4] = {__builtin_bit_cast(us2, hcoef<kX86>(g1.y)), __builtin_bit_cast(us2, hcoef<kX86>(g1.z)),
+                               __builtin_bit_cast(us2, hcoef<kX86>(g1.w)), __builtin_bit_cast(us2, hcoef<kX86>(g2.x))};
+            const int n = min(4, a.w[k] - x);
+            const bool own_x = x >= own.z && x < own.w;  // own column bounds are multiples of 4
+            uint8_t* mid = const_cast<uint8_t*>(a.lv[k].base) + f * a.lv[k].fpitch;
+            const int* ytk = a.yt[k];
+            for (int r = c.x + ry; r <= c.y; r += rps) {
+                const int* yy = ytk + 3 * r;
+                const uint32_t b0 = (uint32_t)yy[2] & 0xffffu, b1 = (uint32_t)yy[2] >> 16;
+                uint32_t t0[4], t1[4];
+                hsum(S, sp, yy[0] - sy, wofs, sh, sel, cf, t0);
+                hsum(S, sp, yy[1] - sy, wofs, sh, sel, cf, t1);
+                const uint32_t packed = resize4<kX86>(t0, t1, b0, b1, x, a.xb[k]);
+                *reinterpret_cast<uint32_t*>(D + (r - c.x) * dp + (x - c.z)) = packed;
+                if (own_x && r >= own.x && r < own.y) {
+                    uint8_t* o = mid + (long long)r * a.lv[k].pitch + x;
+                    if (n == 4) {
+                        *reinterpret_cast<uint32_t*>(o) = packed;
+                    } else {
+                        for (int q = 0; q < n; ++q) o[q] = (uint8_t)(packed >> (8 * q));
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        sy = c.x;
+        sx = c.z;
+    }
+    {   // the tile of the last level (resize_kernel's thread layout)
+        const unsigned char* S = rn_lds + a.lofs[nm];
+        const int sp = a.pitch[nm], dw = a.w[nm];
+        const int ox = (bx % a.tiles_x) * kRsTW, oy = (bx / a.tiles_x) * kRsTH;
+        const int tx = tid & 31, ty = tid >> 5;
+        const int x = ox + 4 * tx;
+        if (x >= dw) return;
+        const int n = min(4, dw - x);
+        const uint4* gp = a.gtab[nm] + 3 * (x >> 2);
+        const uint4 g0 = gp[0], g1 = gp[1], g2 = gp[2];
+        const int xrel = (int)g0.x - sx, wofs = (xrel >> 2) << 2, sh = xrel & 3;
+        const uint32_t sel[4] = {g0.y, g0.z, g0.w, g1.x};
+        const us2 cf[4] = {__builtin_bit_cast(us2, hcoef<kX86>(g1.y)), __builtin_bit_cast(us2, hcoef<kX86>(g1.z)),
+                           __builtin_bit_cast(us2, hcoef<kX86>(g1.w)), __builtin_bit_cast(us2, hcoef<kX86>(g2.x))};
+        uint8_t* dst = const_cast<uint8_t*>(a.lv[nm].base) + f * a.lv[nm].fpitch;
+#pragma unroll
+        for (int j = 0; j < kRsRPT; ++j) {
+            const int y = oy + kRsRPT * ty + j;
+            if (y >= a.dh) break;
+            const int* yy = a.yt[nm] + 3 * y;
+            const uint32_t b0 = (uint32_t)yy[2] & 0xffffu, b1 = (uint32_t)yy[2] >> 16;
+            uint32_t t0[4], t1[4];
+            hsum(S, sp, yy[0] - sy, wofs, sh, sel, cf, t0);
+            hsum(S, sp, yy[1] - sy, wofs, sh, sel, cf, t1);
+            const uint32_t packed = resize4<kX86>(t0, t1, b0, b1, x, a.xb[nm]);
+            uint8_t* o = dst + (long long)y * a.lv[nm].pitch + x;
+            if (n == 4) {
+                *reinterpret_cast<uint32_t*>(o) = packed;
+            } else {
+                for (int q = 0; q < n; ++q) o[q] = (uint8_t)(packed >> (8 * q));
+            }
+        }
+    }
+}
+
 // Column-pass rounding.  The sums carry 0x7fff; the scalar FixedPtCastEx (sum + 2^15) >> 16
 // adds one more, the x86 SIMD body (H6: float sum, exact below 2^24, _mm_cvtps_epi32) rounds
 // half to even: (sum + 0x7fff + bit 16 of sum) >> 16.  v = sum + 0x7fff.
@@ -3601,6 +3749,79 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
             while (g.ptab.size() % 4) g.ptab.push_back(0u);
             g.rs2_off[l] = (int)(g.ptab.size() / 4);
             for (int v : tt) g.ptab.push_back((uint32_t)v);
+        }
+        // resizeN_kernel plans: chains of n = 4 (else 3) levels l .. l + n - 1, tiles of the last.
+        // F_k(y) = the row of made level k that the last level's row y reaches first (through
+        // each level's first source row); level k is partitioned among the tiles by F_k of their
+        // first rows (columns likewise, in whole 4-column groups).  A tile computes, level by
+        // level downwards, its own part plus what the level above it reads.
+        for (int l = 0; l < kMaxLevels; ++l) g.rsn_n[l] = 0;
+        const char* rsn_max = std::getenv("ORBFE_RSN_MAX");  // longest chain planned (A/B)
+        const int nmax = rsn_max ? std::max(3, std::min(kRsNMax, std::atoi(rsn_max))) : kRsNMax;
+        for (int l = 1; l + 2 < L && g.pyr_ok; ++l) {
+            for (int n = std::min(nmax, L - l); n >= 3 && g.rsn_n[l] == 0; --n) {
+                const int last = l + n - 1;
+                const int dw = g.geo.lv[last].w, dh = g.geo.lv[last].h;
+                const int ntx = (dw + kRsTW - 1) / kRsTW, nty = (dh + kRsTH - 1) / kRsTH;
+                auto Y = [&](int k) { return &g.ytab[g.yoff[l + k]]; };  // made level k's tables
+                auto X = [&](int k) { return &g.xtab[g.xoff[l + k]]; };
+                auto Fy = [&](int k, int y) {  // row of level k (< n - 1) that last-level row y reaches
+                    for (int j = n - 1; j > k; --j) y = Y(j)[3 * y];
+                    return y;
+                };
+                auto Fx = [&](int k, int x) {
+                    for (int j = n - 1; j > k; --j) x = X(j)[3 * x] & ~3;
+                    return x;
+                };
+                std::vector<int> tt;
+                tt.reserve((size_t)ntx * nty * 8 * (n - 1));
+                int rows[kRsNMax] = {}, wid[kRsNMax] = {}, gmax = 0;  // image k: staged (0), made k - 1
+                std::vector<int> one(8 * (n - 1));
+                for (int ty = 0; ty < nty; ++ty)
+                    for (int tx = 0; tx < ntx; ++tx) {
+                        const int ox = tx * kRsTW, oy = ty * kRsTH;
+                        const int ex = std::min(ox + kRsTW, dw) - 1, ey = std::min(oy + kRsTH, dh) - 1;
+                        const int exg = std::min(ex | 3, dw - 1);
+                        int r0 = Y(n - 1)[3 * oy], r1 = Y(n - 1)[3 * ey + 1];
+                        int c0 = X(n - 1)[3 * ox] & ~3, c1 = X(n - 1)[3 * exg + 1];
+                        for (int k = n - 2; k >= 0; --k) {
+                            const int mw = g.geo.lv[l + k].w, mh = g.geo.lv[l + k].h;
+                            const int oy0 = ty ? Fy(k, oy) : 0, oy1 = ty + 1 < nty ? Fy(k, oy + kRsTH) : mh;
+                            const int ox0 = tx ? Fx(k, ox) : 0, ox1 = tx + 1 < ntx ? Fx(k, ox + kRsTW) : mw;
+                            const int cy0 = std::min(r0, oy0), cy1 = std::max(r1, oy1 - 1);
+                            const int cx0 = std::min(c0, ox0);
+                            const int cx1 = std::min(mw - 1, std::max(c1, ox1 - 1) | 3);
+                            const int v[8] = {cy0, cy1, cx0, cx1, oy0, oy1, ox0, ox1};
+                            std::copy(v, v + 8, one.begin() + 8 * k);
+                            rows[k + 1] = std::max(rows[k + 1], cy1 - cy0 + 1);
+                            wid[k + 1] = std::max(wid[k + 1], cx1 - cx0 + 1);
+                            gmax = std::max(gmax, ((cx1 - cx0) >> 2) + 1);
+                            r0 = Y(k)[3 * cy0];
+                            r1 = Y(k)[3 * cy1 + 1];
+                            c0 = X(k)[3 * cx0] & ~3;
+                            c1 = X(k)[3 * cx1 + 1];
+                        }
+                        rows[0] = std::max(rows[0], r1 - r0 + 1);
+                        wid[0] = std::max(wid[0], c1 - c0 + 1);
+                        tt.insert(tt.end(), one.begin(), one.end());
+                    }
+                size_t reg[2] = {0, 0};
+                for (int k = 0; k < n; ++k) {
+                    g.rsn_pitch[l][k] = ((wid[k] + 15) & ~15) + 16;
+                    reg[k & 1] = std::max(reg[k & 1], (size_t)rows[k] * g.rsn_pitch[l][k]);
+                }
+                reg[0] = (reg[0] + 15) & ~(size_t)15;
+                for (int k = 0; k < n; ++k) g.rsn_lofs[l][k] = (k & 1) ? (int)reg[0] : 0;
+                const size_t lds = reg[0] + reg[1];
+                if (lds > 64 * 1024 || gmax > 256) continue;
+                g.rsn_n[l] = n;
+                g.rsn_tiles_x[l] = ntx;
+                g.rsn_tiles[l] = ntx * nty;
+                g.rsn_lds[l] = lds;
+                while (g.ptab.size() % 4) g.ptab.push_back(0u);
+                g.rsn_off[l] = (int)(g.ptab.size() / 4);
+                for (int v : tt) g.ptab.push_back((uint32_t)v);
+            }
         }
         // pyramid_roll_kernel plans: the same band rows (plan_bands), streamed in steps of
         // `chunk` level-0 rows.  The host runs the kernel's rule — a level's row is made in the

@@ -102,6 +102,28 @@ struct Resize2Args {
     int xb_m, xb_d;                     // x86 SIMD-body bounds of levels l, l + 1
 };
 
+// resizeN_kernel: levels l .. l + n - 1 in one launch (n = 3 or 4), tiles of the last level;
+// the n - 1 levels before it are made in LDS region by region (see the kernel)
+constexpr int kRsNMax = 4;
+struct ResizeNArgs {
+    LevelPtr src;                       // level l - 1 (staged)
+    int sw;                             // its width
+    int n;                              // levels made
+    LevelPtr lv[kRsNMax];               // levels l .. l + n - 1
+    int w[kRsNMax];
+    int dh;                             // rows of the last level
+    const int* yt[kRsNMax];             // each made level's y / x tables (rows / columns of the level below)
+    const int* xt[kRsNMax];
+    const uint4* gtab[kRsNMax];         // column-group tables
+    int xb[kRsNMax];                    // x86 SIMD-body bounds
+    int pitch[kRsNMax];                 // LDS pitch of the staged level (index 0 .. n - 1: made
+    int lofs[kRsNMax];                  // level k - 1 at lofs[k]; index 0 = the staged level)
+    int tiles_x;
+    // per tile, per level k < n - 1: {computed rows first, last, columns first, last (4-aligned
+    // start)} and {own rows [y0, y1), own columns [x0, x1)}
+    const int4* tiles;
+};
+
 struct PyrArgs {
     LevelPtr src;                  // level 0
     LevelPtr l0_copy;              // base != null: each band also writes its level-0 rows here
@@ -254,6 +276,11 @@ struct Plan {
     int rs2_tiles_x[kMaxLevels] = {}, rs2_tiles[kMaxLevels] = {}, rs2_off[kMaxLevels] = {};
     int rs2_pa[kMaxLevels] = {}, rs2_pb[kMaxLevels] = {}, rs2_bofs[kMaxLevels] = {};
     size_t rs2_lds[kMaxLevels] = {};
+    // resizeN_kernel chains starting at level l: levels made (0 = none), tiles, table, LDS
+    int rsn_n[kMaxLevels] = {};
+    int rsn_tiles_x[kMaxLevels] = {}, rsn_tiles[kMaxLevels] = {}, rsn_off[kMaxLevels] = {};
+    int rsn_pitch[kMaxLevels][kRsNMax] = {}, rsn_lofs[kMaxLevels][kRsNMax] = {};
+    size_t rsn_lds[kMaxLevels] = {};
     // resize_blur_kernel: staging pitch / LDS bytes, offset of its E image
     int rb_pitch[kMaxLevels] = {}, rb_lds_e[kMaxLevels] = {};
     size_t rb_lds[kMaxLevels] = {};
@@ -288,6 +315,7 @@ template <bool kX86> __global__ void resize_blur_kernel(ResizeArgs);
 template <bool kX86> __global__ void pyramid_kernel(PyrArgs);
 template <bool kX86> __global__ void pyramid_roll_kernel(PyrArgs);
 template <bool kX86> __global__ void resize2_kernel(Resize2Args);
+template <bool kX86> __global__ void resizeN_kernel(ResizeNArgs);
 template <int kP> __global__ void fast_kernel(FastArgs);
 constexpr int kFastPitch = 48;  // fast_kernel<kFastPitch>: ROI pitch known at compile time
 template <int BLK> __global__ void octree_kernel(OctArgs);

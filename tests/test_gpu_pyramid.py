@@ -144,14 +144,17 @@ def test_per_level_path_identical(monkeypatch):
 
 @pytest.mark.parametrize("size", [(640, 480), (1920, 1080), (643, 481), (97, 73)])
 @pytest.mark.parametrize("arith", ["scalar", "x86"])
-@pytest.mark.parametrize("table", ["1", "0"])
-def test_per_level_kernels_exact(size, arith, table, monkeypatch):
-    """The per-level path (ORBFE_PYR=0; the default at 1920x1080): resize_kernel's horizontal
-    pass from the column-group table (default) or by byte gathers (ORBFE_RESIZE_TABLE=0), and
-    the one-workgroup tail for batches, every level byte-exact in both readings."""
+@pytest.mark.parametrize("table,chain", [("1", "1"), ("1", "0"), ("0", "1")])
+def test_per_level_kernels_exact(size, arith, table, chain, monkeypatch):
+    """The per-level path (ORBFE_PYR=0; the default at 1920x1080): level pairs per launch
+    (resize2_kernel, default) or chains of 3-4 levels (resizeN_kernel, ORBFE_RSN=1, opt-in),
+    both on the column-group tables; resize_kernel's horizontal pass by byte gathers
+    (ORBFE_RESIZE_TABLE=0); the one-workgroup tail for batches; every level byte-exact in both
+    readings."""
     from orbslam_mapsave_amd.native import ORBextractor
     monkeypatch.setenv("ORBFE_PYR", "0")
     monkeypatch.setenv("ORBFE_RESIZE_TABLE", table)
+    monkeypatch.setenv("ORBFE_RSN", chain)
     w, h = size
     nf = 2000 if w > 1000 else 1000
     p = oracle.params(nf, 1.2, 8, 20, 7)
