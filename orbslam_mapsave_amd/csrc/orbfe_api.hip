@@ -243,6 +243,7 @@ struct orbfe_extractor {
     int num_cus = 256;  // compute units of the device (launch-shape choices)
     // ORBFE_OCT_SMALL=0: small batches keep the 256-thread oct-tree (A/B)
     bool oct_small = !(std::getenv("ORBFE_OCT_SMALL") && std::strcmp(std::getenv("ORBFE_OCT_SMALL"), "0") == 0);
+    int desc_g16 = std::getenv("ORBFE_DESC_G16") ? std::atoi(std::getenv("ORBFE_DESC_G16")) : -1;
     bool graph_broken = std::getenv("ORBFE_NO_GRAPH") != nullptr;  // capture failed once (or
                                  // disabled for A/B runs): keep to the launch path
 
@@ -696,17 +697,23 @@ struct orbfe_extractor {
         // a wave takes kDescGroupSize keypoints (the trig and pattern loads amortised over the
         // group); small batches take kDescGroupSmall, for four times the waves in flight
         // (x86 arithmetic: the rotation FMA-contracted, kFma)
-        const int group = n >= kDescSmallBatch ? kDescGroupSize : kDescGroupSmall;
+        // window source: every level pre-blurred, some levels pre-blurred (VALU blur for the
+        // rest), or none (the matrix-core blur unless ORBFE_DESC_MFMA=0)
+        const int win = all_pre ? kWinPre : (da.pre_mask == 0u && desc_mfma ? kWinMfma : kWinValu);
+        // 16 keypoints per wave in strided x86 matrix-core batches of frames below 1 Mpx (where
+        // the oct-tree's band order is off): c3 describe -0.9 %, +0.8 % frames/s; at 1080p the
+        // longer runs cost L2 reuse (describe +9 %; profiles/r04/experiments/describe_g16/).
+        // ORBFE_DESC_G16=0: never, =1: at every size
+        const bool g16 = (desc_g16 == 1 || (desc_g16 < 0 && !banded)) && n >= kDescSmallBatch &&
+                         desc_stride && x86() && win == kWinMfma;
+        const int group = g16 ? 16 : n >= kDescSmallBatch ? kDescGroupSize : kDescGroupSmall;
         const int per_block = (kDescBlockSize / 64) * group;  // slots per workgroup
         const dim3 dgrid((g.geo.out_total + per_block - 1) / per_block, n);
         // batches: strided slots (a frame's waves sweep its oct-tree output in runs of W
         // consecutive slots, sharing window lines in L2); ORBFE_DESC_STRIDE=0: grouped slots
-        da.wave_stride = group == kDescGroupSize && desc_stride ? (int)dgrid.x * (kDescBlockSize / 64) : 0;
-        // window source: every level pre-blurred, some levels pre-blurred (VALU blur for the
-        // rest), or none (the matrix-core blur unless ORBFE_DESC_MFMA=0)
-        const int win = all_pre ? kWinPre : (da.pre_mask == 0u && desc_mfma ? kWinMfma : kWinValu);
+        da.wave_stride = (group == kDescGroupSize || g16) && desc_stride ? (int)dgrid.x * (kDescBlockSize / 64) : 0;
         da.frags = bslot.as<uint4>() + kDescFragOff;
-        const int variant = (group == kDescGroupSize ? 6 : 0) + (x86() ? 3 : 0) + win;
+        const int variant = g16 ? 12 : (group == kDescGroupSize ? 6 : 0) + (x86() ? 3 : 0) + win;
         switch (variant) {
 #define ORBFE_DESC_CASE(V, G, X, W) \
             case V: ORBFE_LAUNCH(prof, ORBFE_STAGE_DESCRIBE, (describe_kernel<G, X, W>), dgrid, dim3(kDescBlockSize), 0, stream, da); break;
@@ -722,6 +729,7 @@ struct orbfe_extractor {
             ORBFE_DESC_CASE(9, kDescGroupSize, true, kWinValu)
             ORBFE_DESC_CASE(10, kDescGroupSize, true, kWinPre)
             ORBFE_DESC_CASE(11, kDescGroupSize, true, kWinMfma)
+            ORBFE_DESC_CASE(12, 16, true, kWinMfma)
 #undef ORBFE_DESC_CASE
         }
         ORBFE_HIP(hipGetLastError());
