@@ -243,7 +243,7 @@ struct orbfe_extractor {
     int num_cus = 256;  // compute units of the device (launch-shape choices)
     // ORBFE_OCT_SMALL=0: small batches keep the 256-thread oct-tree (A/B)
     bool oct_small = !(std::getenv("ORBFE_OCT_SMALL") && std::strcmp(std::getenv("ORBFE_OCT_SMALL"), "0") == 0);
-    int desc_g16 = std::getenv("ORBFE_DESC_G16") ? std::atoi(std::getenv("ORBFE_DESC_G16")) : -1;
+    int desc_g16 = std::getenv("ORBFE_DESC_G16") ? std::atoi(std::getenv("ORBFE_DESC_G16")) : 0;
     bool graph_broken = std::getenv("ORBFE_NO_GRAPH") != nullptr;  // capture failed once (or
                                  // disabled for A/B runs): keep to the launch path
 
@@ -700,12 +700,11 @@ struct orbfe_extractor {
         // window source: every level pre-blurred, some levels pre-blurred (VALU blur for the
         // rest), or none (the matrix-core blur unless ORBFE_DESC_MFMA=0)
         const int win = all_pre ? kWinPre : (da.pre_mask == 0u && desc_mfma ? kWinMfma : kWinValu);
-        // 16 keypoints per wave in strided x86 matrix-core batches of frames below 1 Mpx (where
-        // the oct-tree's band order is off): c3 describe -0.9 %, +0.8 % frames/s; at 1080p the
-        // longer runs cost L2 reuse (describe +9 %; profiles/r04/experiments/describe_g16/).
-        // ORBFE_DESC_G16=0: never, =1: at every size
-        const bool g16 = (desc_g16 == 1 || (desc_g16 < 0 && !banded)) && n >= kDescSmallBatch &&
-                         desc_stride && x86() && win == kWinMfma;
+        // ORBFE_DESC_G16=1 (opt-in): 16 keypoints per wave in strided x86 matrix-core batches.
+        // At 640 x 480 describe runs 2 % faster (c3 +1.3 % frames/s) but moves 1.30 GB per
+        // 512-frame launch instead of 0.70 (1.65x its algorithmic bytes: the frames in flight
+        // per XCD double); at 1080p it is 9 % slower (profiles/r04/experiments/describe_g16/)
+        const bool g16 = desc_g16 == 1 && n >= kDescSmallBatch && desc_stride && x86() && win == kWinMfma;
         const int group = g16 ? 16 : n >= kDescSmallBatch ? kDescGroupSize : kDescGroupSmall;
         const int per_block = (kDescBlockSize / 64) * group;  // slots per workgroup
         const dim3 dgrid((g.geo.out_total + per_block - 1) / per_block, n);
