@@ -89,15 +89,18 @@ def test_batch_matches_single(ex, p):
         assert np.array_equal(desc[f, :cnt[f]], odesc)
 
 
-@pytest.mark.parametrize("order,stride", [("0", "1"), ("1", "1"), ("2", "1"), ("2", "0")])
-def test_describe_slot_orders(p, order, stride, monkeypatch):
+@pytest.mark.parametrize("order,stride,g16", [("0", "1", "0"), ("1", "1", "0"), ("2", "1", "0"), ("2", "0", "0"),
+                                            ("1", "1", "1"), ("2", "1", "1")])
+def test_describe_slot_orders(p, order, stride, g16, monkeypatch):
     """describe's wave-to-keypoint assignment in batches (>= 8 frames): strided slots in the
     oct-tree's output order (ORBFE_DESC_ORDER=0), in its 32-row band order (2: at every size;
     1, the default: frames of >= 1 Mpx only) or grouped slots (ORBFE_DESC_STRIDE=0, the band
-    order then unused) — the processing order never changes the outputs or their order."""
+    order then unused), 8 or 16 (ORBFE_DESC_G16=1) keypoints per wave — the processing order
+    never changes the outputs or their order."""
     from orbslam_mapsave_amd.native import ORBextractor
     monkeypatch.setenv("ORBFE_DESC_ORDER", order)
     monkeypatch.setenv("ORBFE_DESC_STRIDE", stride)
+    monkeypatch.setenv("ORBFE_DESC_G16", g16)
     e = ORBextractor(1000, 1.2, 8, 32, 7, device=0, max_width=640, max_height=480)
     try:
         imgs = np.stack([synthetic_frame(40 + s, 640, 480) for s in range(9)])
