@@ -333,9 +333,34 @@ struct BfLaneF {
         tb = ts = kBfNoneF;
     }
 };
-__global__ __launch_bounds__(kBfBlock, ORBFE_BF_WAVES) void bf_match_fp4_kernel(
+// A reference set shared by every batch entry (r_pitch 0: config 3's one reference frame) is
+// expanded to FP4 fragments once per call by bf_expand_kernel, in the LDS tile layout
+// E[tile][descriptor dword][row]; the brute force (kPre) then copies each tile with 16-byte loads
+// instead of every workgroup expanding the same bits (a third of its VALU in the MFMA gaps).
+// Rows at or past nr are zero, as the in-kernel expansion pads them.
+constexpr int kBfMaxTiles = (kBfMaxRefs + kBfRefs) / kBfRefs;
+__global__ __launch_bounds__(512) void bf_expand_kernel(const uint8_t* r, const int* nr_arr, int nb,
+                                                        i32x4* E) {
+    __shared__ int s_nr;
+    if (threadIdx.x == 0) s_nr = 0;
+    __syncthreads();
+    int m = 0;
+    for (int b = threadIdx.x; b < nb; b += 512) m = max(m, nr_arr[b]);
+    if (m) atomicMax(&s_nr, m);
+    __syncthreads();
+    const int nr = min(s_nr, kBfMaxRefs);
+    const int t = blockIdx.x;
+    if (t * kBfRefs >= nr) return;
+    const int row = threadIdx.x & 63, dw = threadIdx.x >> 6;  // 8 dwords x 64 rows
+    const int j = t * kBfRefs + row;
+    const uint32_t w = j < nr ? reinterpret_cast<const uint32_t*>(r + (long long)j * 32)[dw] : 0u;
+    E[((size_t)t * 8 + dw) * kBfRefs + row] = ref_fp4(w);
+}
+
+template <bool kPre>
+__device__ __forceinline__ void bf_fp4_body(
     const uint8_t* q, long long q_pitch, const int* nq_arr, int nq_cap, const uint8_t* r,
-    long long r_pitch, const int* nr_arr, int* out) {
+    long long r_pitch, const int* nr_arr, int* out, const i32x4* E) {
     __shared__ i32x4 tile[2][8][kBfRefs];  // [buffer][descriptor dword][row]
     const int b = blockIdx.y;
     const int nq = min(nq_arr[b], nq_cap);
@@ -378,6 +403,13 @@ __global__ __launch_bounds__(kBfBlock, ORBFE_BF_WAVES) void bf_match_fp4_kernel(
     }
     const int lrow = tid & 63, lcp = tid >> 6;
     struct Raw { uint32_t w[kBfWords]; };
+    struct RawE { i32x4 v[kBfWords]; };
+    auto fetch_e = [&](int t) {  // kPre: this thread's kBfWords expanded entries of tile t
+        RawE v;
+#pragma unroll
+        for (int j = 0; j < kBfWords; ++j) v.v[j] = E[((size_t)t * 8 + kBfWords * lcp + j) * kBfRefs + lrow];
+        return v;
+    };
     auto fetch = [&](int t) {
         const int j = t * kBfRefs + lrow;
         const uint32_t* src = reinterpret_cast<const uint32_t*>(
@@ -394,12 +426,27 @@ __global__ __launch_bounds__(kBfBlock, ORBFE_BF_WAVES) void bf_match_fp4_kernel(
     };
     const int nfull = nr / kBfRefs, ntiles = (nr + kBfRefs - 1) / kBfRefs;
     if (nr) {
-        const Raw v = fetch(0);
+        if constexpr (kPre) {
+            const RawE v = fetch_e(0);
 #pragma unroll
-        for (int j = 0; j < kBfWords; ++j) tile[0][kBfWords * lcp + j][lrow] = ref_fp4(v.w[j]);
+            for (int j = 0; j < kBfWords; ++j) tile[0][kBfWords * lcp + j][lrow] = v.v[j];
+        } else {
+            const Raw v = fetch(0);
+#pragma unroll
+            for (int j = 0; j < kBfWords; ++j) tile[0][kBfWords * lcp + j][lrow] = ref_fp4(v.w[j]);
+        }
     }
     __syncthreads();
-    Raw raw = fetch(1);
+    using RawT = std::conditional_t<kPre, RawE, Raw>;
+    auto fetch_any = [&](int t) -> RawT {
+        if constexpr (kPre) {
+            // tiles past the last are stored to the ring but never read: fetch tile 0 for them
+            return fetch_e(t * kBfRefs < nr ? t : 0);
+        } else {
+            return fetch(t);
+        }
+    };
+    RawT raw = fetch_any(1);
     f32x16 accp;
 #pragma unroll
     for (int e = 0; e < 16; ++e) accp[e] = kBfNoneF;
@@ -407,7 +454,7 @@ __global__ __launch_bounds__(kBfBlock, ORBFE_BF_WAVES) void bf_match_fp4_kernel(
     auto step = [&](int t, auto partial_tag) {
         constexpr bool partial = decltype(partial_tag)::value;
         const int cur = t & 1;
-        const Raw raw2 = fetch(t + 2);
+        const RawT raw2 = fetch_any(t + 2);
         const int valid = nr - t * kBfRefs - 4 * h;
         // fragment ring, two reads ahead: fragment f = 4 p + c is chunk c of m-tile p & 1
         auto frag = [&](int f) { return tile[cur][2 * (f & 3) + h][32 * ((f >> 2) & 1) + col]; };
@@ -434,8 +481,12 @@ __global__ __launch_bounds__(kBfBlock, ORBFE_BF_WAVES) void bf_match_fp4_kernel(
                     st[pnt].push(k);
                 }
                 // next tile's expansion: word f / 8 of this thread's kBfWords at gap f % 8 == 7
-                if (f % 8 == 7 && (f >> 3) < kBfWords)
-                    tile[cur ^ 1][kBfWords * lcp + (f >> 3)][lrow] = ref_fp4(raw.w[f >> 3]);
+                if (f % 8 == 7 && (f >> 3) < kBfWords) {
+                    if constexpr (kPre)
+                        tile[cur ^ 1][kBfWords * lcp + (f >> 3)][lrow] = raw.v[f >> 3];
+                    else
+                        tile[cur ^ 1][kBfWords * lcp + (f >> 3)][lrow] = ref_fp4(raw.w[f >> 3]);
+                }
                 a = a1;
                 a1 = a2;
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // fragment read, 2 ahead
@@ -476,6 +527,18 @@ __global__ __launch_bounds__(kBfBlock, ORBFE_BF_WAVES) void bf_match_fp4_kernel(
         o[1] = db;
         o[2] = (ks >> 16) + pc;
     }
+}
+
+__global__ __launch_bounds__(kBfBlock, ORBFE_BF_WAVES) void bf_match_fp4_kernel(
+    const uint8_t* q, long long q_pitch, const int* nq_arr, int nq_cap, const uint8_t* r,
+    long long r_pitch, const int* nr_arr, int* out) {
+    bf_fp4_body<false>(q, q_pitch, nq_arr, nq_cap, r, r_pitch, nr_arr, out, nullptr);
+}
+// the same with the shared reference set pre-expanded (bf_expand_kernel)
+__global__ __launch_bounds__(kBfBlock, ORBFE_BF_WAVES) void bf_match_fp4e_kernel(
+    const uint8_t* q, long long q_pitch, const int* nq_arr, int nq_cap, const uint8_t* r,
+    long long r_pitch, const int* nr_arr, int* out, const i32x4* E) {
+    bf_fp4_body<true>(q, q_pitch, nq_arr, nq_cap, r, r_pitch, nr_arr, out, E);
 }
 
 // The brute-force kernel the ABI launches: the FP4 form, or the i8 form (the measured

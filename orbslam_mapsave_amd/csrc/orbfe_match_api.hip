@@ -2,6 +2,7 @@
 // Every call uploads the flat SoA views, runs the kernels of orbfe_match.hip on the matcher's
 // stream and downloads the results (synchronous, like the reference's member functions).
 #include <hip/hip_runtime.h>
+#include <map>
 
 #include <algorithm>
 #include <climits>
@@ -76,6 +77,12 @@ struct orbfe_matcher {
     // ORBFE_ZERO_COPY=0: uploads and downloads as DMA copies (the staging buffer unmapped)
     bool zero_copy_off = std::getenv("ORBFE_ZERO_COPY") && std::strcmp(std::getenv("ORBFE_ZERO_COPY"), "0") == 0;
     BfKernel bf_kernel = bf_match_fp4_kernel;  // ORBFE_BF_I8=1 at creation: bf_match_kernel
+    // ORBFE_BF_PRE=1: a reference set shared by the whole batch is expanded to FP4 fragments
+    // once per call (bf_expand_kernel) instead of by every workgroup (A/B)
+    bool bf_pre = std::getenv("ORBFE_BF_PRE") && std::strcmp(std::getenv("ORBFE_BF_PRE"), "1") == 0;
+    // the shared reference set as FP4 fragments (bf_expand_kernel), one buffer per stream the
+    // batch form was called on (calls on different streams may overlap)
+    std::map<hipStream_t, DevBuf> bf_e;
 
     ~orbfe_matcher() {
         for (DevBuf* b : {&fa_k, &fa_d, &fa_ur, &fa_cs, &fa_ci, &fa_co, &fb_k, &fb_d, &fb_ur,
@@ -84,6 +91,7 @@ struct orbfe_matcher {
                           &m_i0, &m_i1, &m_d, &o_u, &o_f0, &o_f1, &o_f2, &o_f3, &o_i, &scal,
                           &g_t0, &g_t1, &g_t2, &g_dec, &g_chg, &g_last, &g_bins, &g_hist, &done_ctr})
             b->release();
+        for (auto& kv : bf_e) kv.second.release();
         prof.release();
         if (own) hipStreamDestroy(own);
         if (stat_host) hipHostFree(stat_host);
@@ -662,6 +670,20 @@ int orbfe_bf_match_batch_device(orbfe_matcher* m, const uint8_t* d_q, size_t q_p
     if (nb == 0 || nq_cap == 0) return ORBFE_OK;
     if ((q_pitch | r_pitch) & 15) return ORBFE_ERR_ARG;
     return guarded(m, [&]() {
+        // one reference set for the whole batch (r_pitch 0) on the FP4 path: with ORBFE_BF_PRE=1
+        // expanded to FP4 fragments once (otherwise every workgroup expands it)
+        if (r_pitch == 0 && m->bf_kernel == bf_match_fp4_kernel && m->bf_pre) {
+            int st;
+            DevBuf& e = m->bf_e[m->stream];
+            if ((st = e.ensure((size_t)kBfMaxTiles * 8 * kBfRefs * sizeof(i32x4)))) return st;
+            ORBFE_LAUNCH(m->prof, 0, bf_expand_kernel, dim3(kBfMaxTiles), dim3(512), 0, m->stream,
+                         d_r, d_nr, nb, e.as<i32x4>());
+            ORBFE_LAUNCH(m->prof, 0, bf_match_fp4e_kernel, dim3((nq_cap + kBfBlock - 1) / kBfBlock, nb),
+                         dim3(kBfBlock), 0, m->stream, d_q, (long long)q_pitch, d_nq, nq_cap, d_r,
+                         (long long)r_pitch, d_nr, d_out, (const i32x4*)e.as<i32x4>());
+            ORBFE_HIP(hipGetLastError());
+            return ORBFE_OK;
+        }
         ORBFE_LAUNCH(m->prof, 0, m->bf_kernel, dim3((nq_cap + kBfBlock - 1) / kBfBlock, nb),
                      dim3(kBfBlock), 0, m->stream, d_q, (long long)q_pitch, d_nq, nq_cap, d_r,
                      (long long)r_pitch, d_nr, d_out);

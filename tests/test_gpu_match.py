@@ -192,3 +192,45 @@ def test_search_for_initialization_contended(mt, n_contend, check_ori):
     assert np.array_equal(gprev, eprev)
     assert m.last_rounds() > 0  # the fixed-point rounds resolved it
     m.close()
+
+
+@pytest.mark.parametrize("pre", ["1", "0"])
+def test_bf_match_batch_shared_refs(pre, monkeypatch):
+    """orbfe_bf_match_batch_device with one reference set for the batch (r_pitch 0): expanded to
+    FP4 fragments once per call (ORBFE_BF_PRE=1) or by every workgroup (default); per-entry
+    reference counts that differ (partial tiles, a single row, none, the whole set) and ragged
+    query counts — every (best index, best, second) triple equal to the oracle's."""
+    import torch
+    from orbslam_mapsave_amd.native import ORBmatcher
+    monkeypatch.setenv("ORBFE_BF_PRE", pre)
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(77)
+    nref, cap = 2007, 300
+    nrs = [2007, 65, 1, 0, 64, 1999, 130, 2007]
+    nqs = [300, 17, 256, 5, 0, 299, 64, 1]
+    nb = len(nrs)
+    ref = rng.integers(0, 256, (nref, 32), dtype=np.uint8)
+    ref[5] = ref[9]  # equal distances: the lower index wins
+    q = rng.integers(0, 256, (nb, cap, 32), dtype=np.uint8)
+    q[0, 3] = ref[100]
+    d_r = torch.from_numpy(ref).to(dev)
+    d_q = torch.from_numpy(q).to(dev)
+    d_nq = torch.tensor(nqs, dtype=torch.int32, device=dev)
+    d_nr = torch.tensor(nrs, dtype=torch.int32, device=dev)
+    d_out = torch.full((nb, cap, 3), -7, dtype=torch.int32, device=dev)
+    mt = ORBmatcher(0.9, True, device=0)
+    try:
+        mt.bf_match_batch_device(d_q.data_ptr(), cap * 32, d_nq.data_ptr(), cap, d_r.data_ptr(), 0,
+                                 d_nr.data_ptr(), nb, d_out.data_ptr())
+        torch.cuda.synchronize()
+        out = d_out.cpu().numpy()
+    finally:
+        mt.close()
+    for b in range(nb):
+        if nqs[b] == 0:
+            continue
+        bi, bd, sd = oracle.bf_match(q[b, :nqs[b]], ref[:nrs[b]])
+        got = out[b, :nqs[b]]
+        assert np.array_equal(got[:, 0], bi), b
+        assert np.array_equal(got[:, 1], bd), b
+        assert np.array_equal(got[:, 2], sd), b
