@@ -77,9 +77,10 @@ struct orbfe_matcher {
     // ORBFE_ZERO_COPY=0: uploads and downloads as DMA copies (the staging buffer unmapped)
     bool zero_copy_off = std::getenv("ORBFE_ZERO_COPY") && std::strcmp(std::getenv("ORBFE_ZERO_COPY"), "0") == 0;
     BfKernel bf_kernel = bf_match_fp4_kernel;  // ORBFE_BF_I8=1 at creation: bf_match_kernel
-    // ORBFE_BF_PRE=1: a reference set shared by the whole batch is expanded to FP4 fragments
-    // once per call (bf_expand_kernel) instead of by every workgroup (A/B)
-    bool bf_pre = std::getenv("ORBFE_BF_PRE") && std::strcmp(std::getenv("ORBFE_BF_PRE"), "1") == 0;
+    // a reference set shared by the whole batch is expanded to FP4 fragments once per call
+    // (bf_expand_kernel) instead of by every workgroup: c3 bf_match 0.159 -> 0.148 ms per 512
+    // frames (profiles/r04/experiments/bf_pre/); ORBFE_BF_PRE=0: every workgroup expands it
+    bool bf_pre = !(std::getenv("ORBFE_BF_PRE") && std::strcmp(std::getenv("ORBFE_BF_PRE"), "0") == 0);
     // the shared reference set as FP4 fragments (bf_expand_kernel), one buffer per stream the
     // batch form was called on (calls on different streams may overlap)
     std::map<hipStream_t, DevBuf> bf_e;
@@ -670,8 +671,8 @@ int orbfe_bf_match_batch_device(orbfe_matcher* m, const uint8_t* d_q, size_t q_p
     if (nb == 0 || nq_cap == 0) return ORBFE_OK;
     if ((q_pitch | r_pitch) & 15) return ORBFE_ERR_ARG;
     return guarded(m, [&]() {
-        // one reference set for the whole batch (r_pitch 0) on the FP4 path: with ORBFE_BF_PRE=1
-        // expanded to FP4 fragments once (otherwise every workgroup expands it)
+        // one reference set for the whole batch (r_pitch 0) on the FP4 path: expanded to FP4
+        // fragments once (ORBFE_BF_PRE=0: every workgroup expands it, as for per-entry sets)
         if (r_pitch == 0 && m->bf_kernel == bf_match_fp4_kernel && m->bf_pre) {
             int st;
             DevBuf& e = m->bf_e[m->stream];

@@ -197,7 +197,7 @@ def test_search_for_initialization_contended(mt, n_contend, check_ori):
 @pytest.mark.parametrize("pre", ["1", "0"])
 def test_bf_match_batch_shared_refs(pre, monkeypatch):
     """orbfe_bf_match_batch_device with one reference set for the batch (r_pitch 0): expanded to
-    FP4 fragments once per call (ORBFE_BF_PRE=1) or by every workgroup (default); per-entry
+    FP4 fragments once per call (default) or by every workgroup (ORBFE_BF_PRE=0); per-entry
     reference counts that differ (partial tiles, a single row, none, the whole set) and ragged
     query counts — every (best index, best, second) triple equal to the oracle's."""
     import torch
