@@ -32,7 +32,9 @@ sys.path.insert(0, ROOT)
 ARITH = {"scalar": 0, "x86": 1}  # orbfe_set_arithmetic: ORBFE_ARITH_SCALAR / ORBFE_ARITH_X86_SIMD
 METRIC = "frames/sec ORB extract+match, 640×480 @1000 kp, 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md "HBM3E peak BW 8.0 TB/s spec"
-STAGES = ("mask", "resize", "fast", "octree", "blur", "describe", "bf_match")
+# bf_expand: the batch-shared reference set expanded to FP4 fragments once per match call (its
+# own profiler stage, so bf_match's per-launch figures are the match kernel's alone)
+STAGES = ("mask", "resize", "fast", "octree", "blur", "describe", "bf_match", "bf_expand")
 # ORBextractor.{scaleFactor,nLevels,iniThFAST,minThFAST} of Examples/ORB_RGB640x480.yaml:38-48
 # (its nFeatures, 2000, is config 4's; configs 2/3/5 extract the metric's 1000).  Pinned against
 # the reference text by tests/test_constants.py (tests/golden/constants_fixture.json).
@@ -513,7 +515,7 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
         for e in exs:
             for st, (ms, n) in e.profile_read().items():
                 acc[st] = (acc[st][0] + ms, acc[st][1] + n)
-        acc["bf_match"] = mt.profile_read()
+        acc.update(mt.profile_read_stages())
         return acc
 
     def agreed(flag: bool) -> bool:

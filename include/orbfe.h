@@ -152,7 +152,9 @@ int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int w, int hgt, size_t
  *   orbfe_input_buffer   : the handle's pinned, device-mapped w x h u8 staging buffer (*buf,
  *                          row stride *stride bytes) — wrap it as cv::Mat(h, w, CV_8UC1, buf,
  *                          stride) and let cvtColor write the gray frame straight into it.
- *                          Valid until the next orbfe_input_buffer / orbfe_destroy on h.
+ *                          It is separate from the staging orbfe_extract copies into: no
+ *                          other call writes or moves it, and it stays valid until an
+ *                          orbfe_input_buffer for a larger w x h or orbfe_destroy on h.
  *   orbfe_extract_staged : operator() on that buffer (the GPU reads it in place).  With
  *                          kps_cap == 0 (kps, desc NULL) the outputs stay in the handle's pinned
  *                          output buffers and orbfe_staged_outputs returns them (*n_out is set).
@@ -343,9 +345,14 @@ int orbfe_bf_match_batch_device(orbfe_matcher* m, const uint8_t* d_q, size_t q_p
                                 size_t r_pitch, const int32_t* d_nr, int nb, int32_t* d_out);
 
 /* Timing of orbfe_bf_match_batch_device launches (dispatch-bound HIP events, as
- * orbfe_profile): summed ms and launch count since the previous read. */
+ * orbfe_profile): summed ms and launch count since the previous read.  Stage 0 is the
+ * brute-force match kernels, stage 1 the expansion of a batch-shared reference set (r_pitch 0)
+ * into matrix-core fragments; orbfe_matcher_profile_read reports stage 0,
+ * orbfe_matcher_profile_read_stages fills ORBFE_MATCHER_STAGES entries.  Either read resets. */
+#define ORBFE_MATCHER_STAGES 2
 int orbfe_matcher_profile(orbfe_matcher* m, int enable);
 int orbfe_matcher_profile_read(orbfe_matcher* m, double* total_ms, int32_t* launches);
+int orbfe_matcher_profile_read_stages(orbfe_matcher* m, double* total_ms, int32_t* launches);
 
 /* ORBmatcher::SearchForInitialization (ORBmatcher.cc:408-523), matcher built as
  * ORBmatcher(nnratio, check_ori) (Tracking.cc:843).  prev_matched: inout F1.n (x,y) pairs

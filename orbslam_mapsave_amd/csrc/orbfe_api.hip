@@ -174,11 +174,17 @@ struct orbfe_extractor {
             bytes = 0;
         }
     };
-    Pinned pin_in, pin_kps, pin_desc, pin_n;
+    // pin_in: the copy staging of orbfe_extract (rewritten by every copying call); pin_user: the
+    // buffer orbfe_input_buffer hands out — only orbfe_input_buffer (at a larger size) and
+    // orbfe_destroy reallocate it and no copying call writes it, so the caller's pointer and the
+    // frame staged in it stay valid across orbfe_extract calls of any size.
+    Pinned pin_in, pin_user, pin_kps, pin_desc, pin_n;
     // Every buffer the capture embeds is either in g1_key (outputs, pinned staging) or is a
-    // plan / workspace buffer: set_plan and a growing ensure_frames drop the graph.
-    hipGraphExec_t g1 = nullptr;
-    const void* g1_key[11] = {};  // the buffers, plan and staging mode the graph was captured with
+    // plan / workspace buffer: set_plan and a growing ensure_frames drop the graphs.  One graph
+    // per input source ([0] copy staging, [1] the handed-out buffer), so callers alternating the
+    // two forms do not recapture.
+    hipGraphExec_t g1[2] = {nullptr, nullptr};
+    const void* g1_key[2][11] = {};  // the buffers, plan and staging mode each graph was captured with
     // K4 fused into K5 per keypoint window (default), or its own pass over every level with
     // K5 reading the blurred levels (ORBFE_PREBLUR=1: describe 0.30 -> 0.20 ms per 256 frames,
     // but the pass costs 0.19 ms; profiles/r02/experiments/preblur.json)
@@ -248,8 +254,10 @@ struct orbfe_extractor {
                                  // disabled for A/B runs): keep to the launch path
 
     void drop_graph() {
-        if (g1) hipGraphExecDestroy(g1);
-        g1 = nullptr;
+        for (hipGraphExec_t& g : g1) {
+            if (g) hipGraphExecDestroy(g);
+            g = nullptr;
+        }
     }
 
     // ORBFE_OK with *done = true when the graph path ran; *done = false to take the plain path.
@@ -263,21 +271,26 @@ struct orbfe_extractor {
         if ((st = out_kps.ensure((size_t)cap * sizeof(orbfe_keypoint)))) return st;
         if ((st = out_desc.ensure((size_t)cap * 32))) return st;
         if ((st = out_n.ensure(sizeof(int32_t)))) return st;
-        if ((st = pin_in.ensure((size_t)w * h))) return st;
+        const int gi = img == pin_user.p ? 1 : 0;  // staged: the GPU reads the handed-out buffer
+        Pinned& src = gi ? pin_user : pin_in;
+        if (!gi && (st = pin_in.ensure((size_t)w * h))) return st;
         if ((st = pin_kps.ensure((size_t)cap * sizeof(orbfe_keypoint)))) return st;
         if ((st = pin_desc.ensure((size_t)cap * 32))) return st;
         if ((st = pin_n.ensure(sizeof(int32_t)))) return st;
         // every buffer the capture can embed (the zero-copy outputs write pin_kps / pin_desc /
         // pin_n through their device mappings) and the staging mode
-        const void* key[11] = {pyr.p, out_kps.p, out_desc.p, out_n.p, pin_in.p, pin_kps.p,
+        const void* key[11] = {pyr.p, out_kps.p, out_desc.p, out_n.p, src.p, pin_kps.p,
                                pin_desc.p, pin_n.p,
                                reinterpret_cast<const void*>((uintptr_t)w << 32 | (uint32_t)h),
                                reinterpret_cast<const void*>((uintptr_t)frames_cap),
                                reinterpret_cast<const void*>((uintptr_t)zero_copy)};
-        if (g1 && std::memcmp(key, g1_key, sizeof(key)) != 0) drop_graph();
+        if (g1[gi] && std::memcmp(key, g1_key[gi], sizeof(key)) != 0) {
+            hipGraphExecDestroy(g1[gi]);
+            g1[gi] = nullptr;
+        }
         const Plan& g = plan;
         const LevelGeo& l0 = g.geo.lv[0];
-        if (!g1) {
+        if (!g1[gi]) {
             hipGraph_t graph = nullptr;
             if (hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
                 graph_broken = true;
@@ -287,14 +300,14 @@ struct orbfe_extractor {
             // writes level 0 into the slab as it goes (no H2D copy), describe writes keypoints,
             // descriptors and the count straight into the pinned outputs (no D2H copies)
             const bool zc_out = zero_copy && pin_kps.d && pin_desc.d && pin_n.d;
-            const bool zc_in = zero_copy && pin_in.d && pyr_path(1);
+            const bool zc_in = zero_copy && src.d && pyr_path(1);
             LevelPtr lp0{pyr.as<uint8_t>() + l0.off, g.slab, l0.pitch};
             bool ok = true;
             if (zc_in) {
-                l0_stage = LevelPtr{pin_in.d, (long long)w * h, w};
+                l0_stage = LevelPtr{src.d, (long long)w * h, w};
                 l0_from_stage = true;
             } else {
-                ok = hipMemcpy2DAsync(pyr.as<uint8_t>() + l0.off, l0.pitch, pin_in.p, w, w, h,
+                ok = hipMemcpy2DAsync(pyr.as<uint8_t>() + l0.off, l0.pitch, src.p, w, w, h,
                                       hipMemcpyHostToDevice, stream) == hipSuccess;
             }
             if (zc_out) {
@@ -313,24 +326,24 @@ struct orbfe_extractor {
             l0_from_stage = false;
             const bool ended = hipStreamEndCapture(stream, &graph) == hipSuccess;
             ok = ok && ended && graph &&
-                 hipGraphInstantiate(&g1, graph, nullptr, nullptr, 0) == hipSuccess;
+                 hipGraphInstantiate(&g1[gi], graph, nullptr, nullptr, 0) == hipSuccess;
             if (graph) hipGraphDestroy(graph);
             (void)hipGetLastError();
             if (!ok) {
-                g1 = nullptr;
+                g1[gi] = nullptr;
                 graph_broken = true;
                 return ORBFE_OK;
             }
-            std::memcpy(g1_key, key, sizeof(key));
+            std::memcpy(g1_key[gi], key, sizeof(key));
         }
-        if (img == pin_in.p) {
-            // staged (orbfe_input_buffer): the caller wrote the frame into pin_in already
+        if (gi) {
+            // staged (orbfe_input_buffer): the caller wrote the frame into pin_user already
         } else if (stride == (size_t)w) {
             std::memcpy(pin_in.p, img, (size_t)w * h);
         } else {
             for (int r = 0; r < h; ++r) std::memcpy(pin_in.p + (size_t)r * w, img + r * stride, w);
         }
-        ORBFE_HIP(hipGraphLaunch(g1, stream));
+        ORBFE_HIP(hipGraphLaunch(g1[gi], stream));
         ORBFE_HIP(hipStreamSynchronize(stream));
         last_n = 1;
         *done = true;
@@ -846,7 +859,7 @@ struct orbfe_extractor {
                           &st_sad, &st_status, &st_kl, &st_dl, &st_kr, &st_dr, &st_n, &st_ur, &st_dp})
             b->release();
         drop_graph();
-        for (Pinned* q : {&pin_in, &pin_kps, &pin_desc, &pin_n}) q->release();
+        for (Pinned* q : {&pin_in, &pin_user, &pin_kps, &pin_desc, &pin_n}) q->release();
         prof.release();
         if (own) hipStreamDestroy(own);
     }
@@ -1072,8 +1085,8 @@ int orbfe_input_buffer(orbfe_extractor* h, int w, int hgt, uint8_t** buf, size_t
         DeviceGuard dg(h->device);
         int st;
         if ((st = h->set_plan(w, hgt))) return st;  // the size must be one the plan supports
-        if ((st = h->pin_in.ensure((size_t)w * hgt))) return st;
-        *buf = h->pin_in.p;
+        if ((st = h->pin_user.ensure((size_t)w * hgt))) return st;
+        *buf = h->pin_user.p;
         *stride = (size_t)w;
         return ORBFE_OK;
     } catch (const std::bad_alloc&) {
@@ -1086,9 +1099,9 @@ int orbfe_input_buffer(orbfe_extractor* h, int w, int hgt, uint8_t** buf, size_t
 int orbfe_extract_staged(orbfe_extractor* h, int w, int hgt, orbfe_keypoint* kps, int kps_cap,
                          uint8_t* desc, int* n_out) {
     if (!h || w <= 0 || hgt <= 0 || !n_out || kps_cap < 0 || (kps_cap > 0 && !kps)) return ORBFE_ERR_ARG;
-    if (!h->pin_in.p || h->pin_in.bytes < (size_t)w * hgt) return ORBFE_ERR_ARG;  // no buffer handed out
+    if (!h->pin_user.p || h->pin_user.bytes < (size_t)w * hgt) return ORBFE_ERR_ARG;  // no buffer handed out
     try {
-        const uint8_t* img = h->pin_in.p;
+        const uint8_t* img = h->pin_user.p;
         int32_t cnt = 0;
         const int st = extract_host_common(h, &img, 1, w, hgt, (size_t)w, ORBFE_PIX_GRAY, nullptr, 0,
                                            nullptr, kps_cap ? kps : nullptr, kps_cap, desc, &cnt);

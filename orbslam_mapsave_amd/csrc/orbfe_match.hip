@@ -339,6 +339,9 @@ struct BfLaneF {
 // instead of every workgroup expanding the same bits (a third of its VALU in the MFMA gaps).
 // Rows at or past nr are zero, as the in-kernel expansion pads them.
 constexpr int kBfMaxTiles = (kBfMaxRefs + kBfRefs) / kBfRefs;
+constexpr int kBfExpandBlocks = 64;
+// kBfExpandBlocks workgroups stride over the tiles (the largest count in nr_arr is read once per
+// workgroup, not once per possible tile).
 __global__ __launch_bounds__(512) void bf_expand_kernel(const uint8_t* r, const int* nr_arr, int nb,
                                                         i32x4* E) {
     __shared__ int s_nr;
@@ -349,12 +352,12 @@ __global__ __launch_bounds__(512) void bf_expand_kernel(const uint8_t* r, const 
     if (m) atomicMax(&s_nr, m);
     __syncthreads();
     const int nr = min(s_nr, kBfMaxRefs);
-    const int t = blockIdx.x;
-    if (t * kBfRefs >= nr) return;
     const int row = threadIdx.x & 63, dw = threadIdx.x >> 6;  // 8 dwords x 64 rows
-    const int j = t * kBfRefs + row;
-    const uint32_t w = j < nr ? reinterpret_cast<const uint32_t*>(r + (long long)j * 32)[dw] : 0u;
-    E[((size_t)t * 8 + dw) * kBfRefs + row] = ref_fp4(w);
+    for (int t = blockIdx.x; t * kBfRefs < nr; t += gridDim.x) {
+        const int j = t * kBfRefs + row;
+        const uint32_t w = j < nr ? reinterpret_cast<const uint32_t*>(r + (long long)j * 32)[dw] : 0u;
+        E[((size_t)t * 8 + dw) * kBfRefs + row] = ref_fp4(w);
+    }
 }
 
 template <bool kPre>

@@ -82,8 +82,36 @@ struct orbfe_matcher {
     // frames (profiles/r04/experiments/bf_pre/); ORBFE_BF_PRE=0: every workgroup expands it
     bool bf_pre = !(std::getenv("ORBFE_BF_PRE") && std::strcmp(std::getenv("ORBFE_BF_PRE"), "0") == 0);
     // the shared reference set as FP4 fragments (bf_expand_kernel), one buffer per stream the
-    // batch form was called on (calls on different streams may overlap)
+    // batch form was called on (calls on different streams may overlap), at most kBfStreams of
+    // them: a call on another stream takes the least recently used one after a device
+    // synchronisation (a caller creating a stream per call, or a destroyed stream whose handle is
+    // reused, cannot grow the set or find a buffer another stream still reads)
+    static constexpr int kBfStreams = 4;
     std::map<hipStream_t, DevBuf> bf_e;
+    std::map<hipStream_t, unsigned long long> bf_e_used;
+    unsigned long long bf_e_clock = 0;
+    DevBuf* bf_buffer(hipStream_t s, int* st) {
+        *st = ORBFE_OK;
+        auto it = bf_e.find(s);
+        if (it == bf_e.end() && (int)bf_e.size() >= kBfStreams) {
+            hipStream_t lru = bf_e_used.begin()->first;
+            for (auto& kv : bf_e_used)
+                if (kv.second < bf_e_used[lru]) lru = kv.first;
+            if (hipDeviceSynchronize() != hipSuccess) {
+                *st = ORBFE_ERR_HIP;
+                return nullptr;
+            }
+            DevBuf moved = bf_e[lru];  // reuse the allocation for the new stream
+            bf_e.erase(lru);
+            bf_e_used.erase(lru);
+            bf_e[s] = moved;
+            it = bf_e.find(s);
+        }
+        DevBuf& e = bf_e[s];
+        bf_e_used[s] = ++bf_e_clock;
+        if ((*st = e.ensure((size_t)kBfMaxTiles * 8 * kBfRefs * sizeof(i32x4)))) return nullptr;
+        return &e;
+    }
 
     ~orbfe_matcher() {
         for (DevBuf* b : {&fa_k, &fa_d, &fa_ur, &fa_cs, &fa_ci, &fa_co, &fb_k, &fb_d, &fb_ur,
@@ -675,9 +703,11 @@ int orbfe_bf_match_batch_device(orbfe_matcher* m, const uint8_t* d_q, size_t q_p
         // fragments once (ORBFE_BF_PRE=0: every workgroup expands it, as for per-entry sets)
         if (r_pitch == 0 && m->bf_kernel == bf_match_fp4_kernel && m->bf_pre) {
             int st;
-            DevBuf& e = m->bf_e[m->stream];
-            if ((st = e.ensure((size_t)kBfMaxTiles * 8 * kBfRefs * sizeof(i32x4)))) return st;
-            ORBFE_LAUNCH(m->prof, 0, bf_expand_kernel, dim3(kBfMaxTiles), dim3(512), 0, m->stream,
+            DevBuf* pe = m->bf_buffer(m->stream, &st);
+            if (!pe) return st;
+            DevBuf& e = *pe;
+            // its own profiler stage (1): the bench's per-launch figures are the match kernel's
+            ORBFE_LAUNCH(m->prof, 1, bf_expand_kernel, dim3(kBfExpandBlocks), dim3(512), 0, m->stream,
                          d_r, d_nr, nb, e.as<i32x4>());
             ORBFE_LAUNCH(m->prof, 0, bf_match_fp4e_kernel, dim3((nq_cap + kBfBlock - 1) / kBfBlock, nb),
                          dim3(kBfBlock), 0, m->stream, d_q, (long long)q_pitch, d_nq, nq_cap, d_r,
@@ -700,19 +730,34 @@ int orbfe_matcher_profile(orbfe_matcher* m, int enable) {
     return ORBFE_OK;
 }
 
-int orbfe_matcher_profile_read(orbfe_matcher* m, double* total_ms, int32_t* launches) {
+int orbfe_matcher_profile_read_stages(orbfe_matcher* m, double* total_ms, int32_t* launches) {
     if (!m || !total_ms || !launches) return ORBFE_ERR_ARG;
     DeviceGuard dg(m->device);
     ORBFE_HIP(hipStreamSynchronize(m->stream));
-    *total_ms = 0;
-    *launches = 0;
+    for (int k = 0; k < ORBFE_MATCHER_STAGES; ++k) {
+        total_ms[k] = 0;
+        launches[k] = 0;
+    }
     for (size_t i = 0; i < m->prof.used; ++i) {
         float ms = 0.f;
         ORBFE_HIP(hipEventElapsedTime(&ms, m->prof.a[i], m->prof.b[i]));
-        *total_ms += ms;
-        *launches += 1;
+        const int k = m->prof.kind[i];
+        if (k < 0 || k >= ORBFE_MATCHER_STAGES) continue;
+        total_ms[k] += ms;
+        launches[k] += 1;
     }
     m->prof.used = 0;
+    return ORBFE_OK;
+}
+
+int orbfe_matcher_profile_read(orbfe_matcher* m, double* total_ms, int32_t* launches) {
+    if (!m || !total_ms || !launches) return ORBFE_ERR_ARG;
+    double ms[ORBFE_MATCHER_STAGES];
+    int32_t n[ORBFE_MATCHER_STAGES];
+    const int st = orbfe_matcher_profile_read_stages(m, ms, n);
+    if (st) return st;
+    *total_ms = ms[0];  // the matcher kernels (stage 0); the expansion is stage 1
+    *launches = n[0];
     return ORBFE_OK;
 }
 

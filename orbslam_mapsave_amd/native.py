@@ -37,7 +37,7 @@ EXPORTED = [
     "orbfe_synchronize", "orbfe_compute_stereo_matches", "orbfe_compute_stereo_matches_device",
     "orbfe_stereo_status", "orbfe_profile", "orbfe_profile_read", "orbfe_pyramid_path", "orbfe_get_level", "orbfe_get_blurred_level", "orbfe_get_fast_keys",
     "orbfe_matcher_create", "orbfe_matcher_destroy", "orbfe_matcher_set_stream",
-    "orbfe_matcher_profile", "orbfe_matcher_profile_read", "orbfe_hamming",
+    "orbfe_matcher_profile", "orbfe_matcher_profile_read", "orbfe_matcher_profile_read_stages", "orbfe_hamming",
     "orbfe_bf_match", "orbfe_bf_match_batch_device", "orbfe_search_for_initialization",
     "orbfe_search_by_projection_local", "orbfe_search_by_projection_last",
     "orbfe_search_by_projection_keyframe", "orbfe_distinctive_descriptors",
@@ -551,11 +551,20 @@ class ORBmatcher:
         _check("orbfe_matcher_profile", lib().orbfe_matcher_profile(self._h, int(enable)))
 
     def profile_read(self) -> tuple[float, int]:
-        """(total ms, launches) of bf_match_batch_device since the previous read."""
+        """(total ms, launches) of the brute-force match kernels since the previous read."""
         ms = np.zeros(1, np.float64)
         n = np.zeros(1, np.int32)
         _check("orbfe_matcher_profile_read", lib().orbfe_matcher_profile_read(self._h, ptr(ms), ptr(n)))
         return float(ms[0]), int(n[0])
+
+    def profile_read_stages(self) -> dict:
+        """{"bf_match": (ms, launches), "bf_expand": (ms, launches)} since the previous read:
+        the match kernels and the shared-reference expansion (orbfe_matcher_profile_read_stages)."""
+        ms = np.zeros(2, np.float64)
+        n = np.zeros(2, np.int32)
+        _check("orbfe_matcher_profile_read_stages",
+               lib().orbfe_matcher_profile_read_stages(self._h, ptr(ms), ptr(n)))
+        return {"bf_match": (float(ms[0]), int(n[0])), "bf_expand": (float(ms[1]), int(n[1]))}
 
     def set_stream(self, stream_handle: int | None) -> None:
         _check("orbfe_matcher_set_stream", lib().orbfe_matcher_set_stream(

@@ -1,10 +1,12 @@
-"""Parity at the benchmark's full size (BASELINE configs[2], bench.py's default workload): 256
-640x480 frames extracted as two 128-frame sub-batches on two HIP streams (one extractor handle
-each), every frame brute-force matched against the 2000-keypoint reference frame on the device —
-the exact launch pattern bench.py times — and every one of the 256 frames compared with the CPU
-oracle: keypoints (28-byte records), descriptors, and the (best index, best, second) triple of
-every query.  64 distinct seeds, each used 4 times, so the oracle side runs in about a second
-and repeated frames in different sub-batches / streams must also agree with each other."""
+"""Parity at the benchmark's full size (BASELINE configs[2], bench.py's default workload): 640x480
+frames extracted on the device and every frame brute-force matched against the 2000-keypoint
+reference frame, in the launch patterns bench.py runs — 512 frames as two 256-frame sub-batches
+on two HIP streams (the timed steps; handle 0 planned for 512 frames, as in bench.py), one
+512-frame call on that handle (the probe and roofline legs), and 256 as 2 x 128 — and every frame
+compared with the CPU oracle: keypoints (28-byte records), descriptors, and the (best index,
+best, second) triple of every query.  64 distinct seeds, each used 4-8 times, so the oracle side
+runs in about a second and repeated frames in different sub-batches / streams must also agree
+with each other."""
 import numpy as np
 import pytest
 
@@ -13,21 +15,41 @@ from orbslam_mapsave_amd.abi import KEYPOINT_DTYPE
 
 pytestmark = pytest.mark.gpu
 
-B, S, W, H, NF, NREF, DISTINCT = 256, 2, 640, 480, 1000, 2000, 64
+S, W, H, NF, NREF, DISTINCT = 2, 640, 480, 1000, 2000, 64
+
+# (frames, sub-batch streams, max_batch of handle 0): 256 as 2 x 128; the bench's timed steps,
+# 512 as 2 x 256 on a handle 0 planned for 512 (bench.py run_extract); its probe / roofline legs,
+# one 512-frame call on that handle (step_single)
+LAYOUTS = {"256_as_2x128": (256, 2, 128), "512_as_2x256": (512, 2, 512), "512_single": (512, 1, 512)}
+_EXPECT = {}
 
 
-def test_bench_workload_parity():
+def _expected(frames_np, ref_img, ref_desc_np):
+    if not _EXPECT:
+        _, oref = oracle.extract(oracle.params(NREF, 1.2, 8, 32, 7), ref_img)
+        _EXPECT["ref"] = oref
+        p = oracle.params(NF, 1.2, 8, 32, 7)
+        for s in range(DISTINCT):
+            okps, odesc = oracle.extract(p, frames_np[s])
+            _EXPECT[s] = (okps, odesc, oracle.bf_match(odesc, oref))
+    return _EXPECT
+
+
+@pytest.mark.parametrize("layout", list(LAYOUTS))
+def test_bench_workload_parity(layout):
     import torch
     from orbslam_mapsave_amd.native import ORBextractor, ORBmatcher
     from orbslam_mapsave_amd.synth import synthetic_batch, synthetic_frame
+    B, NS, maxb0 = LAYOUTS[layout]
     dev = torch.device("cuda", 0)
     frames_np = synthetic_batch(B, W, H, first_seed=0, distinct=DISTINCT)
     frames = torch.from_numpy(frames_np).to(dev)
-    C = B // S
-    streams = [torch.cuda.Stream(dev) for _ in range(S)]
+    C = B // NS
+    streams = [torch.cuda.Stream(dev) for _ in range(NS)]
     exs = []
-    for k in range(S):
-        e = ORBextractor(NF, 1.2, 8, 32, 7, device=0, max_width=W, max_height=H, max_batch=C)
+    for k in range(NS):
+        e = ORBextractor(NF, 1.2, 8, 32, 7, device=0, max_width=W, max_height=H,
+                         max_batch=maxb0 if k == 0 else C)
         e.set_stream(streams[k].cuda_stream)
         exs.append(e)
     cap = exs[0].capacity(W, H)
@@ -43,7 +65,7 @@ def test_bench_workload_parity():
     d_nr = torch.full((B,), len(ref_desc_np), dtype=torch.int32, device=dev)
     mt = ORBmatcher(0.9, True, device=0)
     torch.cuda.synchronize()
-    for k in range(S):
+    for k in range(NS):
         f0 = k * C
         exs[k].extract_batch_device(frames[f0].data_ptr(), C, W, H, W, W * H, d_kps[f0].data_ptr(),
                                     cap, d_desc[f0].data_ptr(), d_n[f0:].data_ptr())
@@ -53,14 +75,9 @@ def test_bench_workload_parity():
                                  d_out[f0].data_ptr())
     torch.cuda.synchronize()
     kps, desc, n, out = d_kps.cpu().numpy(), d_desc.cpu().numpy(), d_n.cpu().numpy(), d_out.cpu().numpy()
-    p = oracle.params(NF, 1.2, 8, 32, 7)
+    expect = _expected(frames_np, ref_img, ref_desc_np)
     # the reference frame itself: GPU 2x-feature extraction == oracle
-    _, oref = oracle.extract(oracle.params(NREF, 1.2, 8, 32, 7), ref_img)
-    assert np.array_equal(ref_desc_np, oref)
-    expect = {}
-    for s in range(DISTINCT):
-        okps, odesc = oracle.extract(p, frames_np[s])
-        expect[s] = (okps, odesc, oracle.bf_match(odesc, ref_desc_np))
+    assert np.array_equal(ref_desc_np, expect["ref"])
     for f in range(B):
         okps, odesc, (bi, bd, sd) = expect[f % DISTINCT]
         nf = int(n[f])

@@ -106,3 +106,40 @@ def test_staged_requires_buffer():
             e.extract_staged(640, 480)  # the buffer handed out is smaller than the frame
     finally:
         e.close()
+
+
+def test_staged_buffer_survives_copying_calls():
+    """The handed-out buffer is not the copy staging: orbfe_extract calls of the same and of a
+    larger size between orbfe_input_buffer and orbfe_extract_staged neither move it nor
+    overwrite the frame staged in it."""
+    from orbslam_mapsave_amd.native import ORBextractor
+    p = oracle.params(1000, 1.2, 8, 20, 7)
+    small, big = synthetic_frame(811, 640, 480), synthetic_frame(812, 960, 720)
+    other = synthetic_frame(813, 640, 480)
+    e = ORBextractor(1000, 1.2, 8, 20, 7, device=0, max_width=960, max_height=720)
+    try:
+        buf = e.input_buffer(640, 480)
+        addr = buf.ctypes.data
+        buf[:] = small
+        e(other)   # same size, copying form
+        e(big)     # larger frame, copying form
+        buf2 = e.input_buffer(640, 480)
+        assert buf2.ctypes.data == addr and np.array_equal(buf2, small)
+        k, d = e.extract_staged(640, 480)
+        ok, od = oracle.extract(p, small)
+        assert k.tobytes() == ok.tobytes() and np.array_equal(d, od)
+    finally:
+        e.close()
+
+
+def test_staged_after_copying_call_requires_buffer():
+    """A copying orbfe_extract does not count as a handed-out buffer."""
+    from orbslam_mapsave_amd.abi import OrbfeError
+    from orbslam_mapsave_amd.native import ORBextractor
+    e = ORBextractor(1000, 1.2, 8, 20, 7, device=0)
+    try:
+        e(synthetic_frame(814, 640, 480))
+        with pytest.raises(OrbfeError):
+            e.extract_staged(640, 480)
+    finally:
+        e.close()
