@@ -129,7 +129,7 @@ struct orbfe_extractor {
     Plan plan;
     bool planned = false;
     int frames_cap = 0;
-    DevBuf cells, xtab, ytab, bslot, ptab;
+    DevBuf cells, chunks, xtab, ytab, bslot, ptab;
     DevBuf pyr, blur, cell_cnt, cell_keys, keys, act, oct_out, oct_cnt, oct_ord, level_keys;
     DevBuf out_kps, out_desc, out_n;  // staging for the host-pointer entry points
     DevBuf stage, rects;              // host colour frames / rectangle masks (level-0 inputs)
@@ -249,6 +249,12 @@ struct orbfe_extractor {
     int num_cus = 256;  // compute units of the device (launch-shape choices)
     // ORBFE_OCT_SMALL=0: small batches keep the 256-thread oct-tree (A/B)
     bool oct_small = !(std::getenv("ORBFE_OCT_SMALL") && std::strcmp(std::getenv("ORBFE_OCT_SMALL"), "0") == 0);
+    // ORBFE_FAST_STRIP=1: FAST as a workgroup per run of a cell row's cells (fast_strip_kernel,
+    // SURVEY §7 step 4's layout) instead of one wave per cell (fast_kernel).  Bit-exact, but
+    // measured slower: c3 FAST 0.463 -> 0.834 ms per 512 frames, c4 1.86 -> 3.00 ms per 256
+    // (more VALU per frame, 696 K vs 547 K, and each workgroup's ROI load and
+    // barriers exposed at 24 waves per CU)
+    bool fast_strip = std::getenv("ORBFE_FAST_STRIP") && std::strcmp(std::getenv("ORBFE_FAST_STRIP"), "1") == 0;
     int desc_g16 = std::getenv("ORBFE_DESC_G16") ? std::atoi(std::getenv("ORBFE_DESC_G16")) : 0;
     bool graph_broken = std::getenv("ORBFE_NO_GRAPH") != nullptr;  // capture failed once (or
                                  // disabled for A/B runs): keep to the launch path
@@ -356,6 +362,7 @@ struct orbfe_extractor {
         int st = plan_geometry(tab, w, h, g);
         if (st != ORBFE_OK) return st;
         if ((st = cells.ensure(std::max<size_t>(1, g.cells.size()) * sizeof(CellDesc)))) return st;
+        if ((st = chunks.ensure(std::max<size_t>(1, g.chunks.size()) * sizeof(FastChunk)))) return st;
         if ((st = xtab.ensure(std::max<size_t>(1, g.xtab.size()) * sizeof(int)))) return st;
         if ((st = ytab.ensure(std::max<size_t>(1, g.ytab.size()) * sizeof(int)))) return st;
         if ((st = bslot.ensure(kBlurFragBytes + g.bitems.size() * sizeof(uint32_t)))) return st;
@@ -379,6 +386,9 @@ struct orbfe_extractor {
         }
         ORBFE_HIP(hipMemcpyAsync(cells.p, g.cells.data(), g.cells.size() * sizeof(CellDesc),
                                  hipMemcpyHostToDevice, stream));
+        if (!g.chunks.empty())
+            ORBFE_HIP(hipMemcpyAsync(chunks.p, g.chunks.data(), g.chunks.size() * sizeof(FastChunk),
+                                     hipMemcpyHostToDevice, stream));
         ORBFE_HIP(hipMemcpyAsync(xtab.p, g.xtab.data(), g.xtab.size() * sizeof(int),
                                  hipMemcpyHostToDevice, stream));
         ORBFE_HIP(hipMemcpyAsync(ytab.p, g.ytab.data(), g.ytab.size() * sizeof(int),
@@ -627,7 +637,12 @@ struct orbfe_extractor {
             fa.cell_keys = cell_keys.as<uint32_t>();
             fa.level_keys = level_keys.as<int>();
             for (int l = 0; l < L; ++l) fa.pyr[l] = lp[l];
-            if (g.roi_pitch == kFastPitch)
+            fa.chunks = chunks.as<FastChunk>();
+            if (fast_strip && !g.chunks.empty()) {
+                fa.roi_rows = g.chunk_rows;
+                ORBFE_LAUNCH(prof, ORBFE_STAGE_FAST, fast_strip_kernel, dim3((int)g.chunks.size(), n),
+                             dim3(kChunkBlock), g.chunk_lds, stream, fa);
+            } else if (g.roi_pitch == kFastPitch)
                 ORBFE_LAUNCH(prof, ORBFE_STAGE_FAST, fast_kernel<kFastPitch>, dim3(ncells, n), dim3(kFastBlockSize), g.fast_lds, stream, fa);
             else
                 ORBFE_LAUNCH(prof, ORBFE_STAGE_FAST, fast_kernel<0>, dim3(ncells, n), dim3(kFastBlockSize), g.fast_lds, stream, fa);
@@ -854,7 +869,7 @@ struct orbfe_extractor {
     }
 
     ~orbfe_extractor() {
-        for (DevBuf* b : {&cells, &xtab, &ytab, &bslot, &ptab, &pyr, &blur, &cell_cnt, &cell_keys, &keys, &act,
+        for (DevBuf* b : {&cells, &chunks, &xtab, &ytab, &bslot, &ptab, &pyr, &blur, &cell_cnt, &cell_keys, &keys, &act,
                           &oct_out, &oct_cnt, &oct_ord, &level_keys, &out_kps, &out_desc, &out_n, &stage, &rects, &st_off, &st_items,
                           &st_sad, &st_status, &st_kl, &st_dl, &st_kr, &st_dr, &st_n, &st_ur, &st_dp})
             b->release();

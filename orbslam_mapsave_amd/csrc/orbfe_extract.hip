@@ -1530,14 +1530,16 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
     const int X0 = shift + 3, g0 = X0 >> 2;
     const int gpr = ncand ? ((X0 + nc - 1) >> 2) - g0 + 1 : 1;
     const int rps = 64 / gpr;  // candidate rows per sweep
-    const int lr = lane / gpr, lg = lane - lr * gpr;
+    // lane / gpr through the float reciprocal of the (wave-uniform) gpr <= 18: floor((lane +
+    // 0.5) / gpr) is at least 0.5 / gpr from an integer, far above rcp's error (the integer
+    // division cost ~20 VALU per cell)
+    const int lr = (int)(((float)lane + 0.5f) * __builtin_amdgcn_rcpf((float)gpr)), lg = lane - lr * gpr;
     const int gx = 4 * (g0 + lg);  // roi_base column of the group's byte 0
-    uint32_t vmask = 0;            // 0x80 in every byte whose pixel is a candidate column
-    if (lr < rps) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (gx + k >= X0 && gx + k < X0 + nc) vmask |= 0x80u << (8 * k);
-    }
+    // 0x80 in every byte whose pixel is a candidate column: only the row's first group (bytes
+    // before X0) and last group (bytes from X0 + nc) are partial
+    uint32_t vmask = lr < rps && ncand ? 0x80808080u : 0u;
+    if (lg == 0) vmask &= 0x80808080u << (8 * (X0 - gx));
+    if (lg == gpr - 1) vmask &= 0x80808080u >> (8 * (4 - min(X0 + nc - gx, 4)));
     const uint32_t* lds32 = reinterpret_cast<const uint32_t*>(roi_base);
     const int P4 = P >> 2;
     fast_sync();
@@ -1573,8 +1575,11 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
         // the roles swapped, v - c > t (c < v - t) — checked for every c, v, t in
         // tests/test_oracle_cpu.py.  A 9-arc holds two consecutive cardinal points, so a
         // corner needs (b0 | b8) & (b4 | b12) of one polarity.
-        const uint32_t R1 = (t & 1) ? 0x01010101u : 0u;
+        const uint32_t R1 = (t & 1) ? 0x01010101u : 0u, R0 = R1 ^ 0x01010101u;
         const uint32_t M = (uint32_t)(128 - ((t + 1) >> 1)) * 0x01010101u;
+        // dark test without a per-byte NOT (fast_strip_sweep; tests/test_oracle_cpu.py): at
+        // t = 255 the byte 256 - M wraps to 0 and every pixel passes, but no score reaches 255
+        const uint32_t M2 = (uint32_t)(128 + ((t + 1) >> 1)) * 0x01010101u;
         int cnt = 0, scored = 0, emitted = 0;
         for (int r0 = 0; r0 < nr; r0 += rps) {
             if (cnt + sweep_max > a.cand_max) {  // wave-uniform
@@ -1605,12 +1610,12 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
                 auto hb = [&](uint32_t c) {
                     return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(c, ncur, R1), M, 0u);
                 };
-                auto hd = [&](uint32_t c) {
-                    return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(cur, ~c, R1), M, 0u);
+                auto xd = [&](uint32_t c) {  // NOT (c < v - t) in the high bits
+                    return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(c, ncur, R0), M2, 0u);
                 };
                 const uint32_t br = (hb(dn) | hb(up)) & (hb(c4) | hb(c12));
-                const uint32_t dk = (hd(dn) | hd(up)) & (hd(c4) | hd(c12));
-                fl = (br | dk) & vmask;
+                const uint32_t xk = (xd(dn) & xd(up)) | (xd(c4) & xd(c12));
+                fl = (br | ~xk) & vmask;
             }
             const unsigned long long b0 = __ballot(fl & 0x80u), b1 = __ballot(fl & 0x8000u),
                                      b2 = __ballot(fl & 0x800000u), b3 = __ballot(fl & 0x80000000u);
@@ -1651,6 +1656,398 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
 
 template __global__ void fast_kernel<0>(FastArgs);
 template __global__ void fast_kernel<kFastPitch>(FastArgs);
+
+// ---------------------------------------------------------------------------------------------
+// K2, strip form (default): one 256-thread workgroup per run of 1, 2, 4 or 8 cells of one cell
+// row (one workgroup per (frame, level, cell-row strip)).  The run's ROI —
+// every ROI row of the cell row over the run's columns, neighbouring cells' 6-column overlaps
+// shared — is staged once.  Then:
+//   phase 1 (all four waves, a block of candidate rows each): the pre-test at iniThFAST over
+//     whole run rows (64 / gpr rows per sweep, so 8 / 4 / 2 / 1-cell runs keep ~97 % of the
+//     lanes busy), survivors appended to the wave's list — in no particular order: a score does
+//     not depend on its neighbours — and scored 64 at a time (fast_S) into the run's score
+//     plane; scores >= iniThFAST are appended to the wave's corner list;
+//   phase 2a (all waves): the strict 3x3 NMS of each corner against the score plane, neighbours
+//     outside the corner's cell taken as 0 (H1: cv::FAST on the cell ROI, ORBextractor.cc:
+//     808-815), keepers marked in a bitmap and counted per cell;
+//   phase 2b (a wave per cell): the cell's marks read row by row (lane = row) and written to
+//     the cell's slot in row-major order; an empty cell reruns the pre-test and scoring at
+//     minThFAST over its own columns and emits by the bitmap path (811-815).
+// A corner list that overflows (noise frames at low thresholds) switches the run to the bitmap
+// path for every cell: corners marked from the score plane, NMS and emission per cell.
+__device__ __forceinline__ unsigned lane_below(unsigned long long b, unsigned acc) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, acc));
+}
+constexpr int kChunkClist = 128;  // per-wave corner list entries (more: the bitmap path)
+
+// Pre-test at threshold t (< 255) over candidate rows [ra, re) of a region of gpr <= 64 groups
+// per row (group lg covers ROI columns 4 (g0 + lg) .. + 3; bytes outside the candidate columns
+// masked by vfirst (group 0) / vlast (group gpr - 1)), rps = 64 / gpr rows per sweep.  Survivors
+// are scored into S (max(S, -1) + 1 at o + P + 1, o = r P + c) and scores >= tb either appended
+// to clist (when clist != null: returns -1 if it overflowed, else its length) or marked in the
+// bitmap (bit c of row r).  `list`: the wave's kChunkList entries + 64 trash slots.  Every lane
+// of the wave calls it.
+__device__ __forceinline__ int fast_strip_sweep(const uint8_t* roi, uint8_t* S, uint32_t* bm,
+                                                uint16_t* list, uint16_t* clist, int ra, int re,
+                                                int gpr, int g0, int X0, uint32_t vfirst,
+                                                uint32_t vlast, int t, int tb) {
+    constexpr int P = kChunkP, P4 = kChunkP / 4;
+    const int lane = threadIdx.x & 63;
+    const unsigned inv_p = 0xffffffffu / (unsigned)P + 1u;
+    // bright: c - v > t  <=>  the high bit of lerp(lerp(c, ~v, R1), M, 0) (DESIGN.md "FAST");
+    // dark: v - c > t  <=>  NOT the high bit of lerp(lerp(c, ~v, R1 ^ 1), 256 - M, 0): the dark
+    // test's lerp(v, ~c, R1) is ~lerp(c, ~v, R1 ^ 1), so no per-byte NOT is needed (checked for
+    // every c, v, t < 255 in tests/test_oracle_cpu.py)
+    const uint32_t R1 = (t & 1) ? 0x01010101u : 0u, R0 = R1 ^ 0x01010101u;
+    const uint32_t M = (uint32_t)(128 - ((t + 1) >> 1)) * 0x01010101u;
+    const uint32_t M2 = (uint32_t)(128 + ((t + 1) >> 1)) * 0x01010101u;
+    const uint32_t* lds32 = reinterpret_cast<const uint32_t*>(roi);
+    const uint8_t* cen = roi + X0 + 3 * P;  // candidate (0, 0)
+    // this lane's place in a sweep: row lr of the sweep, group lg
+    const int rps = 64 / gpr;
+    const int lr = lane / gpr, lg = lane - lr * gpr;
+    uint32_t vm = lr < rps ? 0x80808080u : 0u;
+    if (lg == 0) vm &= vfirst;
+    if (lg == gpr - 1) vm &= vlast;
+    const int wl = (lr + 3) * P4 + g0 + lg;       // dword of the group's centres, row ra + lr
+    const int obl = lr * P + 4 * (g0 + lg) - X0;  // candidate offset of the group's byte 0
+    int cnt = 0, done = 0, ncl = 0;
+    auto score = [&](int n) {  // list[done .. done + n), n <= 64
+        int o = 0, sv = 0;
+        if (lane < n) {
+            o = list[done + lane];
+            sv = max(fast_S(cen + o, P), -1) + 1;
+            S[o + P + 1] = (uint8_t)sv;
+        }
+        const bool corner = lane < n && sv >= tb;
+        if (clist) {
+            const unsigned long long cm = __ballot(corner);
+            if (corner) {
+                const int slot = (int)lane_below(cm, (unsigned)ncl);
+                if (slot < kChunkClist) clist[slot] = (uint16_t)o;
+            }
+            ncl = __builtin_amdgcn_readfirstlane(ncl + __popcll(cm));
+        } else if (corner) {
+            const int r = (int)__umulhi((unsigned)o, inv_p), c = o - r * P;
+            atomicOr(&bm[r * kChunkBmW + (c >> 5)], 1u << (c & 31));
+        }
+        done += n;
+    };
+    for (int r0 = ra; r0 < re; r0 += rps) {
+        uint32_t fl = 0;
+        const int ob = obl + r0 * P;
+        if (r0 + lr < re) {
+            const int w = wl + r0 * P4;
+            const uint32_t cur = lds32[w], prv = lds32[w - 1], nxt = lds32[w + 1];
+            const uint32_t up = lds32[w - 3 * P4], dn = lds32[w + 3 * P4];
+            const uint32_t c4 = __builtin_amdgcn_alignbyte(nxt, cur, 3);   // column + 3
+            const uint32_t c12 = __builtin_amdgcn_alignbyte(cur, prv, 1);  // column - 3
+            const uint32_t ncur = ~cur;
+            auto hb = [&](uint32_t c) { return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(c, ncur, R1), M, 0u); };
+            auto xd = [&](uint32_t c) { return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(c, ncur, R0), M2, 0u); };
+            const uint32_t br = (hb(dn) | hb(up)) & (hb(c4) | hb(c12));
+            const uint32_t xk = (xd(dn) & xd(up)) | (xd(c4) & xd(c12));  // NOT dark, in the high bits
+            fl = (br | ~xk) & vm;
+        }
+        const bool f0 = (uint8_t)fl >= 0x80u, f1 = (uint8_t)(fl >> 8) >= 0x80u;
+        const bool f2 = (uint8_t)(fl >> 16) >= 0x80u, f3 = (int)fl < 0;
+        const unsigned long long b0 = __ballot(f0), b1 = __ballot(f1), b2 = __ballot(f2), b3 = __ballot(f3);
+        const int n0 = __popcll(b0), n1 = __popcll(b1), n2 = __popcll(b2), n3 = __popcll(b3);
+        if (fl) {  // byte-major positions (byte 0 of every lane, then byte 1, ...); trash slot else
+            const int tr = kChunkList + lane;
+            const int p0 = (int)lane_below(b0, (unsigned)cnt);
+            const int p1 = (int)lane_below(b1, (unsigned)(cnt + n0));
+            const int p2 = (int)lane_below(b2, (unsigned)(cnt + n0 + n1));
+            const int p3 = (int)lane_below(b3, (unsigned)(cnt + n0 + n1 + n2));
+            list[f0 ? p0 : tr] = (uint16_t)ob;
+            list[f1 ? p1 : tr] = (uint16_t)(ob + 1);
+            list[f2 ? p2 : tr] = (uint16_t)(ob + 2);
+            list[f3 ? p3 : tr] = (uint16_t)(ob + 3);
+        }
+        // (readfirstlane: keeps the counters scalar across the divergent stores above)
+        cnt = __builtin_amdgcn_readfirstlane(cnt + n0 + n1 + n2 + n3);
+        fast_sync();
+        while (cnt - done >= 64) score(64);
+        if (cnt + 256 > kChunkList) {  // make room for a sweep: the < 64 unscored to the front
+            const int rem = cnt - done;
+            const int e = lane < rem ? list[done + lane] : 0;
+            fast_sync();
+            if (lane < rem) list[lane] = (uint16_t)e;
+            fast_sync();
+            cnt = rem;
+            done = 0;
+        }
+    }
+    fast_sync();
+    if (cnt > done) score(cnt - done);
+    fast_sync();
+    return ncl > kChunkClist ? -1 : ncl;
+}
+
+// Bitmap path for one cell: the corner bits of its columns [cs, ce) (scores >= tb) expanded
+// row by row into the wave's list, the strict 3x3 NMS on the score plane with neighbours outside
+// the cell as 0 (H1), survivors -> out[] in row-major order.  Returns the number found (stores
+// stop at cap).  kx / ky: key coordinates of candidate (0, 0).  Every lane of the wave calls it.
+__device__ __forceinline__ int fast_strip_emit(const uint8_t* S, const uint32_t* bm, uint16_t* list,
+                                               int nr, int cs, int ce, int tb, int kx, int ky,
+                                               uint32_t* out, int cap) {
+    constexpr int P = kChunkP;
+    const int lane = threadIdx.x & 63;
+    const unsigned inv_p = 0xffffffffu / (unsigned)P + 1u;
+    const int d0 = cs >> 5, sh = cs & 31, wd = ce - cs;  // wd < 64 (cells are < 60 wide)
+    const unsigned long long wmask = (1ull << wd) - 1;
+    int emitted = 0;
+    for (int rb = 0; rb < nr; rb += 64) {
+        const int r = rb + lane;
+        unsigned long long m = 0;
+        if (r < nr) {
+            const uint32_t* row = bm + r * kChunkBmW + d0;
+            unsigned long long v = (unsigned long long)row[0] | ((unsigned long long)row[1] << 32);
+            if (sh) v = (v >> sh) | ((unsigned long long)row[2] << (64 - sh));
+            m = v & wmask;
+        }
+        const int n = __popcll(m);
+        const int inc = wave_inclusive_sum(n);
+        const int tot = __builtin_amdgcn_readlane(inc, 63);
+        for (int lo = 0; lo < tot; lo += kChunkList) {  // one batch unless > kChunkList corners
+            int pos = inc - n - lo;
+            unsigned long long mm = m;
+            const int rowo = r * P + cs;
+            while (__ballot(mm != 0 && pos < kChunkList)) {
+                if (mm != 0 && pos < kChunkList) {
+                    if (pos >= 0) list[pos] = (uint16_t)(rowo + (int)__builtin_ctzll(mm));
+                    ++pos;
+                    mm &= mm - 1;
+                }
+            }
+            const int nb = min(tot - lo, kChunkList);
+            fast_sync();
+            for (int i0 = 0; i0 < nb; i0 += 64) {
+                const int i = i0 + lane;
+                bool keep = false;
+                uint32_t key = 0;
+                if (i < nb) {
+                    const int o = list[i];
+                    const uint8_t* q = S + o + P + 1;
+                    const int s = q[0];
+                    const int rr = (int)__umulhi((unsigned)o, inv_p), c = o - rr * P;
+                    const int mid = max(q[-P], q[P]);
+                    const int lft = max(max(q[-P - 1], q[-1]), q[P - 1]);
+                    const int rgt = max(max(q[-P + 1], q[1]), q[P + 1]);
+                    const int nbm = max(mid, max(c > cs ? lft : 0, c + 1 < ce ? rgt : 0));
+                    keep = s >= tb && nbm < s;
+                    key = pack_key(kx + c, ky + rr, s - 1);
+                }
+                const unsigned long long km = __ballot(keep);
+                if (keep) {
+                    const int slot = (int)lane_below(km, (unsigned)emitted);
+                    if (slot < cap) out[slot] = key;
+                }
+                emitted += __popcll(km);
+            }
+            fast_sync();
+        }
+    }
+    return emitted;
+}
+
+// The cell's NMS survivors, already marked in the bitmap (phase 2a), to out[] in row-major
+// order: lane = row, each row's marks (usually 0-2) written in column order.
+__device__ __forceinline__ int fast_strip_emit_marked(const uint8_t* S, const uint32_t* bm, int nr,
+                                                      int cs, int ce, int kx, int ky, uint32_t* out,
+                                                      int cap) {
+    constexpr int P = kChunkP;
+    const int lane = threadIdx.x & 63;
+    const int d0 = cs >> 5, sh = cs & 31, wd = ce - cs;
+    const unsigned long long wmask = (1ull << wd) - 1;
+    int emitted = 0;
+    for (int rb = 0; rb < nr; rb += 64) {
+        const int r = rb + lane;
+        unsigned long long m = 0;
+        if (r < nr) {
+            const uint32_t* row = bm + r * kChunkBmW + d0;
+            unsigned long long v = (unsigned long long)row[0] | ((unsigned long long)row[1] << 32);
+            if (sh) v = (v >> sh) | ((unsigned long long)row[2] << (64 - sh));
+            m = v & wmask;
+        }
+        const int n = __popcll(m);
+        const int inc = wave_inclusive_sum(n);
+        int pos = emitted + inc - n;
+        const uint8_t* srow = S + r * P + P + 1 + cs;
+        while (m) {
+            const int c = (int)__builtin_ctzll(m);
+            if (pos < cap) out[pos] = pack_key(kx + cs + c, ky + r, srow[c] - 1);
+            ++pos;
+            m &= m - 1;
+        }
+        emitted += __builtin_amdgcn_readlane(inc, 63);
+    }
+    return emitted;
+}
+
+#ifdef ORBFE_FAST_TIMING
+// diagnostic build only: per (frame < 64, run < 160) phase clocks of fast_strip_kernel
+__device__ long long g_fast_t[64 * 160 * 16];
+#define FS_MARK(i) do { if (lane == 0 && ftm) ftm[(i)] = clock64(); } while (0)
+#define FS_PUT(i, v) do { if (lane == 0 && ftm) ftm[(i)] = (v); } while (0)
+#else
+#define FS_MARK(i) do { } while (0)
+#define FS_PUT(i, v) do { } while (0)
+#endif
+
+__global__ __launch_bounds__(kChunkBlock) void fast_strip_kernel(FastArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char fs_lds[];
+    constexpr int P = kChunkP;
+    constexpr int NW = kChunkBlock / 64;
+    int ci, f;
+    xcd_block(ci, f);
+#ifdef ORBFE_FAST_TIMING
+    long long* ftm = (f < 64 && ci < 160) ? g_fast_t + ((long long)f * 160 + ci) * 16 : nullptr;
+#endif
+    const FastChunk& ch = a.chunks[ci];
+    // wv through readfirstlane: the wave index is wave-uniform, and the loops, list counters and
+    // branches derived from it stay scalar (otherwise the compiler runs them as divergent)
+    const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int R = a.roi_rows;  // the carve's ROI rows (tallest run)
+    // carve: ROI | score plane | bitmap | column info | per-cell counts + flag | lists | corner lists
+    uint8_t* roi = fs_lds;
+    uint8_t* S = fs_lds + R * P;
+    uint32_t* bm = reinterpret_cast<uint32_t*>(S + (R - 4) * P);
+    uint8_t* cinfo = reinterpret_cast<uint8_t*>(bm) + ((((R - 6) * kChunkBmW * 4) + 15) & ~15);
+    int* ccount = reinterpret_cast<int*>(cinfo + P);  // [kChunkCells] + the overflow flag
+    uint16_t* list = reinterpret_cast<uint16_t*>(ccount + 16) + wv * (kChunkList + 64);
+    uint16_t* clist = reinterpret_cast<uint16_t*>(ccount + 16) + NW * (kChunkList + 64) + wv * kChunkClist;
+    const int level = ch.level, nr = ch.nr, nc = ch.nc, X0 = ch.X0, g0 = ch.g0, gpr = ch.gpr;
+    const int ncell = ch.ncell;
+    const bool any = nr > 0 && nc > 0;
+    const LevelPtr lp = a.pyr[level];
+    const int t1 = a.ini_th, t2 = a.min_th;
+    if (wv == 0) FS_MARK(0);
+    // ---- phase 0: the ROI rows (16-byte loads, 4 per thread in flight), a zero score plane and
+    // bitmap, the column -> cell table.  A row's last load ends < 16 bytes past the run's x1 <=
+    // maxBorderX, inside the row.
+    if (any) {
+        const int nq = ch.nq, tot = (nr + 6) * nq;
+        const uint8_t* img = lp.base + f * lp.fpitch + (long long)ch.y0 * lp.pitch + ch.x0a;
+        for (int i0 = 0; i0 < tot; i0 += 4 * kChunkBlock) {
+            uint4 v[4];
+            int off[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int i = i0 + k * kChunkBlock + tid;
+                off[k] = -1;
+                if (i < tot) {
+                    // (inv_nq wraps to 0 for nq = 1: umulhi(i, 2^32) = i)
+                    const int r = nq == 1 ? i : (int)__umulhi((unsigned)i, ch.inv_nq), qq = i - r * nq;
+                    v[k] = load16_a4(img + (long long)r * lp.pitch + 16 * qq);
+                    off[k] = r * P + 16 * qq;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (off[k] >= 0) *reinterpret_cast<uint4*>(roi + off[k]) = v[k];
+        }
+        for (int i = tid; i < ((nr + 2) * P) >> 4; i += kChunkBlock)
+            reinterpret_cast<uint4*>(S)[i] = make_uint4(0u, 0u, 0u, 0u);
+        for (int i = tid; i < nr * kChunkBmW; i += kChunkBlock) bm[i] = 0u;
+        // candidate column -> cell j | 0x10 (the cell's first column) | 0x20 (its last)
+        for (int c = tid; c < nc; c += kChunkBlock) {
+            int j = 0;
+            while (j + 1 < ncell && c >= ch.cs[j + 1]) ++j;
+            cinfo[c] = (uint8_t)(j | (c == ch.cs[j] ? 0x10 : 0) | (c + 1 == ch.cs[j + 1] ? 0x20 : 0));
+        }
+    }
+    if (tid < 16) ccount[tid] = 0;
+    if (wv == 0) FS_MARK(1);
+    __syncthreads();
+    if (wv == 0) FS_MARK(2);
+    // ---- phase 1: pre-test + scores at iniThFAST over the whole run, rows in 4 blocks
+    int ncl = 0;
+    if (any && t1 < 255) {
+        const int rps = 64 / gpr;
+        const int rbw = ((nr + rps - 1) / rps + NW - 1) / NW * rps;  // rows per wave, whole sweeps
+        const int lo = X0 - 4 * g0, hi = X0 + nc - 4 * (g0 + gpr - 1);  // 0..3, 1..4
+        const uint32_t vfirst = 0x80808080u << (8 * lo), vlast = 0x80808080u >> (8 * (4 - hi));
+        ncl = fast_strip_sweep(roi, S, bm, list, clist, min(wv * rbw, nr), min((wv + 1) * rbw, nr),
+                               gpr, g0, X0, vfirst, vlast, t1, max(t1, 1) + 1);
+        if (ncl < 0 && lane == 0) ccount[kChunkCells] = 1;  // a corner list overflowed
+    }
+    FS_MARK(3 + wv);
+    __syncthreads();
+    const bool marked = __builtin_amdgcn_readfirstlane(ccount[kChunkCells]) == 0;  // else the bitmap path
+    const int tb1 = max(t1, 1) + 1;
+    // ---- phase 2a: NMS of the wave's corners (any order), keepers marked and counted per cell
+    if (any && t1 < 255) {
+        if (marked) {
+            const unsigned inv_p = 0xffffffffu / (unsigned)P + 1u;
+            for (int i = lane; i < ncl; i += 64) {
+                const int o = clist[i];
+                const uint8_t* q = S + o + P + 1;
+                const int s = q[0];
+                const int r = (int)__umulhi((unsigned)o, inv_p), c = o - r * P;
+                const int info = cinfo[c];
+                const int mid = max(q[-P], q[P]);
+                const int lft = max(max(q[-P - 1], q[-1]), q[P - 1]);
+                const int rgt = max(max(q[-P + 1], q[1]), q[P + 1]);
+                const int nbm = max(mid, max((info & 0x10) ? 0 : lft, (info & 0x20) ? 0 : rgt));
+                if (nbm < s) {  // s >= tb1 by construction
+                    atomicOr(&bm[r * kChunkBmW + (c >> 5)], 1u << (c & 31));
+                    atomicAdd(&ccount[info & 0xf], 1);
+                }
+            }
+        } else {  // bitmap path: every score >= iniThFAST marked as a corner (dense, 4 per lane)
+            const int cw = (nc + 3) >> 2;
+            const unsigned inv_cw = 0xffffffffu / (unsigned)cw + 1u;  // 0 for cw = 1
+            for (int i = tid; i < nr * cw; i += kChunkBlock) {
+                const int r = cw == 1 ? i : (int)__umulhi((unsigned)i, inv_cw), g = i - r * cw;
+                uint32_t bits = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int c = 4 * g + k;
+                    if (c < nc && S[(r + 1) * P + c + 1] >= tb1) bits |= 1u << k;
+                }
+                const int c0 = 4 * g;
+                if (bits) atomicOr(&bm[r * kChunkBmW + (c0 >> 5)], bits << (c0 & 31));
+            }
+        }
+    }
+    if (wv == 0) FS_MARK(7);
+    __syncthreads();
+    // ---- phase 2b: a wave per cell — ordered emission, the minThFAST rerun if empty
+    const int kx = ch.x0a + X0 - kMinBorder, ky = ch.y0 + 3 - kMinBorder;
+    int wave_total = 0, reruns = 0;
+    for (int j = wv; j < ncell; j += NW) {
+        const int cs = ch.cs[j], ce = ch.cs[j + 1];
+        const CellDesc& cell = a.cells[ch.cell0 + j];
+        uint32_t* out = a.cell_keys + f * a.cell_cap_total + cell.slot;
+        const int cap = cell.cap;
+        int emitted = 0;
+        if (any) {
+            if (t1 < 255)
+                emitted = marked ? (__builtin_amdgcn_readfirstlane(ccount[j]) ? fast_strip_emit_marked(S, bm, nr, cs, ce, kx, ky, out, cap) : 0)
+                                 : fast_strip_emit(S, bm, list, nr, cs, ce, tb1, kx, ky, out, cap);
+            if (emitted == 0 && t2 < 255) {
+                // rerun at minThFAST over the cell's columns (its marks are all 0: no keeper, or
+                // on the bitmap path its corners >= iniThFAST, a subset of those >= minThFAST)
+                ++reruns;
+                const int gb = (X0 + cs) >> 2, ge = (X0 + ce - 1) >> 2, gj = ge - gb + 1;
+                const int lo = X0 + cs - 4 * gb, hi = X0 + ce - 4 * ge;
+                const uint32_t vfirst = 0x80808080u << (8 * lo), vlast = 0x80808080u >> (8 * (4 - hi));
+                fast_strip_sweep(roi, S, bm, list, nullptr, 0, nr, gj, gb, X0, vfirst, vlast, t2,
+                                 max(t2, 1) + 1);
+                emitted = fast_strip_emit(S, bm, list, nr, cs, ce, max(t2, 1) + 1, kx, ky, out, cap);
+            }
+        }
+        const int n = min(emitted, cap);
+        if (lane == 0) a.cell_cnt[f * a.ncells + ch.cell0 + j] = n;
+        wave_total += n;
+    }
+    // the level's key total for the oct-tree (which reads it and resets it to 0)
+    if (lane == 0 && wave_total) atomicAdd(&a.level_keys[f * kMaxLevels + level], wave_total);
+    FS_MARK(8 + wv);
+    FS_PUT(12 + wv, reruns);
+    (void)reruns;
+}
 
 // ---------------------------------------------------------------------------------------------
 // K3 — DistributeOctTree as a data-parallel emulation of the reference's std::list.
@@ -4015,6 +4412,53 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
     if ((long long)rmax * g.roi_pitch >= 65536) return ORBFE_ERR_UNSUPPORTED;
     g.fast_lds = (size_t)rmax * g.roi_pitch + (((rmax - 4) * g.roi_pitch + 15) & ~15) +
                  2 * (size_t)g.cand_max + 16 + 128;  // + a trash slot per lane
+    // fast_strip_kernel runs: each cell row (cells of one level with one y0, consecutive in
+    // g.cells) split greedily into runs of 8, 4, 2 or 1 cells (so 64 / gpr rows per sweep keep
+    // ~97 % of the pre-test lanes busy) whose pre-test groups fit a wave (gpr <= 64) and whose
+    // ROI fits kChunkP bytes
+    g.chunks.clear();
+    int crows = 7;
+    for (size_t i = 0; i < g.cells.size();) {
+        size_t e = i + 1;
+        while (e < g.cells.size() && g.cells[e].level == g.cells[i].level && g.cells[e].y0 == g.cells[i].y0)
+            ++e;
+        for (size_t a = i; a < e;) {
+            FastChunk ch{};
+            for (int k = kChunkCells; k >= 1; k >>= 1) {
+                const size_t b = a + (size_t)k;
+                if (b > e) continue;
+                const CellDesc& c0 = g.cells[a];
+                ch = FastChunk{};
+                ch.level = c0.level;
+                ch.y0 = c0.y0;
+                ch.nr = c0.y1 - c0.y0 - 6;
+                ch.x0a = c0.x0 & ~3;
+                ch.roi_w = g.cells[b - 1].x1 - ch.x0a;
+                ch.X0 = c0.x0 - ch.x0a + 3;
+                ch.nc = g.cells[b - 1].x1 - c0.x0 - 6;
+                ch.g0 = ch.X0 >> 2;
+                ch.gpr = ch.nc > 0 ? ((ch.X0 + ch.nc - 1) >> 2) - ch.g0 + 1 : 1;
+                ch.cell0 = (int)a;
+                ch.ncell = k;
+                if ((ch.gpr <= 64 && ch.roi_w <= kChunkP) || k == 1) break;
+            }
+            if (ch.gpr > 64 || ch.roi_w > kChunkP) return ORBFE_ERR_UNSUPPORTED;  // a cell > 59 px
+            ch.nq = (ch.roi_w + 15) >> 4;
+            ch.inv_nq = 0xffffffffu / (unsigned)ch.nq + 1u;
+            for (int j = 0; j < ch.ncell; ++j) ch.cs[j] = g.cells[a + j].x0 - g.cells[a].x0;
+            ch.cs[ch.ncell] = std::max(ch.nc, 0);
+            crows = std::max(crows, ch.nr + 6);
+            g.chunks.push_back(ch);
+            a += (size_t)ch.ncell;
+        }
+        i = e;
+    }
+    // carve: ROI rows | score plane (rows -1 .. nr) | bitmap | column -> cell table | per-cell
+    // counts | 4 per-wave survivor lists (+ trash) | 4 corner lists
+    g.chunk_rows = crows;
+    g.chunk_lds = (size_t)crows * kChunkP + (size_t)(crows - 4) * kChunkP +
+                  (((size_t)(crows - 6) * kChunkBmW * 4 + 15) & ~(size_t)15) + kChunkP + 64 +
+                  (size_t)(kChunkBlock / 64) * ((kChunkList + 64) * 2 + kChunkClist * 2);
     g.geo.key_total = keys;
     blur_items(g.geo, g.bitems);
     g.geo.out_total = out;
@@ -4036,6 +4480,13 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
 }
 
 }  // namespace orbfe
+
+#ifdef ORBFE_FAST_TIMING
+extern "C" int orbfe_debug_fast_timing(long long* out, int n) {
+    n = n < 64 * 160 * 16 ? n : 64 * 160 * 16;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(orbfe::g_fast_t), (size_t)n * sizeof(long long)) == hipSuccess ? 0 : -3;
+}
+#endif
 
 #ifdef ORBFE_OCT_TIMING
 extern "C" int orbfe_debug_oct_timing(long long* out, int n) {

@@ -165,7 +165,29 @@ struct ResizeTailArgs {
     int simd_xb[kMaxLevels];      // per tail level, as ResizeArgs::simd_xb
 };
 
+// fast_strip_kernel: one workgroup per run of <= kChunkCells consecutive cells of one cell row
+// (SURVEY §7 step 4's layout).  The ROI is every row of the cell row over the run's columns,
+// staged once at the pitch kChunkP; candidate columns c = 0 .. nc - 1 are level columns
+// x0a + X0 + c, candidate rows r = 0 .. nr - 1 level rows y0 + 3 + r.
+constexpr int kChunkP = 272;       // LDS row pitch (ROI rows <= 272 bytes)
+constexpr int kChunkCells = 8;     // cells per run
+constexpr int kChunkBlock = 256;   // 4 waves
+constexpr int kChunkList = 384;    // per-wave survivor list entries (+ 64 trash slots)
+constexpr int kChunkBmW = 11;      // corner-bitmap dwords per candidate row (3-dword windows)
+struct FastChunk {
+    int level;
+    int y0, nr;                    // ROI top row (level coords) = the cells' y0; candidate rows
+    int x0a, roi_w;                // ROI left column (4-byte aligned) and bytes per ROI row
+    int X0, nc;                    // ROI column of candidate column 0 (shift + 3); candidate columns
+    int g0, gpr;                   // pre-test groups: ROI dword of group 0, groups per row
+    int nq;                        // 16-byte loads per ROI row
+    unsigned inv_nq;               // umulhi(i, inv_nq) = i / nq (nq > 1; wraps to 0 for nq = 1)
+    int cell0, ncell;              // the run's cells
+    int cs[kChunkCells + 1];       // cell j's candidate columns [cs[j], cs[j + 1])
+};
+
 struct FastArgs {
+    const FastChunk* chunks;       // fast_strip_kernel
     const CellDesc* cells;
     int ncells;
     long long cell_cap_total;
@@ -269,6 +291,9 @@ struct Plan {
     int oct_keys = 0;      // LDS key capacity of the oct-tree kernel
     int roi_pitch = 0, roi_rows = 0, cand_max = 0;
     size_t fast_lds = 0;
+    std::vector<FastChunk> chunks;  // fast_strip_kernel runs of cells
+    int chunk_rows = 0;             // its LDS carve: ROI rows of the tallest run
+    size_t chunk_lds = 0;
     int rs_tiles_x[kMaxLevels] = {}, rs_tiles[kMaxLevels] = {}, rs_pitch[kMaxLevels] = {};
     size_t rs_lds[kMaxLevels] = {};
     // resize2_kernel plans for the level pairs (l, l + 1): tile table offset (int4 units in ptab)
@@ -317,6 +342,7 @@ template <bool kX86> __global__ void pyramid_roll_kernel(PyrArgs);
 template <bool kX86> __global__ void resize2_kernel(Resize2Args);
 template <bool kX86> __global__ void resizeN_kernel(ResizeNArgs);
 template <int kP> __global__ void fast_kernel(FastArgs);
+__global__ void fast_strip_kernel(FastArgs);
 constexpr int kFastPitch = 48;  // fast_kernel<kFastPitch>: ROI pitch known at compile time
 template <int BLK> __global__ void octree_kernel(OctArgs);
 template <bool kX86> __global__ void blur_mfma_kernel(BlurArgs);

@@ -417,3 +417,17 @@ def test_fast_pretest_lerp_identity():
         dark = ((((v + (255 - c) + r) >> 1) + M) >> 1) >= 128
         assert np.array_equal(bright, c > v + t), t
         assert np.array_equal(dark, c < v - t), t
+
+
+def test_fast_strip_dark_identity():
+    """fast_strip_kernel's dark test without a per-byte NOT: lerp(v, ~c, r) = ~lerp(c, ~v, r ^ 1),
+    so c < v - t equals NOT the high bit of lerp(lerp(c, ~v, (t & 1) ^ 1), 256 - M, 0) with
+    M = 128 - ceil(t / 2), for every byte c, v and threshold t < 255 (t = 255 has no corners and
+    is skipped by the kernel)."""
+    c = np.arange(256)[:, None]
+    v = np.arange(256)[None, :]
+    for t in range(255):
+        r, M = t & 1, 128 - ((t + 1) >> 1)
+        y = (c + (255 - v) + (r ^ 1)) >> 1
+        not_dark = ((y + (256 - M)) >> 1) >= 128
+        assert np.array_equal(~not_dark, c < v - t), t
