@@ -32,6 +32,12 @@ sys.path.insert(0, ROOT)
 ARITH = {"scalar": 0, "x86": 1}  # orbfe_set_arithmetic: ORBFE_ARITH_SCALAR / ORBFE_ARITH_X86_SIMD
 METRIC = "frames/sec ORB extract+match, 640×480 @1000 kp, 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md "HBM3E peak BW 8.0 TB/s spec"
+# VALU issue peak: 256 CUs x 4 SIMD-32 units, a wave64 VALU instruction holds its SIMD for 2
+# cycles (MI355X_MICROARCH.md "Each CU has 4 SIMD-32 units ... over 2 cycles"), 2.4 GHz peak
+# engine clock: 1.2288 T wave-instructions / s
+VALU_PEAK_INSTS = 256 * 4 * 2.4e9 / 2
+# dense FP4 matrix-core peak (MI355X_MICROARCH.md: ~10 PF dense; AMD's 20 PF includes sparsity)
+FP4_PEAK_TFLOPS = 10000.0
 # bf_expand: the batch-shared reference set expanded to FP4 fragments once per match call (its
 # own profiler stage, so bf_match's per-launch figures are the match kernel's alone)
 STAGES = ("mask", "resize", "fast", "octree", "blur", "describe", "bf_match", "bf_expand")
@@ -69,6 +75,30 @@ def algorithmic_bytes(stage: str, w: int, h: int, nkp: float, nref: float = 0.0)
     if stage == "bf_match":  # query + reference descriptors read, 12 B result per query
         return float(32 * (nkp + nref) + 12 * nkp)
     return 0.0
+
+
+def committed_pmc(config: str, arith: str, frames: int) -> tuple[dict, str | None]:
+    """Per-kernel VALU wave-instructions per launch (SQ_INSTS_VALU) from the rocprofv3 --pmc
+    pass of this command committed as profiles/valu_<config>.json (tools/summarize_profile.py):
+    PMC counters cannot be read inside this process.  Empty when absent or for another batch."""
+    path = os.path.join(ROOT, "profiles", f"valu_{config}.json")
+    if not os.path.exists(path):
+        return {}, None
+    with open(path) as fh:
+        j = json.load(fh)
+    if j.get("frames_per_launch") != frames:
+        return {}, None
+    suf = "" if arith == "scalar" else f"@{arith}"
+    out = {k[:-len(suf)] if suf else k: v for k, v in j.items()
+           if isinstance(v, dict) and (k.endswith(suf) if suf else "@" not in k)}
+    return out, f"profiles/valu_{config}.json ({j.get('source', 'rocprofv3 --pmc SQ_INSTS_VALU')})"
+
+
+# bench stage -> the kernels that implement it (the stage's launches in a step)
+STAGE_KERNELS = {"resize": ("pyramid_kernel", "resize2_kernel", "resize_kernel", "resize_tail_kernel"),
+                 "fast": ("fast_kernel", "fast_strip_kernel"), "octree": ("octree_kernel",),
+                 "describe": ("describe_kernel",), "bf_match": ("bf_match_fp4e_kernel", "bf_match_fp4_kernel",
+                                                             "bf_match_kernel")}
 
 
 def host_cpu() -> dict:
@@ -633,6 +663,38 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
             "leg": (f"{K} single-stream steps of {B} frames after the timed region, HIP events on "
                     f"the {dom} launches only (the timed steps run {S} sub-batch streams, "
                     "uninstrumented)")}
+    # the binding resources: VALU issue (SQ_INSTS_VALU of the committed PMC pass over the
+    # launch's event time) for the dominant kernel and each stage, and the matrix cores for the
+    # brute force (algorithmic FP4 flops: 2 x 256 per (query, reference) pair)
+    pmc, pmc_src = committed_pmc(args.config, args.arith, B)
+
+    def valu_of(stage, ms, launches):
+        ks = [k for k in STAGE_KERNELS.get(stage, ()) if k in pmc]
+        if not ks or ms <= 0 or launches <= 0:
+            return None
+        # a stage of several kernels (the 1080p pyramid): their launch-weighted mean
+        nd = sum(pmc[k]["dispatches"] for k in ks)
+        per = sum(pmc[k]["valu_per_launch"] * pmc[k]["dispatches"] for k in ks) / max(nd, 1)
+        rate = per * launches / (ms / 1e3)
+        return {"kernel": "+".join(ks), "insts_per_launch": round(per),
+                "achieved": round(rate / 1e12, 4), "peak": round(VALU_PEAK_INSTS / 1e12, 4),
+                "unit": "T wave-instructions/s", "frac": round(rate / VALU_PEAK_INSTS, 4)}
+    if dom:
+        v = valu_of(dom, dom_ms, dom_launches)
+        if v:
+            v["source"] = pmc_src
+        roof["valu"] = v
+    mfma = None
+    if mode in ("ref", "pred") and per_step.get("bf_match", 0) > 0:
+        pairs = nkp * (nref if mode == "ref" else nkp) * B  # (query, reference) pairs per step
+        flops = 2.0 * 256 * pairs
+        tfl = flops / (per_step["bf_match"] / 1e3) / 1e12
+        mfma = {"kernel": "bf_match_fp4e_kernel" if mode == "ref" else "bf_match_fp4_kernel",
+                "flops_per_step": round(flops), "ms_per_step": round(per_step["bf_match"], 4),
+                "achieved": round(tfl, 1), "peak": FP4_PEAK_TFLOPS, "unit": "TFLOP/s (FP4, dense)",
+                "frac": round(tfl / FP4_PEAK_TFLOPS, 4),
+                "note": "algorithmic flops (2 x 256 per query x reference pair) over the probe "
+                        "steps' event time; the padded tiles the kernel computes are not counted"}
     value = world * B * K / dt
     nq = NF if mode != "none" else 0
     e2e = e2e_bytes(W, H, NF, nq, NREF if mode == "ref" else (NF if mode == "pred" else 0))
@@ -644,9 +706,14 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
         ab = algorithmic_bytes(s_, W, H, nkp, nref) * B
         if ms > 0 and ab > 0:
             gbs = ab / (ms / 1e3) / 1e9
-            stage_roof[f"{s_}_kernel" if s_ != "resize" else "pyramid_kernel"] = {
+            ent = stage_roof[f"{s_}_kernel" if s_ != "resize" else "pyramid_kernel"] = {
                 "ms_per_step": round(ms, 4), "bytes_per_step": round(ab),
                 "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+            v = valu_of(s_, probe[s_][0], probe[s_][1])
+            if v:
+                ent["valu_frac"] = v["frac"]
+    if mfma:
+        roof["mfma"] = mfma
     return {"value": value, "dt": dt, "K": K, "B": B, "S": S, "J": J, "nkp": nkp, "soak": soak,
             "roofline": roof, "per_step": per_step, "probe_steps": probe_steps,
             "stage_roofline": stage_roof,

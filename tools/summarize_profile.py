@@ -90,6 +90,10 @@ for n in sorted(fetch):
     stage = n.replace("_kernel", "")
     traffic[stage] = round(2 * f + w)
 json.dump(summary, open(os.path.join(DST, "pmc_summary.json"), "w"), indent=1)
+# VALU wave-instructions per bench-shape launch (SQ_INSTS_VALU is summed over the dispatch's
+# waves): bench.py's roofline.valu and stage_roofline valu_frac read them
+valu = {n: {"valu_per_launch": round(s_.get("SQ_INSTS_VALU", 0.0)), "waves_per_launch": round(s_.get("SQ_WAVES", 0.0)),
+            "dispatches": int(s_["dispatches"])} for n, s_ in sq.items() if "SQ_INSTS_VALU" in s_}
 CONF = next((c for c in ("c2", "c3", "c4") if f"--config {c}" in open(
     os.path.join(SRC, "bench_args.txt")).read()), "c3") if os.path.exists(
     os.path.join(SRC, "bench_args.txt")) else "c3"
@@ -102,6 +106,14 @@ tj.update({(k if ARITH == "scalar" else f"{k}@{ARITH}"): v for k, v in traffic.i
 tj["frames_per_launch"] = FRAMES
 tj["source"] = f"profiles/{R}: rocprofv3 --pmc, 2 x FETCH_SIZE + WRITE_SIZE per launch"
 json.dump(tj, open(tpath, "w"), indent=1)
+vpath = os.path.join(ROOT, "profiles", f"valu_{CONF}.json")
+vj = json.load(open(vpath)) if os.path.exists(vpath) else {}
+if vj.get("frames_per_launch") not in (None, FRAMES):
+    vj = {}
+vj.update({(k if ARITH == "scalar" else f"{k}@{ARITH}"): v for k, v in valu.items()})
+vj["frames_per_launch"] = FRAMES
+vj["source"] = f"profiles/{R}: rocprofv3 --pmc SQ_INSTS_VALU per launch"
+json.dump(vj, open(vpath, "w"), indent=1)
 for n, v in summary.items():
     print(n, v)
 
