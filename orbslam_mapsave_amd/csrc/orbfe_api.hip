@@ -217,8 +217,16 @@ struct orbfe_extractor {
     bool roll_small = force_roll || (std::getenv("ORBFE_ROLL") && std::atoi(std::getenv("ORBFE_ROLL")) >= 2);
     // ORBFE_PYR_SMALL_BELOW (A/B): batches below it take the small-batch band plans (thin bands)
     int pyr_small_below = std::getenv("ORBFE_PYR_SMALL_BELOW") ? std::atoi(std::getenv("ORBFE_PYR_SMALL_BELOW")) : kTailMinFrames;
+    // Batches of >= pyr_small_below frames take the per-level kernels (resize2 pairs + the
+    // one-workgroup tail) even where the band plan is the faster path alone: under the bench's
+    // two sub-batch streams the band kernel's 1024-thread, 80 KB workgroups find few CUs free
+    // beside the other stream's FAST / describe waves (a 256-frame launch stretched to 0.70 ms
+    // against 0.154 alone), the per-level kernels' 256-thread workgroups co-reside: c3 365.4 K
+    // -> 368.7 K frames/s (profiles/r05/pyramid_overlap/).  ORBFE_PYR_BATCH=band restores it.
+    bool pyr_batch_band = std::getenv("ORBFE_PYR_BATCH") && std::strcmp(std::getenv("ORBFE_PYR_BATCH"), "band") == 0;
     bool band_path(int n) const {  // run() makes the pyramid with pyramid_kernel for n frames
         const int which = n >= pyr_small_below ? 0 : 1;
+        if (which == 0 && !pyr_batch_band && !force_pyr) return false;
         return plan.pyr_ok && (plan.pyr_use[which] || force_pyr) && use_pyr && !force_roll &&
                !(fused_blur && resize_blur) && plan.geo.nlevels >= 2;
     }
@@ -252,7 +260,7 @@ struct orbfe_extractor {
     // ORBFE_FAST_STRIP=1: FAST as a workgroup per run of a cell row's cells (fast_strip_kernel,
     // SURVEY §7 step 4's layout) instead of one wave per cell (fast_kernel).  Bit-exact, but
     // measured slower: c3 FAST 0.463 -> 0.834 ms per 512 frames, c4 1.86 -> 3.00 ms per 256
-    // (more VALU per frame, 696 K vs 547 K, and each workgroup's ROI load and
+    // (more VALU per frame, 667 K vs 547 K, and each workgroup's ROI load and
     // barriers exposed at 24 waves per CU)
     bool fast_strip = std::getenv("ORBFE_FAST_STRIP") && std::strcmp(std::getenv("ORBFE_FAST_STRIP"), "1") == 0;
     int desc_g16 = std::getenv("ORBFE_DESC_G16") ? std::atoi(std::getenv("ORBFE_DESC_G16")) : 0;

@@ -105,13 +105,17 @@ def test_roll_column_tiles_sizes(size, cols, monkeypatch):
         e.close()
 
 
-@pytest.mark.parametrize("size,batch,path", [((640, 480), 1, "bands"), ((640, 480), 9, "bands"),
-                                             ((1920, 1080), 1, "bands"), ((1920, 1080), 9, "per_level")])
-def test_default_paths(size, batch, path, monkeypatch):
-    """The pyramid path each shape takes by default (the measured choices of DESIGN.md §5e)."""
+@pytest.mark.parametrize("size,batch,path,env", [((640, 480), 1, "bands", None), ((640, 480), 9, "per_level", None),
+                                                 ((640, 480), 9, "bands", "band"),
+                                                 ((1920, 1080), 1, "bands", None), ((1920, 1080), 9, "per_level", None)])
+def test_default_paths(size, batch, path, env, monkeypatch):
+    """The pyramid path each shape takes by default (the measured choices of DESIGN.md §5e, §5g:
+    batches take the per-level kernels, ORBFE_PYR_BATCH=band the band kernel where it plans)."""
     from orbslam_mapsave_amd.native import ORBextractor
-    for v in ("ORBFE_PYR", "ORBFE_ROLL", "ORBFE_ROLL_BANDS", "ORBFE_ROLL_CHUNK"):
+    for v in ("ORBFE_PYR", "ORBFE_ROLL", "ORBFE_ROLL_BANDS", "ORBFE_ROLL_CHUNK", "ORBFE_PYR_BATCH"):
         monkeypatch.delenv(v, raising=False)
+    if env:
+        monkeypatch.setenv("ORBFE_PYR_BATCH", env)
     w, h = size
     nf = 2000 if w > 1000 else 1000
     e = ORBextractor(nf, 1.2, 8, 20, 7, device=0, max_width=w, max_height=h)
