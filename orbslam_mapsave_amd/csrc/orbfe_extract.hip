@@ -1419,6 +1419,30 @@ __device__ __forceinline__ int lane_prefix(unsigned long long mask) {
     return __popcll(mask & ((1ull << (threadIdx.x & 63)) - 1));
 }
 
+// The pre-test's per-byte flags (bit 7 of each byte of fl) as lane masks: one SDWA compare of
+// the sign-extended byte each (the compiler's form is a v_bfe and a v_cmp per byte).  The
+// compare honours exec like any VOPC: inactive lanes read 0.
+template <int kB>
+__device__ __forceinline__ unsigned long long byte_ballot(uint32_t fl) {
+    unsigned long long m;
+    if constexpr (kB == 0)
+        asm("v_cmp_lt_i32_sdwa %0, sext(%1), 0 src0_sel:BYTE_0 src1_sel:DWORD" : "=s"(m) : "v"(fl));
+    else if constexpr (kB == 1)
+        asm("v_cmp_lt_i32_sdwa %0, sext(%1), 0 src0_sel:BYTE_1 src1_sel:DWORD" : "=s"(m) : "v"(fl));
+    else if constexpr (kB == 2)
+        asm("v_cmp_lt_i32_sdwa %0, sext(%1), 0 src0_sel:BYTE_2 src1_sel:DWORD" : "=s"(m) : "v"(fl));
+    else
+        m = __ballot((int)fl < 0);
+    return m;
+}
+// b where this lane's bit of m is set, else a: one v_cndmask on the lane mask itself (a
+// ballot's SGPR pair), no per-lane compare to rebuild the condition.
+__device__ __forceinline__ int lane_select(unsigned long long m, int a, int b) {
+    int r;
+    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
+}
+
 // Ordered emission of the NMS survivors at threshold t among the compacted candidates.
 //
 // Candidates are ROI offsets o = r * P + c of their window's top-left (row-major order), and
@@ -1617,8 +1641,8 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
                 const uint32_t xk = (xd(dn) & xd(up)) | (xd(c4) & xd(c12));
                 fl = (br | ~xk) & vmask;
             }
-            const unsigned long long b0 = __ballot(fl & 0x80u), b1 = __ballot(fl & 0x8000u),
-                                     b2 = __ballot(fl & 0x800000u), b3 = __ballot(fl & 0x80000000u);
+            const unsigned long long b0 = byte_ballot<0>(fl), b1 = byte_ballot<1>(fl),
+                                     b2 = byte_ballot<2>(fl), b3 = byte_ballot<3>(fl);
             if (fl) {  // row-major: earlier lanes, then this lane's lower bytes
                 auto below = [](unsigned long long b, uint32_t acc) {  // popc(b & lanes below)
                     return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
@@ -1627,16 +1651,17 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
                 int pos = (int)below(b3, below(b2, below(b1, below(b0, (uint32_t)cnt))));
                 const int ob = cr * P + gx - X0;  // ROI offset of byte 0's window
                 // unconditional stores (no exec-mask branch per byte): a byte that is not a
-                // survivor writes the lane's trash slot past the list
+                // survivor writes the lane's trash slot past the list; the slot is chosen by the
+                // byte's ballot mask directly
                 const int tr = a.cand_max + lane;
-                const int f0 = (fl >> 7) & 1, f1 = (fl >> 15) & 1, f2 = (fl >> 23) & 1, f3 = fl >> 31;
-                list[f0 ? pos : tr] = (uint16_t)ob;
+                const int f0 = (fl >> 7) & 1, f1 = (fl >> 15) & 1, f2 = (fl >> 23) & 1;
+                list[lane_select(b0, tr, pos)] = (uint16_t)ob;
                 pos += f0;
-                list[f1 ? pos : tr] = (uint16_t)(ob + 1);
+                list[lane_select(b1, tr, pos)] = (uint16_t)(ob + 1);
                 pos += f1;
-                list[f2 ? pos : tr] = (uint16_t)(ob + 2);
+                list[lane_select(b2, tr, pos)] = (uint16_t)(ob + 2);
                 pos += f2;
-                list[f3 ? pos : tr] = (uint16_t)(ob + 3);
+                list[lane_select(b3, tr, pos)] = (uint16_t)(ob + 3);
             }
             cnt += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
         }
