@@ -648,6 +648,14 @@ __global__ __launch_bounds__(256) void resizeN_kernel(ResizeNArgs a) {
 // Column-pass rounding.  The sums carry 0x7fff; the scalar FixedPtCastEx (sum + 2^15) >> 16
 // adds one more, the x86 SIMD body (H6: float sum, exact below 2^24, _mm_cvtps_epi32) rounds
 // half to even: (sum + 0x7fff + bit 16 of sum) >> 16.  v = sum + 0x7fff.
+// Lanes whose 32-bit blur sum (+ 0x7fff) has the low half 0xffff — a tie of the x86 body's
+// round half to even — as a lane mask: one v_cmp_eq_u16 (the inline constant -1 is 0xffff at
+// 16 bits).
+__device__ __forceinline__ unsigned long long tie_lanes(uint32_t v) {
+    unsigned long long m;
+    asm("v_cmp_eq_u16_e64 %0, -1, %1" : "=s"(m) : "v"(v));
+    return m;
+}
 __device__ __forceinline__ uint32_t blur_round_bit(uint32_t v, bool even) {
     return even ? ((v - 0x7fffu) >> 16) & 1u : 1u;
 }
@@ -3547,6 +3555,9 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
                 Bhi[3] = 0;
                 // x86: 1 where the column is in the SIMD body (round half to even), else 0
                 const uint32_t em = xs + 16 * s < 0 ? 1u : 0u, nem = 1u - em;
+                // the tile's columns all in the SIMD body (wave-uniform): then only a tie needs
+                // the fix-up below
+                const bool body = !kX86 || __ballot(em == 0u) == 0ull;
                 i32x4m Vs[3];  // (kFragLds & 4: the three V fragments read once per N-tile)
                 if constexpr ((kFragLds & 4) != 0) {
 #pragma unroll
@@ -3560,13 +3571,19 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
                     const i32x4m Dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(Vu, Blo, Kc, 0, 0, 0);
                     uint32_t s4[4];
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        s4[i] = ((uint32_t)Dh[i] << 8) + (uint32_t)Dl[i];
+                    for (int i = 0; i < 4; ++i) s4[i] = ((uint32_t)Dh[i] << 8) + (uint32_t)Dl[i];
+                    if constexpr (kX86) {
                         // x86 (kRndM = 0x7fff): + bit 16 of the sum in the SIMD body, + 1 past
                         // it.  The bit of sum + 0x7fff equals the true sum's bit 16 in the only
-                        // case it matters (a tie, low half 0x8000), and adding it elsewhere
-                        // changes no carry: v_bfe with width em (0 or 1), then one v_add3
-                        if constexpr (kX86) s4[i] = s4[i] + __builtin_amdgcn_ubfe(s4[i], 16u, em) + nem;
+                        // case it matters (a tie, low half 0x8000 -> 0xffff), and adding it
+                        // elsewhere changes no carry: v_bfe with width em (0 or 1), then one
+                        // v_add3 — run only when some lane's sum is a tie or the tile reaches
+                        // the scalar tail (one v_cmp_eq_u16 per sum instead of the two VALU of
+                        // the fix-up; ties are ~1 in 65,536 sums)
+                        if (!body || (tie_lanes(s4[0]) | tie_lanes(s4[1]) | tie_lanes(s4[2]) | tie_lanes(s4[3]))) {
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) s4[i] = s4[i] + __builtin_amdgcn_ubfe(s4[i], 16u, em) + nem;
+                        }
                     }
                     // min(sum >> 16, 255) of two sums at once (sum >> 16 <= 257 < 2^16)
                     const us2 sat = us2{255, 255};
