@@ -121,6 +121,10 @@ struct orbfe_matcher {
                           &g_t0, &g_t1, &g_t2, &g_dec, &g_chg, &g_last, &g_bins, &g_hist, &done_ctr})
             b->release();
         for (auto& kv : bf_e) kv.second.release();
+        for (SbpGraph& sg : sbp_graph) {
+            if (sg.exec) hipGraphExecDestroy(sg.exec);
+            if (sg.graph) hipGraphDestroy(sg.graph);
+        }
         prof.release();
         if (own) hipStreamDestroy(own);
         if (stat_host) hipHostFree(stat_host);
@@ -134,6 +138,24 @@ struct orbfe_matcher {
     // accept kernel's last workgroup (null: read back by a D2H copy)
     int* stat_host = nullptr;
     int* stat_dev = nullptr;
+    // ORBFE_SBP_GRAPH=1: SearchLocalPoints' fast path as one HIP graph per form (kPre = 0/1):
+    // the seven launches built once as a chain of kernel nodes; a later call whose arguments,
+    // grids or LDS size differ rewrites only those nodes in the instantiated graph
+    // (hipGraphExecKernelNodeSetParams), so a new pose or frame costs no re-instantiation.
+    // Measured slower than the plain launches (c5 0.104 vs 0.095 ms per call: the kernels run
+    // back to back either way, the replay costs more host time), so off.
+    static constexpr int kSbpNodes = 7;
+    struct SbpGraph {
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t exec = nullptr;
+        hipGraphNode_t node[kSbpNodes] = {};
+        SbpFusedArgs fu{};
+        GreedyArgs g{};
+        dim3 grid[3];
+        size_t shm = 0;
+    };
+    SbpGraph sbp_graph[2];
+    bool sbp_graph_off = !(std::getenv("ORBFE_SBP_GRAPH") && std::strcmp(std::getenv("ORBFE_SBP_GRAPH"), "1") == 0);
     uint8_t* pin = nullptr;
     uint8_t* pin_dev = nullptr;  // the staging buffer's device-mapped address (null: DMA path)
     size_t pin_cap = 0, pin_used = 0;
@@ -495,6 +517,79 @@ int guarded(orbfe_matcher* m, F&& f) {
         return ORBFE_ERR_HIP;
     }
 }
+// sbp_local_fast's launches through the matcher's graph for this form: the fused kernel (grid[0],
+// shm bytes of LDS), rounds - 1 greedy rounds (grid[1]) and the last round + acceptances
+// (grid[2]).  Built on first use; afterwards only the nodes whose arguments or grids changed are
+// rewritten.  false: not launched (graphs off, or the graph could not be built or updated; the
+// caller then launches the kernels itself).
+template <bool kPre>
+bool sbp_local_graph(orbfe_matcher* m, const SbpFusedArgs& fu, const GreedyArgs& g,
+                     const dim3 grid[3], size_t shm, int rounds) {
+    if (m->sbp_graph_off) return false;
+    orbfe_matcher::SbpGraph& G = m->sbp_graph[kPre ? 1 : 0];
+    SbpFusedArgs fu_arg = fu;
+    GreedyArgs g_arg = g;
+    int r_arg[orbfe_matcher::kSbpNodes];
+    void* fu_params[1] = {&fu_arg};
+    void* g_params[orbfe_matcher::kSbpNodes][2];
+    hipKernelNodeParams p[orbfe_matcher::kSbpNodes];
+    for (int k = 0; k < rounds + 1; ++k) {
+        p[k] = hipKernelNodeParams{};
+        if (k == 0) {
+            p[k].func = reinterpret_cast<void*>(&sbp_local_fused_kernel<kPre>);
+            p[k].gridDim = grid[0];
+            p[k].blockDim = dim3(1024);
+            p[k].sharedMemBytes = (unsigned int)shm;
+            p[k].kernelParams = fu_params;
+            continue;
+        }
+        r_arg[k] = k - 1;
+        g_params[k][0] = &g_arg;
+        g_params[k][1] = &r_arg[k];
+        p[k].func = k < rounds ? reinterpret_cast<void*>(&greedy_round_kernel)
+                               : reinterpret_cast<void*>(&greedy_accept_kernel<true>);
+        p[k].gridDim = k < rounds ? grid[1] : grid[2];
+        p[k].blockDim = dim3(kGreedyBlock);
+        p[k].kernelParams = g_params[k];
+    }
+    auto same_dim = [](const dim3& a, const dim3& b) { return a.x == b.x && a.y == b.y && a.z == b.z; };
+    if (!G.exec) {
+        bool ok = hipGraphCreate(&G.graph, 0) == hipSuccess;
+        for (int k = 0; ok && k < rounds + 1; ++k)
+            ok = hipGraphAddKernelNode(&G.node[k], G.graph, k ? &G.node[k - 1] : nullptr, k ? 1 : 0,
+                                       &p[k]) == hipSuccess;
+        ok = ok && hipGraphInstantiate(&G.exec, G.graph, nullptr, nullptr, 0) == hipSuccess;
+        if (!ok) {
+            (void)hipGetLastError();
+            if (G.exec) hipGraphExecDestroy(G.exec);
+            if (G.graph) hipGraphDestroy(G.graph);
+            G = orbfe_matcher::SbpGraph{};
+            m->sbp_graph_off = true;
+            return false;
+        }
+    } else {
+        bool ok = true;
+        if (std::memcmp(&G.fu, &fu, sizeof(fu)) != 0 || !same_dim(G.grid[0], grid[0]) || G.shm != shm)
+            ok = hipGraphExecKernelNodeSetParams(G.exec, G.node[0], &p[0]) == hipSuccess;
+        const bool g_same = std::memcmp(&G.g, &g, sizeof(g)) == 0;
+        for (int k = 1; ok && k < rounds + 1; ++k)
+            if (!g_same || !same_dim(G.grid[k < rounds ? 1 : 2], p[k].gridDim))
+                ok = hipGraphExecKernelNodeSetParams(G.exec, G.node[k], &p[k]) == hipSuccess;
+        if (!ok) {  // drop the graph (rebuilt on the next call); this call launches directly
+            (void)hipGetLastError();
+            hipGraphExecDestroy(G.exec);
+            hipGraphDestroy(G.graph);
+            G = orbfe_matcher::SbpGraph{};
+            return false;
+        }
+    }
+    G.fu = fu;
+    G.g = g;
+    for (int k = 0; k < 3; ++k) G.grid[k] = grid[k];
+    G.shm = shm;
+    return hipGraphLaunch(G.exec, m->stream) == hipSuccess;
+}
+
 // SearchLocalPoints' fast path (frames of <= kSbpFixKp keypoints): the grid, ONE kernel for
 // isInFrustum (kPre: its outputs already resident) + candidates (fixed per-point slots) + the
 // greedy initialisation, kBlindRounds rounds launched without looking (a round after a change-free
@@ -580,13 +675,18 @@ int sbp_local_fast(orbfe_matcher* m, const orbfe_frame_view* frame, const Frustu
     g.hstats = m->stat_dev;
     if (m->stat_host)  // "not converged" until the last workgroup writes it
         for (int k = 0; k < 6; ++k) m->stat_host[k] = k == 4 ? -1 : 0;
-    hipLaunchKernelGGL(sbp_local_fused_kernel<kPre>, dim3(fblocks), dim3(1024), (size_t)N * 32, m->stream, fu);
     const int rblocks = std::max(1, (std::max(std::max(M, N), 32) + kGreedyBlock - 1) / kGreedyBlock);
-    for (int r = 0; r < kBlindRounds - 1; ++r)
-        hipLaunchKernelGGL(greedy_round_kernel, dim3(rblocks), dim3(kGreedyBlock), 0, m->stream, g, r);
-    // the last blind round and the acceptances in one launch
-    hipLaunchKernelGGL(greedy_accept_kernel<true>, dim3((M + kGreedyBlock - 1) / kGreedyBlock),
-                       dim3(kGreedyBlock), 0, m->stream, g, kBlindRounds - 1);
+    static_assert(kBlindRounds + 1 == orbfe_matcher::kSbpNodes, "one node per launch");
+    const dim3 grid[3] = {dim3(fblocks), dim3(rblocks), dim3((M + kGreedyBlock - 1) / kGreedyBlock)};
+    const size_t shm = (size_t)N * 32;
+    if (!sbp_local_graph<kPre>(m, fu, g, grid, shm, kBlindRounds)) {
+        hipLaunchKernelGGL(sbp_local_fused_kernel<kPre>, grid[0], dim3(1024), shm, m->stream, fu);
+        for (int r = 0; r < kBlindRounds - 1; ++r)
+            hipLaunchKernelGGL(greedy_round_kernel, grid[1], dim3(kGreedyBlock), 0, m->stream, g, r);
+        // the last blind round and the acceptances in one launch
+        hipLaunchKernelGGL(greedy_accept_kernel<true>, grid[2], dim3(kGreedyBlock), 0, m->stream,
+                           g, kBlindRounds - 1);
+    }
     ORBFE_HIP(hipGetLastError());
     m->rounds_on_device = false;
     for (int k = 0; k < 6; ++k) host[k] = 0;

@@ -86,6 +86,28 @@ def test_gpu_search_local_points(seed, m, th, stereo, zc, monkeypatch):
     mt.close()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph", ["1", "0"])
+def test_gpu_local_points_graph_updates(graph, monkeypatch):
+    """One matcher through a sequence of different problems (new buffers, map sizes, keypoint
+    counts and thresholds): with the graph (ORBFE_SBP_GRAPH=1) each call after the first rewrites
+    the changed nodes of the instantiated graph (arguments, grids, LDS bytes) instead of
+    re-instantiating it; every call bit-exact against the oracle, and the same with plain launches."""
+    monkeypatch.setenv("ORBFE_SBP_GRAPH", graph)
+    from orbslam_mapsave_amd.native import ORBmatcher
+    mt = ORBmatcher(0.8, False, device=0)
+    probs = [(0, 50000, 1.0, 1000), (3, 1000, 5.0, 600), (1, 20000, 3.0, 1000), (0, 50000, 1.0, 1000)]
+    for seed, m, th, nf in probs:
+        f = S.extract_frame(seed, nf)
+        lm = synthetic_local_map(f.keys, f.desc, m, seed=seed)
+        inv, fmp, fobs, nm, nto = oracle_search_local_points(f, lm, S.camera(), th)
+        (gnm, gnto), ginv, gfmp, gfobs = _slp_device(mt, f, lm, m, th, calls=2)
+        assert (gnm, gnto) == (nm, nto), (seed, m)
+        assert np.array_equal(ginv, inv) and np.array_equal(gfmp, fmp)
+        assert np.array_equal(gfobs, fobs)
+    mt.close()
+
+
 def dense_frame(seed: int = 5, nfeatures: int = 2000):
     """A frame of ~2000 keypoints for the fused kernel's in-LDS grid (its second keypoint per
     thread, k >= 1024): 300 of them moved into three 64x48-grid cells (~100 per cell, the
