@@ -20,6 +20,7 @@
 // 1.1M-node ORBvoc).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -441,6 +442,150 @@ __global__ __launch_bounds__(kBowSearchBlock) void bow_search_kernel(BowMatchArg
     }
 }
 
+// Host form, one (keyframe, frame) pair with at most kBow1Nodes common nodes: the host walks the
+// two FeatureVectors as the reference does (ORBmatcher.cc:195-256: equal node ids are matched,
+// otherwise the lagging side jumps to lower_bound of the other's id) and gathers each common
+// node's features, in the reference's order, into the device-mapped pinned staging buffer —
+// keyframe features without a good map point (202-207) left out — so a wave reads its node's
+// descriptors, indices and angles in one round of loads with no index chain (the common nodes
+// themselves ride in the kernel arguments).  The node loop is bow_search_kernel's; a match is
+// appended as a (frame feature, keyframe feature, rotation bin) record, and bow_filter1_kernel
+// applies the orientation filter (259-281) and writes the kept pairs to pinned memory.
+constexpr int kBow1Nodes = 192;
+struct Bow1Args {
+    const uint4* kd;  // keyframe features in node order: descriptors (2 x uint4 each),
+    const int* ki;    //   keyframe feature indices,
+    const float* ka;  //   angles (pKF->mvKeysUn[i].angle)
+    const uint4* fd;  // frame features in node order: descriptors,
+    const int* fi;    //   frame feature indices,
+    const float* fa;  //   angles (F.mvKeys[i].angle)
+    int* rec;         // match records (f, kf, bin), appended
+    int* cnt;         // [0] records [32, 62) rotation histogram; zero between calls
+    int* out;         // pinned: [0] kept matches, then (f, kf) pairs
+    int nodes;
+    int4 node[kBow1Nodes];  // (keyframe start, count, frame start, count) per common node
+};
+
+__global__ __launch_bounds__(256) void bow_search1_kernel(Bow1Args a, float nnratio, int check_ori) {
+    const int lane = threadIdx.x & 63;
+    const int c = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (c >= a.nodes) return;
+    const int4 w = a.node[c];
+    const int x0 = w.x, nx = w.y, y0 = w.z, ny = w.w;  // ny <= kBowNodeMax (host-checked)
+    int jf[4];
+    float fang[4];
+    uint4 d0[4], d1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int r = lane + 64 * j;
+        const bool in = r < ny;
+        jf[j] = in ? a.fi[y0 + r] : -1;
+        fang[j] = in ? a.fa[y0 + r] : 0.f;
+        d0[j] = in ? a.fd[2 * (y0 + r)] : make_uint4(0, 0, 0, 0);
+        d1[j] = in ? a.fd[2 * (y0 + r) + 1] : make_uint4(0, 0, 0, 0);
+    }
+    const int nj = (ny + 63) >> 6;
+    bool free_[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) free_[j] = lane + 64 * j < ny;
+    int mkf[4] = {-1, -1, -1, -1};  // the keyframe feature candidate j was matched to
+    int mbin[4] = {0, 0, 0, 0};
+    for (int xb = 0; xb < nx; xb += 64) {
+        const int xl = xb + lane;
+        int my_ikf = -1;
+        float my_ang = 0.f;
+        uint4 my0 = make_uint4(0, 0, 0, 0), my1 = my0;
+        if (xl < nx) {
+            my_ikf = a.ki[x0 + xl];
+            my_ang = a.ka[x0 + xl];
+            my0 = a.kd[2 * (x0 + xl)];
+            my1 = a.kd[2 * (x0 + xl) + 1];
+        }
+        const int cnt = min(64, nx - xb);
+        for (int t = 0; t < cnt; ++t) {
+            const uint4 q0 = make_uint4(__builtin_amdgcn_readlane(my0.x, t), __builtin_amdgcn_readlane(my0.y, t),
+                                        __builtin_amdgcn_readlane(my0.z, t), __builtin_amdgcn_readlane(my0.w, t));
+            const uint4 q1 = make_uint4(__builtin_amdgcn_readlane(my1.x, t), __builtin_amdgcn_readlane(my1.y, t),
+                                        __builtin_amdgcn_readlane(my1.z, t), __builtin_amdgcn_readlane(my1.w, t));
+            uint32_t key = 0xffffffffu;
+            int dist[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                dist[j] = 256;
+                if (j < nj && free_[j]) {
+                    dist[j] = hamming256(q0, q1, d0[j], d1[j]);
+                    key = min(key, ((uint32_t)dist[j] << 16) | (uint32_t)(lane + 64 * j));
+                }
+            }
+            key = __ockl_wfred_min_u32(key);
+            const int b1 = key == 0xffffffffu ? 256 : (int)(key >> 16);
+            const int brank = (int)(key & 0xffff);
+            int sec = 256;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (j < nj && free_[j] && lane + 64 * j != brank) sec = min(sec, dist[j]);
+            sec = __ockl_wfred_min_i32(sec);
+            if (b1 <= kThLow && (float)b1 < nnratio * (float)sec) {  // TH_LOW, ratio (233-237)
+                const int ikf = __builtin_amdgcn_readlane(my_ikf, t);
+                const float kang = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, my_ang), t));
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (lane + 64 * j == brank) {
+                        free_[j] = false;
+                        mkf[j] = ikf;
+                        mbin[j] = check_ori ? rot_bin(kang, fang[j]) : 0;
+                    }
+                }
+            }
+        }
+    }
+    // the node's matches as records: one returning atomic per 64 candidates (a returning atomic
+    // inside the loop above would put a memory round trip on every match's critical path)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (j >= nj) break;
+        const unsigned long long b = __ballot(mkf[j] >= 0);
+        if (!b) continue;
+        int base = 0;
+        if (lane == __builtin_ctzll(b)) base = atomicAdd(&a.cnt[0], __popcll(b));
+        base = __builtin_amdgcn_readlane(base, __builtin_ctzll(b));
+        if (mkf[j] >= 0) {
+            const int k = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+            a.rec[3 * k] = jf[j];
+            a.rec[3 * k + 1] = mkf[j];
+            a.rec[3 * k + 2] = mbin[j];
+            if (check_ori) atomicAdd(&a.cnt[32 + mbin[j]], 1);
+        }
+    }
+}
+
+// The orientation filter over the records (one workgroup after bow_search1_kernel): the kept
+// (frame feature, keyframe feature) pairs and their count (= nmatches after the filter) go to
+// the pinned output; the record counter and the histogram are zeroed for the next call.
+__global__ __launch_bounds__(256) void bow_filter1_kernel(Bow1Args a, int check_ori) {
+    __shared__ int top[3];
+    __shared__ int kept;
+    const int n = a.cnt[0];
+    if (threadIdx.x == 0) {
+        kept = 0;
+        if (check_ori) three_maxima(a.cnt + 32, top[0], top[1], top[2]);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int f = a.rec[3 * i], kf = a.rec[3 * i + 1], bin = a.rec[3 * i + 2];
+        if (check_ori && bin != top[0] && bin != top[1] && bin != top[2]) continue;
+        const int k = atomicAdd(&kept, 1);
+        a.out[1 + 2 * k] = f;
+        a.out[2 + 2 * k] = kf;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a.out[0] = kept;
+        a.cnt[0] = 0;
+    }
+    if (threadIdx.x < kHistLen) a.cnt[32 + threadIdx.x] = 0;
+}
+
 }  // namespace orbfe
 
 using namespace orbfe;
@@ -709,6 +854,120 @@ static bool fv_ok(int nn, const int32_t* off, const int32_t* feat, int n) {
     return true;
 }
 
+// ORBFE_BOW1=0: the host form takes the general two-launch path (bow_search_kernel) instead of
+// the gathered one
+static bool bow1_off() {
+    const char* e = std::getenv("ORBFE_BOW1");
+    return e && std::strcmp(e, "0") == 0;
+}
+
+// The host form's gathered path (bow_search1_kernel + bow_filter1_kernel; inputs validated by
+// the caller).  *done = false: the pair does not fit it (more than kBow1Nodes common nodes or a
+// node of more than kBowNodeMax frame features) and the caller takes the general path.
+static int search_by_bow1(orbfe_matcher* m, float nnratio, int check_ori, const uint8_t* kf_desc,
+                          const float* kf_angle, const uint8_t* kf_mp_ok, int kf_nn,
+                          const int32_t* kf_node_ids, const int32_t* kf_node_off,
+                          const int32_t* kf_feat, const uint8_t* f_desc, const float* f_angle,
+                          int f_nn, const int32_t* f_node_ids, const int32_t* f_node_off,
+                          const int32_t* f_feat, int32_t* matches, int32_t* nmatches, bool* done) {
+    *done = false;
+    Bow1Args a{};
+    int2 pij[kBow1Nodes];  // (keyframe node, frame node) of each common node kept
+    // the reference's walk over the two FeatureVectors (195-256)
+    int ktot = 0, ftot = 0, i = 0, j = 0;
+    while (i < kf_nn && j < f_nn) {
+        if (kf_node_ids[i] == f_node_ids[j]) {
+            int nx = 0;
+            for (int e = kf_node_off[i]; e < kf_node_off[i + 1]; ++e) nx += kf_mp_ok[kf_feat[e]] != 0;
+            const int ny = f_node_off[j + 1] - f_node_off[j];
+            if (ny > kBowNodeMax) return ORBFE_OK;
+            if (nx && ny) {
+                if (a.nodes == kBow1Nodes) return ORBFE_OK;
+                pij[a.nodes] = make_int2(i, j);
+                a.node[a.nodes++] = make_int4(ktot, nx, ftot, ny);
+                ktot += nx;
+                ftot += ny;
+            }
+            ++i;
+            ++j;
+        } else if (kf_node_ids[i] < f_node_ids[j]) {
+            i = (int)(std::lower_bound(kf_node_ids + i, kf_node_ids + kf_nn, f_node_ids[j]) - kf_node_ids);
+        } else {
+            j = (int)(std::lower_bound(f_node_ids + j, f_node_ids + f_nn, kf_node_ids[i]) - f_node_ids);
+        }
+    }
+    if (!a.nodes) {  // no common node with candidates: no match (the caller set matches to NULL)
+        *done = true;
+        *nmatches = 0;
+        return ORBFE_OK;
+    }
+    int st;
+    // one staging block: kd | fd | ki | ka | fi | fa | out
+    const size_t o_fd = (size_t)ktot * 32, o_ki = o_fd + (size_t)ftot * 32, o_ka = o_ki + 4 * (size_t)ktot,
+                 o_fi = o_ka + 4 * (size_t)ktot, o_fa = o_fi + 4 * (size_t)ftot, o_out = o_fa + 4 * (size_t)ftot,
+                 bytes = o_out + 4 * (1 + 2 * (size_t)ftot);
+    uint8_t* q = m->stage(bytes);
+    if (!q) return ORBFE_ERR_NOMEM;
+    if (!m->pin_dev) return ORBFE_OK;  // the staging buffer is not device-mapped: general path
+    *done = true;
+    if ((st = m->b1_rec.ensure((size_t)ftot * 3 * sizeof(int)))) return st;
+    if ((st = m->b1_cnt.ensure(64 * sizeof(int)))) return st;
+    if (!m->b1_zeroed) {
+        ORBFE_HIP(hipMemsetAsync(m->b1_cnt.p, 0, 64 * sizeof(int), m->stream));
+        m->b1_zeroed = true;
+    }
+    // each common node's features in FeatureVector order (keyframe features with a good map
+    // point only), as the node loop visits them (198-245)
+    int* ki = reinterpret_cast<int*>(q + o_ki);
+    float* ka = reinterpret_cast<float*>(q + o_ka);
+    int* fi = reinterpret_cast<int*>(q + o_fi);
+    float* fa = reinterpret_cast<float*>(q + o_fa);
+    for (int c = 0, kx = 0, fy = 0; c < a.nodes; ++c) {
+        for (int e = kf_node_off[pij[c].x]; e < kf_node_off[pij[c].x + 1]; ++e) {
+            const int k = kf_feat[e];
+            if (!kf_mp_ok[k]) continue;
+            std::memcpy(q + 32 * (size_t)kx, kf_desc + 32 * (size_t)k, 32);
+            ki[kx] = k;
+            ka[kx] = kf_angle[k];
+            ++kx;
+        }
+        for (int e = f_node_off[pij[c].y]; e < f_node_off[pij[c].y + 1]; ++e) {
+            const int k = f_feat[e];
+            std::memcpy(q + o_fd + 32 * (size_t)fy, f_desc + 32 * (size_t)k, 32);
+            fi[fy] = k;
+            fa[fy] = f_angle[k];
+            ++fy;
+        }
+    }
+    const uint8_t* d = m->pin_dev + (q - m->pin);
+    a.kd = reinterpret_cast<const uint4*>(d);
+    a.fd = reinterpret_cast<const uint4*>(d + o_fd);
+    a.ki = reinterpret_cast<const int*>(d + o_ki);
+    a.ka = reinterpret_cast<const float*>(d + o_ka);
+    a.fi = reinterpret_cast<const int*>(d + o_fi);
+    a.fa = reinterpret_cast<const float*>(d + o_fa);
+    a.rec = m->b1_rec.as<int>();
+    a.cnt = m->b1_cnt.as<int>();
+    a.out = reinterpret_cast<int*>(const_cast<uint8_t*>(d + o_out));
+    const int* out = reinterpret_cast<const int*>(q + o_out);
+    if ((st = m->flush())) return st;
+    hipLaunchKernelGGL(bow_search1_kernel, dim3((a.nodes + 3) / 4), dim3(256), 0, m->stream, a,
+                       nnratio, check_ori);
+    hipLaunchKernelGGL(bow_filter1_kernel, dim3(1), dim3(256), 0, m->stream, a, check_ori);
+    if (hipGetLastError() != hipSuccess) {
+        m->b1_zeroed = false;
+        return ORBFE_ERR_HIP;
+    }
+    if ((st = m->sync())) {
+        m->b1_zeroed = false;
+        return st;
+    }
+    const int kept = out[0];
+    for (int k = 0; k < kept; ++k) matches[out[1 + 2 * k]] = out[2 + 2 * k];
+    *nmatches = kept;
+    return ORBFE_OK;
+}
+
 int orbfe_search_by_bow(orbfe_matcher* m, float nnratio, int check_ori, int n_kf,
                         const uint8_t* kf_desc, const float* kf_angle, const uint8_t* kf_mp_ok,
                         int kf_nn, const int32_t* kf_node_ids, const int32_t* kf_node_off,
@@ -729,6 +988,14 @@ int orbfe_search_by_bow(orbfe_matcher* m, float nnratio, int check_ori, int n_kf
         for (int i = 0; i < n_f; ++i) matches[i] = -1;  // vpMapPointMatches = NULL (164)
         *nmatches = 0;
         if (!kf_nn || !f_nn || !n_f) return ORBFE_OK;
+        if (!m->zero_copy_off && !bow1_off()) {
+            bool done = false;
+            if ((st = search_by_bow1(m, nnratio, check_ori, kf_desc, kf_angle, kf_mp_ok, kf_nn,
+                                     kf_node_ids, kf_node_off, kf_feat, f_desc, f_angle, f_nn,
+                                     f_node_ids, f_node_off, f_feat, matches, nmatches, &done)))
+                return st;
+            if (done) return ORBFE_OK;
+        }
         // slot 0 of each set; the caps bound every offset and index (validated above)
         const int kf_cap = std::max({n_kf, kf_tot, kf_nn}), f_cap = std::max({n_f, f_tot, f_nn});
         const int nn[2] = {kf_nn, f_nn};

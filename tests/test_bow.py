@@ -274,12 +274,15 @@ def test_gpu_bow_transform_batch(vocab_paths):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("ori,ratio", [(True, 0.75), (False, 0.7), (True, 0.9)])
-@pytest.mark.parametrize("zc", ["1", "0"])
-def test_gpu_search_by_bow(ori, ratio, zc, vocab_paths, frames, monkeypatch):
-    """Host SearchByBoW with the pair's last workgroup writing the results into device-mapped
-    pinned memory (ORBFE_ZERO_COPY=1) and through bow_init_kernel + D2H copies (0); three calls
-    on one matcher (the done counter and staging reused)."""
+@pytest.mark.parametrize("zc,path", [("1", "gathered"), ("1", "general"), ("0", "general")])
+def test_gpu_search_by_bow(ori, ratio, zc, path, vocab_paths, frames, monkeypatch):
+    """Host SearchByBoW: the gathered path (common nodes' features gathered by the host into
+    device-mapped pinned memory, bow_search1_kernel + bow_filter1_kernel), the general path with
+    the pair's last workgroup writing the results into pinned memory (ORBFE_BOW1=0), and through
+    bow_init_kernel + D2H copies (ORBFE_ZERO_COPY=0); three calls on one matcher (counters,
+    histogram and staging reused)."""
     monkeypatch.setenv("ORBFE_ZERO_COPY", zc)
+    monkeypatch.setenv("ORBFE_BOW1", "1" if path == "gathered" else "0")
     from orbslam_mapsave_amd.native import ORBmatcher
     kf, f, kf_ok, kf_fv, f_fv = bow_case(vocab_paths["k10L4_l1_tfidf"], frames, seed=int(ori))
     mt = ORBmatcher(ratio, ori, device=0)
@@ -288,6 +291,49 @@ def test_gpu_search_by_bow(ori, ratio, zc, vocab_paths, frames, monkeypatch):
     for _ in range(3):
         m, nm = mt.SearchByBoW(kf.desc, kf.keys["angle"], kf_ok, kf_fv, f.desc, f.keys["angle"],
                                f_fv)
+        assert nm == onm and np.array_equal(m, om)
+    mt.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("levelsup", [1, 3])
+def test_gpu_search_by_bow_node_levels(levelsup, vocab_paths, frames):
+    """FeatureVectors at level 3 (up to 1000 nodes: more common nodes than the gathered path
+    takes, so the general path runs) and level 1 (10 nodes of ~100 frame features), then a
+    keyframe without any good map point (no common node has candidates: no launch), one matcher."""
+    from orbslam_mapsave_amd.native import ORBmatcher
+    kf, f, kf_ok, kf_fv, f_fv = bow_case(vocab_paths["k10L4_l1_tfidf"], frames, levelsup=levelsup)
+    mt = ORBmatcher(0.75, True, device=0)
+    for ok in (kf_ok, np.zeros_like(kf_ok), kf_ok):
+        om, onm = oracle.search_by_bow(kf.desc, kf.keys["angle"], ok, kf_fv, f.desc,
+                                       f.keys["angle"], f_fv, 0.75, True)
+        m, nm = mt.SearchByBoW(kf.desc, kf.keys["angle"], ok, kf_fv, f.desc, f.keys["angle"], f_fv)
+        assert nm == onm and np.array_equal(m, om)
+    mt.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ori", [True, False])
+def test_gpu_search_by_bow_duplicates(ori, vocab_paths, frames):
+    """Every frame descriptor twice (equal distances everywhere: ties for the best and the second,
+    and a keyframe feature's best or second candidate taken by an earlier one — the gathered
+    kernel's recomputation), the frame against itself and against the keyframe; bit-exact."""
+    from orbslam_mapsave_amd.abi import Frame
+    from orbslam_mapsave_amd.native import ORBmatcher
+    ov = oracle.Vocabulary(vocab_paths["k10L4_l1_tfidf"])
+    kf, f = frames
+    keys = np.concatenate([f.keys, f.keys])
+    keys["angle"][len(f.keys):] = np.mod(keys["angle"][len(f.keys):] + 7.0, 360.0).astype(np.float32)
+    d2 = Frame(keys, np.concatenate([f.desc, f.desc]), S.W, S.H, f.scale_factors)
+    mt = ORBmatcher(0.9, ori, device=0)
+    for a_, b_ in ((d2, d2), (kf, d2), (d2, kf)):
+        afv = ov.transform(a_.desc, 2)[2:]
+        bfv = ov.transform(b_.desc, 2)[2:]
+        ok = np.ones(a_.n, np.uint8)
+        ok[::5] = 0
+        om, onm = oracle.search_by_bow(a_.desc, a_.keys["angle"], ok, afv, b_.desc,
+                                       b_.keys["angle"], bfv, 0.9, ori)
+        m, nm = mt.SearchByBoW(a_.desc, a_.keys["angle"], ok, afv, b_.desc, b_.keys["angle"], bfv)
         assert nm == onm and np.array_equal(m, om)
     mt.close()
 
