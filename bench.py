@@ -380,7 +380,10 @@ def parse_args():
                          "resize / blur bodies + FMA rotation of the reference's x86-64 build "
                          "(the default, as the library's), or OpenCV's portable scalar paths "
                          "(DESIGN.md §2)")
-    ap.add_argument("--steps", type=int, default=20)
+    # 100 timed steps: the two sub-batch streams' fill and drain at the ends of the timed region
+    # (one stream's last kernels alone on the chip) weigh 1/K of it — c3 1.385 ms per step at
+    # K = 20, 1.374 at K = 100 (profiles/r05/steps_k/)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--soak-s", type=float, default=8.0,
                     help="untimed wall-clock seconds of steps after the warmup (c2/c3/c4), so "
