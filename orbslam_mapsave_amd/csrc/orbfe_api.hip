@@ -264,6 +264,9 @@ struct orbfe_extractor {
     // barriers exposed at 24 waves per CU)
     bool fast_strip = std::getenv("ORBFE_FAST_STRIP") && std::strcmp(std::getenv("ORBFE_FAST_STRIP"), "1") == 0;
     int desc_g16 = std::getenv("ORBFE_DESC_G16") ? std::atoi(std::getenv("ORBFE_DESC_G16")) : 0;
+    // ORBFE_DESC_G2=1 (experiment): batches at kDescGroupSmall keypoints per wave, strided — four
+    // times the waves per frame, so a quarter of the frames in flight per XCD
+    bool desc_g2 = std::getenv("ORBFE_DESC_G2") && std::atoi(std::getenv("ORBFE_DESC_G2")) == 1;
     bool graph_broken = std::getenv("ORBFE_NO_GRAPH") != nullptr;  // capture failed once (or
                                  // disabled for A/B runs): keep to the launch path
 
@@ -741,12 +744,13 @@ struct orbfe_extractor {
         // 512-frame launch instead of 0.70 (1.65x its algorithmic bytes: the frames in flight
         // per XCD double); at 1080p it is 9 % slower (profiles/r04/experiments/describe_g16/)
         const bool g16 = desc_g16 == 1 && n >= kDescSmallBatch && desc_stride && x86() && win == kWinMfma;
-        const int group = g16 ? 16 : n >= kDescSmallBatch ? kDescGroupSize : kDescGroupSmall;
+        const bool g2 = desc_g2 && n >= kDescSmallBatch && desc_stride;
+        const int group = g16 ? 16 : n >= kDescSmallBatch && !g2 ? kDescGroupSize : kDescGroupSmall;
         const int per_block = (kDescBlockSize / 64) * group;  // slots per workgroup
         const dim3 dgrid((g.geo.out_total + per_block - 1) / per_block, n);
         // batches: strided slots (a frame's waves sweep its oct-tree output in runs of W
         // consecutive slots, sharing window lines in L2); ORBFE_DESC_STRIDE=0: grouped slots
-        da.wave_stride = (group == kDescGroupSize || g16) && desc_stride ? (int)dgrid.x * (kDescBlockSize / 64) : 0;
+        da.wave_stride = (group == kDescGroupSize || g16 || g2) && desc_stride ? (int)dgrid.x * (kDescBlockSize / 64) : 0;
         da.frags = bslot.as<uint4>() + kDescFragOff;
         const int variant = g16 ? 12 : (group == kDescGroupSize ? 6 : 0) + (x86() ? 3 : 0) + win;
         switch (variant) {
