@@ -3094,6 +3094,10 @@ constexpr int kFragLds = ORBFE_DESC_FRAG_LDS;
 #define ORBFE_DESC_LATE_STORE 1  // descriptor words stored once per wave, after the keypoint loop
 #endif
 constexpr bool kDescLateStore = ORBFE_DESC_LATE_STORE != 0;
+#ifndef ORBFE_DESC_PF2
+#define ORBFE_DESC_PF2 0  // (matrix-core form) two keypoints' windows in flight instead of one
+#endif
+constexpr bool kDescPf2 = ORBFE_DESC_PF2 != 0;
 #ifndef ORBFE_DESC_WAVES
 #define ORBFE_DESC_WAVES 6
 #endif
@@ -3341,7 +3345,7 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
     // rows 43.. feed only window rows >= 37): one 16-byte load per tile straight into registers
     // (staging them in LDS with global_load_lds instead measured no faster: describe 0.2488 vs
     // 0.2467 ms, profiles/r03/experiments/describe_mfma.json)
-    auto load_frag = [&](int j) __attribute__((always_inline)) {
+    auto load_frag_to = [&](int j, uint4 (&dst)[3]) __attribute__((always_inline)) {
         const int kl = __builtin_amdgcn_readlane(my_l, j);
         const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane(my_key, j);
         const int x = key_x(kk), y = key_y(kk), x0 = (x - kDescWinR) & ~3;
@@ -3354,10 +3358,10 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
             const int r = 16 * t + (lane & 15);
-            rv[t] = make_uint4(0u, 0u, 0u, 0u);
+            dst[t] = make_uint4(0u, 0u, 0u, 0u);
             if (r >= kRawRows - 1 || g == 3 || (kDescSkip & 8)) continue;
             if (fast) {
-                rv[t] = load16_a4(fb + (long long)(y - 21 + r) * pp.pitch + x0 - 4 + 16 * g);
+                dst[t] = load16_a4(fb + (long long)(y - 21 + r) * pp.pitch + x0 - 4 + 16 * g);
             } else {
                 // keypoints lie >= 19 px inside their level (>= 39 px wide and high), so the
                 // window overshoots an edge by at most 2 rows / 6 columns: one reflection
@@ -3366,10 +3370,11 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
 #pragma unroll
                 for (int k = 0; k < 16; ++k)
                     bb[k >> 2] |= (uint32_t)row[reflect101_1(x0 - 4 + 16 * g + k, lw)] << (8 * (k & 3));
-                rv[t] = make_uint4(bb[0], bb[1], bb[2], bb[3]);
+                dst[t] = make_uint4(bb[0], bb[1], bb[2], bb[3]);
             }
         }
     };
+    auto load_frag = [&](int j) __attribute__((always_inline)) { load_frag_to(j, rv); };
     auto is_pre = [&](int j) __attribute__((always_inline)) {
         return kPre || (!kMfma && ((a.pre_mask >> __builtin_amdgcn_readlane(my_l, j)) & 1u) != 0u);
     };
@@ -3406,6 +3411,12 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
     };
     unsigned long long dacc = 0;
     load_kp(__ffsll((long long)vmask) - 1);
+    // kDescPf2: the keypoint after next's window in flight too (a second fragment buffer)
+    uint4 rv2[3];
+    if constexpr (kDescPf2 && kMfma) {
+        const unsigned long long r1 = vmask & (vmask - 1);
+        if (r1) load_frag_to(__ffsll((long long)r1) - 1, rv2);
+    }
     // (the first window's loads are in flight during the IC moments and the trig)
     // 1. IC moments.  Lane (r = lane >> 1, hh = lane & 1): row v = r - 15, columns
     //    u = -15 + 16 hh .. +15 (u = 16 never lies in the disc).
@@ -3535,7 +3546,14 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
                 A[t] = i32x4m{(int)(rv[t].x ^ 0x80808080u), (int)(rv[t].y ^ 0x80808080u),
                               (int)(rv[t].z ^ 0x80808080u), (int)(rv[t].w ^ 0x80808080u)};
             const unsigned long long rest = m & (m - 1);
-            if (rest) load_kp(__ffsll((long long)rest) - 1);  // next keypoint's window in flight
+            if constexpr (kDescPf2) {
+#pragma unroll
+                for (int t = 0; t < 3; ++t) rv[t] = rv2[t];
+                const unsigned long long rest2 = rest & (rest - 1);
+                if (rest2) load_frag_to(__ffsll((long long)rest2) - 1, rv2);
+            } else {
+                if (rest) load_kp(__ffsll((long long)rest) - 1);  // next keypoint's window in flight
+            }
             const int xs = kX86 ? (int)__builtin_amdgcn_readlane(my_x0, j) + (lane & 15) -
                                       a.simd_xb[(int)__builtin_amdgcn_readlane(my_l, j)]
                                 : 0;
