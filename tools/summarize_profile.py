@@ -102,6 +102,13 @@ tpath = os.path.join(ROOT, "profiles", f"traffic_{CONF}.json")
 tj = json.load(open(tpath)) if os.path.exists(tpath) else {}
 if tj.get("frames_per_launch") not in (None, FRAMES):
     tj = {}
+def _drop_stale(j):  # this reading's entries are replaced wholesale (a kernel no longer launched goes)
+    for k in [k for k in j if isinstance(j[k], (int, float, dict)) and k != "frames_per_launch"
+              and (k.endswith(f"@{ARITH}") if ARITH != "scalar" else "@" not in k)]:
+        del j[k]
+
+
+_drop_stale(tj)
 tj.update({(k if ARITH == "scalar" else f"{k}@{ARITH}"): v for k, v in traffic.items()})
 tj["frames_per_launch"] = FRAMES
 tj["source"] = f"profiles/{R}: rocprofv3 --pmc, 2 x FETCH_SIZE + WRITE_SIZE per launch"
@@ -110,6 +117,7 @@ vpath = os.path.join(ROOT, "profiles", f"valu_{CONF}.json")
 vj = json.load(open(vpath)) if os.path.exists(vpath) else {}
 if vj.get("frames_per_launch") not in (None, FRAMES):
     vj = {}
+_drop_stale(vj)
 vj.update({(k if ARITH == "scalar" else f"{k}@{ARITH}"): v for k, v in valu.items()})
 vj["frames_per_launch"] = FRAMES
 vj["source"] = f"profiles/{R}: rocprofv3 --pmc SQ_INSTS_VALU per launch"
