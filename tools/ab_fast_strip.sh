@@ -1,6 +1,6 @@
 #!/bin/bash
-# FAST strip kernel (fast_strip_kernel, default) vs one wave per cell (ORBFE_FAST_STRIP=0):
-# FAST parity tests, then interleaved c3 / c4 lines, then the strip kernel's phase clocks
+# FAST strip kernel (fast_strip_kernel, opt-in: ORBFE_FAST_STRIP=1) vs one wave per cell (the
+# default, ORBFE_FAST_STRIP=0): FAST parity tests with the tree as is, then interleaved c3 / c4 lines, then the strip kernel's phase clocks
 # (tools/probe/fast_timing.py, built beforehand).  Output gpurun_out/${1:-fstrip}/
 set -o pipefail
 O=gpurun_out/${1:-fstrip}
