@@ -55,6 +55,56 @@ __device__ __forceinline__ uint4 load16_a1(const uint8_t* p) {
     return v;
 }
 
+// Stages `total` 16-byte chunks of image rows into LDS: chunk i is image row y0 + i / cpr at
+// columns x0 + 16 (i % cpr) (x0 4-aligned), stored at dst + (i / cpr) P + 16 (i % cpr).  NT
+// threads, four chunks each per round, every 16-byte load issued before any is used: the loads
+// are unconditional (an index past the end re-reads the last chunk; a chunk reaching past the
+// row end loads a clamped in-row address, or a zero word for rows narrower than 16 bytes, and
+// is then rebuilt from dwords / bytes that never leave the row: level 0 may be the caller's
+// buffer), since a load under a branch made the compiler wait for it before issuing the next.
+__device__ uint4 g_zero16;
+template <int NT>
+__device__ __forceinline__ void stage_rows16(const uint8_t* src, long long pitch, int y0, int x0,
+                                             int sw, int cpr, int total, unsigned char* dst,
+                                             int P, int tid) {
+    const bool wide = sw >= 16;
+    const int xmax = (sw - 16) & ~3;
+    for (int base = 0; base < total; base += 4 * NT) {
+        uint4 v[4];
+        int ro[4], xo[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = min(base + NT * u + tid, total - 1);
+            const int r = i / cpr, c = i - r * cpr;
+            ro[u] = r;
+            xo[u] = x0 + 16 * c;
+            const uint8_t* p = wide ? src + (long long)(y0 + r) * pitch + min(xo[u], xmax)
+                                    : reinterpret_cast<const uint8_t*>(&g_zero16);
+            v[u] = load16_a4(p);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int x = xo[u];
+            if (x + 16 <= sw) continue;
+            const uint8_t* row = src + (long long)(y0 + ro[u]) * pitch;
+            uint32_t w[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const int xd = x + 4 * d;
+                w[d] = 0;
+                if (xd + 4 <= sw) w[d] = *reinterpret_cast<const uint32_t*>(row + xd);
+                else
+                    for (int q = 0; q < 4 && xd + q < sw; ++q) w[d] |= (uint32_t)row[xd + q] << (8 * q);
+            }
+            v[u] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        // (the stores unconditional too, an index past the end rewriting the last chunk with
+        // its own bytes: a conditional store let the compiler sink the load into its branch)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) *reinterpret_cast<uint4*>(dst + ro[u] * P + (xo[u] - x0)) = v[u];
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // K0 — pyramid level 0 from the caller's frame: cvtColor(CV_{RGB,BGR,RGBA,BGRA}2GRAY) of
 // Tracking::GrabImage* (Tracking.cc:286-310, 350-363, 409-422), then Mat::copyTo(image, mask)
@@ -249,38 +299,7 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
     // reaching past the row end is assembled from dwords / bytes (level 0 may be the caller's
     // buffer: nothing past its last row is read).
     const int total = nrow * cpr;
-    for (int base = 0; base < total; base += 4 * 256) {
-        uint4 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = base + 256 * u + (int)threadIdx.x;
-            if (i >= total) continue;
-            const int r = i / cpr, c = i - r * cpr;
-            const uint8_t* row = src + (long long)(sy0 + r) * a.src.pitch;
-            const int x = sx0 + 16 * c;
-            if (x + 16 <= a.sw) {
-                v[u] = load16_a4(row + x);
-            } else {
-                uint32_t w[4];
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const int xd = x + 4 * d;
-                    w[d] = 0;
-                    if (xd + 4 <= a.sw) w[d] = *reinterpret_cast<const uint32_t*>(row + xd);
-                    else
-                        for (int q = 0; q < 4 && xd + q < a.sw; ++q) w[d] |= (uint32_t)row[xd + q] << (8 * q);
-                }
-                v[u] = make_uint4(w[0], w[1], w[2], w[3]);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = base + 256 * u + (int)threadIdx.x;
-            if (i >= total) continue;
-            const int r = i / cpr, c = i - r * cpr;
-            *reinterpret_cast<uint4*>(rs_lds + r * P + 16 * c) = v[u];
-        }
-    }
+    stage_rows16<256>(src, a.src.pitch, sy0, sx0, a.sw, cpr, total, rs_lds, P, (int)threadIdx.x);
     __syncthreads();
     const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
     const int x = ox + 4 * tx;
@@ -383,38 +402,7 @@ __global__ __launch_bounds__(256) void resize2_kernel(Resize2Args a) {
     {
         const int nrow = ay1 - ay0 + 1, cpr = ((ax1 - ax0) >> 4) + 1, total = nrow * cpr;
         const uint8_t* src = a.src.base + f * a.src.fpitch;
-        for (int base = 0; base < total; base += 4 * 256) {
-            uint4 v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int i = base + 256 * u + tid;
-                if (i >= total) continue;
-                const int r = i / cpr, cc = i - r * cpr;
-                const uint8_t* row = src + (long long)(ay0 + r) * a.src.pitch;
-                const int x = ax0 + 16 * cc;
-                if (x + 16 <= a.sw) {
-                    v[u] = load16_a4(row + x);
-                } else {
-                    uint32_t w[4];
-#pragma unroll
-                    for (int d = 0; d < 4; ++d) {
-                        const int xd = x + 4 * d;
-                        w[d] = 0;
-                        if (xd + 4 <= a.sw) w[d] = *reinterpret_cast<const uint32_t*>(row + xd);
-                        else
-                            for (int q = 0; q < 4 && xd + q < a.sw; ++q) w[d] |= (uint32_t)row[xd + q] << (8 * q);
-                    }
-                    v[u] = make_uint4(w[0], w[1], w[2], w[3]);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int i = base + 256 * u + tid;
-                if (i >= total) continue;
-                const int r = i / cpr, cc = i - r * cpr;
-                *reinterpret_cast<uint4*>(r2_lds + r * a.pa + 16 * cc) = v[u];
-            }
-        }
+        stage_rows16<256>(src, a.src.pitch, ay0, ax0, a.sw, cpr, total, r2_lds, a.pa, tid);
     }
     __syncthreads();
     typedef unsigned short us2 __attribute__((ext_vector_type(2)));
@@ -1247,16 +1235,14 @@ __global__ __launch_bounds__(kTailBlock) void resize_tail_kernel(ResizeTailArgs 
         for (int base = 0; base < total; base += 4 * kTailBlock) {
             uint4 v[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int i = base + kTailBlock * u + tid;
-                if (i >= total) continue;
+            for (int u = 0; u < 4; ++u) {  // (unconditional: an index past the end re-reads the last)
+                const int i = min(base + kTailBlock * u + tid, total - 1);
                 const int r = i / cpr, c = i - r * cpr;
                 v[u] = *reinterpret_cast<const uint4*>(src + (long long)r * sp.pitch + 16 * c);
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int i = base + kTailBlock * u + tid;
-                if (i >= total) continue;
+            for (int u = 0; u < 4; ++u) {  // (unconditional: see stage_rows16)
+                const int i = min(base + kTailBlock * u + tid, total - 1);
                 const int r = i / cpr, c = i - r * cpr;
                 *reinterpret_cast<uint4*>(lds + r * a.lp[0] + 16 * c) = v[u];
             }
@@ -2770,18 +2756,21 @@ __global__ __launch_bounds__(BLK) void octree_kernel(OctArgs a) {
     for (int base = L.cell_begin; base < L.cell_end; base += 2 * BLK) {
         int n[2];
         long long slot[2];
+        // (every load unconditional, at clamped indices inside the cell's own keys: a load under
+        // a branch made the compiler wait for each one before the next, 10 round trips)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int c = base + j * BLK + tid;
-            n[j] = c < L.cell_end ? a.cell_cnt[f * a.ncells + c] : 0;
-            slot[j] = c < L.cell_end ? a.cells[c].slot : 0;
+            const int cc = min(c, L.cell_end - 1);
+            const int nn = a.cell_cnt[f * a.ncells + cc];
+            slot[j] = a.cells[cc].slot;
+            n[j] = c < L.cell_end ? nn : 0;
         }
         uint32_t v[2][8];
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
-                if (i < n[j]) v[j][i] = src[slot[j] + i];
+            for (int i = 0; i < 8; ++i) v[j][i] = src[slot[j] + min(i, max(n[j] - 1, 0))];
         int t0, t1;
         const int o0 = nkeys + block_exclusive_scan<BLK>(n[0], tmp, t0);
         const int o1 = nkeys + t0 + block_exclusive_scan<BLK>(n[1], tmp, t1);
@@ -3143,25 +3132,30 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
     xcd_block(bx, f);
     const int lane = threadIdx.x & 63;
     const int* cnt = a.oct_cnt + f * a.nlevels;
-    if (bx == 0 && threadIdx.x == 0) {
-        int n = 0;
-        for (int l = 0; l < a.nlevels; ++l) n += max(cnt[l], 0);
-        a.n_out[f] = n;  // the true count: entries past kps_cap are not written (truncation
-                         // is visible to the caller as n_out > kps_cap)
+    // The wave's start is a chain of dependent loads (level key counts -> slot order -> key);
+    // the counts, the blur fragments and the pattern pairs for LDS are all loaded first, and the
+    // LDS stores and the barrier wait until the slot mapping below has issued its loads.
+    // (loads without branches, so that no wait lands inside a branch right behind them)
+    const int cq_ld = cnt[min(lane, a.nlevels - 1)];
+    static_assert(kDescBlock == 256, "one fragment / pattern entry per thread (+128)");
+    uint4 fr0 = make_uint4(0u, 0u, 0u, 0u), fr1 = fr0;
+    int patw_lds = 0;
+    if constexpr (kMfma && kFragLds != 0) {
+        fr0 = a.frags[threadIdx.x];
+        fr1 = a.frags[256 + (threadIdx.x & 127)];
+    }
+    if constexpr (kPatLds) patw_lds = reinterpret_cast<const int*>(c_pattern)[threadIdx.x];
+    const int cq_raw = lane < a.nlevels ? cq_ld : 0;
+    if (bx == 0 && threadIdx.x < 64) {
+        const int n = wave_sum(max(cq_raw, 0));
+        if (threadIdx.x == 0)
+            a.n_out[f] = n;  // the true count: entries past kps_cap are not written (truncation
+                             // is visible to the caller as n_out > kps_cap)
     }
     typedef int i32x4m __attribute__((ext_vector_type(4)));
     __shared__ uint4 frag_lds[kMfma && kFragLds ? 384 : 1];
     // kPatLds: the pattern pairs as floats, pat_lds[q][lane] = pair lane + 64 q (x1, y1, x2, y2)
     __shared__ float4 pat_lds[kPatLds ? 256 : 1];
-    if constexpr ((kMfma && kFragLds != 0) || kPatLds) {  // before any wave leaves
-        if constexpr (kMfma && kFragLds != 0)
-            for (int i = threadIdx.x; i < 384; i += kDescBlock) frag_lds[i] = a.frags[i];
-        if constexpr (kPatLds)
-            for (int i = threadIdx.x; i < 256; i += kDescBlock)
-                pat_lds[i] = make_float4((float)c_pattern[4 * i], (float)c_pattern[4 * i + 1],
-                                         (float)c_pattern[4 * i + 2], (float)c_pattern[4 * i + 3]);
-        __syncthreads();
-    }
     // the frame's waves: wave wv takes slots wv * G .. wv * G + G - 1 (grouped), or with
     // a.wave_stride = W (the waves of a frame) slots wv, wv + W, wv + 2 W, ... (strided): then at
     // any moment the frame's waves work on one run of W consecutive oct-tree slots — one level,
@@ -3171,14 +3165,13 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
     const int wv = bx * (kDescBlock / 64) + (threadIdx.x >> 6);
     const int stride = a.wave_stride;
     const int s0 = stride ? wv : wv * kDescGroup;
-    if (s0 >= a.out_total) return;
 
     // lane j < kDescGroup: slot s0 + j (grouped) or s0 + j W (strided) -> level, key, output
     // index.  The level key counts are one load (lane q holds level q's) and their exclusive
     // prefix a wave scan, so a wave's start is one global round trip, not a chain of dependent
     // loads.  Grouped, the group's slots lie in the level of s0 or the next one (every level
     // has >= 20 slots); strided, each lane finds its level.
-    const int cq = lane < a.nlevels ? max(cnt[lane], 0) : 0;
+    const int cq = max(cq_raw, 0);
     const int pre = wave_inclusive_sum(cq) - cq;
     int my_l = 0, my_key = 0, my_o = 0;
     bool valid = false;
@@ -3224,6 +3217,19 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
             }
         }
     }
+    if constexpr ((kMfma && kFragLds != 0) || kPatLds) {  // before any wave leaves
+        if constexpr (kMfma && kFragLds != 0) {
+            frag_lds[threadIdx.x] = fr0;
+            frag_lds[256 + (threadIdx.x & 127)] = fr1;  // (threads 128.. rewrite 0..'s entries)
+        }
+        if constexpr (kPatLds) {
+            const uint32_t w = (uint32_t)patw_lds;
+            pat_lds[threadIdx.x] = make_float4((float)(int8_t)(w & 0xffu), (float)(int8_t)((w >> 8) & 0xffu),
+                                               (float)(int8_t)((w >> 16) & 0xffu), (float)(int8_t)(w >> 24));
+        }
+        __syncthreads();
+    }
+    if (s0 >= a.out_total) return;
     const unsigned long long vmask = __ballot(valid);
     if (!vmask) return;
 
@@ -3441,22 +3447,32 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
     // (4 at a time: 16 VGPRs of loads in flight, not 32)
     constexpr int kIcBatch = kDescGroup < 4 ? kDescGroup : 4;
     int M10 = 0, M01 = 0;
+    // the rows of up to 8 keypoints in flight before the first reduction, every load
+    // unconditional (an empty slot re-reads the first keypoint's rows, lanes past row 30 row
+    // 15; both zeroed): a load under a branch made the compiler wait for it on the spot
+    constexpr int kIcAhead = kDescGroup < 8 ? kDescGroup : 8;
+    const int j_first = __ffsll((long long)vmask) - 1;
 #pragma unroll
-    for (int j0 = 0; j0 < kDescGroup; j0 += kIcBatch) {
+    for (int ja = 0; ja < kDescGroup; ja += kIcAhead) {
+    uint4 pxa[kIcAhead];
+#pragma unroll
+    for (int jb = 0; jb < kIcAhead; ++jb) {
+        const int j = ja + jb;
+        const bool use = !(kDescSkip & 2) && ((vmask >> j) & 1);
+        const int js = use ? j : j_first;
+        const int kl = __builtin_amdgcn_readlane(my_l, js);
+        const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane(my_key, js);
+        const LevelPtr pp = a.pyr[kl];
+        const uint8_t* row = pp.base + f * pp.fpitch + (long long)(key_y(kk) + (r < 31 ? v : 0)) * pp.pitch +
+                             key_x(kk) - 15 + 16 * hh;
+        const uint4 q = load16_a1(row);
+        pxa[jb] = use && r < 31 ? q : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int j0 = ja; j0 < ja + kIcAhead; j0 += kIcBatch) {
         uint4 px[kIcBatch];
 #pragma unroll
-        for (int jb = 0; jb < kIcBatch; ++jb) {
-            const int j = j0 + jb;
-            px[jb] = make_uint4(0u, 0u, 0u, 0u);
-            if (!(kDescSkip & 2) && ((vmask >> j) & 1) && r < 31) {
-                const int kl = __builtin_amdgcn_readlane(my_l, j);
-                const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane(my_key, j);
-                const LevelPtr pp = a.pyr[kl];
-                const uint8_t* row = pp.base + f * pp.fpitch + (long long)(key_y(kk) + v) * pp.pitch +
-                                     key_x(kk) - 15 + 16 * hh;
-                px[jb] = load16_a1(row);
-            }
-        }
+        for (int jb = 0; jb < kIcBatch; ++jb) px[jb] = pxa[j0 - ja + jb];
         int part[2 * kIcBatch];  // lane's partial (m10, m01) of each keypoint of the batch
 #pragma unroll
         for (int jb = 0; jb < kIcBatch; ++jb) {
@@ -3501,6 +3517,7 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
                 }
             }
         }
+    }
     }
 
     // 2. angle and its rotation, one keypoint per lane

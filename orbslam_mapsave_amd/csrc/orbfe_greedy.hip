@@ -194,18 +194,65 @@ __device__ __forceinline__ int greedy_decide_fix(const GreedyArgs& a, const int*
     return acc.result(a);
 }
 
+// The fixed-slot round's per-point state, loaded in one round trip: the previous decision, the
+// Observations() count, the candidate count and the first 4 candidates, and for the T reset the
+// slot's pre-blocked state.  Every load is unconditional at a clamped index (a load under a
+// branch made the compiler wait for it before issuing the next: four round trips per round).
+struct FixPoint {
+    int prev, nb, n, f0, o0;
+    uint4 p0, p1;
+};
+__device__ __forceinline__ FixPoint fix_point_loads(const GreedyArgs& a, int t) {  // a.m >= 1
+    const int tm = min(t, max(a.m - 1, 0)), tk = min(t, max(a.nkp - 1, 0));
+    FixPoint q;
+    q.prev = a.dec[tm];
+    q.nb = (a.nobs ? a.nobs : a.dec)[tm];
+    q.n = a.fcnt[tm];
+    const uint4* cp = reinterpret_cast<const uint4*>(a.cand + (size_t)tm * a.kfix);
+    q.p0 = cp[0];
+    q.p1 = cp[1];
+    // (a frame without keypoints may pass NULL slot arrays: then the point's own state stands in)
+    const int* f0p = a.nkp > 0 ? a.fmp0 : a.dec;
+    q.f0 = f0p[tk];
+    q.o0 = (a.nkp > 0 && a.fobs0 ? a.fobs0 : f0p)[tk];
+    return q;
+}
+// greedy_decide_fix on loaded state
+__device__ __forceinline__ int greedy_decide_fixq(const GreedyArgs& a, const int* Tc, int i, const FixPoint& q) {
+    const int2 c[4] = {make_int2((int)q.p0.x, (int)q.p0.y), make_int2((int)q.p0.z, (int)q.p0.w),
+                       make_int2((int)q.p1.x, (int)q.p1.y), make_int2((int)q.p1.z, (int)q.p1.w)};
+    int tv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tv[k] = Tc[min(max(c[k].x, 0), max(a.nkp - 1, 0))];  // T holds >= 1 entry
+    GreedyAcc acc;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (k < q.n && tv[k] >= i) acc.add_unblocked(a, c[k]);
+    const int2* cp = a.cand + (size_t)i * a.kfix;
+    for (int e = 4; e < q.n; ++e) acc.add(a, Tc, i, cp[e]);
+    return acc.result(a);
+}
+
+// kFix: the fixed-slot layout (a.kfix > 0, the fused SearchLocalPoints path), its per-point
+// loads issued before the round's no-op check; otherwise the CSR layout.
+template <bool kFix>
 __global__ __launch_bounds__(kGreedyBlock) void greedy_round_kernel(GreedyArgs a, int r) {
-    if (r > 0 && a.chg[r - 1] == 0) return;
     const int t = blockIdx.x * kGreedyBlock + threadIdx.x;
+    FixPoint q{};
+    if constexpr (kFix) q = fix_point_loads(a, t);
+    if (r > 0 && a.chg[r - 1] == 0) return;
     const int* Tc = a.T[r % 3];
     int* Tn = a.T[(r + 1) % 3];
     int* Tz = a.T[(r + 2) % 3];
-    if (t < a.nkp) Tz[t] = greedy_preblocked(a, t) ? -1 : INT_MAX;
+    if (t < a.nkp) {
+        const bool pre = kFix ? q.f0 >= 0 && (!a.fobs0 || q.o0 > 0) : greedy_preblocked(a, t);
+        Tz[t] = pre ? -1 : INT_MAX;
+    }
     bool changed = false;
     if (t < a.m) {
-        const int prev = a.dec[t];
-        const bool blocks = !a.nobs || a.nobs[t] > 0;
-        const int d = a.kfix ? greedy_decide_fix(a, Tc, t) : greedy_decide(a, Tc, t);
+        const int prev = kFix ? q.prev : a.dec[t];
+        const bool blocks = !a.nobs || (kFix ? q.nb : a.nobs[t]) > 0;
+        const int d = kFix ? greedy_decide_fixq(a, Tc, t, q) : a.kfix ? greedy_decide_fix(a, Tc, t) : greedy_decide(a, Tc, t);
         // contended slots: an acceptor whose index cannot lower the slot's minimum (as read
         // now; a stale read only costs the atomic) skips the atomic
         if (d >= 0 && blocks && __hip_atomic_load(&Tn[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > t)
@@ -226,18 +273,21 @@ __global__ __launch_bounds__(kGreedyBlock) void greedy_round_kernel(GreedyArgs a
 // nothing the round is a no-op and the decisions are final; otherwise this round's decisions
 // are accepted and chg[r] != 0 reports that they may not be (the host then reruns the call).
 // Either way a point's acceptance needs only its own decision, so no second launch.
+// (kRound is the fused path's, whose layout is the fixed-slot one: its per-point loads go first)
 template <bool kRound>
 __global__ __launch_bounds__(kGreedyBlock) void greedy_accept_kernel(GreedyArgs a, int r) {
     const int i = blockIdx.x * kGreedyBlock + threadIdx.x;
     bool acc = false;
+    FixPoint q{};
+    if constexpr (kRound) q = fix_point_loads(a, i);
     if (kRound && !(r > 0 && a.chg[r - 1] == 0)) {
         const int* Tc = a.T[r % 3];
         int* Tn = a.T[(r + 1) % 3];
         bool changed = false;
         if (i < a.m) {
-            const int prev = a.dec[i];
-            const bool blocks = !a.nobs || a.nobs[i] > 0;
-            const int d = a.kfix ? greedy_decide_fix(a, Tc, i) : greedy_decide(a, Tc, i);
+            const int prev = q.prev;
+            const bool blocks = !a.nobs || q.nb > 0;
+            const int d = greedy_decide_fixq(a, Tc, i, q);
             if (d >= 0 && blocks && __hip_atomic_load(&Tn[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > i)
                 atomicMin(&Tn[d], i);
             changed = d != prev;
@@ -525,6 +575,7 @@ __device__ __forceinline__ int sub_scan(int x, int& total) {
 // kPre: the isInFrustum outputs are already resident (orbfe_search_by_projection_local_device:
 // a.mp's track_in_view / is_bad / projection / level / viewing cosine), so the point reads them
 // instead of evaluating the frustum test and fa.fr is unused.
+__device__ orbfe_keypoint g_dummy_kp;  // sbp_local_fused_kernel: a frame without keypoints
 template <bool kPre>
 __global__ __launch_bounds__(1024) void sbp_local_fused_kernel(SbpFusedArgs fa) {
     const SbpLocalArgs& a = fa.s;
@@ -543,13 +594,14 @@ __global__ __launch_bounds__(1024) void sbp_local_fused_kernel(SbpFusedArgs fa) 
     const int i = blockIdx.x * kSbpPts + tid / kSbpLpp;
     if (sub == 0) {  // greedy_init_kernel's work, spread over the grid (max(m, nkp) points)
         const GreedyArgs& g = fa.g;
-        if (i < g.nkp) {
-            const int v = greedy_preblocked(g, i) ? -1 : INT_MAX;
+        if (i < g.nkp) {  // (both words loaded together, each once)
+            const int f0 = g.fmp0[i], o0 = g.fobs0[i];
+            const int v = f0 >= 0 && o0 > 0 ? -1 : INT_MAX;  // greedy_preblocked (fobs0 set here)
             g.T[0][i] = v;
             g.T[1][i] = v;
             g.last[i] = -1;
-            g.save_fmp[i] = g.fmp0[i];
-            g.save_fobs[i] = g.fobs0[i];
+            g.save_fmp[i] = f0;
+            g.save_fobs[i] = o0;
         }
         if (i < g.m) g.dec[i] = -2;
         if (i <= fa.rounds) g.chg[i] = 0;
@@ -570,16 +622,17 @@ __global__ __launch_bounds__(1024) void sbp_local_fused_kernel(SbpFusedArgs fa) 
     static_assert(kSbpFixKp == 2 * 1024, "two keypoints per thread");
     int mine[2] = {-1, -1};  // AssignFeaturesToGrid's cell of keypoints tid, tid + 1024
     {
+        // (unconditional loads at clamped indices: a load under a branch was waited for on the
+        // spot; a frame without keypoints reads a dummy record)
         float kx[2], ky[2];
         int ko[2];
+        const orbfe_keypoint* kp = F.n > 0 ? F.k : &g_dummy_kp;
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
-            const int k = tid + 1024 * b;
-            if (k < F.n) {
-                kx[b] = F.k[k].x;
-                ky[b] = F.k[k].y;
-                ko[b] = F.k[k].octave;
-            }
+            const int k = min(tid + 1024 * b, max(F.n - 1, 0));
+            kx[b] = kp[k].x;
+            ky[b] = kp[k].y;
+            ko[b] = kp[k].octave;
         }
         __syncthreads();  // cs cleared
 #pragma unroll
@@ -601,15 +654,11 @@ __global__ __launch_bounds__(1024) void sbp_local_fused_kernel(SbpFusedArgs fa) 
     for (int q0 = 0; q0 < 2 * F.n; q0 += 4 * 1024) {
         uint4 d[4];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int q = q0 + tid + 1024 * b;
-            if (q < 2 * F.n) d[b] = F.desc[q];
-        }
+        for (int b = 0; b < 4; ++b) d[b] = F.desc[min(q0 + tid + 1024 * b, 2 * F.n - 1)];
+        // (stores at the same clamped indices, unconditional too: a conditional store let the
+        // compiler sink each load into its branch, one global latency per load again)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int q = q0 + tid + 1024 * b;
-            if (q < 2 * F.n) fdesc[q] = d[b];
-        }
+        for (int b = 0; b < 4; ++b) fdesc[min(q0 + tid + 1024 * b, 2 * F.n - 1)] = d[b];
     }
     // The frame's grid built in this workgroup's LDS (grid_lds_kernel's counting sort): cs[c]
     // the start of cell c, ci its keypoints in index (insertion) order.

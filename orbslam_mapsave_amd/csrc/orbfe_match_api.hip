@@ -462,7 +462,7 @@ struct orbfe_matcher {
         while (true) {
             const int r0 = r;
             for (int b = 0; b < batch && r <= M; ++b, ++r)
-                hipLaunchKernelGGL(greedy_round_kernel, dim3(blocks), dim3(kGreedyBlock), 0, stream, g, r);
+                hipLaunchKernelGGL(greedy_round_kernel<false>, dim3(blocks), dim3(kGreedyBlock), 0, stream, g, r);
             chg_h.assign(r - r0, 0);
             ORBFE_HIP(hipMemcpyAsync(chg_h.data(), g.chg + r0, (r - r0) * sizeof(int), hipMemcpyDeviceToHost, stream));
             ORBFE_HIP(hipStreamSynchronize(stream));
@@ -549,7 +549,7 @@ bool sbp_local_graph(orbfe_matcher* m, const SbpFusedArgs& fu, const GreedyArgs&
         r_arg[k] = k - 1;
         g_params[k][0] = &g_arg;
         g_params[k][1] = &r_arg[k];
-        p[k].func = k < rounds ? reinterpret_cast<void*>(&greedy_round_kernel)
+        p[k].func = k < rounds ? reinterpret_cast<void*>(&greedy_round_kernel<true>)
                                : reinterpret_cast<void*>(&greedy_accept_kernel<true>);
         p[k].gridDim = k < rounds ? grid[1] : grid[2];
         p[k].blockDim = dim3(kGreedyBlock);
@@ -685,7 +685,7 @@ int sbp_local_fast(orbfe_matcher* m, const orbfe_frame_view* frame, const Frustu
     if (!sbp_local_graph<kPre>(m, fu, g, grid, shm, kBlindRounds)) {
         hipLaunchKernelGGL(sbp_local_fused_kernel<kPre>, grid[0], dim3(1024), shm, m->stream, fu);
         for (int r = 0; r < kBlindRounds - 1; ++r)
-            hipLaunchKernelGGL(greedy_round_kernel, grid[1], dim3(kGreedyBlock), 0, m->stream, g, r);
+            hipLaunchKernelGGL(greedy_round_kernel<true>, grid[1], dim3(kGreedyBlock), 0, m->stream, g, r);
         // the last blind round and the acceptances in one launch
         hipLaunchKernelGGL(greedy_accept_kernel<true>, grid[2], dim3(kGreedyBlock), 0, m->stream,
                            g, kBlindRounds - 1);
