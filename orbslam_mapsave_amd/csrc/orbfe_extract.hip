@@ -282,6 +282,7 @@ __device__ __forceinline__ uint32_t resize4(const uint32_t (&h0)[4], const uint3
 #endif
 constexpr int kRsTW = 128, kRsTH = ORBFE_RS_TH;  // output tile; 8 thread rows of kRsTH / 8
 constexpr int kRsRPT = kRsTH / 8;
+constexpr int kR2Rows = 96;  // resize2_kernel: level-l region rows per tile (host-checked)
 template <bool kX86>
 __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
@@ -294,6 +295,15 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
     const int nrow = sy1 - sy0 + 1, P = a.lds_pitch;  // P % 16 == 0
     const int cpr = ((sx1 - sx0) >> 4) + 1;                 // 16-byte chunks per source row
     const uint8_t* src = a.src.base + f * a.src.fpitch;
+    // this thread's output rows' table entries, loaded with the staging (clamped rows,
+    // unconditional): read inside the row loop they cost one round trip per row
+    int ytr[kRsRPT][3];
+#pragma unroll
+    for (int j = 0; j < kRsRPT; ++j) {
+        const int yc = min(oy + kRsRPT * (int)(threadIdx.x >> 5) + j, a.dh - 1);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ytr[j][k] = a.yt[3 * yc + k];
+    }
     // source rows -> LDS in 16-byte chunks (global dwordx4 needs 4-byte alignment: sx0 % 4 ==
     // 0, pitch % 4 == 0); four chunks per thread in flight before any LDS store.  A chunk
     // reaching past the row end is assembled from dwords / bytes (level 0 may be the caller's
@@ -329,7 +339,7 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
         for (int j = 0; j < kRsRPT; ++j) {
             const int y = oy + kRsRPT * ty + j;
             if (y >= a.dh) break;
-            const int ry0 = a.yt[3 * y] - sy0, ry1 = a.yt[3 * y + 1] - sy0, bb = a.yt[3 * y + 2];
+            const int ry0 = ytr[j][0] - sy0, ry1 = ytr[j][1] - sy0, bb = ytr[j][2];
             const uint32_t b0 = (uint32_t)bb & 0xffffu, b1 = (uint32_t)bb >> 16;
             uint32_t t0[4], t1[4];
             hsum(ry0, t0);
@@ -358,7 +368,7 @@ __global__ __launch_bounds__(256) void resize_kernel(ResizeArgs a) {
     for (int j = 0; j < kRsRPT; ++j) {
         const int y = oy + kRsRPT * ty + j;
         if (y >= a.dh) break;
-        const int ry0 = a.yt[3 * y] - sy0, ry1 = a.yt[3 * y + 1] - sy0, bb = a.yt[3 * y + 2];
+        const int ry0 = ytr[j][0] - sy0, ry1 = ytr[j][1] - sy0, bb = ytr[j][2];
         const int b0 = bb & 0xffff, b1 = (int)((unsigned)bb >> 16);
         const uint8_t* s0 = rs_lds + ry0 * P;
         const uint8_t* s1 = rs_lds + ry1 * P;
@@ -396,6 +406,21 @@ __global__ __launch_bounds__(256) void resize2_kernel(Resize2Args a) {
     xcd_block(bx, f);
     const int4 c = a.tiles[2 * bx], own = a.tiles[2 * bx + 1];
     const int tid = threadIdx.x;
+    const int oy = (bx / a.tiles_x) * kRsTH;
+    // The row tables both passes walk (level l's rows c.x .. c.y, the tile's level l + 1 rows),
+    // staged in LDS beside the image rows: read from global inside the row loops they cost one
+    // round trip per row.  Loads and stores unconditional at clamped indices.
+    __shared__ int ytm_s[3 * kR2Rows];  // c.y - c.x < kR2Rows (host plan)
+    __shared__ int ytd_s[3 * kRsTH];
+    {
+        const int n3 = 3 * (c.y - c.x + 1);
+        const int i0 = min(tid, n3 - 1), i1 = min(tid + 256, n3 - 1), i2 = min(tid, 3 * kRsTH - 1);
+        const int yd = min(oy + i2 / 3, a.dh - 1);
+        const int v0 = a.yt_m[3 * c.x + i0], v1 = a.yt_m[3 * c.x + i1], v2 = a.yt_d[3 * yd + i2 % 3];
+        ytm_s[i0] = v0;
+        ytm_s[i1] = v1;
+        ytd_s[i2] = v2;
+    }
     // level l - 1 rectangle the level-l region reads
     const int ay0 = a.yt_m[3 * c.x], ay1 = a.yt_m[3 * c.y + 1];
     const int ax0 = a.xt_m[3 * c.z] & ~3, ax1 = a.xt_m[3 * c.w + 1];
@@ -432,7 +457,7 @@ __global__ __launch_bounds__(256) void resize2_kernel(Resize2Args a) {
             const bool own_x = x >= own.z && x < own.w;  // own column bounds are multiples of 4
             uint8_t* mid = const_cast<uint8_t*>(a.mid.base) + f * a.mid.fpitch;
             for (int r = c.x + ry; r <= c.y; r += rps) {
-                const int* yy = a.yt_m + 3 * r;
+                const int* yy = ytm_s + 3 * (r - c.x);
                 const uint32_t b0 = (uint32_t)yy[2] & 0xffffu, b1 = (uint32_t)yy[2] >> 16;
                 uint32_t t0[4], t1[4];
                 hsum(r2_lds, a.pa, yy[0] - ay0, wofs, sh, sel, cf, t0);
@@ -453,7 +478,7 @@ __global__ __launch_bounds__(256) void resize2_kernel(Resize2Args a) {
     __syncthreads();
     {   // level l + 1 tile from the level-l region (resize_kernel's thread layout)
         const int tiles_x = a.tiles_x;
-        const int ox = (bx % tiles_x) * kRsTW, oy = (bx / tiles_x) * kRsTH;
+        const int ox = (bx % tiles_x) * kRsTW;
         const int tx = tid & 31, ty = tid >> 5;
         const int x = ox + 4 * tx;
         if (x >= a.dw) return;
@@ -469,7 +494,7 @@ __global__ __launch_bounds__(256) void resize2_kernel(Resize2Args a) {
         for (int j = 0; j < kRsRPT; ++j) {
             const int y = oy + kRsRPT * ty + j;
             if (y >= a.dh) break;
-            const int* yy = a.yt_d + 3 * y;
+            const int* yy = ytd_s + 3 * (y - oy);
             const uint32_t b0 = (uint32_t)yy[2] & 0xffffu, b1 = (uint32_t)yy[2] >> 16;
             uint32_t t0[4], t1[4];
             hsum(B, a.pb, yy[0] - c.x, wofs, sh, sel, cf, t0);
@@ -1227,6 +1252,27 @@ __global__ __launch_bounds__(kTailBlock) void resize_tail_kernel(ResizeTailArgs 
     __shared__ __attribute__((aligned(16))) uint8_t lds[kTailLds];
     const int f = blockIdx.x;
     const int tid = threadIdx.x;
+    // The tables of each level (its y table for LDS, this thread's four x entries) are loaded
+    // one level ahead, so they arrive while the level before is made: loaded at the top of
+    // their own level, each level began with two global round trips.  Loads unconditional at
+    // clamped indices (3 dh <= 3 kTailRows: entries tid and tid + kTailBlock).
+    static_assert(3 * kTailRows <= 2 * kTailBlock, "two y-table entries per thread");
+    int yn[2], xn[4][3];
+    auto fetch_tables = [&](int k) __attribute__((always_inline)) {
+        const int n3 = 3 * a.dh[k], dw = a.dw[k];
+        const int* yt = a.yt[k];
+        const int* xt = a.xt[k];
+        yn[0] = yt[min(tid, n3 - 1)];
+        yn[1] = yt[min(tid + kTailBlock, n3 - 1)];
+        const int x = 4 * (tid % ((dw + 3) >> 2));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int dx = min(x + q, dw - 1);
+#pragma unroll
+            for (int e = 0; e < 3; ++e) xn[q][e] = xt[3 * dx + e];
+        }
+    };
+    fetch_tables(0);
     {   // level ts-1 from the pyramid in 16-byte chunks (LDS pitch lp[0] % 16 == 0, inside the
         // slab's 64-byte row pitch), four per thread in flight before the LDS stores
         const LevelPtr sp = a.src;
@@ -1258,9 +1304,16 @@ __global__ __launch_bounds__(kTailBlock) void resize_tail_kernel(ResizeTailArgs 
         uint8_t* d = lds + (((k + 1) & 1) ? a.buf_b : 0);
         const int sp_l = a.lp[k], dp_l = a.lp[k + 1];
         const int dw = a.dw[k], dh = a.dh[k], xb = a.simd_xb[k];
-        const int* xt = a.xt[k];
         const int* yt = yts;
-        for (int i = tid; i < 3 * dh; i += kTailBlock) yts[i] = a.yt[k][i];
+        const int ycur[2] = {yn[0], yn[1]};
+        int xc[4][3];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int e = 0; e < 3; ++e) xc[q][e] = xn[q][e];
+        if (k + 1 < a.nt) fetch_tables(k + 1);
+        yts[min(tid, 3 * dh - 1)] = ycur[0];
+        yts[min(tid + kTailBlock, 3 * dh - 1)] = ycur[1];
         __syncthreads();
         const int gpr = (dw + 3) >> 2;           // 4-pixel groups per row
         const int rps = kTailBlock / gpr;        // rows per sweep
@@ -1273,10 +1326,9 @@ __global__ __launch_bounds__(kTailBlock) void resize_tail_kernel(ResizeTailArgs 
             int x0[4], x1[4], a0[4], a1[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int dx = min(x + q, dw - 1);
-                x0[q] = xt[3 * dx];
-                x1[q] = xt[3 * dx + 1];
-                const int aa = xt[3 * dx + 2];
+                x0[q] = xc[q][0];
+                x1[q] = xc[q][1];
+                const int aa = xc[q][2];
                 a0[q] = (int)(hcoef<kX86>((uint32_t)aa) & 0xffffu);  // x86: 16 a0, 16 a1 (hcoef)
                 a1[q] = (int)(hcoef<kX86>((uint32_t)aa) >> 16);
             }
@@ -4212,7 +4264,7 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
             const int pa = ((awid + 15) & ~15) + 16, pb = ((bwid + 15) & ~15) + 16;
             const size_t bofs = ((size_t)arows * pa + 15) & ~(size_t)15;
             const size_t lds = bofs + (size_t)brows * pb;
-            g.rs2_ok[l] = lds <= 64 * 1024 && gmax <= 256;
+            g.rs2_ok[l] = lds <= 64 * 1024 && gmax <= 256 && brows <= kR2Rows;
             if (!g.rs2_ok[l]) continue;
             g.rs2_tiles_x[l] = ntx;
             g.rs2_tiles[l] = ntx * nty;
