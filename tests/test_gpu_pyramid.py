@@ -70,6 +70,29 @@ def test_band_plans(lds_kb, monkeypatch):
         e.close()
 
 
+@pytest.mark.parametrize("size", [(50, 40), (41, 33)])
+@pytest.mark.parametrize("arith", ["scalar", "x86"])
+def test_narrow_levels_exact(size, arith, monkeypatch):
+    """Frames whose top levels are narrower than 16 bytes (50 px: level 7 is 14 px wide): the
+    per-level staging (stage_rows16) then rebuilds every chunk from bytes instead of its
+    unconditional 16-byte load; levels byte-exact in both readings, batch and single frame."""
+    from orbslam_mapsave_amd.native import ORBextractor
+    monkeypatch.setenv("ORBFE_PYR", "0")
+    w, h = size
+    p = oracle.params(200, 1.2, 8, 20, 7)
+    e = ORBextractor(200, 1.2, 8, 20, 7, device=0, max_width=w, max_height=h)
+    var = oracle.VAR_H5_SSE2 if arith == "x86" else 0
+    e.set_arithmetic(e.ARITH_X86_SIMD if arith == "x86" else e.ARITH_SCALAR)
+    try:
+        imgs = np.stack([synthetic_frame(11 * w + s, w, h) for s in range(9)])
+        e.extract_batch(imgs)
+        _levels_exact(e, p, imgs[:3], var)
+        e(imgs[4])
+        _levels_exact(e, p, imgs[4:5], var)
+    finally:
+        e.close()
+
+
 @pytest.mark.parametrize("sf,nl", [(1.5, 5), (2.0, 4), (1.1, 10)])
 def test_other_scale_factors(sf, nl, monkeypatch):
     """Fallback (or band kernel, where the window fits) for other scale factors."""
