@@ -155,10 +155,19 @@ struct CandCache {
     int e0, e1;
     int2 c[kCandCache];
 };
+// (the 16 loads unconditional, at indices clamped into the point's own list — a point without
+// candidates reads a zero word — so they are in flight together: loaded under the per-candidate
+// condition, each was waited for before the next was issued)
+__device__ int2 g_zero_int2;
 __device__ __forceinline__ void cand_cache_load(const GreedyArgs& a, int i, CandCache& cc) {
     greedy_range(a, i, cc.e0, cc.e1);
+    const bool any = cc.e1 > cc.e0;
 #pragma unroll
-    for (int k = 0; k < kCandCache; ++k) cc.c[k] = cc.e0 + k < cc.e1 ? a.cand[cc.e0 + k] : make_int2(0, 0);
+    for (int k = 0; k < kCandCache; ++k) {
+        // (no select on the value: the compiler turned it into a branch around the load;
+        // greedy_decide_cached reads only entries below e1)
+        cc.c[k] = *(any ? a.cand + min(cc.e0 + k, cc.e1 - 1) : &g_zero_int2);
+    }
 }
 __device__ __forceinline__ int greedy_decide_cached(const GreedyArgs& a, const int* Tc, int i,
                                                     const CandCache& cc) {
@@ -440,7 +449,9 @@ __global__ __launch_bounds__(kGreedySmallBlock) void greedy_small_kernel(GreedyA
     int* last = lds + 2 * a.nkp;
     int* pre = lds + 3 * a.nkp;  // blocked-before state per slot
     for (int s = tid; s < a.nkp; s += kGreedySmallBlock) {
-        const int v = greedy_preblocked(a, s) ? -1 : INT_MAX;
+        // (both words loaded together: greedy_preblocked's short circuit chained them)
+        const int f0 = a.fmp0[s], o0 = a.fobs0 ? a.fobs0[s] : 1;
+        const int v = f0 >= 0 && o0 > 0 ? -1 : INT_MAX;
         pre[s] = v;  // the per-round reset reads LDS, not the slot arrays
         T[0][s] = v;
         T[1][s] = v;
@@ -453,7 +464,8 @@ __global__ __launch_bounds__(kGreedySmallBlock) void greedy_small_kernel(GreedyA
     if (tid < a.m) cand_cache_load(a, tid, cc);
     else cc.e0 = cc.e1 = 0;
     int my_dec = -2;
-    const bool my_blocks = tid < a.m && (!a.nobs || a.nobs[tid] > 0);
+    const int my_nobs = a.nobs ? a.nobs[min(tid, max(a.m - 1, 0))] : 1;  // (unconditional)
+    const bool my_blocks = tid < a.m && my_nobs > 0;
     if (tid < kHistoLength) h[tid] = 0;
     if (tid == 0) nm = 0;
     __syncthreads();

@@ -1112,10 +1112,14 @@ template <bool FILL>
 __global__ __launch_bounds__(256) void sbp_last_cand_kernel(SbpLastArgs a) {
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per last-frame point
     if (i >= a.n_last) return;
-    if (FILL && a.off[i + 1] > a.cand_cap) return;
+    // Inputs read up front, as in sbp_kf_cand_kernel.
+    const bool room = !FILL || a.off[i + 1] <= a.cand_cap;
+    const bool live = a.valid[i] && !a.outlier[i];
+    const float P[3] = {a.xyz[3 * i], a.xyz[3 * i + 1], a.xyz[3 * i + 2]};
+    const int o = a.lk[i].octave;
+    if (!room) return;
     int n = 0;
-    if (a.valid[i] && !a.outlier[i]) {
-        const float* P = a.xyz + 3 * i;
+    {
         float pc[3];
 #pragma unroll
         for (int r = 0; r < 3; ++r)
@@ -1123,8 +1127,7 @@ __global__ __launch_bounds__(256) void sbp_last_cand_kernel(SbpLastArgs a) {
         const float invz = (float)(1.0 / (double)pc[2]);
         const float u = a.fx * pc[0] * invz + a.cx;
         const float v = a.fy * pc[1] * invz + a.cy;
-        if (!(invz < 0) && !(u < a.minx || u > a.maxx) && !(v < a.miny || v > a.maxy)) {
-            const int o = a.lk[i].octave;
+        if (live && !(invz < 0) && !(u < a.minx || u > a.maxx) && !(v < a.miny || v > a.maxy)) {
             const float radius = a.th * a.scale[o];
             const int lo = a.mode == 0 ? o - 1 : a.mode == 1 ? o : 0;
             const int hi = a.mode == 0 ? o + 1 : a.mode == 1 ? -1 : o;
@@ -1178,10 +1181,15 @@ template <bool FILL>
 __global__ __launch_bounds__(256) void sbp_kf_cand_kernel(SbpKfArgs a) {
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per keyframe map point
     if (i >= a.n) return;
-    if (FILL && a.off[i + 1] > a.cand_cap) return;
+    // Every per-point input is read up front and feeds the unconditional arithmetic below, so
+    // the loads issue together instead of one flag test (and one memory round trip) at a time.
+    const bool room = !FILL || a.off[i + 1] <= a.cand_cap;
+    const bool live = a.valid[i] && !a.bad[i] && !a.found[i];
+    const float P[3] = {a.xyz[3 * i], a.xyz[3 * i + 1], a.xyz[3 * i + 2]};
+    const float maxd = a.maxd[i], mind = a.mind[i];
+    if (!room) return;
     int n = 0;
-    if (a.valid[i] && !a.bad[i] && !a.found[i]) {
-        const float* P = a.xyz + 3 * i;
+    {
         float pc[3];
 #pragma unroll
         for (int r = 0; r < 3; ++r)
@@ -1189,16 +1197,13 @@ __global__ __launch_bounds__(256) void sbp_kf_cand_kernel(SbpKfArgs a) {
         const float invz = (float)(1.0 / (double)pc[2]);  // 1.0/x3Dc.at<float>(2): double divide
         const float u = a.fx * pc[0] * invz + a.cx;
         const float v = a.fy * pc[1] * invz + a.cy;
-        bool ok = !(u < a.minx || u > a.maxx) && !(v < a.miny || v > a.maxy);
-        float dist = 0.f;
+        const float po0 = P[0] - a.ow[0], po1 = P[1] - a.ow[1], po2 = P[2] - a.ow[2];
+        const float dist = (float)sqrt((double)po0 * po0 + (double)po1 * po1 + (double)po2 * po2);
+        const float dmax = 1.2f * maxd, dmin = 0.8f * mind;  // MapPoint.cc:621-631
+        const bool ok = live && !(u < a.minx || u > a.maxx) && !(v < a.miny || v > a.maxy) &&
+                        !(dist < dmin || dist > dmax);
         if (ok) {
-            const float po0 = P[0] - a.ow[0], po1 = P[1] - a.ow[1], po2 = P[2] - a.ow[2];
-            dist = (float)sqrt((double)po0 * po0 + (double)po1 * po1 + (double)po2 * po2);
-            const float dmax = 1.2f * a.maxd[i], dmin = 0.8f * a.mind[i];  // MapPoint.cc:621-631
-            ok = !(dist < dmin || dist > dmax);
-        }
-        if (ok) {
-            const float ratio = a.maxd[i] / dist;
+            const float ratio = maxd / dist;
             const int lvl = (int)ceilf((float)log((double)ratio) / a.log_scale);
             if (lvl < 0 || lvl >= a.nlevels) {
                 if ((threadIdx.x & 63) == 0) atomicExch(a.status, ORBFE_ERR_UNSUPPORTED);  // mvScaleFactors[lvl]
