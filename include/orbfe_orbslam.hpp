@@ -113,6 +113,15 @@ private:
 };
 
 // Flat stand-in for the Frame members the matchers read (Frame.h): owns nothing.
+// A DBoW2 FeatureVector (node id -> feature indices, ids ascending) as flat arrays: node i's
+// features are feat[node_off[i] .. node_off[i + 1]).
+struct FeatureVectorView {
+    const int32_t* node_ids;
+    const int32_t* node_off;  // nn + 1
+    const int32_t* feat;
+    int nn;
+};
+
 struct FrameData {
     std::vector<orbfe_keypoint> keys_un;   // mvKeysUn
     std::vector<uint8_t> descriptors;      // mDescriptors, N x 32
@@ -211,6 +220,29 @@ public:
         return n;
     }
 
+    // SearchByBoW(KeyFrame* pKF, Frame& F, vpMapPointMatches) (ORBmatcher.cc:159-291).
+    // kf_mp_ok[i]: the keyframe's feature i holds a MapPoint that is not bad (202-207); the two
+    // FeatureVectors as their (node id, features) lists; vpMapPointMatches[f] = the keyframe
+    // feature matched to frame feature f, or -1.
+    int SearchByBoW(const FrameData& KF, const std::vector<uint8_t>& kf_mp_ok,
+                    const FeatureVectorView& kf_fv, const FrameData& F,
+                    const FeatureVectorView& f_fv, std::vector<int>& vpMapPointMatches) {
+        kf_angle_.resize(KF.keys_un.size());
+        for (size_t i = 0; i < KF.keys_un.size(); ++i) kf_angle_[i] = KF.keys_un[i].angle;
+        f_angle_.resize(F.keys_un.size());
+        for (size_t i = 0; i < F.keys_un.size(); ++i) f_angle_[i] = F.keys_un[i].angle;
+        vpMapPointMatches.resize(F.keys_un.size());
+        int n = 0;
+        check("orbfe_search_by_bow",
+              orbfe_search_by_bow(m_, mfNNratio, mbCheckOrientation, (int)KF.keys_un.size(),
+                                  KF.descriptors.data(), kf_angle_.data(), kf_mp_ok.data(),
+                                  kf_fv.nn, kf_fv.node_ids, kf_fv.node_off, kf_fv.feat,
+                                  (int)F.keys_un.size(), F.descriptors.data(), f_angle_.data(),
+                                  f_fv.nn, f_fv.node_ids, f_fv.node_off, f_fv.feat,
+                                  vpMapPointMatches.data(), &n));
+        return n;
+    }
+
     orbfe_matcher* handle() { return m_; }
 
 private:
@@ -221,6 +253,7 @@ private:
     orbfe_matcher* m_ = nullptr;
     float mfNNratio;
     bool mbCheckOrientation;
+    std::vector<float> kf_angle_, f_angle_;  // SearchByBoW: the keypoints' angles as arrays
 };
 
 }  // namespace orbfe

@@ -1,6 +1,7 @@
 // GPU parity check of the C++ adapter (include/orbfe_orbslam.hpp) against the CPU oracle, as
 // C++ host code of the reference would use it.  Built by __graft_entry__.build(); run by
 // tests/test_gpu_cpp.py on the MI355X.  Prints "ADAPTER PASS" on success.
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -113,6 +114,65 @@ int main() {
     const bool sfi_same = nm == onm && m12 == om12 && prev == oprev;
     std::printf("SearchForInitialization: %d matches (oracle %d) %s\n", nm, onm, sfi_same ? "exact" : "MISMATCH");
     fails += !sfi_same;
+    // SearchByBoW(KeyFrame*, Frame&) on two 1000-keypoint views of one scene: FeatureVectors with
+    // a feature's node given by its descriptor's first byte (64 nodes, ~16 features each, ids
+    // ascending, features in index order as DBoW2 fills them); every fifth keyframe feature has
+    // no good MapPoint.  Parity against the oracle, then the latency of both from C++ (mean over
+    // 2,000 calls after 100 warm-up calls; the CPU port single-threaded).
+    {
+        orbfe::FrameData K, F;
+        std::vector<uint8_t> b1 = make_image(W, H, 11), b2 = make_image(W, H, 11);
+        std::memmove(b2.data() + 2 * W + 2, b2.data(), b2.size() - 2 * W - 2);  // shifted view
+        ex(b1.data(), W, H, W, nullptr, 0, K.keys_un, K.descriptors);
+        ex(b2.data(), W, H, W, nullptr, 0, F.keys_un, F.descriptors);
+        struct Fv { std::vector<int32_t> ids, off, feat; };
+        auto make_fv = [](const std::vector<uint8_t>& d, int n) {
+            std::vector<std::vector<int32_t>> nodes(64);
+            for (int i = 0; i < n; ++i) nodes[d[32 * (size_t)i] >> 2].push_back(i);
+            Fv v;
+            v.off.push_back(0);
+            for (int k = 0; k < 64; ++k) {
+                if (nodes[k].empty()) continue;
+                v.ids.push_back(k);
+                v.feat.insert(v.feat.end(), nodes[k].begin(), nodes[k].end());
+                v.off.push_back((int32_t)v.feat.size());
+            }
+            return v;
+        };
+        const int nk = (int)K.keys_un.size(), nf = (int)F.keys_un.size();
+        const Fv kfv = make_fv(K.descriptors, nk), ffv = make_fv(F.descriptors, nf);
+        const orbfe::FeatureVectorView kv{kfv.ids.data(), kfv.off.data(), kfv.feat.data(), (int)kfv.ids.size()};
+        const orbfe::FeatureVectorView fv{ffv.ids.data(), ffv.off.data(), ffv.feat.data(), (int)ffv.ids.size()};
+        std::vector<uint8_t> ok(nk);
+        for (int i = 0; i < nk; ++i) ok[i] = i % 5 != 0;
+        std::vector<float> ka(nk), fa(nf);
+        for (int i = 0; i < nk; ++i) ka[i] = K.keys_un[i].angle;
+        for (int i = 0; i < nf; ++i) fa[i] = F.keys_un[i].angle;
+        orbfe::ORBmatcher bm(0.75f, true);
+        std::vector<int> mg;
+        const int ng = bm.SearchByBoW(K, ok, kv, F, fv, mg);
+        std::vector<int32_t> mo(nf, -1);
+        int no = 0;
+        auto cpu = [&] {
+            return oracle_search_by_bow(0.75f, 1, K.descriptors.data(), ka.data(), ok.data(), kfv.ids.data(),
+                                        kfv.off.data(), kfv.feat.data(), kv.nn, nf, F.descriptors.data(),
+                                        fa.data(), ffv.ids.data(), ffv.off.data(), ffv.feat.data(), fv.nn,
+                                        mo.data(), &no);
+        };
+        if (cpu()) return 2;
+        const bool bow_same = ng == no && std::equal(mg.begin(), mg.end(), mo.begin());
+        std::printf("SearchByBoW: %d matches (oracle %d) %s\n", ng, no, bow_same ? "exact" : "MISMATCH");
+        fails += !bow_same;
+        auto mean_us = [&](auto&& call) {
+            for (int i = 0; i < 100; ++i) call();
+            const auto t0 = std::chrono::steady_clock::now();
+            for (int i = 0; i < 2000; ++i) call();
+            return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / 2000;
+        };
+        const double gpu_us = mean_us([&] { bm.SearchByBoW(K, ok, kv, F, fv, mg); });
+        const double cpu_us = mean_us([&] { fails += cpu() != 0; });
+        std::printf("BOW_LATENCY gpu_us=%.2f cpu_us=%.2f nodes=%d/%d\n", gpu_us, cpu_us, kv.nn, fv.nn);
+    }
     std::printf(fails ? "ADAPTER FAIL\n" : "ADAPTER PASS\n");
     return fails ? 1 : 0;
 }

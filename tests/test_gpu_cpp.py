@@ -16,3 +16,4 @@ def test_cpp_adapter_parity():
     print(r.stdout)
     assert r.returncode == 0 and "ADAPTER PASS" in r.stdout, r.stdout + r.stderr
     assert "LATENCY" in r.stdout  # the C++ caller's single-frame latency (tools/bench_rows.py row)
+    assert "BOW_LATENCY" in r.stdout  # SearchByBoW from C++: GPU and the one-thread CPU port
