@@ -1398,16 +1398,58 @@ __device__ __forceinline__ half2v fast_h2(uint32_t b) {
 __device__ __forceinline__ _Float16 fast_dn(uint32_t b) {
     return __builtin_bit_cast(_Float16, (unsigned short)b);
 }
+#ifndef ORBFE_FAST_ROWREAD
+#define ORBFE_FAST_ROWREAD 0
+#endif
+// ORBFE_FAST_ROWREAD (experiment, off): the 16 circle bytes and the centre from seven unaligned
+// row reads (2 x 4 + 5 x 8 bytes: ds_read_b32 / ds_read_b64 at byte addresses; 6 LDS
+// instructions instead of 17 ds_read_u8), each pair of bytes zero-extended into the two halves
+// of one register by a v_perm and selected by op_sel.  Bit-exact, but the unaligned LDS reads
+// stall: c3 382 K -> 257 K frames/s, c4 76.0 K -> 50.4 K (profiles/r05/fast_rowread/)
+__device__ __forceinline__ void fast_rows(const uint8_t* p, int st, uint32_t (&x)[16], uint32_t& c) {
+    uint32_t rm3, rp3;
+    uint64_t rm2, rp2, rm1, rp1, r0;
+    __builtin_memcpy(&rm3, p - 3 * st - 1, 4);
+    __builtin_memcpy(&rp3, p + 3 * st - 1, 4);
+    __builtin_memcpy(&rm2, p - 2 * st - 2, 8);
+    __builtin_memcpy(&rp2, p + 2 * st - 2, 8);
+    __builtin_memcpy(&rm1, p - st - 3, 8);
+    __builtin_memcpy(&rp1, p + st - 3, 8);
+    __builtin_memcpy(&r0, p - 3, 8);
+    // perm(hi, lo, sel): selector bytes 0-3 = lo's bytes, 4-7 = hi's, 0x0c = 0; the pair
+    // (a, b) -> a in bits 0-7, b in bits 16-23
+    auto pr = [](uint32_t hi, uint32_t lo, uint32_t a, uint32_t b) {
+        return __builtin_amdgcn_perm(hi, lo, 0x0c000c00u | (b << 16) | a);
+    };
+    const uint32_t P1 = pr(rp3, rm3, 5, 6);   // x0, x1
+    const uint32_t P2 = pr(rp3, rm3, 2, 1);   // x7, x8
+    const uint32_t P3 = pr(rp3, rm3, 0, 4);   // x9, x15
+    const uint32_t P4 = pr((uint32_t)(rp2 >> 32), (uint32_t)rp2, 4, 0);  // x2, x14
+    const uint32_t P5 = pr((uint32_t)(rm2 >> 32), (uint32_t)rm2, 4, 0);  // x6, x10
+    const uint32_t P6 = pr((uint32_t)(rp1 >> 32), (uint32_t)rp1, 6, 0);  // x3, x13
+    const uint32_t P7 = pr((uint32_t)(rm1 >> 32), (uint32_t)rm1, 6, 0);  // x5, x11
+    const uint32_t P8 = pr((uint32_t)(r0 >> 32), (uint32_t)r0, 6, 0);    // x4, x12
+    x[0] = P1; x[1] = P1 >> 16; x[7] = P2; x[8] = P2 >> 16; x[9] = P3; x[15] = P3 >> 16;
+    x[2] = P4; x[14] = P4 >> 16; x[6] = P5; x[10] = P5 >> 16; x[3] = P6; x[13] = P6 >> 16;
+    x[5] = P7; x[11] = P7 >> 16; x[4] = P8; x[12] = P8 >> 16;
+    c = ((uint32_t)r0 >> 24) & 0xffu;
+}
 __device__ __forceinline__ int fast_S(const uint8_t* p, int st) {
+#if ORBFE_FAST_ROWREAD
+    uint32_t x[16], cv;
+    fast_rows(p, st, x, cv);
+    const _Float16 V = fast_dn(cv);
+#else
     const _Float16 V = fast_dn(p[0]);
     const uint32_t x[16] = {p[3 * st],      p[3 * st + 1],  p[2 * st + 2],  p[st + 3],
                             p[3],           p[-st + 3],     p[-2 * st + 2], p[-3 * st + 1],
                             p[-3 * st],     p[-3 * st - 1], p[-2 * st - 2], p[-st - 3],
                             p[-3],          p[st - 3],      p[2 * st - 2],  p[3 * st - 1]};
+#endif
     half2v e[16], m3[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        const _Float16 X = fast_dn(x[k]);
+        const _Float16 X = fast_dn(x[k] & 0xffffu);
         e[k] = half2v{-X, X};
     }
 #pragma unroll
