@@ -40,12 +40,17 @@ def predecessor_index(rank: int, world: int, per_rank: int, parts: int = 1) -> l
 
 
 def gather_slabs(desc: torch.Tensor, counts: torch.Tensor, g_desc: torch.Tensor,
-                 g_counts: torch.Tensor, world: int, async_op: bool = False) -> list:
+                 g_counts: torch.Tensor, world: int, async_op: bool = False,
+                 collective: bool | None = None) -> list:
     """All-gather the per-rank descriptor slabs (B x cap x 32 u8) and keypoint counts into the
     rank-major g_desc / g_counts.  With async_op (RCCL) the collectives are queued behind the
     current stream's work and the returned handles are waited on later; gloo (the CPU tests) and
-    world 1 complete before returning."""
-    if world == 1:
+    world 1 complete before returning.  collective (default: world > 1) = False copies instead of
+    calling the collective; True calls it at world 1 too (tests/test_gpu_rccl.py runs the RCCL
+    path on one GPU that way)."""
+    if collective is None:
+        collective = world > 1
+    if not collective:
         g_desc.copy_(desc)
         g_counts.copy_(counts)
         return []
@@ -76,10 +81,11 @@ class PredecessorMatch:
     stream that runs the match.  step() does both in sequence."""
 
     def __init__(self, rank: int, world: int, per_rank: int, cap: int, device, match,
-                 parts: int = 1):
+                 parts: int = 1, collective: bool | None = None):
         if parts < 1 or per_rank % parts:
             raise ValueError(f"per_rank {per_rank} is not a multiple of parts {parts}")
         self.world = world
+        self.collective = collective
         self.parts = parts
         self.per_part = per_rank // parts
         self.match = match
@@ -97,7 +103,8 @@ class PredecessorMatch:
         a, b = p * self.per_part, (p + 1) * self.per_part
         ga, gb = p * self.world * self.per_part, (p + 1) * self.world * self.per_part
         self._works += gather_slabs(desc[a:b], counts[a:b], self.g_desc[ga:gb],
-                                    self.g_n[ga:gb], self.world, async_op=True)
+                                    self.g_n[ga:gb], self.world, async_op=True,
+                                    collective=self.collective)
 
     def finish(self, desc: torch.Tensor, counts: torch.Tensor, out) -> None:
         """Make the current stream wait for every queued gather, select the predecessors and
