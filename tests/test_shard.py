@@ -91,3 +91,32 @@ def test_gloo_world2_exchange_and_match():
         pd, pn = _slab((f - 1) % total)
         bi, bd, sd = oracle.bf_match(d[:n], pd[:pn])
         assert merged[f] == (bi.tolist(), bd.tolist(), sd.tolist())
+
+
+def test_collective_forced_at_world1():
+    """gather_slabs / PredecessorMatch with the collective forced at world 1 (the path
+    tests/test_gpu_rccl.py drives through RCCL on one GPU): over a one-rank gloo group the
+    gathered slabs and the predecessor selection equal the copy path's."""
+    from orbslam_mapsave_amd.shard import PredecessorMatch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        per, cap = 4, 16
+        g = torch.Generator().manual_seed(3)
+        desc = torch.randint(0, 256, (per, cap, 32), dtype=torch.uint8, generator=g)
+        cnt = torch.randint(1, cap + 1, (per,), dtype=torch.int32, generator=g)
+        seen = {}
+        for collective in (True, False):
+            got = []
+
+            def match(d, n, prev, prev_n, out, got=got):
+                got.append((prev.clone(), prev_n.clone()))
+
+            pm = PredecessorMatch(0, 1, per, cap, "cpu", match, parts=2, collective=collective)
+            pm.step(desc, cnt, None)
+            seen[collective] = got[0]
+        assert torch.equal(seen[True][0], seen[False][0]) and torch.equal(seen[True][1], seen[False][1])
+        # frame f's predecessor is f - 1 (frame 0's the last)
+        assert torch.equal(seen[True][0], desc[[per - 1, 0, 1, 2]])
+    finally:
+        dist.destroy_process_group()
