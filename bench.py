@@ -788,9 +788,13 @@ def torch_from_numpy(a):
 def run_dry(args) -> None:
     """`--dry-run`: the multi-rank plumbing on CPU (gloo) — rendezvous, world-size check, the
     config-4 exchange (shard.PredecessorMatch in `parts` sub-batches), barrier-bracketed timing
-    and the max over ranks — on small random descriptor slabs.  Not a GPU measurement."""
+    and the max over ranks — at configs[3]'s shape: a global batch of 256 frames dealt
+    round-robin (32 per rank at 8 ranks; --per-rank overrides), slabs of capacity(1920, 1080)
+    rows (orbfe_keypoint_capacity_params, host arithmetic), random descriptors with up to 96
+    keypoints per frame so the CPU stand-in matcher stays cheap.  Not a GPU measurement."""
     import torch
     import torch.distributed as dist
+    from orbslam_mapsave_amd.native import keypoint_capacity
     from orbslam_mapsave_amd.shard import PredecessorMatch, global_frame
 
     rank = int(os.environ.get("RANK", "0"))
@@ -800,13 +804,15 @@ def run_dry(args) -> None:
     if rank == 0 and world != args.gpus:
         print(f"bench.py: {world} ranks running but --gpus {args.gpus}", file=sys.stderr)
         sys.exit(3)
-    B, cap = max(2, 8 // world), 64  # a global batch of 8 frames (so results compare)
+    B = args.per_rank if args.per_rank > 0 else max(2, 256 // world)
+    cap = keypoint_capacity(ORB_YAML_NFEATURES, *ORB, 1920, 1080)
     desc = torch.zeros((B, cap, 32), dtype=torch.uint8)
     cnt = torch.zeros(B, dtype=torch.int32)
     for j in range(B):
         rng = np.random.default_rng(global_frame(rank, world, j))
-        desc[j] = torch.from_numpy(rng.integers(0, 256, (cap, 32), dtype=np.uint8))
-        cnt[j] = int(rng.integers(cap // 2, cap + 1))
+        n = int(rng.integers(48, 97))
+        desc[j, :n] = torch.from_numpy(rng.integers(0, 256, (n, 32), dtype=np.uint8))
+        cnt[j] = n
     out = torch.zeros((B, cap, 3), dtype=torch.int32)
     parts = 2
     pm = PredecessorMatch(rank, world, B, cap, "cpu", _cpu_bf, parts=parts)
@@ -843,7 +849,8 @@ def run_dry(args) -> None:
             "value": round(world * B * K / dt, 2), "unit": "frames/s", "n_gpus": world,
             "steps": K, "warmup": args.warmup, "ms_per_step": round(dt / K * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": f"synthetic random descriptor slabs ({B} frames x 64 x 32 B per rank)",
+            "data": f"synthetic random descriptor slabs ({B} frames x {cap} x 32 B per rank, "
+                    "48-96 keypoints each)",
             "dry_run": True,
             "config": {"workload": "config-4 exchange step on CPU: gloo all-gather in 2 "
                                    "sub-batches + frame f vs f-1 brute force",

@@ -129,6 +129,11 @@ int   orbfe_keypoint_capacity(const orbfe_extractor* h);
  * can return per level at that size, summed.  <= orbfe_keypoint_capacity(h); negative status
  * for an unsupported size. */
 int   orbfe_keypoint_capacity_for(const orbfe_extractor* h, int w, int hgt);
+/* orbfe_keypoint_capacity_for without a handle (host arithmetic only, no device): the bound
+ * for extractor parameters `p` at w x hgt, so a caller can size its output slabs (e.g. config
+ * 4's all-gathered descriptor slabs) before any extractor exists.  Negative status for bad
+ * parameters or an unsupported size. */
+int   orbfe_keypoint_capacity_params(const orbfe_params* p, int w, int hgt);
 
 /* Replaces ORBextractor::operator()(image, mask, keypoints, descriptors)
  * (ORBextractor.h:64-66, ORBextractor.cc:1042-1108), called from Frame::ExtractORB
@@ -236,11 +241,11 @@ int orbfe_profile_read(orbfe_extractor* h, double* total_ms, int32_t* launches);
 
 /* Which pyramid path an extraction of `nframes` frames at the extractor's current frame size
  * takes (the last extracted size; a test hook, no reference counterpart): ORBFE_PYR_PER_LEVEL
- * (resize_kernel per level), ORBFE_PYR_BANDS (pyramid_kernel), ORBFE_PYR_ROLL
- * (pyramid_roll_kernel); ORBFE_ERR_ARG before any extraction. */
+ * (resize2_kernel pairs / resize_kernel + resize_tail_kernel), ORBFE_PYR_BANDS
+ * (pyramid_kernel); ORBFE_ERR_ARG before any extraction.  (Value 2, the rolling-band kernel of
+ * rounds 4-5, was removed with that kernel and is never returned.) */
 #define ORBFE_PYR_PER_LEVEL 0
 #define ORBFE_PYR_BANDS     1
-#define ORBFE_PYR_ROLL      2
 int orbfe_pyramid_path(const orbfe_extractor* h, int nframes);
 
 /* Pyramid access — replaces the public member mvImagePyramid (ORBextractor.h:90) read by

@@ -129,7 +129,7 @@ struct orbfe_extractor {
     Plan plan;
     bool planned = false;
     int frames_cap = 0;
-    DevBuf cells, chunks, xtab, ytab, bslot, ptab;
+    DevBuf cells, xtab, ytab, bslot, ptab;
     DevBuf pyr, blur, cell_cnt, cell_keys, keys, act, oct_out, oct_cnt, oct_ord, level_keys;
     DevBuf out_kps, out_desc, out_n;  // staging for the host-pointer entry points
     DevBuf stage, rects;              // host colour frames / rectangle masks (level-0 inputs)
@@ -192,11 +192,6 @@ struct orbfe_extractor {
     // ORBFE_PREBLUR with ORBFE_PRE_MASK=<hex>: the describe reads blurred windows only for the
     // levels in the mask and blurs the others per keypoint (experiments)
     uint32_t pre_mask_env = std::getenv("ORBFE_PRE_MASK") ? (uint32_t)std::strtoul(std::getenv("ORBFE_PRE_MASK"), nullptr, 16) : 0xffffffffu;
-    // ORBFE_RESIZE_BLUR=1: levels made by per-level resize launches are blurred by them
-    // (resize_blur_kernel) and describe reads their blurred windows.  Bit-exact, but measured
-    // slower overall (resize +0.125 ms, describe -0.076 ms per 256 frames;
-    // profiles/r03/experiments/resize_blur.json), so off by default.
-    bool resize_blur = std::getenv("ORBFE_RESIZE_BLUR") && std::strcmp(std::getenv("ORBFE_RESIZE_BLUR"), "1") == 0;
     // the pyramid in one launch (pyramid_kernel); ORBFE_PYR=0: per-level resize launches + the
     // one-workgroup tail
     bool use_pyr = !(std::getenv("ORBFE_PYR") && std::strcmp(std::getenv("ORBFE_PYR"), "0") == 0);
@@ -208,13 +203,6 @@ struct orbfe_extractor {
     // run(): the pyramid kernel reads level 0 from l0_stage and writes it to the slab level 0
     LevelPtr l0_stage{};
     bool l0_from_stage = false;
-    // The rolling-band kernel, opt-in: one launch where the band plan is not the faster path
-    // (1920 x 1080), measured slower there than the per-level kernels;
-    // ORBFE_ROLL=1: batches, ORBFE_ROLL=2: also small batches; ORBFE_PYR=3: wherever it plans
-    // (measured slower than the band kernel at 640 x 480 too)
-    bool force_roll = std::getenv("ORBFE_PYR") && std::strcmp(std::getenv("ORBFE_PYR"), "3") == 0;
-    bool use_roll = force_roll || (std::getenv("ORBFE_ROLL") && std::atoi(std::getenv("ORBFE_ROLL")) >= 1);
-    bool roll_small = force_roll || (std::getenv("ORBFE_ROLL") && std::atoi(std::getenv("ORBFE_ROLL")) >= 2);
     // ORBFE_PYR_SMALL_BELOW (A/B): batches below it take the small-batch band plans (thin bands)
     int pyr_small_below = std::getenv("ORBFE_PYR_SMALL_BELOW") ? std::atoi(std::getenv("ORBFE_PYR_SMALL_BELOW")) : kTailMinFrames;
     // Batches of >= pyr_small_below frames take the per-level kernels (resize2 pairs + the
@@ -227,23 +215,11 @@ struct orbfe_extractor {
     bool band_path(int n) const {  // run() makes the pyramid with pyramid_kernel for n frames
         const int which = n >= pyr_small_below ? 0 : 1;
         if (which == 0 && !pyr_batch_band && !force_pyr) return false;
-        return plan.pyr_ok && (plan.pyr_use[which] || force_pyr) && use_pyr && !force_roll &&
-               !(fused_blur && resize_blur) && plan.geo.nlevels >= 2;
+        return plan.pyr_ok && (plan.pyr_use[which] || force_pyr) && use_pyr && plan.geo.nlevels >= 2;
     }
-    // ... or with pyramid_roll_kernel: where the band plan is not the faster path (1920 x 1080)
-    bool roll_path(int n) const {
-        const int which = n >= pyr_small_below ? 0 : 1;
-        return plan.roll_ok[which] && use_pyr && use_roll && !force_pyr && (which == 0 || roll_small) &&
-               !(fused_blur && resize_blur) && plan.geo.nlevels >= 2 &&
-               (force_roll || !band_path(n));
-    }
-    bool pyr_path(int n) const { return band_path(n) || roll_path(n); }  // one launch
+    bool pyr_path(int n) const { return band_path(n); }  // one launch
     // ORBFE_RS2=0: one resize launch per level where resize2_kernel would take two (A/B)
     bool use_rs2 = !(std::getenv("ORBFE_RS2") && std::strcmp(std::getenv("ORBFE_RS2"), "0") == 0);
-    // ORBFE_RSN=1: chains of 3-4 levels per launch (resizeN_kernel) instead of resize2_kernel's
-    // pairs; bit-exact but measured slower at 1920 x 1080 (c4 resize 0.870 ms per 256 frames with
-    // pairs, 1.015 with chains of <= 3, 1.135 with <= 4; profiles/r04/experiments/resize_chain/)
-    bool use_rsn = std::getenv("ORBFE_RSN") && std::strcmp(std::getenv("ORBFE_RSN"), "1") == 0;
     // ORBFE_RESIZE_TABLE=0: resize_kernel's horizontal pass by byte gathers (A/B)
     bool table_off = std::getenv("ORBFE_RESIZE_TABLE") && std::strcmp(std::getenv("ORBFE_RESIZE_TABLE"), "0") == 0;
     // ORBFE_DESC_MFMA=0: describe blurs its raw windows on the VALU instead of the matrix cores
@@ -257,16 +233,7 @@ struct orbfe_extractor {
     int num_cus = 256;  // compute units of the device (launch-shape choices)
     // ORBFE_OCT_SMALL=0: small batches keep the 256-thread oct-tree (A/B)
     bool oct_small = !(std::getenv("ORBFE_OCT_SMALL") && std::strcmp(std::getenv("ORBFE_OCT_SMALL"), "0") == 0);
-    // ORBFE_FAST_STRIP=1: FAST as a workgroup per run of a cell row's cells (fast_strip_kernel,
-    // SURVEY §7 step 4's layout) instead of one wave per cell (fast_kernel).  Bit-exact, but
-    // measured slower: c3 FAST 0.463 -> 0.834 ms per 512 frames, c4 1.86 -> 3.00 ms per 256
-    // (more VALU per frame, 667 K vs 547 K, and each workgroup's ROI load and
-    // barriers exposed at 24 waves per CU)
-    bool fast_strip = std::getenv("ORBFE_FAST_STRIP") && std::strcmp(std::getenv("ORBFE_FAST_STRIP"), "1") == 0;
     int desc_g16 = std::getenv("ORBFE_DESC_G16") ? std::atoi(std::getenv("ORBFE_DESC_G16")) : 0;
-    // ORBFE_DESC_G2=1 (experiment): batches at kDescGroupSmall keypoints per wave, strided — four
-    // times the waves per frame, so a quarter of the frames in flight per XCD
-    bool desc_g2 = std::getenv("ORBFE_DESC_G2") && std::atoi(std::getenv("ORBFE_DESC_G2")) == 1;
     bool graph_broken = std::getenv("ORBFE_NO_GRAPH") != nullptr;  // capture failed once (or
                                  // disabled for A/B runs): keep to the launch path
 
@@ -373,7 +340,6 @@ struct orbfe_extractor {
         int st = plan_geometry(tab, w, h, g);
         if (st != ORBFE_OK) return st;
         if ((st = cells.ensure(std::max<size_t>(1, g.cells.size()) * sizeof(CellDesc)))) return st;
-        if ((st = chunks.ensure(std::max<size_t>(1, g.chunks.size()) * sizeof(FastChunk)))) return st;
         if ((st = xtab.ensure(std::max<size_t>(1, g.xtab.size()) * sizeof(int)))) return st;
         if ((st = ytab.ensure(std::max<size_t>(1, g.ytab.size()) * sizeof(int)))) return st;
         if ((st = bslot.ensure(kBlurFragBytes + g.bitems.size() * sizeof(uint32_t)))) return st;
@@ -381,13 +347,6 @@ struct orbfe_extractor {
         if (!g.ptab.empty())
             ORBFE_HIP(hipMemcpyAsync(ptab.p, g.ptab.data(), g.ptab.size() * sizeof(uint32_t),
                                      hipMemcpyHostToDevice, stream));
-        if (g.roll_ok[0] || g.roll_ok[1]) {
-            const int mx = (int)std::max(g.roll_ok[0] ? g.roll_lds[0] : 0, g.roll_ok[1] ? g.roll_lds[1] : 0);
-            hipFuncSetAttribute(reinterpret_cast<const void*>(&pyramid_roll_kernel<false>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-            hipFuncSetAttribute(reinterpret_cast<const void*>(&pyramid_roll_kernel<true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        }
         if (g.pyr_ok) {  // dynamic LDS above 64 KB must be allowed per kernel
             const int mx = (int)std::max(g.pyr_lds[0], g.pyr_lds[1]);
             hipFuncSetAttribute(reinterpret_cast<const void*>(&pyramid_kernel<false>),
@@ -397,9 +356,6 @@ struct orbfe_extractor {
         }
         ORBFE_HIP(hipMemcpyAsync(cells.p, g.cells.data(), g.cells.size() * sizeof(CellDesc),
                                  hipMemcpyHostToDevice, stream));
-        if (!g.chunks.empty())
-            ORBFE_HIP(hipMemcpyAsync(chunks.p, g.chunks.data(), g.chunks.size() * sizeof(FastChunk),
-                                     hipMemcpyHostToDevice, stream));
         ORBFE_HIP(hipMemcpyAsync(xtab.p, g.xtab.data(), g.xtab.size() * sizeof(int),
                                  hipMemcpyHostToDevice, stream));
         ORBFE_HIP(hipMemcpyAsync(ytab.p, g.ytab.data(), g.ytab.size() * sizeof(int),
@@ -457,13 +413,9 @@ struct orbfe_extractor {
         // top levels (tail_start ..) in one K1b launch, a workgroup per frame
         // (a batch of a few frames would leave most CUs idle in the tail: per-level launches)
         const int ts = n >= kTailMinFrames ? std::min(g.tail_start, L) : L;
-        // levels 1 .. ts-1 blurred with their resize (K1 + K4 fused) unless K4 runs as its own
-        // pass (PREBLUR) or ORBFE_RESIZE_BLUR=0
-        const bool rb = fused_blur && resize_blur;
-        uint32_t pre_mask = 0;
         // K1 as one launch (pyramid_kernel): every level of a band of every frame in LDS
         const int which = n >= pyr_small_below ? 0 : 1;
-        const bool one_pyr = pyr_path(n), roll = roll_path(n);
+        const bool one_pyr = pyr_path(n);
         if (l0_from_stage && !one_pyr) return ORBFE_ERR_ARG;  // callers check pyr_path first
         if (one_pyr) {
             PyrArgs pa;
@@ -482,28 +434,7 @@ struct orbfe_extractor {
             pa.ybuf = g.pyr_ybuf[which];
             pa.ymax = g.pyr_ymax[which];
             pa.bands = reinterpret_cast<const int4*>(ptab.as<uint4>() + g.band_off[which]);
-            if (roll) {
-                pa.bands = reinterpret_cast<const int4*>(ptab.as<uint4>() + g.roll_band_off[which]);
-                pa.sched = reinterpret_cast<const int*>(ptab.as<uint32_t>() + g.roll_sched_off[which]);
-                pa.nsteps = g.roll_steps[which];
-                pa.ydoff = reinterpret_cast<const int*>(ptab.as<uint32_t>() + g.roll_ydoff_off[which]);
-                pa.ydtab = reinterpret_cast<const int4*>(ptab.as<uint4>() + g.roll_ydtab_off[which]);
-                pa.ydesc = g.roll_ydesc[which];
-                for (int l = 0; l < L; ++l) {
-                    pa.ring_rows[l] = g.roll_ring_rows[which][l];
-                    pa.ring_off[l] = g.roll_ring_off[which][l];
-                    pa.lp[l] = g.roll_pitch[which][l];
-                }
-                pa.cols = reinterpret_cast<const int4*>(ptab.as<uint4>() + g.roll_col_off[which]);
-                pa.ncols = g.roll_cols[which];
-                const dim3 rgrid(g.roll_bands[which] * g.roll_cols[which], n);
-                if (x86())
-                    ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, pyramid_roll_kernel<true>, rgrid,
-                                 dim3(kPyrBlockSize), g.roll_lds[which], stream, pa);
-                else
-                    ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, pyramid_roll_kernel<false>, rgrid,
-                                 dim3(kPyrBlockSize), g.roll_lds[which], stream, pa);
-            } else if (x86())
+            if (x86())
                 ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, pyramid_kernel<true>, dim3(g.nbands[which], n),
                              dim3(kPyrBlockSize), g.pyr_lds[which], stream, pa);
             else
@@ -511,39 +442,9 @@ struct orbfe_extractor {
                              dim3(kPyrBlockSize), g.pyr_lds[which], stream, pa);
         }
         for (int l = 1; l < (one_pyr ? 1 : ts); ++l) {
-            // levels l .. l + n - 1 in one launch (resizeN_kernel, n = 3 or 4) where planned
-            // and ORBFE_RSN=1 (opt-in: slower than the pairs below)
-            if (use_rsn && use_rs2 && g.rsn_n[l] >= 3 && l + g.rsn_n[l] - 1 < ts && !rb && !table_off) {
-                ResizeNArgs rn;
-                const int nl = g.rsn_n[l];
-                rn.src = lp[l - 1];
-                rn.sw = g.geo.lv[l - 1].w;
-                rn.n = nl;
-                for (int k = 0; k < nl; ++k) {
-                    rn.lv[k] = lp[l + k];
-                    rn.w[k] = g.geo.lv[l + k].w;
-                    rn.yt[k] = ytab.as<int>() + g.yoff[l + k];
-                    rn.xt[k] = xtab.as<int>() + g.xoff[l + k];
-                    rn.gtab[k] = ptab.as<uint4>() + g.gtab_off[l + k];
-                    rn.xb[k] = x86() ? sse2_body_resize(rn.w[k]) : 0;
-                    rn.pitch[k] = g.rsn_pitch[l][k];
-                    rn.lofs[k] = g.rsn_lofs[l][k];
-                }
-                rn.dh = g.geo.lv[l + nl - 1].h;
-                rn.tiles_x = g.rsn_tiles_x[l];
-                rn.tiles = reinterpret_cast<const int4*>(ptab.as<uint4>() + g.rsn_off[l]);
-                if (x86())
-                    ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resizeN_kernel<true>, dim3(g.rsn_tiles[l], n),
-                                 dim3(256), g.rsn_lds[l], stream, rn);
-                else
-                    ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resizeN_kernel<false>, dim3(g.rsn_tiles[l], n),
-                                 dim3(256), g.rsn_lds[l], stream, rn);
-                l += nl - 1;
-                continue;
-            }
             // levels l and l + 1 in one launch (resize2_kernel) where planned; ORBFE_RS2=0: one
             // launch per level
-            if (use_rs2 && l + 1 < ts && g.rs2_ok[l] && !rb && !table_off) {
+            if (use_rs2 && l + 1 < ts && g.rs2_ok[l] && !table_off) {
                 Resize2Args r2;
                 r2.src = lp[l - 1];
                 r2.mid = lp[l];
@@ -587,20 +488,7 @@ struct orbfe_extractor {
             ra.yt = ytab.as<int>() + g.yoff[l];
             ra.simd_xb = x86() ? sse2_body_resize(ra.dw) : 0;
             ra.gtab = g.pyr_ok && !table_off ? ptab.as<uint4>() + g.gtab_off[l] : nullptr;
-            if (rb && g.rb_lds[l]) {  // the level and its blur (describe reads this level's blurred windows)
-                ra.lds_pitch = g.rb_pitch[l];
-                ra.lds_e = g.rb_lds_e[l];
-                ra.bdst = bp[l];
-                ra.blur_xb = x86() ? sse2_body_blur(ra.dw) : 0;
-                for (int i = 0; i < 4; ++i) ra.taps[i] = tab.taps[i];
-                pre_mask |= 1u << l;
-                if (x86())
-                    ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resize_blur_kernel<true>, dim3(g.rs_tiles[l], n),
-                                 dim3(256), g.rb_lds[l], stream, ra);
-                else
-                    ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resize_blur_kernel<false>, dim3(g.rs_tiles[l], n),
-                                 dim3(256), g.rb_lds[l], stream, ra);
-            } else if (x86()) {
+            if (x86()) {
                 ORBFE_LAUNCH(prof, ORBFE_STAGE_RESIZE, resize_kernel<true>, dim3(g.rs_tiles[l], n),
                              dim3(256), g.rs_lds[l], stream, ra);
             } else {
@@ -648,12 +536,7 @@ struct orbfe_extractor {
             fa.cell_keys = cell_keys.as<uint32_t>();
             fa.level_keys = level_keys.as<int>();
             for (int l = 0; l < L; ++l) fa.pyr[l] = lp[l];
-            fa.chunks = chunks.as<FastChunk>();
-            if (fast_strip && !g.chunks.empty()) {
-                fa.roi_rows = g.chunk_rows;
-                ORBFE_LAUNCH(prof, ORBFE_STAGE_FAST, fast_strip_kernel, dim3((int)g.chunks.size(), n),
-                             dim3(kChunkBlock), g.chunk_lds, stream, fa);
-            } else if (g.roi_pitch == kFastPitch)
+            if (g.roi_pitch == kFastPitch)
                 ORBFE_LAUNCH(prof, ORBFE_STAGE_FAST, fast_kernel<kFastPitch>, dim3(ncells, n), dim3(kFastBlockSize), g.fast_lds, stream, fa);
             else
                 ORBFE_LAUNCH(prof, ORBFE_STAGE_FAST, fast_kernel<0>, dim3(ncells, n), dim3(kFastBlockSize), g.fast_lds, stream, fa);
@@ -732,7 +615,7 @@ struct orbfe_extractor {
         da.desc = d_desc;
         da.n_out = d_n;
         const bool all_pre = !fused_blur && pre_mask_env == 0xffffffffu;
-        da.pre_mask = fused_blur ? pre_mask : pre_mask_env;
+        da.pre_mask = fused_blur ? 0u : pre_mask_env;
         // a wave takes kDescGroupSize keypoints (the trig and pattern loads amortised over the
         // group); small batches take kDescGroupSmall, for four times the waves in flight
         // (x86 arithmetic: the rotation FMA-contracted, kFma)
@@ -744,13 +627,12 @@ struct orbfe_extractor {
         // 512-frame launch instead of 0.70 (1.65x its algorithmic bytes: the frames in flight
         // per XCD double); at 1080p it is 9 % slower (profiles/r04/experiments/describe_g16/)
         const bool g16 = desc_g16 == 1 && n >= kDescSmallBatch && desc_stride && x86() && win == kWinMfma;
-        const bool g2 = desc_g2 && n >= kDescSmallBatch && desc_stride;
-        const int group = g16 ? 16 : n >= kDescSmallBatch && !g2 ? kDescGroupSize : kDescGroupSmall;
+        const int group = g16 ? 16 : n >= kDescSmallBatch ? kDescGroupSize : kDescGroupSmall;
         const int per_block = (kDescBlockSize / 64) * group;  // slots per workgroup
         const dim3 dgrid((g.geo.out_total + per_block - 1) / per_block, n);
         // batches: strided slots (a frame's waves sweep its oct-tree output in runs of W
         // consecutive slots, sharing window lines in L2); ORBFE_DESC_STRIDE=0: grouped slots
-        da.wave_stride = (group == kDescGroupSize || g16 || g2) && desc_stride ? (int)dgrid.x * (kDescBlockSize / 64) : 0;
+        da.wave_stride = (group == kDescGroupSize || g16) && desc_stride ? (int)dgrid.x * (kDescBlockSize / 64) : 0;
         da.frags = bslot.as<uint4>() + kDescFragOff;
         const int variant = g16 ? 12 : (group == kDescGroupSize ? 6 : 0) + (x86() ? 3 : 0) + win;
         switch (variant) {
@@ -881,7 +763,7 @@ struct orbfe_extractor {
     }
 
     ~orbfe_extractor() {
-        for (DevBuf* b : {&cells, &chunks, &xtab, &ytab, &bslot, &ptab, &pyr, &blur, &cell_cnt, &cell_keys, &keys, &act,
+        for (DevBuf* b : {&cells, &xtab, &ytab, &bslot, &ptab, &pyr, &blur, &cell_cnt, &cell_keys, &keys, &act,
                           &oct_out, &oct_cnt, &oct_ord, &level_keys, &out_kps, &out_desc, &out_n, &stage, &rects, &st_off, &st_items,
                           &st_sad, &st_status, &st_kl, &st_dl, &st_kr, &st_dr, &st_n, &st_ur, &st_dp})
             b->release();
@@ -1012,6 +894,20 @@ int orbfe_keypoint_capacity_for(const orbfe_extractor* h, int w, int hgt) {
     try {
         Plan g;
         const int st = plan_geometry(h->tab, w, hgt, g);
+        return st != ORBFE_OK ? st : g.geo.out_total;
+    } catch (const std::bad_alloc&) {
+        return ORBFE_ERR_NOMEM;
+    }
+}
+
+int orbfe_keypoint_capacity_params(const orbfe_params* p, int w, int hgt) {
+    if (!p || w <= 0 || hgt <= 0) return ORBFE_ERR_ARG;
+    try {
+        HostTables t{};
+        int st = make_tables(*p, t);
+        if (st != ORBFE_OK) return st;
+        Plan g;
+        st = plan_geometry(t, w, hgt, g);
         return st != ORBFE_OK ? st : g.geo.out_total;
     } catch (const std::bad_alloc&) {
         return ORBFE_ERR_NOMEM;
@@ -1415,7 +1311,7 @@ int orbfe_profile_read(orbfe_extractor* h, double* total_ms, int32_t* launches) 
 
 int orbfe_pyramid_path(const orbfe_extractor* h, int nframes) {
     if (!h || !h->planned || nframes < 1) return ORBFE_ERR_ARG;
-    return h->band_path(nframes) ? ORBFE_PYR_BANDS : h->roll_path(nframes) ? ORBFE_PYR_ROLL : ORBFE_PYR_PER_LEVEL;
+    return h->band_path(nframes) ? ORBFE_PYR_BANDS : ORBFE_PYR_PER_LEVEL;
 }
 
 int orbfe_set_stream(orbfe_extractor* h, void* s) {
@@ -1460,7 +1356,7 @@ int orbfe_get_blurred_level(orbfe_extractor* h, int frame, int level, uint8_t* o
     LevelPtr bp{h->blur.as<uint8_t>() + lv.off, g.slab, lv.pitch};
     // K4 on demand (the default extraction path blurs level 0 and the tail levels inside K5);
     // ORBFE_PROBE_AS_EXTRACTED=1 copies the slab as the extraction left it (the levels
-    // resize_blur_kernel made)
+    // ORBFE_PREBLUR's pass made)
     if (out && !std::getenv("ORBFE_PROBE_AS_EXTRACTED")) {
         DeviceGuard dg(h->device);
         BlurArgs ba;

@@ -510,153 +510,6 @@ __global__ __launch_bounds__(256) void resize2_kernel(Resize2Args a) {
     }
 }
 
-// K1, three or four levels per launch (1920 x 1080): resize2_kernel's scheme carried through
-// more levels.  A workgroup owns a 128 x 32 tile of the chain's last level.  It stages the
-// level l - 1 rows and columns its first made level's region reads, makes each intermediate
-// level's region in LDS from the image before it (writing the part of that level it owns: the
-// host partitions every intermediate level among the tiles by the row / column of it that each
-// tile's first row / column reaches first), then the tile.  Two LDS regions alternate (the
-// staged level and odd made levels in one, even ones in the other), so of a chain's levels only
-// level l - 1 is read from HBM: at 1080p the chains (1-4) (5-7) read levels 0 and 4 instead of
-// resize2's 0, 2, 4 and 6.  Bit-exact, but slower than the pairs (a workgroup's phases run
-// one after another behind its barriers, and the larger LDS leaves fewer workgroups per CU to
-// overlap them): opt-in, ORBFE_RSN=1.
-template <bool kX86>
-__global__ __launch_bounds__(256) void resizeN_kernel(ResizeNArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char rn_lds[];
-    int bx, f;
-    xcd_block(bx, f);
-    const int nm = a.n - 1;  // levels made region by region before the tile
-    const int4* tt = a.tiles + (size_t)bx * 2 * nm;
-    const int tid = threadIdx.x;
-    int sy, sx;  // level coordinates of the current source image's first row / column
-    {
-        const int4 c = tt[0];
-        sy = a.yt[0][3 * c.x];
-        sx = a.xt[0][3 * c.z] & ~3;
-        const int ay1 = a.yt[0][3 * c.y + 1], ax1 = a.xt[0][3 * c.w + 1];
-        const int nrow = ay1 - sy + 1, cpr = ((ax1 - sx) >> 4) + 1, total = nrow * cpr;
-        const uint8_t* src = a.src.base + f * a.src.fpitch;
-        unsigned char* img = rn_lds + a.lofs[0];
-        for (int base = 0; base < total; base += 4 * 256) {
-            uint4 v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int i = base + 256 * u + tid;
-                if (i >= total) continue;
-                const int r = i / cpr, cc = i - r * cpr;
-                const uint8_t* row = src + (long long)(sy + r) * a.src.pitch;
-                const int x = sx + 16 * cc;
-                if (x + 16 <= a.sw) {
-                    v[u] = load16_a4(row + x);
-                } else {
-                    uint32_t w[4];
-#pragma unroll
-                    for (int d = 0; d < 4; ++d) {
-                        const int xd = x + 4 * d;
-                        w[d] = 0;
-                        if (xd + 4 <= a.sw) w[d] = *reinterpret_cast<const uint32_t*>(row + xd);
-                        else
-                            for (int q = 0; q < 4 && xd + q < a.sw; ++q) w[d] |= (uint32_t)row[xd + q] << (8 * q);
-                    }
-                    v[u] = make_uint4(w[0], w[1], w[2], w[3]);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int i = base + 256 * u + tid;
-                if (i >= total) continue;
-                const int r = i / cpr, cc = i - r * cpr;
-                *reinterpret_cast<uint4*>(img + r * a.pitch[0] + 16 * cc) = v[u];
-            }
-        }
-    }
-    __syncthreads();
-    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-    auto hsum = [&](const unsigned char* base, int pitch, int r, int wofs, int sh, const uint32_t (&sel)[4],
-                    const us2 (&cf)[4], uint32_t (&t)[4]) {
-        const uint32_t* row = reinterpret_cast<const uint32_t*>(base + r * pitch + wofs);
-        const uint32_t w0 = row[0], w1 = row[1], w2 = row[2];
-        const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh), hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            t[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(hi, lo, sel[k])), cf[k], 0u, false);
-    };
-    for (int k = 0; k < nm; ++k) {  // level k's region: rows c.x .. c.y, column groups c.z / 4 .. c.w / 4
-        const int4 c = tt[2 * k], own = tt[2 * k + 1];
-        const unsigned char* S = rn_lds + a.lofs[k];
-        unsigned char* D = rn_lds + a.lofs[k + 1];
-        const int sp = a.pitch[k], dp = a.pitch[k + 1];
-        const int gpr = ((c.w - c.z) >> 2) + 1, rps = 256 / gpr;
-        const int gx = tid % gpr, ry = tid / gpr;
-        if (ry < rps) {
-            const int x = c.z + 4 * gx;
-            const uint4* gp = a.gtab[k] + 3 * (x >> 2);
-            const uint4 g0 = gp[0], g1 = gp[1], g2 = gp[2];
-            const int xrel = (int)g0.x - sx, wofs = (xrel >> 2) << 2, sh = xrel & 3;
-            const uint32_t sel[4] = {g0.y, g0.z, g0.w, g1.x};
-            const us2 cf[4] = {__builtin_bit_cast(us2, hcoef<kX86>(g1.y)), __builtin_bit_cast(us2, hcoef<kX86>(g1.z)),
-                               __builtin_bit_cast(us2, hcoef<kX86>(g1.w)), __builtin_bit_cast(us2, hcoef<kX86>(g2.x))};
-            const int n = min(4, a.w[k] - x);
-            const bool own_x = x >= own.z && x < own.w;  // own column bounds are multiples of 4
-            uint8_t* mid = const_cast<uint8_t*>(a.lv[k].base) + f * a.lv[k].fpitch;
-            const int* ytk = a.yt[k];
-            for (int r = c.x + ry; r <= c.y; r += rps) {
-                const int* yy = ytk + 3 * r;
-                const uint32_t b0 = (uint32_t)yy[2] & 0xffffu, b1 = (uint32_t)yy[2] >> 16;
-                uint32_t t0[4], t1[4];
-                hsum(S, sp, yy[0] - sy, wofs, sh, sel, cf, t0);
-                hsum(S, sp, yy[1] - sy, wofs, sh, sel, cf, t1);
-                const uint32_t packed = resize4<kX86>(t0, t1, b0, b1, x, a.xb[k]);
-                *reinterpret_cast<uint32_t*>(D + (r - c.x) * dp + (x - c.z)) = packed;
-                if (own_x && r >= own.x && r < own.y) {
-                    uint8_t* o = mid + (long long)r * a.lv[k].pitch + x;
-                    if (n == 4) {
-                        *reinterpret_cast<uint32_t*>(o) = packed;
-                    } else {
-                        for (int q = 0; q < n; ++q) o[q] = (uint8_t)(packed >> (8 * q));
-                    }
-                }
-            }
-        }
-        __syncthreads();
-        sy = c.x;
-        sx = c.z;
-    }
-    {   // the tile of the last level (resize_kernel's thread layout)
-        const unsigned char* S = rn_lds + a.lofs[nm];
-        const int sp = a.pitch[nm], dw = a.w[nm];
-        const int ox = (bx % a.tiles_x) * kRsTW, oy = (bx / a.tiles_x) * kRsTH;
-        const int tx = tid & 31, ty = tid >> 5;
-        const int x = ox + 4 * tx;
-        if (x >= dw) return;
-        const int n = min(4, dw - x);
-        const uint4* gp = a.gtab[nm] + 3 * (x >> 2);
-        const uint4 g0 = gp[0], g1 = gp[1], g2 = gp[2];
-        const int xrel = (int)g0.x - sx, wofs = (xrel >> 2) << 2, sh = xrel & 3;
-        const uint32_t sel[4] = {g0.y, g0.z, g0.w, g1.x};
-        const us2 cf[4] = {__builtin_bit_cast(us2, hcoef<kX86>(g1.y)), __builtin_bit_cast(us2, hcoef<kX86>(g1.z)),
-                           __builtin_bit_cast(us2, hcoef<kX86>(g1.w)), __builtin_bit_cast(us2, hcoef<kX86>(g2.x))};
-        uint8_t* dst = const_cast<uint8_t*>(a.lv[nm].base) + f * a.lv[nm].fpitch;
-#pragma unroll
-        for (int j = 0; j < kRsRPT; ++j) {
-            const int y = oy + kRsRPT * ty + j;
-            if (y >= a.dh) break;
-            const int* yy = a.yt[nm] + 3 * y;
-            const uint32_t b0 = (uint32_t)yy[2] & 0xffffu, b1 = (uint32_t)yy[2] >> 16;
-            uint32_t t0[4], t1[4];
-            hsum(S, sp, yy[0] - sy, wofs, sh, sel, cf, t0);
-            hsum(S, sp, yy[1] - sy, wofs, sh, sel, cf, t1);
-            const uint32_t packed = resize4<kX86>(t0, t1, b0, b1, x, a.xb[nm]);
-            uint8_t* o = dst + (long long)y * a.lv[nm].pitch + x;
-            if (n == 4) {
-                *reinterpret_cast<uint32_t*>(o) = packed;
-            } else {
-                for (int q = 0; q < n; ++q) o[q] = (uint8_t)(packed >> (8 * q));
-            }
-        }
-    }
-}
 
 // Column-pass rounding.  The sums carry 0x7fff; the scalar FixedPtCastEx (sum + 2^15) >> 16
 // adds one more, the x86 SIMD body (H6: float sum, exact below 2^24, _mm_cvtps_epi32) rounds
@@ -682,234 +535,6 @@ __device__ __forceinline__ int reflect101(int p, int len) {
 __device__ __forceinline__ int reflect101_1(int p, int len) {  // |overshoot| < len - 1
     return p < 0 ? -p : (p >= len ? 2 * len - 2 - p : p);
 }
-// K1 + K4 fused — the level's 128 x 32 tile AND its GaussianBlur (7x7, sigma 2, REFLECT_101,
-// ORBextractor.cc:1088-1089; K4's exact integer passes, App. A.2), so describe reads blurred
-// windows for this level instead of blurring one per keypoint.  The tile's resize outputs are
-// made for the rows / columns the blur reaches (3 beyond every edge, clipped to the level:
-// 1.24x the tile's resize work) into an LDS image E whose column 0 is level column ox - 4 and
-// row 0 level row oy - 3; positions outside the level are then copied from their reflect-101
-// images (which lie inside E: tiles are >= 4 px from the far edge's reflection).  Rows pass:
-// v_dot4 on dword-aligned E reads into u16 row pairs (the source staging region is dead by
-// then and holds them); columns pass: v_dot2 + 2^15 >> 16 saturated (x86: half to even on
-// the SIMD body, H6) straight to the blurred slab.  The level itself is written as by
-// resize_kernel.
-constexpr int kRbEP = 144;                 // E row pitch: level columns ox - 4 .. ox + 139
-constexpr int kRbERows = kRsTH + 8;        // E rows: oy - 3 .. oy + th + 2, + pad rows for pairs
-constexpr int kRbQ = kRsTW / 4 + 2;        // 34 column quads of E computed (ox - 4 .. ox + 131)
-constexpr int kRbPairs = (kRsTH + 6 + 1) / 2;  // 19 u16 row pairs of the rows pass
-constexpr int kRbRowpBytes = kRbPairs * (kRsTW / 4) * 16;
-template <bool kX86>
-__global__ __launch_bounds__(256) void resize_blur_kernel(ResizeArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char rs_lds[];
-    int bx, f;
-    xcd_block(bx, f);
-    const int ox = (bx % a.tiles_x) * kRsTW, oy = (bx / a.tiles_x) * kRsTH;
-    const int ex = min(ox + kRsTW, a.dw) - 1, ey = min(oy + kRsTH, a.dh) - 1;
-    const int th = ey - oy + 1, tw = ex - ox + 1;
-    // the level rows / columns the blur reaches, clipped (their reflections lie inside)
-    const int er0 = max(oy - 3, 0), er1 = min(ey + 3, a.dh - 1);
-    const int ec0 = max(ox - 3, 0), ec1 = min(ex + 3, a.dw - 1);
-    const int sy0 = a.yt[3 * er0], sy1 = a.yt[3 * er1 + 1];
-    const int sx0 = a.xt[3 * ec0] & ~3, sx1 = a.xt[3 * ec1 + 1];
-    const int nrow = sy1 - sy0 + 1, P = a.lds_pitch;  // P % 16 == 0
-    const int cpr = ((sx1 - sx0) >> 4) + 1;
-    uint8_t* E = rs_lds + a.lds_e;                      // 16-byte aligned, kRbEP % 16 == 0
-    int* ys = reinterpret_cast<int*>(E + kRbERows * kRbEP);  // y tables of rows er0 .. er1
-    const uint8_t* src = a.src.base + f * a.src.fpitch;
-    const int nyt = 3 * (er1 - er0 + 1);
-    const int yv = threadIdx.x < nyt ? a.yt[3 * er0 + threadIdx.x] : 0;
-    if (threadIdx.x < nyt) ys[threadIdx.x] = yv;
-    const int total = nrow * cpr;
-    for (int base = 0; base < total; base += 4 * 256) {
-        uint4 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = base + 256 * u + (int)threadIdx.x;
-            if (i >= total) continue;
-            const int r = i / cpr, c = i - r * cpr;
-            const uint8_t* row = src + (long long)(sy0 + r) * a.src.pitch;
-            const int x = sx0 + 16 * c;
-            if (x + 16 <= a.sw) {
-                v[u] = load16_a4(row + x);
-            } else {
-                uint32_t w[4];
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const int xd = x + 4 * d;
-                    w[d] = 0;
-                    if (xd + 4 <= a.sw) w[d] = *reinterpret_cast<const uint32_t*>(row + xd);
-                    else
-                        for (int q = 0; q < 4 && xd + q < a.sw; ++q) w[d] |= (uint32_t)row[xd + q] << (8 * q);
-                }
-                v[u] = make_uint4(w[0], w[1], w[2], w[3]);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = base + 256 * u + (int)threadIdx.x;
-            if (i >= total) continue;
-            const int r = i / cpr, c = i - r * cpr;
-            *reinterpret_cast<uint4*>(rs_lds + r * P + 16 * c) = v[u];
-        }
-    }
-    __syncthreads();
-    // resize outputs: thread -> (E quad k, row phase rp); quads 1 .. 32 are the tile's columns
-    uint8_t* dst = const_cast<uint8_t*>(a.dst.base) + f * a.dst.fpitch;
-    if (threadIdx.x < kRbQ * 7) {
-        const int k = threadIdx.x % kRbQ, rp = threadIdx.x / kRbQ;
-        const int x = ox - 4 + 4 * k;  // level column of the quad's byte 0
-        int x0[4], x1[4], a0[4], a1[4];
-        bool in[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            in[q] = x + q >= ec0 && x + q <= ec1;
-            const int dx = min(max(x + q, 0), a.dw - 1);
-            x0[q] = a.xt[3 * dx] - sx0;
-            x1[q] = a.xt[3 * dx + 1] - sx0;
-            const int aa = a.xt[3 * dx + 2];
-            a0[q] = aa & 0xffff;
-            a1[q] = (int)((unsigned)aa >> 16);
-        }
-        const bool tile_col = k >= 1 && k <= kRsTW / 4 && x < a.dw;
-        const int n = min(4, a.dw - x);
-        if (in[0] || in[1] || in[2] || in[3]) {
-#pragma unroll
-            for (int j = 0; j < (kRsTH + 6 + 6) / 7; ++j) {
-                const int y = er0 + rp + 7 * j;
-                if (y > er1) break;
-                const int* yy = ys + 3 * (y - er0);
-                const int ry0 = yy[0] - sy0, ry1 = yy[1] - sy0, bb = yy[2];
-                const int b0 = bb & 0xffff, b1 = (int)((unsigned)bb >> 16);
-                const uint8_t* s0 = rs_lds + ry0 * P;
-                const uint8_t* s1 = rs_lds + ry1 * P;
-                uint32_t packed = 0;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    if (!in[q]) continue;
-                    const uint32_t t0 = __umul24(s0[x0[q]], a0[q]) + __umul24(s0[x1[q]], a1[q]);
-                    const uint32_t t1 = __umul24(s1[x0[q]], a0[q]) + __umul24(s1[x1[q]], a1[q]);
-                    packed |= resize_px<kX86>(t0, t1, b0, b1, x + q < a.simd_xb) << (8 * q);
-                }
-                *reinterpret_cast<uint32_t*>(E + (y - oy + 3) * kRbEP + 4 * k) = packed;
-                if (tile_col && y >= oy && y <= ey) {
-                    uint8_t* d = dst + (long long)y * a.dst.pitch + x;
-                    if (n >= 4) {
-                        *reinterpret_cast<uint32_t*>(d) = packed;
-                    } else {
-                        for (int q = 0; q < n; ++q) d[q] = (uint8_t)(packed >> (8 * q));
-                    }
-                }
-            }
-        }
-    }
-    __syncthreads();
-    // border tiles: E positions outside the level take their reflect-101 images
-    // (the strips: 3 rows above / below the tile across its width + 6, 3 columns left / right
-    // across its height + 6; corners are written by both with the same in-level image)
-    if (oy < 3 || ey + 3 >= a.dh || ox < 3 || ex + 3 >= a.dw) {
-        const int er = th + 6, ecn = tw + 6;
-        auto fix = [&](int r, int c) {
-            const int y = oy - 3 + r, x = ox - 3 + c;
-            if (y >= 0 && y < a.dh && x >= 0 && x < a.dw) return;
-            const int yr = reflect101_1(y, a.dh), xr = reflect101_1(x, a.dw);
-            E[r * kRbEP + c + 1] = E[(yr - oy + 3) * kRbEP + (xr - ox + 4)];
-        };
-        for (int c = threadIdx.x; c < ecn; c += 256) {
-#pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                fix(r, c);
-                fix(er - 1 - r, c);
-            }
-        }
-        for (int r = threadIdx.x; r < er; r += 256) {
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                fix(r, c);
-                fix(r, ecn - 1 - c);
-            }
-        }
-        __syncthreads();
-    }
-    // rows pass: item (pair pr, quad q) -> E rows 2pr, 2pr + 1, output columns 4q .. 4q + 3
-    uint32_t* rowp = reinterpret_cast<uint32_t*>(rs_lds);
-    const uint32_t KLO = (uint32_t)(a.taps[0] | (a.taps[1] << 8) | (a.taps[2] << 16) | (a.taps[3] << 24));
-    const uint32_t KHI = (uint32_t)(a.taps[2] | (a.taps[1] << 8) | (a.taps[0] << 16));
-    const int npairs = (th + 7) >> 1, nq = (tw + 3) >> 2;
-#pragma unroll
-    for (int u = 0; u < (kRbPairs * (kRsTW / 4) + 255) / 256; ++u) {
-        const int it = threadIdx.x + 256 * u;
-        const int pr = it >> 5, q = it & 31;
-        if (pr >= npairs || q >= nq) continue;
-        uint32_t hh[2][4];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const uint32_t* row = reinterpret_cast<const uint32_t*>(E + (2 * pr + e) * kRbEP + 4 * q);
-            const uint32_t w0 = row[0], w1 = row[1], w2 = row[2];
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-                const uint32_t lo = jj < 3 ? __builtin_amdgcn_alignbyte(w1, w0, jj + 1) : w1;
-                const uint32_t hi = jj < 3 ? __builtin_amdgcn_alignbyte(w2, w1, jj + 1) : w2;
-                hh[e][jj] = __builtin_amdgcn_udot4(hi, KHI, __builtin_amdgcn_udot4(lo, KLO, 0u, false), false);
-            }
-        }
-        *reinterpret_cast<uint4*>(rowp + 4 * it) =
-            make_uint4(__builtin_amdgcn_perm(hh[1][0], hh[0][0], 0x05040100u),
-                       __builtin_amdgcn_perm(hh[1][1], hh[0][1], 0x05040100u),
-                       __builtin_amdgcn_perm(hh[1][2], hh[0][2], 0x05040100u),
-                       __builtin_amdgcn_perm(hh[1][3], hh[0][3], 0x05040100u));
-    }
-    __syncthreads();
-    // columns pass: item (output rows 2jp, 2jp + 1; quad q) from pairs jp .. jp + 3
-    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-    const unsigned short k0 = (unsigned short)a.taps[0], k1 = (unsigned short)a.taps[1],
-                         k2 = (unsigned short)a.taps[2], k3 = (unsigned short)a.taps[3];
-    const us2 T01 = us2{k0, k1}, T23 = us2{k2, k3}, T21 = us2{k2, k1}, T0L = us2{k0, 0},
-              T0H = us2{0, k0}, T12 = us2{k1, k2}, T32 = us2{k3, k2}, T10 = us2{k1, k0};
-    constexpr uint32_t kRnd = kX86 ? 0x7fffu : 0x8000u;
-    uint8_t* bdst = const_cast<uint8_t*>(a.bdst.base) + f * a.bdst.fpitch;
-#pragma unroll
-    for (int u = 0; u < (kRsTH / 2) * (kRsTW / 4) / 256; ++u) {
-        const int it = threadIdx.x + 256 * u;
-        const int jp = it >> 5, q = it & 31;
-        if (2 * jp >= th || q >= nq) continue;
-        const int x = ox + 4 * q;
-        const bool even = x < a.blur_xb;
-        uint4 P4[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) P4[i] = *reinterpret_cast<const uint4*>(rowp + 4 * (it + i * (kRsTW / 4)));
-        uint32_t ev[4], od[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const uint32_t p0 = (&P4[0].x)[c], p1 = (&P4[1].x)[c], p2 = (&P4[2].x)[c], p3 = (&P4[3].x)[c];
-            uint32_t v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T01, kRnd, false);
-            v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), T23, v, false);
-            v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), T21, v, false);
-            v = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), T0L, v, false);
-            if constexpr (kX86) v += blur_round_bit(v, even);
-            ev[c] = min(v, 0xffffffu);  // byte 2 = min(acc >> 16, 255)
-            uint32_t u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), T0H, kRnd, false);
-            u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), T12, u, false);
-            u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p2), T32, u, false);
-            u = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p3), T10, u, false);
-            if constexpr (kX86) u += blur_round_bit(u, even);
-            od[c] = min(u, 0xffffffu);
-        }
-        const uint32_t pe = __builtin_amdgcn_perm(ev[1], ev[0], 0x0c0c0602u) | __builtin_amdgcn_perm(ev[3], ev[2], 0x06020c0cu);
-        const uint32_t po = __builtin_amdgcn_perm(od[1], od[0], 0x0c0c0602u) | __builtin_amdgcn_perm(od[3], od[2], 0x06020c0cu);
-        const int y = oy + 2 * jp, n = min(4, a.dw - x);
-        uint8_t* d = bdst + (long long)y * a.bdst.pitch + x;
-        if (n == 4) {
-            *reinterpret_cast<uint32_t*>(d) = pe;
-            if (y + 1 <= ey) *reinterpret_cast<uint32_t*>(d + a.bdst.pitch) = po;
-        } else {
-            for (int i = 0; i < n; ++i) d[i] = (uint8_t)(pe >> (8 * i));
-            if (y + 1 <= ey)
-                for (int i = 0; i < n; ++i) d[a.bdst.pitch + i] = (uint8_t)(po >> (8 * i));
-        }
-    }
-}
-template __global__ void resize_blur_kernel<false>(ResizeArgs);
-template __global__ void resize_blur_kernel<true>(ResizeArgs);
 
 // K1 as one launch — the whole pyramid of a horizontal band of every frame per workgroup.
 // The host partitions every level's rows into nbands bands (proportionally) and derives, top
@@ -1050,167 +675,6 @@ __global__ __launch_bounds__(kPyrBlock) void pyramid_kernel(PyrArgs a) {
 template __global__ void pyramid_kernel<false>(PyrArgs);
 template __global__ void pyramid_kernel<true>(PyrArgs);
 
-// K1 as one launch for any frame size — the band streams down its rows.  pyramid_kernel holds
-// a band's computed rows of two levels in LDS at once, so 1920 x 1080 needs ~90 thin bands
-// (twice the pyramid's pixels in seam rows) and takes the per-level kernels instead.  Here a
-// band (a few per frame) advances in steps of about `chunk` level-0 rows: each step stages
-// its new level-0 rows in an LDS ring, then makes, level by level, every row whose two source
-// rows are now in the ring below (sched, from the host's simulation of the same rule), into the
-// level's own ring (and to the pyramid for the band's own rows).  A ring keeps the rows its
-// next level still needs plus those of the step (the host sizes it), so each level makes its
-// rows once and the seams are only between the few bands.  The next step's level-0 chunks are
-// loaded into registers while this step's levels are made.  Arithmetic as pyramid_kernel's.
-template <bool kX86>
-__global__ __launch_bounds__(kPyrBlock) void pyramid_roll_kernel(PyrArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char pr_lds[];
-    const int band = (int)blockIdx.x / a.ncols, f = blockIdx.y, tid = threadIdx.x;
-    const int L = a.nlevels;
-    const int4* bt = a.bands + band * L;
-    // the workgroup's column tile: cc[l] = {first, last computed column, own [z, w)}; rings
-    // hold the computed columns from cc[l].x (a multiple of 4) at pitch lp[l]
-    const int4* cc = a.cols + ((int)blockIdx.x - band * a.ncols) * L;
-    const int* sc = a.sched + (size_t)band * a.nsteps * L;
-    const int w0 = a.w[0], P0 = a.lp[0], R0 = a.ring_rows[0];
-    const int x00 = cc[0].x, cpr = (cc[0].y - x00 + 16) >> 4;
-    const uint8_t* src = a.src.base + f * a.src.fpitch;
-    const int4 b0 = bt[0];
-    int4* yd = reinterpret_cast<int4*>(pr_lds + a.ydesc);
-    constexpr int kPre = kPyrRollPre;  // level-0 chunks in flight per thread (host-bounded)
-    uint4 v[kPre];
-    auto load_rows = [&](int r0, int r1) __attribute__((always_inline)) {
-        const int total = (r1 - r0) * cpr;
-#pragma unroll
-        for (int u = 0; u < kPre; ++u) {
-            const int i = kPyrBlock * u + tid;
-            if (i >= total) continue;
-            const int r = r0 + i / cpr, c = i - (i / cpr) * cpr;
-            const uint8_t* row = src + (long long)r * a.src.pitch;
-            const int x = x00 + 16 * c;
-            if (x + 16 <= w0) {
-                v[u] = load16_a4(row + x);
-            } else {
-                uint32_t wd[4];
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const int xd = x + 4 * d;
-                    wd[d] = 0;
-                    if (xd + 4 <= w0) wd[d] = *reinterpret_cast<const uint32_t*>(row + xd);
-                    else
-                        for (int q = 0; q < 4 && xd + q < w0; ++q) wd[d] |= (uint32_t)row[xd + q] << (8 * q);
-                }
-                v[u] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
-            }
-        }
-    };
-    auto store_rows = [&](int r0, int r1) __attribute__((always_inline)) {
-        const int total = (r1 - r0) * cpr;
-        const int slot0 = r0 % R0;
-#pragma unroll
-        for (int u = 0; u < kPre; ++u) {
-            const int i = kPyrBlock * u + tid;
-            if (i >= total) continue;
-            const int j = i / cpr, c = i - j * cpr;
-            int slot = slot0 + j;
-            if (slot >= R0) slot -= R0;
-            *reinterpret_cast<uint4*>(pr_lds + a.ring_off[0] + slot * P0 + 16 * c) = v[u];
-            const int r = r0 + j;
-            if (a.l0_copy.base && r >= b0.z && r < b0.w)
-                *reinterpret_cast<uint4*>(const_cast<uint8_t*>(a.l0_copy.base) + f * a.l0_copy.fpitch +
-                                          (long long)r * a.l0_copy.pitch + x00 + 16 * c) = v[u];
-        }
-    };
-    // row descriptors of every step (host-made): per level l >= 1 in order, the rows the step
-    // makes as {source row 0 LDS offset, source row 1 LDS offset, b0 | b1 << 16, own ring row
-    // offset}; step s's are [yo[s], yo[s + 1]) (<= kPyrBlock), one per thread, loaded a step
-    // ahead.  The thread's column-group table of the next level to make is loaded a level ahead
-    // (they sit behind this level's work and barrier instead of in front of the next one's).
-    const int* yo = a.ydoff + (size_t)band * (a.nsteps + 1);
-    int4 ydn = make_int4(0, 0, 0, 0);
-    auto yload = [&](int s) __attribute__((always_inline)) {
-        const int i0 = yo[s], n = yo[s + 1] - i0;
-        if (tid < n) ydn = a.ydtab[i0 + tid];
-    };
-    uint4 gn0 = make_uint4(0u, 0u, 0u, 0u), gn1 = gn0, gn2 = gn0;
-    auto gload = [&](int l) __attribute__((always_inline)) {
-        const int gpr = (cc[l].y - cc[l].x + 4) >> 2;
-        if (tid / gpr < kPyrBlock / gpr) {
-            const uint4* gp = a.gtab[l] + 3 * ((cc[l].x >> 2) + tid % gpr);
-            gn0 = gp[0];
-            gn1 = gp[1];
-            gn2 = gp[2];
-        }
-    };
-    int e0 = b0.x;
-    load_rows(e0, sc[0]);
-    yload(0);
-    gload(1);
-    for (int s = 0; s < a.nsteps; ++s) {
-        const int* cur = sc + s * L;
-        const int* prv = s ? cur - L : nullptr;
-        if (tid < yo[s + 1] - yo[s]) yd[tid] = ydn;
-        store_rows(e0, cur[0]);
-        e0 = cur[0];
-        if (s + 1 < a.nsteps) {  // next step's level-0 rows and row descriptors, in flight
-            load_rows(e0, cur[L]);
-            yload(s + 1);
-        }
-        __syncthreads();
-        int base = 0;
-        for (int l = 1; l < L; ++l) {
-            const uint4 g0 = gn0, g1 = gn1, g2 = gn2;
-            gload(l + 1 < L ? l + 1 : 1);
-            const int r0 = prv ? prv[l] : bt[l].x, nrows = cur[l] - r0;
-            if (nrows <= 0) continue;  // uniform: nothing made, nothing to order
-            const int4 bl = bt[l], cl = cc[l];
-            const int w = a.w[l], gpr = (cl.y - cl.x + 4) >> 2, rps = kPyrBlock / gpr;
-            const int gx = tid % gpr, ry = tid / gpr;
-            if (ry < rps) {
-                // the group's source window, relative to the ring row's first column
-                const int xrel = (int)g0.x - cc[l - 1].x, wofs = (xrel >> 2) << 2, sh = xrel & 3;
-                const uint32_t sel[4] = {g0.y, g0.z, g0.w, g1.x};
-                typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-                const us2 cf[4] = {__builtin_bit_cast(us2, hcoef<kX86>(g1.y)), __builtin_bit_cast(us2, hcoef<kX86>(g1.z)),
-                                   __builtin_bit_cast(us2, hcoef<kX86>(g1.w)), __builtin_bit_cast(us2, hcoef<kX86>(g2.x))};
-                const int x = cl.x + 4 * gx, n = min(4, w - x);
-                const bool own_x = x >= cl.z && x < cl.w;  // own bounds are multiples of 4
-                const int xb = a.simd_xb[l];
-                const LevelPtr dp = a.dst[l];
-                uint8_t* dst = const_cast<uint8_t*>(dp.base) + f * dp.fpitch;
-                const bool ring = l + 1 < L;
-                auto hsum = [&](int off, uint32_t (&t)[4]) {
-                    const uint32_t* row = reinterpret_cast<const uint32_t*>(pr_lds + off + wofs);
-                    const uint32_t q0 = row[0], q1 = row[1], q2 = row[2];
-                    const uint32_t lo = __builtin_amdgcn_alignbyte(q1, q0, sh), hi = __builtin_amdgcn_alignbyte(q2, q1, sh);
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        t[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, __builtin_amdgcn_perm(hi, lo, sel[k])), cf[k], 0u, false);
-                };
-                for (int j = ry; j < nrows; j += rps) {
-                    const int4 d = yd[base + j];
-                    const uint32_t bb0 = (uint32_t)d.z & 0xffffu, bb1 = (uint32_t)d.z >> 16;
-                    uint32_t t0[4], t1[4];
-                    hsum(d.x, t0);
-                    hsum(d.y, t1);
-                    const uint32_t packed = resize4<kX86>(t0, t1, bb0, bb1, x, xb);
-                    if (ring) *reinterpret_cast<uint32_t*>(pr_lds + d.w + x - cl.x) = packed;
-                    const int r = r0 + j;
-                    if (own_x && r >= bl.z && r < bl.w) {
-                        uint8_t* o = dst + (long long)r * dp.pitch + x;
-                        if (n == 4) {
-                            *reinterpret_cast<uint32_t*>(o) = packed;
-                        } else {
-                            for (int k = 0; k < n; ++k) o[k] = (uint8_t)(packed >> (8 * k));
-                        }
-                    }
-                }
-            }
-            base += nrows;
-            __syncthreads();
-        }
-    }
-}
-template __global__ void pyramid_roll_kernel<false>(PyrArgs);
-template __global__ void pyramid_roll_kernel<true>(PyrArgs);
 
 // Host: pyramid_kernel's per-level column-group tables (3 uint4 per group of 4 output columns:
 // x0[0], the 4 perm selectors pairing bytes x0[k] - x0[0], x1[k] - x0[0] as u16 (0x0c = zero),
@@ -1398,54 +862,12 @@ __device__ __forceinline__ half2v fast_h2(uint32_t b) {
 __device__ __forceinline__ _Float16 fast_dn(uint32_t b) {
     return __builtin_bit_cast(_Float16, (unsigned short)b);
 }
-#ifndef ORBFE_FAST_ROWREAD
-#define ORBFE_FAST_ROWREAD 0
-#endif
-// ORBFE_FAST_ROWREAD (experiment, off): the 16 circle bytes and the centre from seven unaligned
-// row reads (2 x 4 + 5 x 8 bytes: ds_read_b32 / ds_read_b64 at byte addresses; 6 LDS
-// instructions instead of 17 ds_read_u8), each pair of bytes zero-extended into the two halves
-// of one register by a v_perm and selected by op_sel.  Bit-exact, but the unaligned LDS reads
-// stall: c3 382 K -> 257 K frames/s, c4 76.0 K -> 50.4 K (profiles/r05/fast_rowread/)
-__device__ __forceinline__ void fast_rows(const uint8_t* p, int st, uint32_t (&x)[16], uint32_t& c) {
-    uint32_t rm3, rp3;
-    uint64_t rm2, rp2, rm1, rp1, r0;
-    __builtin_memcpy(&rm3, p - 3 * st - 1, 4);
-    __builtin_memcpy(&rp3, p + 3 * st - 1, 4);
-    __builtin_memcpy(&rm2, p - 2 * st - 2, 8);
-    __builtin_memcpy(&rp2, p + 2 * st - 2, 8);
-    __builtin_memcpy(&rm1, p - st - 3, 8);
-    __builtin_memcpy(&rp1, p + st - 3, 8);
-    __builtin_memcpy(&r0, p - 3, 8);
-    // perm(hi, lo, sel): selector bytes 0-3 = lo's bytes, 4-7 = hi's, 0x0c = 0; the pair
-    // (a, b) -> a in bits 0-7, b in bits 16-23
-    auto pr = [](uint32_t hi, uint32_t lo, uint32_t a, uint32_t b) {
-        return __builtin_amdgcn_perm(hi, lo, 0x0c000c00u | (b << 16) | a);
-    };
-    const uint32_t P1 = pr(rp3, rm3, 5, 6);   // x0, x1
-    const uint32_t P2 = pr(rp3, rm3, 2, 1);   // x7, x8
-    const uint32_t P3 = pr(rp3, rm3, 0, 4);   // x9, x15
-    const uint32_t P4 = pr((uint32_t)(rp2 >> 32), (uint32_t)rp2, 4, 0);  // x2, x14
-    const uint32_t P5 = pr((uint32_t)(rm2 >> 32), (uint32_t)rm2, 4, 0);  // x6, x10
-    const uint32_t P6 = pr((uint32_t)(rp1 >> 32), (uint32_t)rp1, 6, 0);  // x3, x13
-    const uint32_t P7 = pr((uint32_t)(rm1 >> 32), (uint32_t)rm1, 6, 0);  // x5, x11
-    const uint32_t P8 = pr((uint32_t)(r0 >> 32), (uint32_t)r0, 6, 0);    // x4, x12
-    x[0] = P1; x[1] = P1 >> 16; x[7] = P2; x[8] = P2 >> 16; x[9] = P3; x[15] = P3 >> 16;
-    x[2] = P4; x[14] = P4 >> 16; x[6] = P5; x[10] = P5 >> 16; x[3] = P6; x[13] = P6 >> 16;
-    x[5] = P7; x[11] = P7 >> 16; x[4] = P8; x[12] = P8 >> 16;
-    c = ((uint32_t)r0 >> 24) & 0xffu;
-}
 __device__ __forceinline__ int fast_S(const uint8_t* p, int st) {
-#if ORBFE_FAST_ROWREAD
-    uint32_t x[16], cv;
-    fast_rows(p, st, x, cv);
-    const _Float16 V = fast_dn(cv);
-#else
     const _Float16 V = fast_dn(p[0]);
     const uint32_t x[16] = {p[3 * st],      p[3 * st + 1],  p[2 * st + 2],  p[st + 3],
                             p[3],           p[-st + 3],     p[-2 * st + 2], p[-3 * st + 1],
                             p[-3 * st],     p[-3 * st - 1], p[-2 * st - 2], p[-st - 3],
                             p[-3],          p[st - 3],      p[2 * st - 2],  p[3 * st - 1]};
-#endif
     half2v e[16], m3[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -1769,398 +1191,6 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
 
 template __global__ void fast_kernel<0>(FastArgs);
 template __global__ void fast_kernel<kFastPitch>(FastArgs);
-
-// ---------------------------------------------------------------------------------------------
-// K2, strip form (default): one 256-thread workgroup per run of 1, 2, 4 or 8 cells of one cell
-// row (one workgroup per (frame, level, cell-row strip)).  The run's ROI —
-// every ROI row of the cell row over the run's columns, neighbouring cells' 6-column overlaps
-// shared — is staged once.  Then:
-//   phase 1 (all four waves, a block of candidate rows each): the pre-test at iniThFAST over
-//     whole run rows (64 / gpr rows per sweep, so 8 / 4 / 2 / 1-cell runs keep ~97 % of the
-//     lanes busy), survivors appended to the wave's list — in no particular order: a score does
-//     not depend on its neighbours — and scored 64 at a time (fast_S) into the run's score
-//     plane; scores >= iniThFAST are appended to the wave's corner list;
-//   phase 2a (all waves): the strict 3x3 NMS of each corner against the score plane, neighbours
-//     outside the corner's cell taken as 0 (H1: cv::FAST on the cell ROI, ORBextractor.cc:
-//     808-815), keepers marked in a bitmap and counted per cell;
-//   phase 2b (a wave per cell): the cell's marks read row by row (lane = row) and written to
-//     the cell's slot in row-major order; an empty cell reruns the pre-test and scoring at
-//     minThFAST over its own columns and emits by the bitmap path (811-815).
-// A corner list that overflows (noise frames at low thresholds) switches the run to the bitmap
-// path for every cell: corners marked from the score plane, NMS and emission per cell.
-__device__ __forceinline__ unsigned lane_below(unsigned long long b, unsigned acc) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, acc));
-}
-constexpr int kChunkClist = 128;  // per-wave corner list entries (more: the bitmap path)
-
-// Pre-test at threshold t (< 255) over candidate rows [ra, re) of a region of gpr <= 64 groups
-// per row (group lg covers ROI columns 4 (g0 + lg) .. + 3; bytes outside the candidate columns
-// masked by vfirst (group 0) / vlast (group gpr - 1)), rps = 64 / gpr rows per sweep.  Survivors
-// are scored into S (max(S, -1) + 1 at o + P + 1, o = r P + c) and scores >= tb either appended
-// to clist (when clist != null: returns -1 if it overflowed, else its length) or marked in the
-// bitmap (bit c of row r).  `list`: the wave's kChunkList entries + 64 trash slots.  Every lane
-// of the wave calls it.
-__device__ __forceinline__ int fast_strip_sweep(const uint8_t* roi, uint8_t* S, uint32_t* bm,
-                                                uint16_t* list, uint16_t* clist, int ra, int re,
-                                                int gpr, int g0, int X0, uint32_t vfirst,
-                                                uint32_t vlast, int t, int tb) {
-    constexpr int P = kChunkP, P4 = kChunkP / 4;
-    const int lane = threadIdx.x & 63;
-    const unsigned inv_p = 0xffffffffu / (unsigned)P + 1u;
-    // bright: c - v > t  <=>  the high bit of lerp(lerp(c, ~v, R1), M, 0) (DESIGN.md "FAST");
-    // dark: v - c > t  <=>  NOT the high bit of lerp(lerp(c, ~v, R1 ^ 1), 256 - M, 0): the dark
-    // test's lerp(v, ~c, R1) is ~lerp(c, ~v, R1 ^ 1), so no per-byte NOT is needed (checked for
-    // every c, v, t < 255 in tests/test_oracle_cpu.py)
-    const uint32_t R1 = (t & 1) ? 0x01010101u : 0u, R0 = R1 ^ 0x01010101u;
-    const uint32_t M = (uint32_t)(128 - ((t + 1) >> 1)) * 0x01010101u;
-    const uint32_t M2 = (uint32_t)(128 + ((t + 1) >> 1)) * 0x01010101u;
-    const uint32_t* lds32 = reinterpret_cast<const uint32_t*>(roi);
-    const uint8_t* cen = roi + X0 + 3 * P;  // candidate (0, 0)
-    // this lane's place in a sweep: row lr of the sweep, group lg
-    const int rps = 64 / gpr;
-    const int lr = lane / gpr, lg = lane - lr * gpr;
-    uint32_t vm = lr < rps ? 0x80808080u : 0u;
-    if (lg == 0) vm &= vfirst;
-    if (lg == gpr - 1) vm &= vlast;
-    const int wl = (lr + 3) * P4 + g0 + lg;       // dword of the group's centres, row ra + lr
-    const int obl = lr * P + 4 * (g0 + lg) - X0;  // candidate offset of the group's byte 0
-    int cnt = 0, done = 0, ncl = 0;
-    auto score = [&](int n) {  // list[done .. done + n), n <= 64
-        int o = 0, sv = 0;
-        if (lane < n) {
-            o = list[done + lane];
-            sv = max(fast_S(cen + o, P), -1) + 1;
-            S[o + P + 1] = (uint8_t)sv;
-        }
-        const bool corner = lane < n && sv >= tb;
-        if (clist) {
-            const unsigned long long cm = __ballot(corner);
-            if (corner) {
-                const int slot = (int)lane_below(cm, (unsigned)ncl);
-                if (slot < kChunkClist) clist[slot] = (uint16_t)o;
-            }
-            ncl = __builtin_amdgcn_readfirstlane(ncl + __popcll(cm));
-        } else if (corner) {
-            const int r = (int)__umulhi((unsigned)o, inv_p), c = o - r * P;
-            atomicOr(&bm[r * kChunkBmW + (c >> 5)], 1u << (c & 31));
-        }
-        done += n;
-    };
-    for (int r0 = ra; r0 < re; r0 += rps) {
-        uint32_t fl = 0;
-        const int ob = obl + r0 * P;
-        if (r0 + lr < re) {
-            const int w = wl + r0 * P4;
-            const uint32_t cur = lds32[w], prv = lds32[w - 1], nxt = lds32[w + 1];
-            const uint32_t up = lds32[w - 3 * P4], dn = lds32[w + 3 * P4];
-            const uint32_t c4 = __builtin_amdgcn_alignbyte(nxt, cur, 3);   // column + 3
-            const uint32_t c12 = __builtin_amdgcn_alignbyte(cur, prv, 1);  // column - 3
-            const uint32_t ncur = ~cur;
-            auto hb = [&](uint32_t c) { return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(c, ncur, R1), M, 0u); };
-            auto xd = [&](uint32_t c) { return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(c, ncur, R0), M2, 0u); };
-            const uint32_t br = (hb(dn) | hb(up)) & (hb(c4) | hb(c12));
-            const uint32_t xk = (xd(dn) & xd(up)) | (xd(c4) & xd(c12));  // NOT dark, in the high bits
-            fl = (br | ~xk) & vm;
-        }
-        const bool f0 = (uint8_t)fl >= 0x80u, f1 = (uint8_t)(fl >> 8) >= 0x80u;
-        const bool f2 = (uint8_t)(fl >> 16) >= 0x80u, f3 = (int)fl < 0;
-        const unsigned long long b0 = __ballot(f0), b1 = __ballot(f1), b2 = __ballot(f2), b3 = __ballot(f3);
-        const int n0 = __popcll(b0), n1 = __popcll(b1), n2 = __popcll(b2), n3 = __popcll(b3);
-        if (fl) {  // byte-major positions (byte 0 of every lane, then byte 1, ...); trash slot else
-            const int tr = kChunkList + lane;
-            const int p0 = (int)lane_below(b0, (unsigned)cnt);
-            const int p1 = (int)lane_below(b1, (unsigned)(cnt + n0));
-            const int p2 = (int)lane_below(b2, (unsigned)(cnt + n0 + n1));
-            const int p3 = (int)lane_below(b3, (unsigned)(cnt + n0 + n1 + n2));
-            list[f0 ? p0 : tr] = (uint16_t)ob;
-            list[f1 ? p1 : tr] = (uint16_t)(ob + 1);
-            list[f2 ? p2 : tr] = (uint16_t)(ob + 2);
-            list[f3 ? p3 : tr] = (uint16_t)(ob + 3);
-        }
-        // (readfirstlane: keeps the counters scalar across the divergent stores above)
-        cnt = __builtin_amdgcn_readfirstlane(cnt + n0 + n1 + n2 + n3);
-        fast_sync();
-        while (cnt - done >= 64) score(64);
-        if (cnt + 256 > kChunkList) {  // make room for a sweep: the < 64 unscored to the front
-            const int rem = cnt - done;
-            const int e = lane < rem ? list[done + lane] : 0;
-            fast_sync();
-            if (lane < rem) list[lane] = (uint16_t)e;
-            fast_sync();
-            cnt = rem;
-            done = 0;
-        }
-    }
-    fast_sync();
-    if (cnt > done) score(cnt - done);
-    fast_sync();
-    return ncl > kChunkClist ? -1 : ncl;
-}
-
-// Bitmap path for one cell: the corner bits of its columns [cs, ce) (scores >= tb) expanded
-// row by row into the wave's list, the strict 3x3 NMS on the score plane with neighbours outside
-// the cell as 0 (H1), survivors -> out[] in row-major order.  Returns the number found (stores
-// stop at cap).  kx / ky: key coordinates of candidate (0, 0).  Every lane of the wave calls it.
-__device__ __forceinline__ int fast_strip_emit(const uint8_t* S, const uint32_t* bm, uint16_t* list,
-                                               int nr, int cs, int ce, int tb, int kx, int ky,
-                                               uint32_t* out, int cap) {
-    constexpr int P = kChunkP;
-    const int lane = threadIdx.x & 63;
-    const unsigned inv_p = 0xffffffffu / (unsigned)P + 1u;
-    const int d0 = cs >> 5, sh = cs & 31, wd = ce - cs;  // wd < 64 (cells are < 60 wide)
-    const unsigned long long wmask = (1ull << wd) - 1;
-    int emitted = 0;
-    for (int rb = 0; rb < nr; rb += 64) {
-        const int r = rb + lane;
-        unsigned long long m = 0;
-        if (r < nr) {
-            const uint32_t* row = bm + r * kChunkBmW + d0;
-            unsigned long long v = (unsigned long long)row[0] | ((unsigned long long)row[1] << 32);
-            if (sh) v = (v >> sh) | ((unsigned long long)row[2] << (64 - sh));
-            m = v & wmask;
-        }
-        const int n = __popcll(m);
-        const int inc = wave_inclusive_sum(n);
-        const int tot = __builtin_amdgcn_readlane(inc, 63);
-        for (int lo = 0; lo < tot; lo += kChunkList) {  // one batch unless > kChunkList corners
-            int pos = inc - n - lo;
-            unsigned long long mm = m;
-            const int rowo = r * P + cs;
-            while (__ballot(mm != 0 && pos < kChunkList)) {
-                if (mm != 0 && pos < kChunkList) {
-                    if (pos >= 0) list[pos] = (uint16_t)(rowo + (int)__builtin_ctzll(mm));
-                    ++pos;
-                    mm &= mm - 1;
-                }
-            }
-            const int nb = min(tot - lo, kChunkList);
-            fast_sync();
-            for (int i0 = 0; i0 < nb; i0 += 64) {
-                const int i = i0 + lane;
-                bool keep = false;
-                uint32_t key = 0;
-                if (i < nb) {
-                    const int o = list[i];
-                    const uint8_t* q = S + o + P + 1;
-                    const int s = q[0];
-                    const int rr = (int)__umulhi((unsigned)o, inv_p), c = o - rr * P;
-                    const int mid = max(q[-P], q[P]);
-                    const int lft = max(max(q[-P - 1], q[-1]), q[P - 1]);
-                    const int rgt = max(max(q[-P + 1], q[1]), q[P + 1]);
-                    const int nbm = max(mid, max(c > cs ? lft : 0, c + 1 < ce ? rgt : 0));
-                    keep = s >= tb && nbm < s;
-                    key = pack_key(kx + c, ky + rr, s - 1);
-                }
-                const unsigned long long km = __ballot(keep);
-                if (keep) {
-                    const int slot = (int)lane_below(km, (unsigned)emitted);
-                    if (slot < cap) out[slot] = key;
-                }
-                emitted += __popcll(km);
-            }
-            fast_sync();
-        }
-    }
-    return emitted;
-}
-
-// The cell's NMS survivors, already marked in the bitmap (phase 2a), to out[] in row-major
-// order: lane = row, each row's marks (usually 0-2) written in column order.
-__device__ __forceinline__ int fast_strip_emit_marked(const uint8_t* S, const uint32_t* bm, int nr,
-                                                      int cs, int ce, int kx, int ky, uint32_t* out,
-                                                      int cap) {
-    constexpr int P = kChunkP;
-    const int lane = threadIdx.x & 63;
-    const int d0 = cs >> 5, sh = cs & 31, wd = ce - cs;
-    const unsigned long long wmask = (1ull << wd) - 1;
-    int emitted = 0;
-    for (int rb = 0; rb < nr; rb += 64) {
-        const int r = rb + lane;
-        unsigned long long m = 0;
-        if (r < nr) {
-            const uint32_t* row = bm + r * kChunkBmW + d0;
-            unsigned long long v = (unsigned long long)row[0] | ((unsigned long long)row[1] << 32);
-            if (sh) v = (v >> sh) | ((unsigned long long)row[2] << (64 - sh));
-            m = v & wmask;
-        }
-        const int n = __popcll(m);
-        const int inc = wave_inclusive_sum(n);
-        int pos = emitted + inc - n;
-        const uint8_t* srow = S + r * P + P + 1 + cs;
-        while (m) {
-            const int c = (int)__builtin_ctzll(m);
-            if (pos < cap) out[pos] = pack_key(kx + cs + c, ky + r, srow[c] - 1);
-            ++pos;
-            m &= m - 1;
-        }
-        emitted += __builtin_amdgcn_readlane(inc, 63);
-    }
-    return emitted;
-}
-
-#ifdef ORBFE_FAST_TIMING
-// diagnostic build only: per (frame < 64, run < 160) phase clocks of fast_strip_kernel
-__device__ long long g_fast_t[64 * 160 * 16];
-#define FS_MARK(i) do { if (lane == 0 && ftm) ftm[(i)] = clock64(); } while (0)
-#define FS_PUT(i, v) do { if (lane == 0 && ftm) ftm[(i)] = (v); } while (0)
-#else
-#define FS_MARK(i) do { } while (0)
-#define FS_PUT(i, v) do { } while (0)
-#endif
-
-__global__ __launch_bounds__(kChunkBlock) void fast_strip_kernel(FastArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char fs_lds[];
-    constexpr int P = kChunkP;
-    constexpr int NW = kChunkBlock / 64;
-    int ci, f;
-    xcd_block(ci, f);
-#ifdef ORBFE_FAST_TIMING
-    long long* ftm = (f < 64 && ci < 160) ? g_fast_t + ((long long)f * 160 + ci) * 16 : nullptr;
-#endif
-    const FastChunk& ch = a.chunks[ci];
-    // wv through readfirstlane: the wave index is wave-uniform, and the loops, list counters and
-    // branches derived from it stay scalar (otherwise the compiler runs them as divergent)
-    const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int R = a.roi_rows;  // the carve's ROI rows (tallest run)
-    // carve: ROI | score plane | bitmap | column info | per-cell counts + flag | lists | corner lists
-    uint8_t* roi = fs_lds;
-    uint8_t* S = fs_lds + R * P;
-    uint32_t* bm = reinterpret_cast<uint32_t*>(S + (R - 4) * P);
-    uint8_t* cinfo = reinterpret_cast<uint8_t*>(bm) + ((((R - 6) * kChunkBmW * 4) + 15) & ~15);
-    int* ccount = reinterpret_cast<int*>(cinfo + P);  // [kChunkCells] + the overflow flag
-    uint16_t* list = reinterpret_cast<uint16_t*>(ccount + 16) + wv * (kChunkList + 64);
-    uint16_t* clist = reinterpret_cast<uint16_t*>(ccount + 16) + NW * (kChunkList + 64) + wv * kChunkClist;
-    const int level = ch.level, nr = ch.nr, nc = ch.nc, X0 = ch.X0, g0 = ch.g0, gpr = ch.gpr;
-    const int ncell = ch.ncell;
-    const bool any = nr > 0 && nc > 0;
-    const LevelPtr lp = a.pyr[level];
-    const int t1 = a.ini_th, t2 = a.min_th;
-    if (wv == 0) FS_MARK(0);
-    // ---- phase 0: the ROI rows (16-byte loads, 4 per thread in flight), a zero score plane and
-    // bitmap, the column -> cell table.  A row's last load ends < 16 bytes past the run's x1 <=
-    // maxBorderX, inside the row.
-    if (any) {
-        const int nq = ch.nq, tot = (nr + 6) * nq;
-        const uint8_t* img = lp.base + f * lp.fpitch + (long long)ch.y0 * lp.pitch + ch.x0a;
-        for (int i0 = 0; i0 < tot; i0 += 4 * kChunkBlock) {
-            uint4 v[4];
-            int off[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int i = i0 + k * kChunkBlock + tid;
-                off[k] = -1;
-                if (i < tot) {
-                    // (inv_nq wraps to 0 for nq = 1: umulhi(i, 2^32) = i)
-                    const int r = nq == 1 ? i : (int)__umulhi((unsigned)i, ch.inv_nq), qq = i - r * nq;
-                    v[k] = load16_a4(img + (long long)r * lp.pitch + 16 * qq);
-                    off[k] = r * P + 16 * qq;
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (off[k] >= 0) *reinterpret_cast<uint4*>(roi + off[k]) = v[k];
-        }
-        for (int i = tid; i < ((nr + 2) * P) >> 4; i += kChunkBlock)
-            reinterpret_cast<uint4*>(S)[i] = make_uint4(0u, 0u, 0u, 0u);
-        for (int i = tid; i < nr * kChunkBmW; i += kChunkBlock) bm[i] = 0u;
-        // candidate column -> cell j | 0x10 (the cell's first column) | 0x20 (its last)
-        for (int c = tid; c < nc; c += kChunkBlock) {
-            int j = 0;
-            while (j + 1 < ncell && c >= ch.cs[j + 1]) ++j;
-            cinfo[c] = (uint8_t)(j | (c == ch.cs[j] ? 0x10 : 0) | (c + 1 == ch.cs[j + 1] ? 0x20 : 0));
-        }
-    }
-    if (tid < 16) ccount[tid] = 0;
-    if (wv == 0) FS_MARK(1);
-    __syncthreads();
-    if (wv == 0) FS_MARK(2);
-    // ---- phase 1: pre-test + scores at iniThFAST over the whole run, rows in 4 blocks
-    int ncl = 0;
-    if (any && t1 < 255) {
-        const int rps = 64 / gpr;
-        const int rbw = ((nr + rps - 1) / rps + NW - 1) / NW * rps;  // rows per wave, whole sweeps
-        const int lo = X0 - 4 * g0, hi = X0 + nc - 4 * (g0 + gpr - 1);  // 0..3, 1..4
-        const uint32_t vfirst = 0x80808080u << (8 * lo), vlast = 0x80808080u >> (8 * (4 - hi));
-        ncl = fast_strip_sweep(roi, S, bm, list, clist, min(wv * rbw, nr), min((wv + 1) * rbw, nr),
-                               gpr, g0, X0, vfirst, vlast, t1, max(t1, 1) + 1);
-        if (ncl < 0 && lane == 0) ccount[kChunkCells] = 1;  // a corner list overflowed
-    }
-    FS_MARK(3 + wv);
-    __syncthreads();
-    const bool marked = __builtin_amdgcn_readfirstlane(ccount[kChunkCells]) == 0;  // else the bitmap path
-    const int tb1 = max(t1, 1) + 1;
-    // ---- phase 2a: NMS of the wave's corners (any order), keepers marked and counted per cell
-    if (any && t1 < 255) {
-        if (marked) {
-            const unsigned inv_p = 0xffffffffu / (unsigned)P + 1u;
-            for (int i = lane; i < ncl; i += 64) {
-                const int o = clist[i];
-                const uint8_t* q = S + o + P + 1;
-                const int s = q[0];
-                const int r = (int)__umulhi((unsigned)o, inv_p), c = o - r * P;
-                const int info = cinfo[c];
-                const int mid = max(q[-P], q[P]);
-                const int lft = max(max(q[-P - 1], q[-1]), q[P - 1]);
-                const int rgt = max(max(q[-P + 1], q[1]), q[P + 1]);
-                const int nbm = max(mid, max((info & 0x10) ? 0 : lft, (info & 0x20) ? 0 : rgt));
-                if (nbm < s) {  // s >= tb1 by construction
-                    atomicOr(&bm[r * kChunkBmW + (c >> 5)], 1u << (c & 31));
-                    atomicAdd(&ccount[info & 0xf], 1);
-                }
-            }
-        } else {  // bitmap path: every score >= iniThFAST marked as a corner (dense, 4 per lane)
-            const int cw = (nc + 3) >> 2;
-            const unsigned inv_cw = 0xffffffffu / (unsigned)cw + 1u;  // 0 for cw = 1
-            for (int i = tid; i < nr * cw; i += kChunkBlock) {
-                const int r = cw == 1 ? i : (int)__umulhi((unsigned)i, inv_cw), g = i - r * cw;
-                uint32_t bits = 0;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int c = 4 * g + k;
-                    if (c < nc && S[(r + 1) * P + c + 1] >= tb1) bits |= 1u << k;
-                }
-                const int c0 = 4 * g;
-                if (bits) atomicOr(&bm[r * kChunkBmW + (c0 >> 5)], bits << (c0 & 31));
-            }
-        }
-    }
-    if (wv == 0) FS_MARK(7);
-    __syncthreads();
-    // ---- phase 2b: a wave per cell — ordered emission, the minThFAST rerun if empty
-    const int kx = ch.x0a + X0 - kMinBorder, ky = ch.y0 + 3 - kMinBorder;
-    int wave_total = 0, reruns = 0;
-    for (int j = wv; j < ncell; j += NW) {
-        const int cs = ch.cs[j], ce = ch.cs[j + 1];
-        const CellDesc& cell = a.cells[ch.cell0 + j];
-        uint32_t* out = a.cell_keys + f * a.cell_cap_total + cell.slot;
-        const int cap = cell.cap;
-        int emitted = 0;
-        if (any) {
-            if (t1 < 255)
-                emitted = marked ? (__builtin_amdgcn_readfirstlane(ccount[j]) ? fast_strip_emit_marked(S, bm, nr, cs, ce, kx, ky, out, cap) : 0)
-                                 : fast_strip_emit(S, bm, list, nr, cs, ce, tb1, kx, ky, out, cap);
-            if (emitted == 0 && t2 < 255) {
-                // rerun at minThFAST over the cell's columns (its marks are all 0: no keeper, or
-                // on the bitmap path its corners >= iniThFAST, a subset of those >= minThFAST)
-                ++reruns;
-                const int gb = (X0 + cs) >> 2, ge = (X0 + ce - 1) >> 2, gj = ge - gb + 1;
-                const int lo = X0 + cs - 4 * gb, hi = X0 + ce - 4 * ge;
-                const uint32_t vfirst = 0x80808080u << (8 * lo), vlast = 0x80808080u >> (8 * (4 - hi));
-                fast_strip_sweep(roi, S, bm, list, nullptr, 0, nr, gj, gb, X0, vfirst, vlast, t2,
-                                 max(t2, 1) + 1);
-                emitted = fast_strip_emit(S, bm, list, nr, cs, ce, max(t2, 1) + 1, kx, ky, out, cap);
-            }
-        }
-        const int n = min(emitted, cap);
-        if (lane == 0) a.cell_cnt[f * a.ncells + ch.cell0 + j] = n;
-        wave_total += n;
-    }
-    // the level's key total for the oct-tree (which reads it and resets it to 0)
-    if (lane == 0 && wave_total) atomicAdd(&a.level_keys[f * kMaxLevels + level], wave_total);
-    FS_MARK(8 + wv);
-    FS_PUT(12 + wv, reruns);
-    (void)reruns;
-}
 
 // ---------------------------------------------------------------------------------------------
 // K3 — DistributeOctTree as a data-parallel emulation of the reference's std::list.
@@ -3177,10 +2207,6 @@ constexpr int kFragLds = ORBFE_DESC_FRAG_LDS;
 #define ORBFE_DESC_LATE_STORE 1  // descriptor words stored once per wave, after the keypoint loop
 #endif
 constexpr bool kDescLateStore = ORBFE_DESC_LATE_STORE != 0;
-#ifndef ORBFE_DESC_PF2
-#define ORBFE_DESC_PF2 0  // (matrix-core form) two keypoints' windows in flight instead of one
-#endif
-constexpr bool kDescPf2 = ORBFE_DESC_PF2 != 0;
 #ifndef ORBFE_DESC_WAVES
 #define ORBFE_DESC_WAVES 6
 #endif
@@ -3511,12 +2537,6 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
     };
     unsigned long long dacc = 0;
     load_kp(__ffsll((long long)vmask) - 1);
-    // kDescPf2: the keypoint after next's window in flight too (a second fragment buffer)
-    uint4 rv2[3];
-    if constexpr (kDescPf2 && kMfma) {
-        const unsigned long long r1 = vmask & (vmask - 1);
-        if (r1) load_frag_to(__ffsll((long long)r1) - 1, rv2);
-    }
     // (the first window's loads are in flight during the IC moments and the trig)
     // 1. IC moments.  Lane (r = lane >> 1, hh = lane & 1): row v = r - 15, columns
     //    u = -15 + 16 hh .. +15 (u = 16 never lies in the disc).
@@ -3657,14 +2677,7 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
                 A[t] = i32x4m{(int)(rv[t].x ^ 0x80808080u), (int)(rv[t].y ^ 0x80808080u),
                               (int)(rv[t].z ^ 0x80808080u), (int)(rv[t].w ^ 0x80808080u)};
             const unsigned long long rest = m & (m - 1);
-            if constexpr (kDescPf2) {
-#pragma unroll
-                for (int t = 0; t < 3; ++t) rv[t] = rv2[t];
-                const unsigned long long rest2 = rest & (rest - 1);
-                if (rest2) load_frag_to(__ffsll((long long)rest2) - 1, rv2);
-            } else {
-                if (rest) load_kp(__ffsll((long long)rest) - 1);  // next keypoint's window in flight
-            }
+            if (rest) load_kp(__ffsll((long long)rest) - 1);  // next keypoint's window in flight
             const int xs = kX86 ? (int)__builtin_amdgcn_readlane(my_x0, j) + (lane & 15) -
                                       a.simd_xb[(int)__builtin_amdgcn_readlane(my_l, j)]
                                 : 0;
@@ -4142,27 +3155,6 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
                     // + 2 dwords: the table path reads 3 dwords from a group's first source dword
                     need_w = std::max(need_w, ((a1 - a0) >> 2) + 1 + 2);
                 }
-                {   // resize_blur_kernel: the source of the rows / columns 3 beyond the tile
-                    int rb_rows = 0, rb_w = 0;
-                    for (int oy = 0; oy < dh; oy += kRsTH) {
-                        const int e0 = std::max(oy - 3, 0), e1 = std::min(std::min(oy + kRsTH, dh) - 1 + 3, dh - 1);
-                        auto sy = [&](int dy) { return (int)std::floor((float)((dy + 0.5) * scale_y - 0.5)); };
-                        const int r0 = std::min(std::max(sy(e0), 0), sh - 1), r1 = std::min(std::max(sy(e1) + 1, 0), sh - 1);
-                        rb_rows = std::max(rb_rows, r1 - r0 + 1);
-                    }
-                    for (int ox = 0; ox < dw; ox += kRsTW) {
-                        const int e0 = std::max(ox - 3, 0), e1 = std::min(std::min(ox + kRsTW, dw) - 1 + 3, dw - 1);
-                        const int a0 = g.xtab[xb + 3 * e0] & ~3, a1 = g.xtab[xb + 3 * e1 + 1];
-                        rb_w = std::max(rb_w, ((a1 - a0) >> 2) + 1);
-                    }
-                    g.rb_pitch[l] = 16 * ((rb_w + 3) / 4);
-                    const size_t stage = std::max((size_t)rb_rows * g.rb_pitch[l], (size_t)kRbRowpBytes);
-                    g.rb_lds_e[l] = (int)((stage + 15) & ~(size_t)15);
-                    g.rb_lds[l] = (size_t)g.rb_lds_e[l] + (size_t)kRbERows * kRbEP + 3 * (kRsTH + 6) * sizeof(int);
-                    // over 64 KB (scale factors around 3.3 and up) the opt-in fused kernel is
-                    // unavailable for this level: resize_kernel makes it (rb_lds = 0)
-                    if (g.rb_lds[l] > 64 * 1024) g.rb_lds[l] = 0;
-                }
                 g.rs_tiles_x[l] = (dw + kRsTW - 1) / kRsTW;
                 g.rs_tiles[l] = g.rs_tiles_x[l] * ((dh + kRsTH - 1) / kRsTH);
                 // 16-byte chunks: the widest tile's dwords rounded up to whole chunks
@@ -4204,7 +3196,6 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
             g.gtab_off[l] = (int)(g.ptab.size() / 4);
             g.pyr_ok = pyramid_group_table(g.xtab, g.xoff[l], g.geo.lv[l].w, g.ptab);
         }
-        const bool groups_ok = g.pyr_ok;  // every level's column groups fit 8 source bytes
         for (int l = 0; l < L; ++l) g.pyr_lp[l] = ((g.geo.lv[l].w + 15) & ~15) + 16;
         double work = 0, own = 0;  // pixels computed by the bands vs the pyramid's
         for (int l = 1; l < L; ++l) own += (double)g.geo.lv[l].w * g.geo.lv[l].h;
@@ -4318,257 +3309,6 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
             g.rs2_off[l] = (int)(g.ptab.size() / 4);
             for (int v : tt) g.ptab.push_back((uint32_t)v);
         }
-        // resizeN_kernel plans: chains of n = 4 (else 3) levels l .. l + n - 1, tiles of the last.
-        // F_k(y) = the row of made level k that the last level's row y reaches first (through
-        // each level's first source row); level k is partitioned among the tiles by F_k of their
-        // first rows (columns likewise, in whole 4-column groups).  A tile computes, level by
-        // level downwards, its own part plus what the level above it reads.
-        for (int l = 0; l < kMaxLevels; ++l) g.rsn_n[l] = 0;
-        const char* rsn_max = std::getenv("ORBFE_RSN_MAX");  // longest chain planned (A/B)
-        const int nmax = rsn_max ? std::max(3, std::min(kRsNMax, std::atoi(rsn_max))) : kRsNMax;
-        for (int l = 1; l + 2 < L && g.pyr_ok; ++l) {
-            for (int n = std::min(nmax, L - l); n >= 3 && g.rsn_n[l] == 0; --n) {
-                const int last = l + n - 1;
-                const int dw = g.geo.lv[last].w, dh = g.geo.lv[last].h;
-                const int ntx = (dw + kRsTW - 1) / kRsTW, nty = (dh + kRsTH - 1) / kRsTH;
-                auto Y = [&](int k) { return &g.ytab[g.yoff[l + k]]; };  // made level k's tables
-                auto X = [&](int k) { return &g.xtab[g.xoff[l + k]]; };
-                auto Fy = [&](int k, int y) {  // row of level k (< n - 1) that last-level row y reaches
-                    for (int j = n - 1; j > k; --j) y = Y(j)[3 * y];
-                    return y;
-                };
-                auto Fx = [&](int k, int x) {
-                    for (int j = n - 1; j > k; --j) x = X(j)[3 * x] & ~3;
-                    return x;
-                };
-                std::vector<int> tt;
-                tt.reserve((size_t)ntx * nty * 8 * (n - 1));
-                int rows[kRsNMax] = {}, wid[kRsNMax] = {}, gmax = 0;  // image k: staged (0), made k - 1
-                std::vector<int> one(8 * (n - 1));
-                for (int ty = 0; ty < nty; ++ty)
-                    for (int tx = 0; tx < ntx; ++tx) {
-                        const int ox = tx * kRsTW, oy = ty * kRsTH;
-                        const int ex = std::min(ox + kRsTW, dw) - 1, ey = std::min(oy + kRsTH, dh) - 1;
-                        const int exg = std::min(ex | 3, dw - 1);
-                        int r0 = Y(n - 1)[3 * oy], r1 = Y(n - 1)[3 * ey + 1];
-                        int c0 = X(n - 1)[3 * ox] & ~3, c1 = X(n - 1)[3 * exg + 1];
-                        for (int k = n - 2; k >= 0; --k) {
-                            const int mw = g.geo.lv[l + k].w, mh = g.geo.lv[l + k].h;
-                            const int oy0 = ty ? Fy(k, oy) : 0, oy1 = ty + 1 < nty ? Fy(k, oy + kRsTH) : mh;
-                            const int ox0 = tx ? Fx(k, ox) : 0, ox1 = tx + 1 < ntx ? Fx(k, ox + kRsTW) : mw;
-                            const int cy0 = std::min(r0, oy0), cy1 = std::max(r1, oy1 - 1);
-                            const int cx0 = std::min(c0, ox0);
-                            const int cx1 = std::min(mw - 1, std::max(c1, ox1 - 1) | 3);
-                            const int v[8] = {cy0, cy1, cx0, cx1, oy0, oy1, ox0, ox1};
-                            std::copy(v, v + 8, one.begin() + 8 * k);
-                            rows[k + 1] = std::max(rows[k + 1], cy1 - cy0 + 1);
-                            wid[k + 1] = std::max(wid[k + 1], cx1 - cx0 + 1);
-                            gmax = std::max(gmax, ((cx1 - cx0) >> 2) + 1);
-                            r0 = Y(k)[3 * cy0];
-                            r1 = Y(k)[3 * cy1 + 1];
-                            c0 = X(k)[3 * cx0] & ~3;
-                            c1 = X(k)[3 * cx1 + 1];
-                        }
-                        rows[0] = std::max(rows[0], r1 - r0 + 1);
-                        wid[0] = std::max(wid[0], c1 - c0 + 1);
-                        tt.insert(tt.end(), one.begin(), one.end());
-                    }
-                size_t reg[2] = {0, 0};
-                for (int k = 0; k < n; ++k) {
-                    g.rsn_pitch[l][k] = ((wid[k] + 15) & ~15) + 16;
-                    reg[k & 1] = std::max(reg[k & 1], (size_t)rows[k] * g.rsn_pitch[l][k]);
-                }
-                reg[0] = (reg[0] + 15) & ~(size_t)15;
-                for (int k = 0; k < n; ++k) g.rsn_lofs[l][k] = (k & 1) ? (int)reg[0] : 0;
-                const size_t lds = reg[0] + reg[1];
-                if (lds > 64 * 1024 || gmax > 256) continue;
-                g.rsn_n[l] = n;
-                g.rsn_tiles_x[l] = ntx;
-                g.rsn_tiles[l] = ntx * nty;
-                g.rsn_lds[l] = lds;
-                while (g.ptab.size() % 4) g.ptab.push_back(0u);
-                g.rsn_off[l] = (int)(g.ptab.size() / 4);
-                for (int v : tt) g.ptab.push_back((uint32_t)v);
-            }
-        }
-        // pyramid_roll_kernel plans: the same band rows (plan_bands), streamed in steps of
-        // `chunk` level-0 rows.  The host runs the kernel's rule — a level's row is made in the
-        // first step after which both its source rows exist — to get every step's row ranges
-        // and each ring's size (the rows its next level still needs when the step starts, plus
-        // the rows the step makes).  Large batches: a few bands per frame (2 or 3 workgroups
-        // per CU by LDS); small ones: thin bands for latency.
-        // Column tiles (ORBFE_ROLL_COLS): a band can also be split into column tiles, each
-        // computing its own columns of every level plus the source columns its next level's
-        // columns read (derived top-down like the rows; whole 4-column groups), so a tile's
-        // rings are narrower (two workgroups per CU).  Plan: the tallest step (32, 24, 16, 8
-        // rows), then the fewest tiles, whose LDS fits 160 KB.
-        auto plan_cols = [&](int nct, std::vector<int>& ct, int (&pitch)[kMaxLevels]) {
-            ct.assign((size_t)nct * L * 4, 0);
-            for (int l = 0; l < L; ++l) pitch[l] = 0;
-            for (int t = 0; t < nct; ++t) {
-                auto O = [&](int l, int tt) {  // own column boundaries: multiples of 4, w at the end
-                    return tt >= nct ? g.geo.lv[l].w : (int)(((long long)tt * g.geo.lv[l].w / nct) & ~3LL);
-                };
-                int c0[kMaxLevels], c1[kMaxLevels];
-                for (int l = L - 1; l >= 0; --l) {
-                    const int w = g.geo.lv[l].w;
-                    int a0 = O(l, t), a1 = O(l, t + 1) - 1;
-                    if (l + 1 < L) {  // the source columns of level l + 1's computed groups
-                        const int xo = g.xoff[l + 1], wn = g.geo.lv[l + 1].w;
-                        a0 = std::min(a0, g.xtab[xo + 3 * c0[l + 1]]);
-                        a1 = std::max(a1, g.xtab[xo + 3 * std::min(c1[l + 1] | 3, wn - 1) + 1]);
-                    }
-                    c0[l] = a0 & ~3;
-                    c1[l] = std::min(w - 1, a1 | 3);
-                    int* e = &ct[((size_t)t * L + l) * 4];
-                    e[0] = c0[l];
-                    e[1] = c1[l];
-                    e[2] = O(l, t);
-                    e[3] = O(l, t + 1);
-                    pitch[l] = std::max(pitch[l], ((c1[l] - c0[l] + 1 + 15) & ~15) + 16);
-                }
-            }
-        };
-        for (int which = 0; which < 2 && groups_ok; ++which) {
-            const char* be = std::getenv(which == 0 ? "ORBFE_ROLL_BANDS" : "ORBFE_ROLL_BANDS_SMALL");
-            const char* ce = std::getenv(which == 0 ? "ORBFE_ROLL_CHUNK" : "ORBFE_ROLL_CHUNK_SMALL");
-            const char* te = std::getenv(which == 0 ? "ORBFE_ROLL_COLS" : "ORBFE_ROLL_COLS_SMALL");
-            // large batches: ~180 level-0 rows per band (1080p: 6 bands); small ones: thin
-            // bands of one column tile for latency
-            int nb = be ? std::atoi(be) : (which == 0 ? std::max(1, std::min(16, (h0 + 179) / 180))
-                                                      : std::max(1, std::min(std::min(64, htop), h0 / 24)));
-            nb = std::max(1, std::min(nb, htop));
-            std::vector<int> rbt;
-            size_t lds_unused;
-            int u1, u2, u3;
-            plan_bands(nb, rbt, lds_unused, u1, u2, u3);
-            auto B4 = [&](int b, int l, int k) { return rbt[((size_t)b * L + l) * 4 + k]; };
-            auto y0 = [&](int l, int r) { return g.ytab[g.yoff[l] + 3 * r]; };
-            auto y1 = [&](int l, int r) { return g.ytab[g.yoff[l] + 3 * r + 1]; };
-            // the kernel's rule for a step of C0 level-0 rows: every step's made rows, each
-            // ring's rows, the rows made per step at most
-            struct Sim {
-                int S = 1, ymax = 1, R[kMaxLevels] = {};
-                std::vector<int> sched;
-                bool ok = true;
-            };
-            auto simulate = [&](int C0) {
-                Sim m;
-                for (int b = 0; b < nb; ++b)
-                    m.S = std::max(m.S, (B4(b, 0, 1) - B4(b, 0, 0) + 1 + C0 - 1) / C0);
-                m.sched.assign((size_t)nb * m.S * L, 0);
-                for (int b = 0; b < nb && m.ok; ++b) {
-                    int e[kMaxLevels], ep[kMaxLevels];
-                    for (int l = 0; l < L; ++l) e[l] = B4(b, l, 0);
-                    for (int st = 0; st < m.S; ++st) {
-                        for (int l = 0; l < L; ++l) ep[l] = e[l];
-                        e[0] = std::min(B4(b, 0, 0) + (st + 1) * C0, B4(b, 0, 1) + 1);
-                        int made = 0;
-                        for (int l = 1; l < L; ++l) {
-                            int r = e[l];
-                            while (r <= B4(b, l, 1) && y1(l, r) < e[l - 1]) ++r;
-                            e[l] = r;
-                            made += e[l] - ep[l];
-                        }
-                        m.ymax = std::max(m.ymax, made);
-                        for (int l = 0; l + 1 < L; ++l) {
-                            // rows of level l the ring must hold during the step
-                            const int need = ep[l + 1] <= B4(b, l + 1, 1) ? y0(l + 1, ep[l + 1]) : e[l];
-                            m.R[l] = std::max(m.R[l], e[l] - std::min(need, ep[l]));
-                        }
-                        for (int l = 0; l < L; ++l) m.sched[((size_t)b * m.S + st) * L + l] = e[l];
-                    }
-                    for (int l = 0; l < L; ++l) m.ok = m.ok && e[l] == B4(b, l, 1) + 1;  // every row made
-                }
-                for (int l = 0; l + 1 < L; ++l) m.R[l] = std::max(m.R[l], 2);
-                return m;
-            };
-            auto lds_of = [&](const Sim& m, const int (&pitch)[kMaxLevels]) {
-                size_t off = 0;
-                for (int l = 0; l + 1 < L; ++l) off += ((size_t)m.R[l] * pitch[l] + 15) & ~(size_t)15;
-                return off + (size_t)m.ymax * 16;
-            };
-            std::vector<std::pair<int, int>> cand;  // (column tiles, rows per step)
-            // column tiles only on request (ORBFE_ROLL_COLS): at 1080p 2-4 tiles per band
-            // measured 1.76-2.76 ms per 256 frames against one tile's 1.34
-            const int nct_max = 1;
-            for (int C0 : {32, 24, 16, 8})  // the tallest step first, then the fewest tiles
-                for (int nct = te ? std::atoi(te) : 1; nct <= (te ? std::atoi(te) : nct_max); ++nct)
-                    if (ce ? C0 == 32 : (which == 0 || C0 == 8)) cand.emplace_back(std::max(1, nct), ce ? std::atoi(ce) : C0);
-            int pick = -1;
-            std::vector<Sim> sims(cand.size());
-            std::vector<std::vector<int>> cts(cand.size());
-            std::vector<std::array<int, kMaxLevels>> pitches(cand.size());
-            for (size_t k = 0; k < cand.size() && pick < 0; ++k) {
-                int pitch[kMaxLevels];
-                plan_cols(cand[k].first, cts[k], pitch);
-                for (int l = 0; l < L; ++l) pitches[k][l] = pitch[l];
-                const int cpr0 = (pitch[0] - 16) >> 4;  // level-0 chunks per tile row
-                const int C0 = std::max(2, std::min(cand[k].second, (kPyrRollPre * kPyrBlockSize) / std::max(cpr0, 1)));
-                cand[k].second = C0;
-                sims[k] = simulate(C0);
-                bool groups = true;  // a tile's groups of every level fit one thread each
-                for (int t = 0; t < cand[k].first; ++t)
-                    for (int l = 1; l < L; ++l) {
-                        const int* e = &cts[k][((size_t)t * L + l) * 4];
-                        groups = groups && ((e[1] - e[0] + 4) >> 2) <= kPyrBlockSize;
-                    }
-                const size_t lds = lds_of(sims[k], pitch);
-                const bool ok = sims[k].ok && groups && sims[k].ymax <= kPyrBlockSize && lds <= 160 * 1024 &&
-                                C0 * cpr0 <= kPyrRollPre * kPyrBlockSize;
-                if (ok) pick = (int)k;
-            }
-            g.roll_ok[which] = pick >= 0;
-            if (!g.roll_ok[which]) continue;
-            const Sim& m = sims[pick];
-            const int S = m.S, nct = cand[pick].first;
-            size_t off = 0;
-            for (int l = 0; l < L; ++l) g.roll_pitch[which][l] = pitches[pick][l];
-            for (int l = 0; l + 1 < L; ++l) {
-                g.roll_ring_rows[which][l] = m.R[l];
-                g.roll_ring_off[which][l] = (int)off;
-                off += ((size_t)m.R[l] * g.roll_pitch[which][l] + 15) & ~(size_t)15;
-            }
-            g.roll_ydesc[which] = (int)off;
-            g.roll_lds[which] = off + (size_t)m.ymax * 16;
-            // every step's row descriptors (the kernel's LDS offsets of the two source rows in
-            // the ring below, the coefficients, the row's own ring offset)
-            std::vector<int> ydoff((size_t)nb * (S + 1)), ydtab;
-            for (int b = 0; b < nb; ++b) {
-                for (int st = 0; st < S; ++st) {
-                    ydoff[(size_t)b * (S + 1) + st] = (int)(ydtab.size() / 4);
-                    for (int l = 1; l < L; ++l) {
-                        const int r0 = st ? m.sched[((size_t)b * S + st - 1) * L + l] : B4(b, l, 0);
-                        const int r1 = m.sched[((size_t)b * S + st) * L + l];
-                        const int so = g.roll_ring_off[which][l - 1], ps = g.roll_pitch[which][l - 1];
-                        const int R0 = m.R[l - 1];
-                        for (int r = r0; r < r1; ++r) {
-                            const int* yy = &g.ytab[g.yoff[l] + 3 * r];
-                            ydtab.push_back(so + (yy[0] % R0) * ps);
-                            ydtab.push_back(so + (yy[1] % R0) * ps);
-                            ydtab.push_back(yy[2]);
-                            ydtab.push_back(l + 1 < L ? g.roll_ring_off[which][l] + (r % m.R[l]) * g.roll_pitch[which][l] : 0);
-                        }
-                    }
-                }
-                ydoff[(size_t)b * (S + 1) + S] = (int)(ydtab.size() / 4);
-            }
-            g.roll_bands[which] = nb;
-            g.roll_cols[which] = nct;
-            g.roll_steps[which] = S;
-            while (g.ptab.size() % 4) g.ptab.push_back(0u);
-            g.roll_band_off[which] = (int)(g.ptab.size() / 4);
-            for (int v : rbt) g.ptab.push_back((uint32_t)v);
-            g.roll_col_off[which] = (int)(g.ptab.size() / 4);
-            for (int v : cts[pick]) g.ptab.push_back((uint32_t)v);
-            g.roll_sched_off[which] = (int)g.ptab.size();
-            for (int v : m.sched) g.ptab.push_back((uint32_t)v);
-            g.roll_ydoff_off[which] = (int)g.ptab.size();
-            for (int v : ydoff) g.ptab.push_back((uint32_t)v);
-            while (g.ptab.size() % 4) g.ptab.push_back(0u);
-            g.roll_ydtab_off[which] = (int)(g.ptab.size() / 4);
-            for (int v : ydtab) g.ptab.push_back((uint32_t)v);
-        }
     }
     int rmax = 7, cmax = 7;
     for (const CellDesc& c : g.cells) {
@@ -4583,53 +3323,6 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
     if ((long long)rmax * g.roi_pitch >= 65536) return ORBFE_ERR_UNSUPPORTED;
     g.fast_lds = (size_t)rmax * g.roi_pitch + (((rmax - 4) * g.roi_pitch + 15) & ~15) +
                  2 * (size_t)g.cand_max + 16 + 128;  // + a trash slot per lane
-    // fast_strip_kernel runs: each cell row (cells of one level with one y0, consecutive in
-    // g.cells) split greedily into runs of 8, 4, 2 or 1 cells (so 64 / gpr rows per sweep keep
-    // ~97 % of the pre-test lanes busy) whose pre-test groups fit a wave (gpr <= 64) and whose
-    // ROI fits kChunkP bytes
-    g.chunks.clear();
-    int crows = 7;
-    for (size_t i = 0; i < g.cells.size();) {
-        size_t e = i + 1;
-        while (e < g.cells.size() && g.cells[e].level == g.cells[i].level && g.cells[e].y0 == g.cells[i].y0)
-            ++e;
-        for (size_t a = i; a < e;) {
-            FastChunk ch{};
-            for (int k = kChunkCells; k >= 1; k >>= 1) {
-                const size_t b = a + (size_t)k;
-                if (b > e) continue;
-                const CellDesc& c0 = g.cells[a];
-                ch = FastChunk{};
-                ch.level = c0.level;
-                ch.y0 = c0.y0;
-                ch.nr = c0.y1 - c0.y0 - 6;
-                ch.x0a = c0.x0 & ~3;
-                ch.roi_w = g.cells[b - 1].x1 - ch.x0a;
-                ch.X0 = c0.x0 - ch.x0a + 3;
-                ch.nc = g.cells[b - 1].x1 - c0.x0 - 6;
-                ch.g0 = ch.X0 >> 2;
-                ch.gpr = ch.nc > 0 ? ((ch.X0 + ch.nc - 1) >> 2) - ch.g0 + 1 : 1;
-                ch.cell0 = (int)a;
-                ch.ncell = k;
-                if ((ch.gpr <= 64 && ch.roi_w <= kChunkP) || k == 1) break;
-            }
-            if (ch.gpr > 64 || ch.roi_w > kChunkP) return ORBFE_ERR_UNSUPPORTED;  // a cell > 59 px
-            ch.nq = (ch.roi_w + 15) >> 4;
-            ch.inv_nq = 0xffffffffu / (unsigned)ch.nq + 1u;
-            for (int j = 0; j < ch.ncell; ++j) ch.cs[j] = g.cells[a + j].x0 - g.cells[a].x0;
-            ch.cs[ch.ncell] = std::max(ch.nc, 0);
-            crows = std::max(crows, ch.nr + 6);
-            g.chunks.push_back(ch);
-            a += (size_t)ch.ncell;
-        }
-        i = e;
-    }
-    // carve: ROI rows | score plane (rows -1 .. nr) | bitmap | column -> cell table | per-cell
-    // counts | 4 per-wave survivor lists (+ trash) | 4 corner lists
-    g.chunk_rows = crows;
-    g.chunk_lds = (size_t)crows * kChunkP + (size_t)(crows - 4) * kChunkP +
-                  (((size_t)(crows - 6) * kChunkBmW * 4 + 15) & ~(size_t)15) + kChunkP + 64 +
-                  (size_t)(kChunkBlock / 64) * ((kChunkList + 64) * 2 + kChunkClist * 2);
     g.geo.key_total = keys;
     blur_items(g.geo, g.bitems);
     g.geo.out_total = out;
@@ -4652,12 +3345,6 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
 
 }  // namespace orbfe
 
-#ifdef ORBFE_FAST_TIMING
-extern "C" int orbfe_debug_fast_timing(long long* out, int n) {
-    n = n < 64 * 160 * 16 ? n : 64 * 160 * 16;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(orbfe::g_fast_t), (size_t)n * sizeof(long long)) == hipSuccess ? 0 : -3;
-}
-#endif
 
 #ifdef ORBFE_OCT_TIMING
 extern "C" int orbfe_debug_oct_timing(long long* out, int n) {

@@ -77,11 +77,6 @@ struct ResizeArgs {
     const int* yt;
     int simd_xb;           // x86 arithmetic: columns [0, simd_xb) use the SSE2 rounding (H5)
     const uint4* gtab;     // resize_kernel: the level's pyramid_kernel column-group table, or null
-    // resize_blur_kernel: the blurred level, its x86 SIMD-body bound (H6), taps, LDS offset of E
-    LevelPtr bdst;
-    int blur_xb;
-    int taps[4];
-    int lds_e;
 };
 
 // resize2_kernel: levels l and l + 1 in one launch, tiles of level l + 1 (see the kernel)
@@ -102,28 +97,6 @@ struct Resize2Args {
     int xb_m, xb_d;                     // x86 SIMD-body bounds of levels l, l + 1
 };
 
-// resizeN_kernel: levels l .. l + n - 1 in one launch (n = 3 or 4), tiles of the last level;
-// the n - 1 levels before it are made in LDS region by region (see the kernel)
-constexpr int kRsNMax = 4;
-struct ResizeNArgs {
-    LevelPtr src;                       // level l - 1 (staged)
-    int sw;                             // its width
-    int n;                              // levels made
-    LevelPtr lv[kRsNMax];               // levels l .. l + n - 1
-    int w[kRsNMax];
-    int dh;                             // rows of the last level
-    const int* yt[kRsNMax];             // each made level's y / x tables (rows / columns of the level below)
-    const int* xt[kRsNMax];
-    const uint4* gtab[kRsNMax];         // column-group tables
-    int xb[kRsNMax];                    // x86 SIMD-body bounds
-    int pitch[kRsNMax];                 // LDS pitch of the staged level (index 0 .. n - 1: made
-    int lofs[kRsNMax];                  // level k - 1 at lofs[k]; index 0 = the staged level)
-    int tiles_x;
-    // per tile, per level k < n - 1: {computed rows first, last, columns first, last (4-aligned
-    // start)} and {own rows [y0, y1), own columns [x0, x1)}
-    const int4* tiles;
-};
-
 struct PyrArgs {
     LevelPtr src;                  // level 0
     LevelPtr l0_copy;              // base != null: each band also writes its level-0 rows here
@@ -137,19 +110,6 @@ struct PyrArgs {
     const uint4* gtab[kMaxLevels]; // per level >= 1: 3 uint4 per column group
     const int* yt[kMaxLevels];     // per level >= 1: the resize y table
     int simd_xb[kMaxLevels];
-    // pyramid_roll_kernel: the band streams down its rows in steps (about `chunk` level-0 rows
-    // each); level l < L-1 keeps its rows in an LDS ring of ring_rows[l] rows at ring_off[l];
-    // sched[(band * nsteps + step) * L + l] = the level's rows made once the step is done
-    // (exclusive end row); row descriptors of a step at ydesc (4 ints per row)
-    const int* sched;
-    const int* ydoff;              // [band][step 0 .. nsteps]: start of the step's descriptors
-    const int4* ydtab;
-    int nsteps, ydesc;
-    int ring_rows[kMaxLevels], ring_off[kMaxLevels];
-    // column tiles: blockIdx.x = band * ncols + tile; cols[tile * nlevels + l] = {first, last
-    // computed column, own columns [z, w)}; lp[] is then the rings' row pitch
-    const int4* cols;
-    int ncols;
 };
 
 struct ResizeTailArgs {
@@ -165,29 +125,7 @@ struct ResizeTailArgs {
     int simd_xb[kMaxLevels];      // per tail level, as ResizeArgs::simd_xb
 };
 
-// fast_strip_kernel: one workgroup per run of <= kChunkCells consecutive cells of one cell row
-// (SURVEY §7 step 4's layout).  The ROI is every row of the cell row over the run's columns,
-// staged once at the pitch kChunkP; candidate columns c = 0 .. nc - 1 are level columns
-// x0a + X0 + c, candidate rows r = 0 .. nr - 1 level rows y0 + 3 + r.
-constexpr int kChunkP = 272;       // LDS row pitch (ROI rows <= 272 bytes)
-constexpr int kChunkCells = 8;     // cells per run
-constexpr int kChunkBlock = 256;   // 4 waves
-constexpr int kChunkList = 384;    // per-wave survivor list entries (+ 64 trash slots)
-constexpr int kChunkBmW = 11;      // corner-bitmap dwords per candidate row (3-dword windows)
-struct FastChunk {
-    int level;
-    int y0, nr;                    // ROI top row (level coords) = the cells' y0; candidate rows
-    int x0a, roi_w;                // ROI left column (4-byte aligned) and bytes per ROI row
-    int X0, nc;                    // ROI column of candidate column 0 (shift + 3); candidate columns
-    int g0, gpr;                   // pre-test groups: ROI dword of group 0, groups per row
-    int nq;                        // 16-byte loads per ROI row
-    unsigned inv_nq;               // umulhi(i, inv_nq) = i / nq (nq > 1; wraps to 0 for nq = 1)
-    int cell0, ncell;              // the run's cells
-    int cs[kChunkCells + 1];       // cell j's candidate columns [cs[j], cs[j + 1])
-};
-
 struct FastArgs {
-    const FastChunk* chunks;       // fast_strip_kernel
     const CellDesc* cells;
     int ncells;
     long long cell_cap_total;
@@ -291,9 +229,6 @@ struct Plan {
     int oct_keys = 0;      // LDS key capacity of the oct-tree kernel
     int roi_pitch = 0, roi_rows = 0, cand_max = 0;
     size_t fast_lds = 0;
-    std::vector<FastChunk> chunks;  // fast_strip_kernel runs of cells
-    int chunk_rows = 0;             // its LDS carve: ROI rows of the tallest run
-    size_t chunk_lds = 0;
     int rs_tiles_x[kMaxLevels] = {}, rs_tiles[kMaxLevels] = {}, rs_pitch[kMaxLevels] = {};
     size_t rs_lds[kMaxLevels] = {};
     // resize2_kernel plans for the level pairs (l, l + 1): tile table offset (int4 units in ptab)
@@ -301,14 +236,6 @@ struct Plan {
     int rs2_tiles_x[kMaxLevels] = {}, rs2_tiles[kMaxLevels] = {}, rs2_off[kMaxLevels] = {};
     int rs2_pa[kMaxLevels] = {}, rs2_pb[kMaxLevels] = {}, rs2_bofs[kMaxLevels] = {};
     size_t rs2_lds[kMaxLevels] = {};
-    // resizeN_kernel chains starting at level l: levels made (0 = none), tiles, table, LDS
-    int rsn_n[kMaxLevels] = {};
-    int rsn_tiles_x[kMaxLevels] = {}, rsn_tiles[kMaxLevels] = {}, rsn_off[kMaxLevels] = {};
-    int rsn_pitch[kMaxLevels][kRsNMax] = {}, rsn_lofs[kMaxLevels][kRsNMax] = {};
-    size_t rsn_lds[kMaxLevels] = {};
-    // resize_blur_kernel: staging pitch / LDS bytes, offset of its E image
-    int rb_pitch[kMaxLevels] = {}, rb_lds_e[kMaxLevels] = {};
-    size_t rb_lds[kMaxLevels] = {};
     int tail_start = kMaxLevels;  // levels >= tail_start come from resize_tail_kernel
     // pyramid_kernel: column-group tables (all levels) then the band tables of the two band
     // plans (batches >= kTailMinFrames / smaller), in one device table of u32
@@ -319,14 +246,6 @@ struct Plan {
     int band_off[2] = {}, nbands[2] = {}, pyr_bufb[2] = {}, pyr_ybuf[2] = {}, pyr_ymax[2] = {};
     int pyr_lp[kMaxLevels] = {};
     size_t pyr_lds[2] = {};
-    // pyramid_roll_kernel plans (same two batch classes): bands, steps, rings, LDS bytes
-    bool roll_ok[2] = {false, false};
-    int roll_bands[2] = {}, roll_steps[2] = {}, roll_band_off[2] = {}, roll_sched_off[2] = {};
-    int roll_ydoff_off[2] = {}, roll_ydtab_off[2] = {};
-    int roll_ring_rows[2][kMaxLevels] = {}, roll_ring_off[2][kMaxLevels] = {}, roll_ydesc[2] = {};
-    int roll_cols[2] = {1, 1}, roll_col_off[2] = {};   // column tiles per band, their table
-    int roll_pitch[2][kMaxLevels] = {};                // ring row pitch per level
-    size_t roll_lds[2] = {};
 };
 
 int make_tables(const orbfe_params& p, HostTables& t);
@@ -336,13 +255,9 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g);
 __global__ void level0_kernel(Level0Args);
 template <bool kX86> __global__ void resize_kernel(ResizeArgs);
 template <bool kX86> __global__ void resize_tail_kernel(ResizeTailArgs);
-template <bool kX86> __global__ void resize_blur_kernel(ResizeArgs);
 template <bool kX86> __global__ void pyramid_kernel(PyrArgs);
-template <bool kX86> __global__ void pyramid_roll_kernel(PyrArgs);
 template <bool kX86> __global__ void resize2_kernel(Resize2Args);
-template <bool kX86> __global__ void resizeN_kernel(ResizeNArgs);
 template <int kP> __global__ void fast_kernel(FastArgs);
-__global__ void fast_strip_kernel(FastArgs);
 constexpr int kFastPitch = 48;  // fast_kernel<kFastPitch>: ROI pitch known at compile time
 template <int BLK> __global__ void octree_kernel(OctArgs);
 template <bool kX86> __global__ void blur_mfma_kernel(BlurArgs);
@@ -362,7 +277,6 @@ extern __constant__ int c_umax[16];
 constexpr int kPyrLdsCapKB = 80;
 constexpr int kPyrBlockSize = 1024;
 constexpr int kPyrSmallRows = 12;
-constexpr int kPyrRollPre = 4;  // pyramid_roll_kernel: level-0 chunks in flight per thread
 // band plans whose rows computed exceed the pyramid's by more than this use the per-level
 // kernels instead (large batches: throughput; small ones: latency)
 constexpr double kPyrMaxWork = 1.25, kPyrMaxWorkSmall = 3.0;

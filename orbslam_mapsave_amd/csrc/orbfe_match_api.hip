@@ -85,33 +85,42 @@ struct orbfe_matcher {
     bool bf_pre = !(std::getenv("ORBFE_BF_PRE") && std::strcmp(std::getenv("ORBFE_BF_PRE"), "0") == 0);
     // the shared reference set as FP4 fragments (bf_expand_kernel), one buffer per stream the
     // batch form was called on (calls on different streams may overlap), at most kBfStreams of
-    // them: a call on another stream takes the least recently used one after a device
-    // synchronisation (a caller creating a stream per call, or a destroyed stream whose handle is
-    // reused, cannot grow the set or find a buffer another stream still reads)
+    // them.  Each buffer carries an event recorded behind the last launch that reads it; a call
+    // on another stream takes the least recently used buffer once that event has completed — a
+    // wait on that one buffer's readers, not on the device (a caller creating a stream per call,
+    // or a destroyed stream whose handle is reused, cannot grow the set or find a buffer another
+    // stream still reads; the event stays valid after its stream is destroyed).
     static constexpr int kBfStreams = 4;
-    std::map<hipStream_t, DevBuf> bf_e;
-    std::map<hipStream_t, unsigned long long> bf_e_used;
+    struct BfSlot {
+        DevBuf buf;
+        hipEvent_t done = nullptr;  // recorded after the last launch reading buf
+        unsigned long long used = 0;
+    };
+    std::map<hipStream_t, BfSlot> bf_e;
     unsigned long long bf_e_clock = 0;
-    DevBuf* bf_buffer(hipStream_t s, int* st) {
+    BfSlot* bf_buffer(hipStream_t s, int* st) {
         *st = ORBFE_OK;
         auto it = bf_e.find(s);
         if (it == bf_e.end() && (int)bf_e.size() >= kBfStreams) {
-            hipStream_t lru = bf_e_used.begin()->first;
-            for (auto& kv : bf_e_used)
-                if (kv.second < bf_e_used[lru]) lru = kv.first;
-            if (hipDeviceSynchronize() != hipSuccess) {
+            auto lru = bf_e.begin();
+            for (auto i = bf_e.begin(); i != bf_e.end(); ++i)
+                if (i->second.used < lru->second.used) lru = i;
+            if (lru->second.done && hipEventSynchronize(lru->second.done) != hipSuccess) {
                 *st = ORBFE_ERR_HIP;
                 return nullptr;
             }
-            DevBuf moved = bf_e[lru];  // reuse the allocation for the new stream
+            BfSlot moved = lru->second;  // reuse the allocation and the event for the new stream
             bf_e.erase(lru);
-            bf_e_used.erase(lru);
-            bf_e[s] = moved;
-            it = bf_e.find(s);
+            it = bf_e.emplace(s, moved).first;
         }
-        DevBuf& e = bf_e[s];
-        bf_e_used[s] = ++bf_e_clock;
-        if ((*st = e.ensure((size_t)kBfMaxTiles * 8 * kBfRefs * sizeof(i32x4)))) return nullptr;
+        BfSlot& e = bf_e[s];
+        e.used = ++bf_e_clock;
+        if (!e.done && hipEventCreateWithFlags(&e.done, hipEventDisableTiming) != hipSuccess) {
+            e.done = nullptr;
+            *st = ORBFE_ERR_HIP;
+            return nullptr;
+        }
+        if ((*st = e.buf.ensure((size_t)kBfMaxTiles * 8 * kBfRefs * sizeof(i32x4)))) return nullptr;
         return &e;
     }
 
@@ -123,10 +132,9 @@ struct orbfe_matcher {
                           &g_t0, &g_t1, &g_t2, &g_dec, &g_chg, &g_last, &g_bins, &g_hist, &done_ctr,
                           &b1_rec, &b1_cnt})
             b->release();
-        for (auto& kv : bf_e) kv.second.release();
-        for (SbpGraph& sg : sbp_graph) {
-            if (sg.exec) hipGraphExecDestroy(sg.exec);
-            if (sg.graph) hipGraphDestroy(sg.graph);
+        for (auto& kv : bf_e) {
+            kv.second.buf.release();
+            if (kv.second.done) hipEventDestroy(kv.second.done);
         }
         prof.release();
         if (own) hipStreamDestroy(own);
@@ -141,24 +149,6 @@ struct orbfe_matcher {
     // accept kernel's last workgroup (null: read back by a D2H copy)
     int* stat_host = nullptr;
     int* stat_dev = nullptr;
-    // ORBFE_SBP_GRAPH=1: SearchLocalPoints' fast path as one HIP graph per form (kPre = 0/1):
-    // the seven launches built once as a chain of kernel nodes; a later call whose arguments,
-    // grids or LDS size differ rewrites only those nodes in the instantiated graph
-    // (hipGraphExecKernelNodeSetParams), so a new pose or frame costs no re-instantiation.
-    // Measured slower than the plain launches (c5 0.104 vs 0.095 ms per call: the kernels run
-    // back to back either way, the replay costs more host time), so off.
-    static constexpr int kSbpNodes = 7;
-    struct SbpGraph {
-        hipGraph_t graph = nullptr;
-        hipGraphExec_t exec = nullptr;
-        hipGraphNode_t node[kSbpNodes] = {};
-        SbpFusedArgs fu{};
-        GreedyArgs g{};
-        dim3 grid[3];
-        size_t shm = 0;
-    };
-    SbpGraph sbp_graph[2];
-    bool sbp_graph_off = !(std::getenv("ORBFE_SBP_GRAPH") && std::strcmp(std::getenv("ORBFE_SBP_GRAPH"), "1") == 0);
     uint8_t* pin = nullptr;
     uint8_t* pin_dev = nullptr;  // the staging buffer's device-mapped address (null: DMA path)
     size_t pin_cap = 0, pin_used = 0;
@@ -520,79 +510,6 @@ int guarded(orbfe_matcher* m, F&& f) {
         return ORBFE_ERR_HIP;
     }
 }
-// sbp_local_fast's launches through the matcher's graph for this form: the fused kernel (grid[0],
-// shm bytes of LDS), rounds - 1 greedy rounds (grid[1]) and the last round + acceptances
-// (grid[2]).  Built on first use; afterwards only the nodes whose arguments or grids changed are
-// rewritten.  false: not launched (graphs off, or the graph could not be built or updated; the
-// caller then launches the kernels itself).
-template <bool kPre>
-bool sbp_local_graph(orbfe_matcher* m, const SbpFusedArgs& fu, const GreedyArgs& g,
-                     const dim3 grid[3], size_t shm, int rounds) {
-    if (m->sbp_graph_off) return false;
-    orbfe_matcher::SbpGraph& G = m->sbp_graph[kPre ? 1 : 0];
-    SbpFusedArgs fu_arg = fu;
-    GreedyArgs g_arg = g;
-    int r_arg[orbfe_matcher::kSbpNodes];
-    void* fu_params[1] = {&fu_arg};
-    void* g_params[orbfe_matcher::kSbpNodes][2];
-    hipKernelNodeParams p[orbfe_matcher::kSbpNodes];
-    for (int k = 0; k < rounds + 1; ++k) {
-        p[k] = hipKernelNodeParams{};
-        if (k == 0) {
-            p[k].func = reinterpret_cast<void*>(&sbp_local_fused_kernel<kPre>);
-            p[k].gridDim = grid[0];
-            p[k].blockDim = dim3(1024);
-            p[k].sharedMemBytes = (unsigned int)shm;
-            p[k].kernelParams = fu_params;
-            continue;
-        }
-        r_arg[k] = k - 1;
-        g_params[k][0] = &g_arg;
-        g_params[k][1] = &r_arg[k];
-        p[k].func = k < rounds ? reinterpret_cast<void*>(&greedy_round_kernel<true>)
-                               : reinterpret_cast<void*>(&greedy_accept_kernel<true>);
-        p[k].gridDim = k < rounds ? grid[1] : grid[2];
-        p[k].blockDim = dim3(kGreedyBlock);
-        p[k].kernelParams = g_params[k];
-    }
-    auto same_dim = [](const dim3& a, const dim3& b) { return a.x == b.x && a.y == b.y && a.z == b.z; };
-    if (!G.exec) {
-        bool ok = hipGraphCreate(&G.graph, 0) == hipSuccess;
-        for (int k = 0; ok && k < rounds + 1; ++k)
-            ok = hipGraphAddKernelNode(&G.node[k], G.graph, k ? &G.node[k - 1] : nullptr, k ? 1 : 0,
-                                       &p[k]) == hipSuccess;
-        ok = ok && hipGraphInstantiate(&G.exec, G.graph, nullptr, nullptr, 0) == hipSuccess;
-        if (!ok) {
-            (void)hipGetLastError();
-            if (G.exec) hipGraphExecDestroy(G.exec);
-            if (G.graph) hipGraphDestroy(G.graph);
-            G = orbfe_matcher::SbpGraph{};
-            m->sbp_graph_off = true;
-            return false;
-        }
-    } else {
-        bool ok = true;
-        if (std::memcmp(&G.fu, &fu, sizeof(fu)) != 0 || !same_dim(G.grid[0], grid[0]) || G.shm != shm)
-            ok = hipGraphExecKernelNodeSetParams(G.exec, G.node[0], &p[0]) == hipSuccess;
-        const bool g_same = std::memcmp(&G.g, &g, sizeof(g)) == 0;
-        for (int k = 1; ok && k < rounds + 1; ++k)
-            if (!g_same || !same_dim(G.grid[k < rounds ? 1 : 2], p[k].gridDim))
-                ok = hipGraphExecKernelNodeSetParams(G.exec, G.node[k], &p[k]) == hipSuccess;
-        if (!ok) {  // drop the graph (rebuilt on the next call); this call launches directly
-            (void)hipGetLastError();
-            hipGraphExecDestroy(G.exec);
-            hipGraphDestroy(G.graph);
-            G = orbfe_matcher::SbpGraph{};
-            return false;
-        }
-    }
-    G.fu = fu;
-    G.g = g;
-    for (int k = 0; k < 3; ++k) G.grid[k] = grid[k];
-    G.shm = shm;
-    return hipGraphLaunch(G.exec, m->stream) == hipSuccess;
-}
-
 // SearchLocalPoints' fast path (frames of <= kSbpFixKp keypoints): the grid, ONE kernel for
 // isInFrustum (kPre: its outputs already resident) + candidates (fixed per-point slots) + the
 // greedy initialisation, kBlindRounds rounds launched without looking (a round after a change-free
@@ -679,17 +596,14 @@ int sbp_local_fast(orbfe_matcher* m, const orbfe_frame_view* frame, const Frustu
     if (m->stat_host)  // "not converged" until the last workgroup writes it
         for (int k = 0; k < 6; ++k) m->stat_host[k] = k == 4 ? -1 : 0;
     const int rblocks = std::max(1, (std::max(std::max(M, N), 32) + kGreedyBlock - 1) / kGreedyBlock);
-    static_assert(kBlindRounds + 1 == orbfe_matcher::kSbpNodes, "one node per launch");
     const dim3 grid[3] = {dim3(fblocks), dim3(rblocks), dim3((M + kGreedyBlock - 1) / kGreedyBlock)};
     const size_t shm = (size_t)N * 32;
-    if (!sbp_local_graph<kPre>(m, fu, g, grid, shm, kBlindRounds)) {
-        hipLaunchKernelGGL(sbp_local_fused_kernel<kPre>, grid[0], dim3(1024), shm, m->stream, fu);
-        for (int r = 0; r < kBlindRounds - 1; ++r)
-            hipLaunchKernelGGL(greedy_round_kernel<true>, grid[1], dim3(kGreedyBlock), 0, m->stream, g, r);
-        // the last blind round and the acceptances in one launch
-        hipLaunchKernelGGL(greedy_accept_kernel<true>, grid[2], dim3(kGreedyBlock), 0, m->stream,
-                           g, kBlindRounds - 1);
-    }
+    hipLaunchKernelGGL(sbp_local_fused_kernel<kPre>, grid[0], dim3(1024), shm, m->stream, fu);
+    for (int r = 0; r < kBlindRounds - 1; ++r)
+        hipLaunchKernelGGL(greedy_round_kernel<true>, grid[1], dim3(kGreedyBlock), 0, m->stream, g, r);
+    // the last blind round and the acceptances in one launch
+    hipLaunchKernelGGL(greedy_accept_kernel<true>, grid[2], dim3(kGreedyBlock), 0, m->stream,
+                       g, kBlindRounds - 1);
     ORBFE_HIP(hipGetLastError());
     m->rounds_on_device = false;
     for (int k = 0; k < 6; ++k) host[k] = 0;
@@ -806,15 +720,16 @@ int orbfe_bf_match_batch_device(orbfe_matcher* m, const uint8_t* d_q, size_t q_p
         // fragments once (ORBFE_BF_PRE=0: every workgroup expands it, as for per-entry sets)
         if (r_pitch == 0 && m->bf_kernel == bf_match_fp4_kernel && m->bf_pre) {
             int st;
-            DevBuf* pe = m->bf_buffer(m->stream, &st);
+            orbfe_matcher::BfSlot* pe = m->bf_buffer(m->stream, &st);
             if (!pe) return st;
-            DevBuf& e = *pe;
+            DevBuf& e = pe->buf;
             // its own profiler stage (1): the bench's per-launch figures are the match kernel's
             ORBFE_LAUNCH(m->prof, 1, bf_expand_kernel, dim3(kBfExpandBlocks), dim3(512), 0, m->stream,
                          d_r, d_nr, nb, e.as<i32x4>());
             ORBFE_LAUNCH(m->prof, 0, bf_match_fp4e_kernel, dim3((nq_cap + kBfBlock - 1) / kBfBlock, nb),
                          dim3(kBfBlock), 0, m->stream, d_q, (long long)q_pitch, d_nq, nq_cap, d_r,
                          (long long)r_pitch, d_nr, d_out, (const i32x4*)e.as<i32x4>());
+            ORBFE_HIP(hipEventRecord(pe->done, m->stream));
             ORBFE_HIP(hipGetLastError());
             return ORBFE_OK;
         }

@@ -29,7 +29,7 @@ _lib: C.CDLL | None = None
 EXPORTED = [
     "orbfe_create", "orbfe_destroy", "orbfe_get_levels", "orbfe_get_scale_factor",
     "orbfe_get_scale_tables", "orbfe_get_features_per_level", "orbfe_keypoint_capacity",
-    "orbfe_keypoint_capacity_for", "orbfe_set_arithmetic", "orbfe_get_arithmetic",
+    "orbfe_keypoint_capacity_for", "orbfe_keypoint_capacity_params", "orbfe_set_arithmetic", "orbfe_get_arithmetic",
     "orbfe_get_reference_constants",
     "orbfe_extract", "orbfe_input_buffer", "orbfe_extract_staged", "orbfe_staged_outputs",
     "orbfe_extract_color", "orbfe_human_mask_rect", "orbfe_extract_batch",
@@ -100,6 +100,16 @@ def reference_constants() -> dict:
     _check("orbfe_get_reference_constants", lib().orbfe_get_reference_constants(out))
     return dict(zip(("PATCH_SIZE", "HALF_PATCH_SIZE", "EDGE_THRESHOLD", "TH_HIGH", "TH_LOW",
                      "HISTO_LENGTH"), list(out)))
+
+
+def keypoint_capacity(nfeatures: int, scaleFactor: float, nlevels: int, iniThFAST: int,
+                      minThFAST: int, w: int, h: int) -> int:
+    """Per-frame keypoint capacity at w x h for these extractor parameters, without a handle or
+    a device (orbfe_keypoint_capacity_params): the slab rows an extraction can fill."""
+    p = Params(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
+    c = lib().orbfe_keypoint_capacity_params(C.byref(p), int(w), int(h))
+    _check("orbfe_keypoint_capacity_params", min(c, 0))
+    return c
 
 
 # ORBFE_PIX_* (include/orbfe.h): the cvtColor codes of Tracking::GrabImage*
@@ -371,11 +381,11 @@ class ORBextractor:
         _check("orbfe_profile_read", lib().orbfe_profile_read(self._h, ptr(ms), ptr(n)))
         return {s: (float(ms[i]), int(n[i])) for i, s in enumerate(self.STAGES)}
 
-    PYR_PATHS = ("per_level", "bands", "roll")
+    PYR_PATHS = ("per_level", "bands")
 
     def pyramid_path(self, nframes: int) -> str:
         """The pyramid kernel an extraction of `nframes` frames at the last extracted size takes
-        (orbfe_pyramid_path): "per_level", "bands" or "roll"."""
+        (orbfe_pyramid_path): "per_level" or "bands"."""
         r = lib().orbfe_pyramid_path(self._h, int(nframes))
         _check("orbfe_pyramid_path", r if r < 0 else 0)
         return self.PYR_PATHS[r]

@@ -1,7 +1,9 @@
 """bench.py's own multi-rank launch (`--gpus N` with no WORLD_SIZE: the script starts N rank
 processes before anything touches a GPU) rehearsed on CPU with `--dry-run` (gloo, the config-4
-exchange step on small random slabs): the line reports n_gpus = N, the matches are identical to
-the one-rank run, and a launcher/--gpus mismatch exits non-zero."""
+exchange step at configs[3]'s shape: global batch 256, 32 frames per rank at N = 8, slabs of
+capacity(1920, 1080) rows): for N = 1, 2, 4, 8 the line reports n_gpus = N and the matches of
+every global frame are identical to the one-rank run; a launcher/--gpus mismatch exits
+non-zero."""
 import json
 import os
 import subprocess
@@ -27,12 +29,15 @@ def _line(p):
 
 
 def test_dry_run_spawns_ranks():
-    one = _line(_run("--gpus", "1", "--dry-run", "--steps", "2", "--warmup", "1"))
+    one = _line(_run("--config", "c4", "--gpus", "1", "--dry-run", "--steps", "2", "--warmup", "1"))
     assert one["n_gpus"] == 1 and one["dry_run"]
-    for n in (2, 4):
-        got = _line(_run("--gpus", str(n), "--dry-run", "--steps", "2", "--warmup", "1"))
+    assert one["config"]["global_batch"] == 256
+    for n in (2, 4, 8):
+        got = _line(_run("--config", "c4", "--gpus", str(n), "--dry-run", "--steps", "2",
+                         "--warmup", "1"))
         assert got["n_gpus"] == n
-        assert got["config"]["global_batch"] == 8
+        assert got["config"]["global_batch"] == 256
+        assert got["config"]["frames_per_rank_per_step"] == 256 // n
         assert got["match_checksum"] == one["match_checksum"]
         assert got["value"] > 0 and got["steps"] == 2
 

@@ -51,14 +51,11 @@ def test_fast_lists_with_flushes(kind, ini, mn):
 @pytest.mark.parametrize("size,ini,mn", [((1280, 720), 20, 7), ((331, 247), 32, 7), ((700, 500), 20, 7),
                                          ((1000, 333), 32, 7), ((96, 80), 20, 7), ((1920, 1080), 32, 7),
                                          ((853, 481), 12, 3)])
-@pytest.mark.parametrize("strip", ["0", "1"])
-def test_fast_strip_runs(size, ini, mn, strip, monkeypatch):
-    """Both FAST kernels at frame sizes whose cell rows end in odd cells (a last cell 2-9 px
-    wide; for fast_strip_kernel (ORBFE_FAST_STRIP=1) runs of 8 / 4 / 2 / 1 cells, a run of one
-    16-byte ROI load, cells 32-37 px wide): the per-level FAST lists (order included) and the
+def test_fast_odd_cells(size, ini, mn):
+    """FAST at frame sizes whose cell rows end in odd cells (a last cell 2-9 px wide, cells
+    32-37 px wide, ROIs of one 16-byte load): the per-level FAST lists (order included) and the
     keypoints equal the oracle's."""
     from orbslam_mapsave_amd.native import ORBextractor
-    monkeypatch.setenv("ORBFE_FAST_STRIP", strip)
     w, h = size
     img = synthetic_frame(21, w, h)
     p = oracle.params(1000, 1.2, 8, ini, mn)

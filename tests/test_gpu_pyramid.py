@@ -108,26 +108,6 @@ def test_other_scale_factors(sf, nl, monkeypatch):
         e.close()
 
 
-@pytest.mark.parametrize("size,cols", [((1281, 722), "2"), ((643, 481), "3"), ((331, 247), "2")])
-def test_roll_column_tiles_sizes(size, cols, monkeypatch):
-    """Column tiles of the rolling kernel at odd sizes (tile seams on unaligned level widths,
-    the SSE2 body boundary inside a tile): every level of every frame byte-exact."""
-    from orbslam_mapsave_amd.native import ORBextractor
-    monkeypatch.setenv("ORBFE_PYR", "3")
-    monkeypatch.setenv("ORBFE_ROLL_COLS", cols)
-    w, h = size
-    nf = 1500 if w > 1000 else 1000
-    p = oracle.params(nf, 1.2, 8, 20, 7)
-    e = ORBextractor(nf, 1.2, 8, 20, 7, device=0, max_width=w, max_height=h)
-    try:
-        imgs = np.stack([synthetic_frame(13 * w + s, w, h) for s in range(9)])
-        e.extract_batch(imgs)
-        assert e.pyramid_path(9) == "roll"
-        _levels_exact(e, p, imgs[:3], oracle.DEFAULT_VARIANT)
-    finally:
-        e.close()
-
-
 @pytest.mark.parametrize("size,batch,path,env", [((640, 480), 1, "bands", None), ((640, 480), 9, "per_level", None),
                                                  ((640, 480), 9, "bands", "band"),
                                                  ((1920, 1080), 1, "bands", None), ((1920, 1080), 9, "per_level", None)])
@@ -135,7 +115,7 @@ def test_default_paths(size, batch, path, env, monkeypatch):
     """The pyramid path each shape takes by default (the measured choices of DESIGN.md §5e, §5g:
     batches take the per-level kernels, ORBFE_PYR_BATCH=band the band kernel where it plans)."""
     from orbslam_mapsave_amd.native import ORBextractor
-    for v in ("ORBFE_PYR", "ORBFE_ROLL", "ORBFE_ROLL_BANDS", "ORBFE_ROLL_CHUNK", "ORBFE_PYR_BATCH"):
+    for v in ("ORBFE_PYR", "ORBFE_PYR_BATCH"):
         monkeypatch.delenv(v, raising=False)
     if env:
         monkeypatch.setenv("ORBFE_PYR_BATCH", env)
@@ -171,17 +151,17 @@ def test_per_level_path_identical(monkeypatch):
 
 @pytest.mark.parametrize("size", [(640, 480), (1920, 1080), (643, 481), (97, 73)])
 @pytest.mark.parametrize("arith", ["scalar", "x86"])
-@pytest.mark.parametrize("table,chain", [("1", "1"), ("1", "0"), ("0", "1")])
-def test_per_level_kernels_exact(size, arith, table, chain, monkeypatch):
-    """The per-level path (ORBFE_PYR=0; the default at 1920x1080): level pairs per launch
-    (resize2_kernel, default) or chains of 3-4 levels (resizeN_kernel, ORBFE_RSN=1, opt-in),
-    both on the column-group tables; resize_kernel's horizontal pass by byte gathers
+@pytest.mark.parametrize("table,rs2", [("1", "1"), ("1", "0"), ("0", "1")])
+def test_per_level_kernels_exact(size, arith, table, rs2, monkeypatch):
+    """The per-level path (ORBFE_PYR=0; the default for batches): level pairs per launch
+    (resize2_kernel, default) or one level per launch (resize_kernel, ORBFE_RS2=0), on the
+    column-group tables or with resize_kernel's horizontal pass by byte gathers
     (ORBFE_RESIZE_TABLE=0); the one-workgroup tail for batches; every level byte-exact in both
     readings."""
     from orbslam_mapsave_amd.native import ORBextractor
     monkeypatch.setenv("ORBFE_PYR", "0")
     monkeypatch.setenv("ORBFE_RESIZE_TABLE", table)
-    monkeypatch.setenv("ORBFE_RSN", chain)
+    monkeypatch.setenv("ORBFE_RS2", rs2)
     w, h = size
     nf = 2000 if w > 1000 else 1000
     p = oracle.params(nf, 1.2, 8, 20, 7)
@@ -195,57 +175,5 @@ def test_per_level_kernels_exact(size, arith, table, chain, monkeypatch):
         _levels_exact(e, p, imgs[:3], var)
         e(imgs[4])
         _levels_exact(e, p, imgs[4:5], var)
-    finally:
-        e.close()
-
-
-@pytest.mark.parametrize("size", [(1920, 1080), (640, 480), (643, 481), (331, 247), (97, 73), (1281, 722)])
-@pytest.mark.parametrize("batch", [1, 9])
-@pytest.mark.parametrize("arith", ["scalar", "x86"])
-def test_roll_levels_bit_exact(size, batch, arith, monkeypatch):
-    """pyramid_roll_kernel (the one-launch pyramid at any size; opt-in, ORBFE_PYR=3 forces it
-    everywhere): every level of every frame byte-exact against the oracle in both readings,
-    single frames (thin bands) and batches — and the rolling kernel is the one that ran."""
-    from orbslam_mapsave_amd.native import ORBextractor
-    monkeypatch.setenv("ORBFE_PYR", "3")
-    w, h = size
-    nf = 2000 if w > 1000 else 1000
-    p = oracle.params(nf, 1.2, 8, 20, 7)
-    e = ORBextractor(nf, 1.2, 8, 20, 7, device=0, max_width=w, max_height=h)
-    var = oracle.VAR_H5_SSE2 if arith == "x86" else 0
-    e.set_arithmetic(e.ARITH_X86_SIMD if arith == "x86" else e.ARITH_SCALAR)
-    try:
-        imgs = np.stack([synthetic_frame(5 * w + s, w, h) for s in range(batch)])
-        if batch == 1:
-            e(imgs[0])
-        else:
-            e.extract_batch(imgs)
-        assert e.pyramid_path(batch) == "roll"
-        _levels_exact(e, p, imgs[:3], var)
-    finally:
-        e.close()
-
-
-@pytest.mark.parametrize("bands,chunk,cols", [("1", "2", "1"), ("3", "5", "1"), ("7", "16", "1"), ("2", "24", "1"),
-                                              ("2", "16", "2"), ("5", "8", "3"), ("1", "32", "4")])
-def test_roll_plans(bands, chunk, cols, monkeypatch):
-    """Other rolling plans (band counts, level-0 rows per step, column tiles per band: ring
-    sizes, step counts, tile seams and the per-thread chunk bound change) give the same levels
-    and keypoints."""
-    from orbslam_mapsave_amd.native import ORBextractor
-    monkeypatch.setenv("ORBFE_PYR", "3")
-    monkeypatch.setenv("ORBFE_ROLL_BANDS", bands)
-    monkeypatch.setenv("ORBFE_ROLL_CHUNK", chunk)
-    monkeypatch.setenv("ORBFE_ROLL_COLS", cols)
-    p = oracle.params(2000, 1.2, 8, 20, 7)
-    e = ORBextractor(2000, 1.2, 8, 20, 7, device=0, max_width=1920, max_height=1080)
-    try:
-        imgs = np.stack([synthetic_frame(170 + s, 1920, 1080) for s in range(8)])
-        kps, desc, cnt = e.extract_batch(imgs)
-        assert e.pyramid_path(len(imgs)) == "roll"
-        _levels_exact(e, p, imgs[:2], oracle.DEFAULT_VARIANT)
-        okps, odesc = oracle.extract(p, imgs[1])
-        assert kps[1, :cnt[1]].tobytes() == okps.tobytes()
-        assert np.array_equal(desc[1, :cnt[1]], odesc)
     finally:
         e.close()

@@ -87,13 +87,9 @@ def test_gpu_search_local_points(seed, m, th, stereo, zc, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("graph", ["1", "0"])
-def test_gpu_local_points_graph_updates(graph, monkeypatch):
+def test_gpu_local_points_problem_sequence():
     """One matcher through a sequence of different problems (new buffers, map sizes, keypoint
-    counts and thresholds): with the graph (ORBFE_SBP_GRAPH=1) each call after the first rewrites
-    the changed nodes of the instantiated graph (arguments, grids, LDS bytes) instead of
-    re-instantiating it; every call bit-exact against the oracle, and the same with plain launches."""
-    monkeypatch.setenv("ORBFE_SBP_GRAPH", graph)
+    counts and thresholds): every call bit-exact against the oracle."""
     from orbslam_mapsave_amd.native import ORBmatcher
     mt = ORBmatcher(0.8, False, device=0)
     probs = [(0, 50000, 1.0, 1000), (3, 1000, 5.0, 600), (1, 20000, 3.0, 1000), (0, 50000, 1.0, 1000)]

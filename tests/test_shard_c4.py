@@ -1,8 +1,13 @@
 """Config 4's real step function (orbslam_mapsave_amd.shard.PredecessorMatch: all-gather of the
 descriptor slabs, predecessor selection, frame f vs f - 1 match) — the one bench.py --config c4
-runs over RCCL — executed over gloo at world sizes 1, 2 and 4 on oracle-extracted 1920x1080
-@2000-keypoint frames.  SURVEY §4: the rank-sharded results must be byte-identical to the
-single-process run, for every global frame."""
+runs over RCCL — executed over gloo at world sizes 1, 2, 4 and 8 at configs[3]'s shape: a global
+batch of 256 frames (32 per rank at world 8), slabs of capacity(1920, 1080) rows of descriptors
+of oracle-extracted 1920x1080 @2000-keypoint frames.  SURVEY §4: the rank-sharded results must be
+byte-identical to the single-process run, for every global frame.
+
+Eight frames are extracted by the oracle; the other 248 slabs are those eight with each frame's
+descriptors XOR-ed with a per-frame 32-byte mask and its count trimmed by f % 13, so every global
+frame's slab is distinct (a wrong predecessor row cannot match by accident)."""
 import os
 import socket
 
@@ -12,10 +17,15 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from orbslam_mapsave_amd.native import keypoint_capacity
 from orbslam_mapsave_amd.shard import PredecessorMatch, global_frame
 
-GLOBAL = 8     # global batch (the bench's is 256; the step does not depend on it)
-CAP = 2112     # slab capacity (>= any count of these frames)
+GLOBAL = 256   # global batch (BASELINE configs[3])
+BASE = 8       # oracle-extracted frames the slabs derive from
+# slab rows: the keypoint capacity of a 1920 x 1080 frame at 2000 keypoints, as the library
+# plans it (orbfe_keypoint_capacity_params: host arithmetic, no device) — the rows bench.py
+# --config c4 all-gathers per frame
+CAP = keypoint_capacity(2000, 1.2, 8, 32, 7, 1920, 1080)
 
 
 def _free_port():
@@ -26,18 +36,27 @@ def _free_port():
     return port
 
 
-@pytest.fixture(scope="module")
-def slabs():
+def _extract(f):
     import oracle
     from orbslam_mapsave_amd.synth import synthetic_frame
-    p = oracle.params(2000, 1.2, 8, 32, 7)
+    return oracle.extract(oracle.params(2000, 1.2, 8, 32, 7), synthetic_frame(500 + f, 1920, 1080))[1]
+
+
+@pytest.fixture(scope="module")
+def slabs():
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(4) as ex:
+        base = list(ex.map(_extract, range(BASE)))
     desc = np.zeros((GLOBAL, CAP, 32), np.uint8)
     cnt = np.zeros(GLOBAL, np.int32)
+    rng = np.random.default_rng(2024)
     for f in range(GLOBAL):
-        _, d = oracle.extract(p, synthetic_frame(500 + f, 1920, 1080))
+        d = base[f % BASE]
         assert len(d) <= CAP
-        desc[f, :len(d)] = d
-        cnt[f] = len(d)
+        n = len(d) - f % 13
+        mask = rng.integers(0, 256, 32, dtype=np.uint8) if f >= BASE else np.zeros(32, np.uint8)
+        desc[f, :n] = d[:n] ^ mask
+        cnt[f] = n
     return desc, cnt
 
 
@@ -93,9 +112,9 @@ def test_c4_step_identical_across_world_sizes(slabs):
         bi, bd, sd = oracle.bf_match(desc[f, :cnt[f]], desc[p, :cnt[p]])
         got = np.frombuffer(base[f], np.int32).reshape(CAP, 3)[:cnt[f]]
         assert np.array_equal(got, np.stack([bi, bd, sd], 1))
-    for world in (2, 4):
+    for world in (2, 4, 8):
         assert run_world(world, desc, cnt) == base, f"world {world} differs from world 1"
-    # the overlapped exchange: two sub-batches per rank gathered separately (world 4 has one
-    # frame per rank, so one part)
-    for world, parts in ((1, 2), (2, 2), (1, 4)):
+    # the overlapped exchange: sub-batches per rank gathered separately (bench.py --config c4
+    # runs two, one per extraction stream; world 8 is the 8-GPU node's 32 frames per rank)
+    for world, parts in ((8, 2), (4, 2), (2, 2), (1, 4)):
         assert run_world(world, desc, cnt, parts) == base, f"world {world} parts {parts}"

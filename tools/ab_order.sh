@@ -22,6 +22,4 @@ for C in c4 c3; do
   done
 done
 unset ORBFE_DESC_ORDER
-# the rolling pyramid at 1080p (opt-in) against the per-level default
-bash tools/ab_cfg.sh c4 perlevel=ORBFE_ROLL=0 roll6c24=ORBFE_ROLL=1 roll4c24=ORBFE_ROLL=1,ORBFE_ROLL_BANDS=4,ORBFE_ROLL_CHUNK=24 roll8c16=ORBFE_ROLL=1,ORBFE_ROLL_BANDS=8,ORBFE_ROLL_CHUNK=16 || exit 1
 echo ORDER_DONE
