@@ -218,7 +218,10 @@ int orbfe_extract_color_batch_device(orbfe_extractor* h, const uint8_t* d_imgs, 
                                      orbfe_keypoint* d_kps, int kps_cap, uint8_t* d_desc,
                                      int32_t* d_n_out);
 
-/* Stream control: `hip_stream` is a hipStream_t (NULL => the handle's own stream). */
+/* Stream control: `hip_stream` is a hipStream_t (NULL => the handle's own stream, which is
+ * non-blocking: it does not order against the legacy default stream).  To run on the device's
+ * legacy default stream (handle 0 in frameworks that expose it, e.g. torch's default stream),
+ * pass hipStreamLegacy ((void*)1); the same holds for the matcher and vocabulary handles. */
 int orbfe_set_stream(orbfe_extractor* h, void* hip_stream);
 int orbfe_synchronize(orbfe_extractor* h);
 
@@ -533,7 +536,11 @@ int orbfe_bow_transform_batch_device(orbfe_vocabulary* v, int nframes, const uin
  * GetMapPointMatches()[i] != NULL && !isBad(), its FeatureVector (kf_nn nodes, CSR).  Frame: n_f
  * descriptors, angles (mvKeys) and FeatureVector.  matches[f] = the keyframe feature whose map
  * point lands in vpMapPointMatches[f], or -1; *nmatches as returned.  A common node holding more
- * than 256 frame features returns ORBFE_ERR_UNSUPPORTED (ORBvoc level-2 nodes hold ~10). */
+ * than 256 frame features returns ORBFE_ERR_UNSUPPORTED (ORBvoc level-2 nodes hold ~10).  Each
+ * FeatureVector must list a feature index under at most one node, as DBoW2 builds it
+ * (FeatureVector.cpp:31-45); one that repeats an index returns ORBFE_ERR_ARG.  One kernel
+ * launch per call (the common nodes' features gathered into pinned memory); the orientation
+ * filter (ORBmatcher.cc:259-281) runs on the host, as in the reference. */
 int orbfe_search_by_bow(orbfe_matcher* m, float nnratio, int check_ori, int n_kf,
                         const uint8_t* kf_desc, const float* kf_angle, const uint8_t* kf_mp_ok,
                         int kf_nn, const int32_t* kf_node_ids, const int32_t* kf_node_off,

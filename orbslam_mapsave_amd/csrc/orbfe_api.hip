@@ -247,7 +247,8 @@ struct orbfe_extractor {
     // ORBFE_OK with *done = true when the graph path ran; *done = false to take the plain path.
     int run_single_graph(const uint8_t* img, int w, int h, size_t stride, bool* done) {
         *done = false;
-        if (graph_broken || prof.on) return ORBFE_OK;
+        // (the legacy default stream cannot be captured: plain launches there)
+        if (graph_broken || prof.on || stream == hipStreamLegacy) return ORBFE_OK;
         int st;
         if ((st = set_plan(w, h))) return st;
         if ((st = ensure_frames(1))) return st;

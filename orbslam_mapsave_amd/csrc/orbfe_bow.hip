@@ -448,9 +448,11 @@ __global__ __launch_bounds__(kBowSearchBlock) void bow_search_kernel(BowMatchArg
 // node's features, in the reference's order, into the device-mapped pinned staging buffer —
 // keyframe features without a good map point (202-207) left out — so a wave reads its node's
 // descriptors, indices and angles in one round of loads with no index chain (the common nodes
-// themselves ride in the kernel arguments).  The node loop is bow_search_kernel's; a match is
-// appended as a (frame feature, keyframe feature, rotation bin) record, and bow_filter1_kernel
-// applies the orientation filter (259-281) and writes the kept pairs to pinned memory.
+// themselves ride in the kernel arguments).  The node loop is bow_search_kernel's; each frame
+// feature's outcome — its keyframe feature and rotation bin, or -1 — is written to its own slot
+// of the pinned output (one slot per gathered frame feature: no counter, no atomics), and the
+// host applies the orientation filter (259-281, ComputeThreeMaxima over the slots) as the
+// reference does on the CPU: one launch per call.
 constexpr int kBow1Nodes = 192;
 struct Bow1Args {
     const uint4* kd;  // keyframe features in node order: descriptors (2 x uint4 each),
@@ -459,9 +461,7 @@ struct Bow1Args {
     const uint4* fd;  // frame features in node order: descriptors,
     const int* fi;    //   frame feature indices,
     const float* fa;  //   angles (F.mvKeys[i].angle)
-    int* rec;         // match records (f, kf, bin), appended
-    int* cnt;         // [0] records [32, 62) rotation histogram; zero between calls
-    int* out;         // pinned: [0] kept matches, then (f, kf) pairs
+    int* out;         // pinned, one slot per gathered frame feature: kf << 5 | bin, or -1
     int nodes;
     int4 node[kBow1Nodes];  // (keyframe start, count, frame start, count) per common node
 };
@@ -539,51 +539,10 @@ __global__ __launch_bounds__(256) void bow_search1_kernel(Bow1Args a, float nnra
             }
         }
     }
-    // the node's matches as records: one returning atomic per 64 candidates (a returning atomic
-    // inside the loop above would put a memory round trip on every match's critical path)
+    // every frame feature's outcome to its slot (the node's frame features are slots y0 ..)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        if (j >= nj) break;
-        const unsigned long long b = __ballot(mkf[j] >= 0);
-        if (!b) continue;
-        int base = 0;
-        if (lane == __builtin_ctzll(b)) base = atomicAdd(&a.cnt[0], __popcll(b));
-        base = __builtin_amdgcn_readlane(base, __builtin_ctzll(b));
-        if (mkf[j] >= 0) {
-            const int k = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-            a.rec[3 * k] = jf[j];
-            a.rec[3 * k + 1] = mkf[j];
-            a.rec[3 * k + 2] = mbin[j];
-            if (check_ori) atomicAdd(&a.cnt[32 + mbin[j]], 1);
-        }
-    }
-}
-
-// The orientation filter over the records (one workgroup after bow_search1_kernel): the kept
-// (frame feature, keyframe feature) pairs and their count (= nmatches after the filter) go to
-// the pinned output; the record counter and the histogram are zeroed for the next call.
-__global__ __launch_bounds__(256) void bow_filter1_kernel(Bow1Args a, int check_ori) {
-    __shared__ int top[3];
-    __shared__ int kept;
-    const int n = a.cnt[0];
-    if (threadIdx.x == 0) {
-        kept = 0;
-        if (check_ori) three_maxima(a.cnt + 32, top[0], top[1], top[2]);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const int f = a.rec[3 * i], kf = a.rec[3 * i + 1], bin = a.rec[3 * i + 2];
-        if (check_ori && bin != top[0] && bin != top[1] && bin != top[2]) continue;
-        const int k = atomicAdd(&kept, 1);
-        a.out[1 + 2 * k] = f;
-        a.out[2 + 2 * k] = kf;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        a.out[0] = kept;
-        a.cnt[0] = 0;
-    }
-    if (threadIdx.x < kHistLen) a.cnt[32 + threadIdx.x] = 0;
+    for (int j = 0; j < 4; ++j)
+        if (lane + 64 * j < ny) a.out[y0 + lane + 64 * j] = mkf[j] >= 0 ? (mkf[j] << 5) | mbin[j] : -1;
 }
 
 }  // namespace orbfe
@@ -844,13 +803,21 @@ static int bow_search_launch(orbfe_matcher* m, const BowMatchArgs& a, int n_pair
     return ORBFE_OK;
 }
 
+// A FeatureVector as DBoW2 builds it (FeatureVector::addFeature, FeatureVector.cpp:31-45): node
+// offsets ascending from 0, every feature index in [0, n) and listed under at most one node —
+// the gathered path blocks a matched frame feature only within its node (the reference's
+// vpMapPointMatches check, ORBmatcher.cc:212, spans nodes), so a repeated index is refused.
 static bool fv_ok(int nn, const int32_t* off, const int32_t* feat, int n) {
     if (!nn) return true;
     if (off[0] != 0) return false;
     for (int i = 0; i < nn; ++i)
         if (off[i + 1] < off[i]) return false;
-    for (int i = 0; i < off[nn]; ++i)
-        if (feat[i] < 0 || feat[i] >= n) return false;
+    if (off[nn] > n) return false;  // more entries than features: some index repeats
+    std::vector<uint8_t> seen((size_t)n, 0);
+    for (int i = 0; i < off[nn]; ++i) {
+        if (feat[i] < 0 || feat[i] >= n || seen[feat[i]]) return false;
+        seen[feat[i]] = 1;
+    }
     return true;
 }
 
@@ -861,8 +828,8 @@ static bool bow1_off() {
     return e && std::strcmp(e, "0") == 0;
 }
 
-// The host form's gathered path (bow_search1_kernel + bow_filter1_kernel; inputs validated by
-// the caller).  *done = false: the pair does not fit it (more than kBow1Nodes common nodes or a
+// The host form's gathered path (bow_search1_kernel, then the orientation filter on the host;
+// inputs validated by the caller).  *done = false: the pair does not fit it (more than kBow1Nodes common nodes or a
 // node of more than kBowNodeMax frame features) and the caller takes the general path.
 static int search_by_bow1(orbfe_matcher* m, float nnratio, int check_ori, const uint8_t* kf_desc,
                           const float* kf_angle, const uint8_t* kf_mp_ok, int kf_nn,
@@ -905,17 +872,11 @@ static int search_by_bow1(orbfe_matcher* m, float nnratio, int check_ori, const 
     // one staging block: kd | fd | ki | ka | fi | fa | out
     const size_t o_fd = (size_t)ktot * 32, o_ki = o_fd + (size_t)ftot * 32, o_ka = o_ki + 4 * (size_t)ktot,
                  o_fi = o_ka + 4 * (size_t)ktot, o_fa = o_fi + 4 * (size_t)ftot, o_out = o_fa + 4 * (size_t)ftot,
-                 bytes = o_out + 4 * (1 + 2 * (size_t)ftot);
+                 bytes = o_out + 4 * (size_t)ftot;
     uint8_t* q = m->stage(bytes);
     if (!q) return ORBFE_ERR_NOMEM;
     if (!m->pin_dev) return ORBFE_OK;  // the staging buffer is not device-mapped: general path
     *done = true;
-    if ((st = m->b1_rec.ensure((size_t)ftot * 3 * sizeof(int)))) return st;
-    if ((st = m->b1_cnt.ensure(64 * sizeof(int)))) return st;
-    if (!m->b1_zeroed) {
-        ORBFE_HIP(hipMemsetAsync(m->b1_cnt.p, 0, 64 * sizeof(int), m->stream));
-        m->b1_zeroed = true;
-    }
     // each common node's features in FeatureVector order (keyframe features with a good map
     // point only), as the node loop visits them (198-245)
     int* ki = reinterpret_cast<int*>(q + o_ki);
@@ -946,24 +907,33 @@ static int search_by_bow1(orbfe_matcher* m, float nnratio, int check_ori, const 
     a.ka = reinterpret_cast<const float*>(d + o_ka);
     a.fi = reinterpret_cast<const int*>(d + o_fi);
     a.fa = reinterpret_cast<const float*>(d + o_fa);
-    a.rec = m->b1_rec.as<int>();
-    a.cnt = m->b1_cnt.as<int>();
     a.out = reinterpret_cast<int*>(const_cast<uint8_t*>(d + o_out));
-    const int* out = reinterpret_cast<const int*>(q + o_out);
+    const volatile int* out = reinterpret_cast<const volatile int*>(q + o_out);
     if ((st = m->flush())) return st;
     hipLaunchKernelGGL(bow_search1_kernel, dim3((a.nodes + 3) / 4), dim3(256), 0, m->stream, a,
                        nnratio, check_ori);
-    hipLaunchKernelGGL(bow_filter1_kernel, dim3(1), dim3(256), 0, m->stream, a, check_ori);
-    if (hipGetLastError() != hipSuccess) {
-        m->b1_zeroed = false;
-        return ORBFE_ERR_HIP;
+    if (hipGetLastError() != hipSuccess) return ORBFE_ERR_HIP;
+    if ((st = m->sync())) return st;
+    // the orientation filter (259-281) on the host, as in the reference: the rotation histogram
+    // of every match, ComputeThreeMaxima (1604-1645), matches outside the three bins dropped
+    int hist[kHistLen] = {};
+    int top[3] = {-1, -1, -1};
+    if (check_ori) {
+        for (int s = 0; s < ftot; ++s) {
+            const int r = out[s];
+            if (r >= 0) ++hist[r & 31];
+        }
+        three_maxima(hist, top[0], top[1], top[2]);
     }
-    if ((st = m->sync())) {
-        m->b1_zeroed = false;
-        return st;
+    int kept = 0;
+    for (int s = 0; s < ftot; ++s) {
+        const int r = out[s];
+        if (r < 0) continue;
+        const int bin = r & 31;
+        if (check_ori && bin != top[0] && bin != top[1] && bin != top[2]) continue;
+        matches[fi[s]] = r >> 5;
+        ++kept;
     }
-    const int kept = out[0];
-    for (int k = 0; k < kept; ++k) matches[out[1 + 2 * k]] = out[2 + 2 * k];
     *nmatches = kept;
     return ORBFE_OK;
 }

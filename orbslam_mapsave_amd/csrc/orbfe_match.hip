@@ -867,7 +867,7 @@ __device__ __forceinline__ int rot_bin(float a1, float a2) {  // ORBmatcher.cc:4
 }
 
 // ComputeThreeMaxima (ORBmatcher.cc:1604-1645) over 30 bin counts.
-__device__ __forceinline__ void three_maxima(const int* h, int& i1, int& i2, int& i3) {
+__host__ __device__ __forceinline__ void three_maxima(const int* h, int& i1, int& i2, int& i3) {
     int m1 = 0, m2 = 0, m3 = 0;
     i1 = i2 = i3 = -1;
     for (int i = 0; i < kHistLen; ++i) {

@@ -70,8 +70,6 @@ struct orbfe_matcher {
     DevBuf o_u, o_f0, o_f1, o_f2, o_f3, o_i;        // frustum outputs
     DevBuf scal, done_ctr;
     DevBuf g_t0, g_t1, g_t2, g_dec, g_chg, g_last, g_bins, g_hist;  // greedy resolver
-    DevBuf b1_rec, b1_cnt;  // SearchByBoW host form: match records, counter + histogram
-    bool b1_zeroed = false;  // b1_cnt cleared once (bow_filter1_kernel re-zeroes it per call)
     Profiler prof;
     int last_rounds = 0;  // rounds the most recent greedy resolution took (diagnostics)
     int capacity_retries = 0;  // calls rerun because the candidates outgrew the buffer
@@ -129,8 +127,7 @@ struct orbfe_matcher {
                           &fb_cs, &fb_ci, &fb_co, &q, &r, &nq, &nr, &out, &cnt, &off, &cand, &s1,
                           &s2, &s3, &s4, &s5, &m_f0, &m_f1, &m_f2, &m_f3, &m_f4, &m_u0, &m_u1,
                           &m_i0, &m_i1, &m_d, &o_u, &o_f0, &o_f1, &o_f2, &o_f3, &o_i, &scal,
-                          &g_t0, &g_t1, &g_t2, &g_dec, &g_chg, &g_last, &g_bins, &g_hist, &done_ctr,
-                          &b1_rec, &b1_cnt})
+                          &g_t0, &g_t1, &g_t2, &g_dec, &g_chg, &g_last, &g_bins, &g_hist, &done_ctr})
             b->release();
         for (auto& kv : bf_e) {
             kv.second.buf.release();

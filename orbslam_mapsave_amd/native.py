@@ -88,6 +88,19 @@ def lib() -> C.CDLL:
     return _lib
 
 
+# hipStreamLegacy (hip_runtime_api.h): the device's legacy default stream as an explicit handle
+HIP_STREAM_LEGACY = 1
+
+
+def _stream_arg(stream_handle: int | None):
+    """set_stream's argument: None = the handle's own stream; 0 (torch's default stream, the
+    legacy null stream) = hipStreamLegacy, since a NULL hip_stream selects the handle's own
+    stream in the C ABI; anything else is a hipStream_t as is."""
+    if stream_handle is None:
+        return None
+    return C.c_void_p(HIP_STREAM_LEGACY if stream_handle == 0 else stream_handle)
+
+
 def _check(fn: str, st: int) -> None:
     if st != ORBFE_OK:
         raise OrbfeError(fn, st)
@@ -357,7 +370,7 @@ class ORBextractor:
 
     def set_stream(self, stream_handle: int | None) -> None:
         _check("orbfe_set_stream", lib().orbfe_set_stream(
-            self._h, C.c_void_p(stream_handle) if stream_handle else None))
+            self._h, _stream_arg(stream_handle)))
 
     def synchronize(self) -> None:
         _check("orbfe_synchronize", lib().orbfe_synchronize(self._h))
@@ -507,7 +520,7 @@ class Vocabulary:
 
     def set_stream(self, stream_handle: int | None) -> None:
         _check("orbfe_vocabulary_set_stream", lib().orbfe_vocabulary_set_stream(
-            self._h, C.c_void_p(stream_handle) if stream_handle else None))
+            self._h, _stream_arg(stream_handle)))
 
 
 class ORBmatcher:
@@ -578,7 +591,7 @@ class ORBmatcher:
 
     def set_stream(self, stream_handle: int | None) -> None:
         _check("orbfe_matcher_set_stream", lib().orbfe_matcher_set_stream(
-            self._h, C.c_void_p(stream_handle) if stream_handle else None))
+            self._h, _stream_arg(stream_handle)))
 
     def SearchForInitialization(self, F1: Frame, F2: Frame, vbPrevMatched: np.ndarray,
                                 windowSize: int = 10):

@@ -277,7 +277,8 @@ def test_gpu_bow_transform_batch(vocab_paths):
 @pytest.mark.parametrize("zc,path", [("1", "gathered"), ("1", "general"), ("0", "general")])
 def test_gpu_search_by_bow(ori, ratio, zc, path, vocab_paths, frames, monkeypatch):
     """Host SearchByBoW: the gathered path (common nodes' features gathered by the host into
-    device-mapped pinned memory, bow_search1_kernel + bow_filter1_kernel), the general path with
+    device-mapped pinned memory, one bow_search1_kernel launch writing each frame feature's
+    outcome to its pinned slot, the orientation filter on the host), the general path with
     the pair's last workgroup writing the results into pinned memory (ORBFE_BOW1=0), and through
     bow_init_kernel + D2H copies (ORBFE_ZERO_COPY=0); three calls on one matcher (counters,
     histogram and staging reused)."""
@@ -411,3 +412,22 @@ def test_gpu_search_by_bow_batch(ori, ratio, vocab_paths):
         assert (got[p, len(fd):] == -1).all()
     assert gnm[0] > 50 and gnm[4] == 0 and gnm[5] == 0
     mt.close()
+
+
+@pytest.mark.gpu
+def test_gpu_search_by_bow_rejects_repeated_feature(vocab_paths, frames):
+    """A FeatureVector listing one feature index under two nodes (DBoW2 never builds one:
+    FeatureVector.cpp:31-45) is refused with ORBFE_ERR_ARG instead of double-counting a match."""
+    from orbslam_mapsave_amd.abi import ORBFE_ERR_ARG
+    from orbslam_mapsave_amd.native import ORBmatcher, OrbfeError
+    kf, f, kf_ok, kf_fv, f_fv = bow_case(vocab_paths["k10L4_l1_tfidf"], frames)
+    ids, off, feat = (np.array(x, copy=True) for x in f_fv)
+    feat[int(off[1])] = feat[0]  # node 1's first feature repeats node 0's first
+    mt = ORBmatcher(0.75, True, device=0)
+    try:
+        with pytest.raises(OrbfeError) as e:
+            mt.SearchByBoW(kf.desc, kf.keys["angle"], kf_ok, kf_fv, f.desc, f.keys["angle"],
+                           (ids, off, feat))
+        assert e.value.status == ORBFE_ERR_ARG
+    finally:
+        mt.close()
