@@ -1013,6 +1013,25 @@ __device__ __forceinline__ int fast_emit(const uint8_t* S, uint16_t* list, int c
     return o;
 }
 
+// ORBFE_FAST_TIMING (attribution builds only, tools/probe/fast_phases.py): lane 0 of each wave
+// records per-phase shader-clock totals of cells < kFtCells of frames < kFtFrames into
+// g_fast_t[frame][cell][16]: 0 staging (ROI loads + score-plane zeroing), 1 pre-test sweeps,
+// 2 list writes, 3 scoring, 4 emission (NMS + key stores), 5 overflow flushes, 6 the minThFAST
+// rerun pass (all of it), 7 total, then counts: 8 sweeps, 9 survivors scored, 10 corners
+// emitted, 11 flushes, 12 rerun (0 / 1).  Every mark waits for the wave's outstanding memory
+// operations first (s_waitcnt 0), so a phase owns the latency of its own loads.
+#ifdef ORBFE_FAST_TIMING
+constexpr int kFtFrames = 8, kFtCells = 8192;
+__device__ long long g_fast_t[kFtFrames * kFtCells * 16];
+#define FT_NOW() (__builtin_amdgcn_s_waitcnt(0), (long long)clock64())
+#define FT_ADD(k, t0) do { const long long t1_ = FT_NOW(); ft[k] += t1_ - (t0); (t0) = t1_; } while (0)
+#define FT_CNT(k, v) do { ft[k] += (v); } while (0)
+#else
+#define FT_NOW() 0ll
+#define FT_ADD(k, t0) do { (void)(t0); } while (0)
+#define FT_CNT(k, v) do { } while (0)
+#endif
+
 // kP: the ROI pitch as a compile-time constant (48 for every cell width up to 45 px, i.e. the
 // common frame sizes), so the 16 circle offsets of fast_S become LDS immediates; 0 = runtime.
 // Measured and dropped (profiles/r02/experiments/fast_variants.json): several cells per wave
@@ -1024,6 +1043,11 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
     int c, f;
     xcd_block(c, f);
     const int lane = threadIdx.x;
+#ifdef ORBFE_FAST_TIMING
+    long long ft[16] = {};
+    const long long ft_start = FT_NOW();
+    long long ftc = ft_start;
+#endif
     const CellDesc cell = a.cells[c];
     const LevelPtr lp = a.pyr[cell.level];
     const int rows = cell.y1 - cell.y0, cols = cell.x1 - cell.x0;
@@ -1077,6 +1101,9 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
     const uint32_t* lds32 = reinterpret_cast<const uint32_t*>(roi_base);
     const int P4 = P >> 2;
     fast_sync();
+#ifdef ORBFE_FAST_TIMING
+    FT_ADD(0, ftc);
+#endif
     // Pass at iniThFAST: only pixels passing the pre-test at that threshold can have S >= t,
     // and every other pixel counts as 0 in the NMS, so S is computed for those alone.
     uint32_t* out = a.cell_keys + f * a.cell_cap_total + cell.slot;
@@ -1103,6 +1130,10 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
     int total = 0;
     for (int pass = 0; pass < 2 && total == 0; ++pass) {
         const int t = pass ? a.min_th : a.ini_th;  // rerun at minThFAST when empty (811-815)
+#ifdef ORBFE_FAST_TIMING
+        const long long ft_pass = ftc;
+        FT_CNT(12, pass);
+#endif
         // Byte-parallel pre-test (4 pixels per lane): with v_lerp_u8,
         // lerp(c, ~v, R1) = floor((c - v + 255 + (t & 1)) / 2) per byte, and the high bit of
         // lerp(that, M, 0) with M = 128 - ceil(t / 2) is exactly c - v > t (c > v + t); with
@@ -1117,6 +1148,10 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
         int cnt = 0, scored = 0, emitted = 0;
         for (int r0 = 0; r0 < nr; r0 += rps) {
             if (cnt + sweep_max > a.cand_max) {  // wave-uniform
+#ifdef ORBFE_FAST_TIMING
+                FT_CNT(11, 1);
+                FT_CNT(9, cnt - scored);
+#endif
                 fast_sync();
                 score(scored, cnt);
                 fast_sync();
@@ -1131,6 +1166,9 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
                 if (lane < n1) list[lane] = (uint16_t)e0;
                 if (lane + 64 < n1) list[lane + 64] = (uint16_t)e1;
                 cnt = scored = n1;
+#ifdef ORBFE_FAST_TIMING
+                FT_ADD(5, ftc);
+#endif
             }
             const int cr = r0 + lr;
             uint32_t fl = 0;
@@ -1153,6 +1191,10 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
             }
             const unsigned long long b0 = byte_ballot<0>(fl), b1 = byte_ballot<1>(fl),
                                      b2 = byte_ballot<2>(fl), b3 = byte_ballot<3>(fl);
+#ifdef ORBFE_FAST_TIMING
+            FT_ADD(1, ftc);
+            FT_CNT(8, 1);
+#endif
             if (fl) {  // row-major: earlier lanes, then this lane's lower bytes
                 auto below = [](unsigned long long b, uint32_t acc) {  // popc(b & lanes below)
                     return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
@@ -1174,12 +1216,23 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
                 list[lane_select(b3, tr, pos)] = (uint16_t)(ob + 3);
             }
             cnt += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+#ifdef ORBFE_FAST_TIMING
+            FT_ADD(2, ftc);
+#endif
         }
         fast_sync();
         score(scored, cnt);
         fast_sync();
+#ifdef ORBFE_FAST_TIMING
+        FT_ADD(3, ftc);
+        FT_CNT(9, cnt - scored);
+#endif
         total = emitted + fast_emit(S, list, cnt, P, inv_p, t, cell, out + emitted, cell.cap - emitted);
         fast_sync();
+#ifdef ORBFE_FAST_TIMING
+        FT_ADD(4, ftc);
+        if (pass) ft[6] += ftc - ft_pass;
+#endif
     }
     if (lane == 0) {
         const int n = min(total, cell.cap);
@@ -1187,6 +1240,12 @@ __global__ __launch_bounds__(kFastBlock) void fast_kernel(FastArgs a) {
         // the level's key total for the oct-tree (which reads it and resets it to 0)
         if (n) atomicAdd(&a.level_keys[f * kMaxLevels + cell.level], n);
     }
+#ifdef ORBFE_FAST_TIMING
+    ft[7] = FT_NOW() - ft_start;
+    ft[10] = total;
+    if (lane == 0 && f < kFtFrames && c < kFtCells)
+        for (int k = 0; k < 16; ++k) g_fast_t[((long long)f * kFtCells + c) * 16 + k] = ft[k];
+#endif
 }
 
 template __global__ void fast_kernel<0>(FastArgs);
@@ -3345,6 +3404,17 @@ int plan_geometry(const HostTables& t, int w, int h, Plan& g) {
 
 }  // namespace orbfe
 
+#ifdef ORBFE_FAST_TIMING
+extern "C" int orbfe_debug_fast_timing_reset() {  // device globals start uninitialised
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(orbfe::g_fast_t)) != hipSuccess) return -3;
+    return hipMemset(p, 0, sizeof(orbfe::g_fast_t)) == hipSuccess ? 0 : -3;
+}
+extern "C" int orbfe_debug_fast_timing(long long* out, int n) {
+    n = n < orbfe::kFtFrames * orbfe::kFtCells * 16 ? n : orbfe::kFtFrames * orbfe::kFtCells * 16;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(orbfe::g_fast_t), (size_t)n * sizeof(long long)) == hipSuccess ? 0 : -3;
+}
+#endif
 
 #ifdef ORBFE_OCT_TIMING
 extern "C" int orbfe_debug_oct_timing(long long* out, int n) {

@@ -918,6 +918,12 @@ struct SfiRoundArgs {
 };
 
 __global__ __launch_bounds__(256) void sfi_round_kernel(SfiRoundArgs a, int r) {
+    // A round after a change-free one (the host launches rounds in batches, past convergence)
+    // exits before touching anything: it would repeat the converged round's decisions, but it
+    // would also clear the list buffer the converged round filled two rounds earlier in the
+    // rotation, which the final kernel reads (found by tests/cpp/threads_test.cpp: a problem
+    // converging at round 3 of a 6-round batch returned no matches)
+    if (r > 0 && a.chg[r - 1] == 0) return;
     const int gid = blockIdx.x * 256 + threadIdx.x;
     if (gid < a.n2) a.lcnt[(r + 2) % 3][gid] = 0;  // the list round r + 1 fills
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);

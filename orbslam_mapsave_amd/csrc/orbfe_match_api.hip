@@ -833,6 +833,8 @@ int orbfe_search_for_initialization(orbfe_matcher* m, float nnratio, int check_o
         const int rb = std::max(1, (std::max(n1 * 64, n2) + 255) / 256);
         // slot lists of 64 acceptors; a slot drawing more in some round (one query per slot is
         // the usual case) reruns the rounds with room for every query
+        // conv: the first round without a change; the rounds a batch launches past it exit at
+        // once (sfi_round_kernel), so conv's decision and list buffers hold the final state
         int conv = -1;
         for (int k : {kSfiSlotK, std::max(n1, 1)}) {
             r.k = k;

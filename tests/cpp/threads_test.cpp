@@ -101,6 +101,17 @@ int main(int argc, char** argv) {
         const orbfe_frame_view v1 = F1.view(), v2 = F2.view();
         oracle_search_for_initialization(0.9f, 1, &v1, &v2, oprev.data(), 100, om12.data(), &onm);
     }
+    if (const char* dump = std::getenv("THREADS_DUMP")) {  // the matcher problem, for debugging
+        if (FILE* fp = std::fopen(dump, "wb")) {
+            for (const orbfe::FrameData* F : {&F1, &F2}) {
+                const int n = (int)F->keys_un.size();
+                std::fwrite(&n, 4, 1, fp);
+                std::fwrite(F->keys_un.data(), sizeof(orbfe_keypoint), n, fp);
+                std::fwrite(F->descriptors.data(), 32, n, fp);
+            }
+            std::fclose(fp);
+        }
+    }
     const int nq = (int)F1.keys_un.size(), nr = (int)F2.keys_un.size();
     std::vector<int32_t> obi(nq), obd(nq), osd(nq);
     oracle_bf_match(F1.descriptors.data(), nq, F2.descriptors.data(), nr, obi.data(), obd.data(), osd.data());
@@ -108,6 +119,16 @@ int main(int argc, char** argv) {
     orbfe::ORBextractor exL(1000, 1.2f, 8, 20, 7), exR(1000, 1.2f, 8, 20, 7), exI(2000, 1.2f, 8, 20, 7);
     orbfe::ORBmatcher matcher(0.9f, true);
     std::atomic<int> fails{0}, done_ini{0}, done_match{0}, stereo_pairs{0};
+    {   // the matcher's problem once on this thread before any concurrency
+        std::vector<float> prev = prev0;
+        std::vector<int> m12;
+        const int nm = matcher.SearchForInitialization(F1, F2, prev, m12, 100);
+        int diff = 0;
+        for (size_t i = 0; i < m12.size(); ++i) diff += m12[i] != om12[i];
+        std::printf("single-thread SearchForInitialization: %d matches (oracle %d), %d entries differ, "
+                    "%zu / %zu keypoints\n", nm, onm, diff, F1.keys_un.size(), F2.keys_un.size());
+        if (nm != onm || m12 != om12 || prev != oprev) ++fails;
+    }
     std::atomic<bool> stop{false};
     // Ini extractor: its own thread for the whole run
     std::thread ini([&] {

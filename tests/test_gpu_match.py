@@ -234,3 +234,44 @@ def test_bf_match_batch_shared_refs(pre, monkeypatch):
         assert np.array_equal(got[:, 0], bi), b
         assert np.array_equal(got[:, 1], bd), b
         assert np.array_equal(got[:, 2], sd), b
+
+
+def _load_sfi_problem(path):
+    from orbslam_mapsave_amd.abi import KEYPOINT_DTYPE, Frame
+    raw = open(path, "rb").read()
+    o, fr = 0, []
+    scale = oracle.tables(oracle.params(2000, 1.2, 8, 20, 7))["scale"]
+    for _ in range(2):
+        n = int(np.frombuffer(raw, np.int32, 1, o)[0])
+        o += 4
+        k = np.frombuffer(raw, KEYPOINT_DTYPE, n, o).copy()
+        o += 28 * n
+        d = np.frombuffer(raw, np.uint8, 32 * n, o).reshape(n, 32).copy()
+        o += 32 * n
+        fr.append(Frame(k, d, 640, 480, scale))
+    return fr
+
+
+@pytest.mark.parametrize("check_ori", [True, False])
+def test_search_for_initialization_convergence_rounds(check_ori):
+    """Two Ini frames (2000 keypoints) of tests/cpp/threads_test.cpp's images
+    (tests/golden/sfi_conv3_problem.bin, written by that program with THREADS_DUMP set; oracle
+    extractions): at windows 60-100 the fixed-point rounds converge at round 3 of a 6-round
+    batch, where the rounds launched past convergence used to clear the converged acceptor
+    lists (0 matches instead of 37-62).  Every window 20-200 bit-exact, on one matcher."""
+    import os
+    from orbslam_mapsave_amd.native import ORBmatcher
+    f1, f2 = _load_sfi_problem(os.path.join(os.path.dirname(__file__), "golden", "sfi_conv3_problem.bin"))
+    prev = np.stack([f1.keys["x"], f1.keys["y"]], 1).astype(np.float32)
+    m = ORBmatcher(0.9, check_ori, device=0)
+    rounds = set()
+    try:
+        for win in range(20, 201, 10):
+            g12, gn, gprev = m.SearchForInitialization(f1, f2, prev, win)
+            e12, en, eprev = oracle.search_for_initialization(f1, f2, prev, win, 0.9, check_ori)
+            assert gn == en, (win, gn, en)
+            assert np.array_equal(g12, e12) and np.array_equal(gprev, eprev), win
+            rounds.add(m.last_rounds())
+    finally:
+        m.close()
+    assert 4 in rounds, rounds  # the converge-at-round-3 case is exercised
