@@ -250,6 +250,10 @@ int orbfe_profile_read(orbfe_extractor* h, double* total_ms, int32_t* launches);
 #define ORBFE_PYR_PER_LEVEL 0
 #define ORBFE_PYR_BANDS     1
 int orbfe_pyramid_path(const orbfe_extractor* h, int nframes);
+/* Measurement hook: relaunch the stages in `stage_mask` (bits 1 << ORBFE_STAGE_*) of the most
+ * recent extraction on its own buffers, `reps` times, asynchronously on the handle's stream
+ * (outputs meaningful only for a full mask). */
+int orbfe_debug_replay(orbfe_extractor* h, unsigned stage_mask, int reps);
 
 /* Pyramid access — replaces the public member mvImagePyramid (ORBextractor.h:90) read by
  * stereo matching (Frame.cc:589, 679, 696).  Copies level `level` of frame `frame` of the

@@ -78,6 +78,7 @@ int check_device(int device) {
 struct Profiler {
     bool on = false;
     unsigned mask = ~0u;  // stages that get events (orbfe_profile)
+    unsigned run_mask = ~0u;  // stages whose launches run (orbfe_debug_replay: one stage alone)
     std::vector<hipEvent_t> a, b;
     std::vector<int> kind;
     size_t used = 0;
@@ -111,6 +112,7 @@ struct Profiler {
 // Kernel launch through hipExtLaunchKernelGGL with the stage's profiling events.
 #define ORBFE_LAUNCH(prof, stage, kernel, grid, block, shmem, stream, ...)                 \
     do {                                                                                   \
+        if (!(((prof).run_mask >> (stage)) & 1u)) break;                                   \
         hipEvent_t e0_, e1_;                                                               \
         (prof).slot(stage, &e0_, &e1_);                                                    \
         hipExtLaunchKernelGGL(kernel, grid, block, shmem, stream, e0_, e1_, 0, __VA_ARGS__); \
@@ -399,8 +401,11 @@ struct orbfe_extractor {
     }
 
     // Runs the whole pipeline on `n` frames whose level 0 is described by `l0`.
+    // the last run's arguments (orbfe_debug_replay)
+    struct LastRun { int n = 0; LevelPtr l0{}; orbfe_keypoint* kps = nullptr; int cap = 0; uint8_t* desc = nullptr; int32_t* nout = nullptr; } last_run;
     int run(int n, LevelPtr l0, orbfe_keypoint* d_kps, int kps_cap, uint8_t* d_desc,
             int32_t* d_n) {
+        last_run = LastRun{n, l0, d_kps, kps_cap, d_desc, d_n};
         const Plan& g = plan;
         const int L = g.geo.nlevels;
         LevelPtr lp[kMaxLevels], bp[kMaxLevels];
@@ -1308,6 +1313,25 @@ int orbfe_profile_read(orbfe_extractor* h, double* total_ms, int32_t* launches) 
     }
     h->prof.used = 0;
     return ORBFE_OK;
+}
+
+// Test / measurement hook (no reference counterpart): relaunch the stages in `stage_mask`
+// (bit ORBFE_STAGE_*) of the most recent device-batch extraction on the handle's stream, on
+// that extraction's buffers, `reps` times, asynchronously.  A stage alone reads what the
+// previous stages left (the replayed FAST re-adds its per-level key totals, which only the
+// oct-tree reads), so the outputs are only meaningful for a full mask; used to time kernels of
+// different stages running concurrently on two handles.
+int orbfe_debug_replay(orbfe_extractor* h, unsigned stage_mask, int reps) {
+    if (!h || !h->planned || h->last_run.n < 1 || reps < 0 || !h->last_run.kps) return ORBFE_ERR_ARG;
+    DeviceGuard dg(h->device);
+    h->prof.run_mask = stage_mask;
+    int st = ORBFE_OK;
+    for (int i = 0; i < reps && st == ORBFE_OK; ++i) {
+        const auto& r = h->last_run;
+        st = h->run(r.n, r.l0, r.kps, r.cap, r.desc, r.nout);
+    }
+    h->prof.run_mask = ~0u;
+    return st;
 }
 
 int orbfe_pyramid_path(const orbfe_extractor* h, int nframes) {

@@ -412,6 +412,7 @@ __global__ __launch_bounds__(256) void resize2_kernel(Resize2Args a) {
     // round trip per row.  Loads and stores unconditional at clamped indices.
     __shared__ int ytm_s[3 * kR2Rows];  // c.y - c.x < kR2Rows (host plan)
     __shared__ int ytd_s[3 * kRsTH];
+    static_assert(3 * kRsTH <= 256, "ytd_s is filled with one entry per thread (ORBFE_RS_TH <= 85)");
     {
         const int n3 = 3 * (c.y - c.x + 1);
         const int i0 = min(tid, n3 - 1), i1 = min(tid + 256, n3 - 1), i2 = min(tid, 3 * kRsTH - 1);
