@@ -405,6 +405,11 @@ def parse_args():
                          "table and the choice of the dominant kernel")
     ap.add_argument("--chunks", type=int, default=1,
                     help="extraction calls per stream per step (each a sub-batch / chunks)")
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="1 (c3): each sub-batch extracted in two calls (orbfe_set_stage_mask: "
+                         "pyramid + FAST + oct-tree, then describe + its match), and stream k's "
+                         "first call waits for stream k-1's first, so one sub-batch's describe "
+                         "runs beside the next one's FAST (DESIGN.md §5h)")
     ap.add_argument("--skew", type=int, default=0,
                     help="1: stream k starts k/streams of a step late (its first chunk waits "
                          "for stream 0's chunk k*chunks/streams - 1), so the streams run "
@@ -502,9 +507,33 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
                                      d_desc[0].data_ptr(), cap * 32, d_n.data_ptr(), B,
                                      d_out[0].data_ptr())
 
+    G1, G2 = ("resize", "fast", "octree"), ("describe",)
+    pipe_ev = [torch.cuda.Event() for _ in range(S)]
+
+    def step_pipeline():
+        """--pipeline 1: per sub-batch, stages up to the oct-tree, then describe + the match,
+        with stream k's first part queued behind stream k-1's first part."""
+        for k in range(S):
+            f0 = k * C
+            if k:
+                streams[k].wait_event(pipe_ev[k - 1])
+            exs[k].set_stages(G1)
+            extract_chunk(k)
+            pipe_ev[k].record(streams[k])
+            exs[k].set_stages(G2)
+            extract_chunk(k)
+            exs[k].set_stages(None)
+            if mode == "ref":
+                mt.set_stream(streams[k].cuda_stream)
+                mt.bf_match_batch_device(d_desc[f0].data_ptr(), cap * 32, d_n[f0:].data_ptr(), cap,
+                                         ref_desc.data_ptr(), 0, d_nr[f0:].data_ptr(), C,
+                                         d_out[f0].data_ptr())
+
     def step():
         if S == 1 and mode != "pred":
             return step_single()
+        if args.pipeline and mode != "pred" and J == 1:
+            return step_pipeline()
         if mode != "pred":  # sub-batch k: extract (+ match) on stream k, no cross-stream deps
             ev = {}
             for j in range(J):
@@ -952,6 +981,7 @@ def main() -> None:
                        "frames_per_rank_per_step": B,
                        "streams_per_rank": S, "chunks_per_stream": J,
                        "stream_skew": bool(args.skew) and S > 1 and J >= S,
+                       "stage_pipeline": bool(args.pipeline) and S > 1 and args.config == "c3",
                        "global_batch": B * world, "nfeatures": NF, "reference_kp": r["ref_kp"],
                        "mean_kp_per_frame": round(r["nkp"], 1), "parallelism": parallelism},
             "roofline": r["roofline"],

@@ -254,6 +254,12 @@ int orbfe_pyramid_path(const orbfe_extractor* h, int nframes);
  * recent extraction on its own buffers, `reps` times, asynchronously on the handle's stream
  * (outputs meaningful only for a full mask). */
 int orbfe_debug_replay(orbfe_extractor* h, unsigned stage_mask, int reps);
+/* Stage pipelining: later extraction calls on `h` run only the stages in `stage_mask` (bits
+ * 1 << ORBFE_STAGE_*; 0 = all, the default).  A batch extracted in two calls on the same handle,
+ * buffers and frames — stages up to the oct-tree, then describe — equals one full call; the
+ * caller orders the calls (e.g. on two streams, so that one sub-batch's describe runs beside
+ * another's FAST). */
+int orbfe_set_stage_mask(orbfe_extractor* h, unsigned stage_mask);
 
 /* Pyramid access — replaces the public member mvImagePyramid (ORBextractor.h:90) read by
  * stereo matching (Frame.cc:589, 679, 696).  Copies level `level` of frame `frame` of the

@@ -250,7 +250,7 @@ struct orbfe_extractor {
     int run_single_graph(const uint8_t* img, int w, int h, size_t stride, bool* done) {
         *done = false;
         // (the legacy default stream cannot be captured: plain launches there)
-        if (graph_broken || prof.on || stream == hipStreamLegacy) return ORBFE_OK;
+        if (graph_broken || prof.on || stream == hipStreamLegacy || stage_mask != ~0u) return ORBFE_OK;
         int st;
         if ((st = set_plan(w, h))) return st;
         if ((st = ensure_frames(1))) return st;
@@ -402,6 +402,7 @@ struct orbfe_extractor {
 
     // Runs the whole pipeline on `n` frames whose level 0 is described by `l0`.
     // the last run's arguments (orbfe_debug_replay)
+    unsigned stage_mask = ~0u;  // orbfe_set_stage_mask: the stages extraction calls run
     struct LastRun { int n = 0; LevelPtr l0{}; orbfe_keypoint* kps = nullptr; int cap = 0; uint8_t* desc = nullptr; int32_t* nout = nullptr; } last_run;
     int run(int n, LevelPtr l0, orbfe_keypoint* d_kps, int kps_cap, uint8_t* d_desc,
             int32_t* d_n) {
@@ -1330,8 +1331,15 @@ int orbfe_debug_replay(orbfe_extractor* h, unsigned stage_mask, int reps) {
         const auto& r = h->last_run;
         st = h->run(r.n, r.l0, r.kps, r.cap, r.desc, r.nout);
     }
-    h->prof.run_mask = ~0u;
+    h->prof.run_mask = h->stage_mask;
     return st;
+}
+
+int orbfe_set_stage_mask(orbfe_extractor* h, unsigned stage_mask) {
+    if (!h) return ORBFE_ERR_ARG;
+    h->stage_mask = stage_mask ? stage_mask : ~0u;
+    h->prof.run_mask = h->stage_mask;
+    return ORBFE_OK;
 }
 
 int orbfe_pyramid_path(const orbfe_extractor* h, int nframes) {

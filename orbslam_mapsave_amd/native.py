@@ -35,7 +35,7 @@ EXPORTED = [
     "orbfe_extract_color", "orbfe_human_mask_rect", "orbfe_extract_batch",
     "orbfe_extract_batch_device", "orbfe_extract_color_batch_device", "orbfe_set_stream",
     "orbfe_synchronize", "orbfe_compute_stereo_matches", "orbfe_compute_stereo_matches_device",
-    "orbfe_stereo_status", "orbfe_profile", "orbfe_profile_read", "orbfe_pyramid_path", "orbfe_debug_replay", "orbfe_get_level", "orbfe_get_blurred_level", "orbfe_get_fast_keys",
+    "orbfe_stereo_status", "orbfe_profile", "orbfe_profile_read", "orbfe_pyramid_path", "orbfe_debug_replay", "orbfe_set_stage_mask", "orbfe_get_level", "orbfe_get_blurred_level", "orbfe_get_fast_keys",
     "orbfe_matcher_create", "orbfe_matcher_destroy", "orbfe_matcher_set_stream",
     "orbfe_matcher_profile", "orbfe_matcher_profile_read", "orbfe_matcher_profile_read_stages", "orbfe_hamming",
     "orbfe_bf_match", "orbfe_bf_match_batch_device", "orbfe_search_for_initialization",
@@ -386,6 +386,13 @@ class ORBextractor:
             for st in stages:
                 mode |= 2 << self.STAGES.index(st)
         _check("orbfe_profile", lib().orbfe_profile(self._h, mode))
+
+    def set_stages(self, stages=None) -> None:
+        """orbfe_set_stage_mask: later extraction calls run only the named stages (None: all)."""
+        mask = 0
+        for st in stages or ():
+            mask |= 1 << self.STAGES.index(st)
+        _check("orbfe_set_stage_mask", lib().orbfe_set_stage_mask(self._h, C.c_uint(mask)))
 
     def replay(self, stages, reps: int = 1) -> None:
         """orbfe_debug_replay: relaunch the named stages of the last extraction reps times."""

@@ -71,3 +71,32 @@ def test_null_and_bad_arguments_do_not_crash():
     assert not lib.orbfe_create(C.byref(p), 0, 0, 0, 0, C.byref(st))
     assert st.value in (abi.ORBFE_ERR_ARG, abi.ORBFE_ERR_HIP)
     assert lib.orbfe_hamming(None, None, None, -1, None) == abi.ORBFE_ERR_ARG
+
+
+@pytest.mark.parametrize("nf,sf,nl,w,h", [(2000, 1.2, 8, 1920, 1080), (1000, 1.2, 8, 640, 480),
+                                          (1000, 1.5, 4, 1280, 720), (500, 1.2, 8, 3000, 300)])
+def test_keypoint_capacity_params_host_only(nf, sf, nl, w, h):
+    """orbfe_keypoint_capacity_params needs no device (host arithmetic only): the sum over levels
+    of the oct-tree output bound max(N_l + 4, 4 nIni_l, 20) (ORBextractor.cc:538-762), restated
+    here from the oracle's level sizes and feature budgets (ORBextractor.cc:434-445, 772-775, 542)."""
+    import numpy as np
+    import oracle
+    p = oracle.params(nf, sf, nl, 20, 7)
+    lw, lh = oracle.level_sizes(p, w, h)
+    nfeat = oracle.tables(p)["nfeat"] if "nfeat" in oracle.tables(p) else None
+    if nfeat is None:  # ORBextractor.cc:434-445 in float, as the ctor computes it
+        f = np.float32(1.0) / np.float32(sf)
+        desired = np.float32(nf) * (np.float32(1) - f) / (np.float32(1) - np.float32(f ** nl))
+        nfeat, tot = [], 0
+        for _ in range(nl - 1):
+            n = int(np.rint(desired))
+            nfeat.append(n)
+            tot += n
+            desired = np.float32(desired * f)
+        nfeat.append(max(nf - tot, 0))
+    cap = 0
+    for l in range(nl):
+        bw, bh = int(lw[l]) - 32, int(lh[l]) - 32  # maxBorder - minBorder = size - 16 - 16
+        nini = int(round(bw / bh)) if bw >= 30 and bh >= 30 else 0
+        cap += max(int(nfeat[l]) + 4, 4 * nini, 20)
+    assert native.keypoint_capacity(nf, sf, nl, 20, 7, w, h) == cap
