@@ -134,6 +134,7 @@ struct orbfe_extractor {
     DevBuf cells, xtab, ytab, bslot, ptab;
     DevBuf pyr, blur, cell_cnt, cell_keys, keys, act, oct_out, oct_cnt, oct_ord, level_keys;
     DevBuf out_kps, out_desc, out_n;  // staging for the host-pointer entry points
+    DevBuf lk_snap;                   // orbfe_debug_replay: one FAST's per-level key totals
     DevBuf stage, rects;              // host colour frames / rectangle masks (level-0 inputs)
     DevBuf st_off, st_items, st_sad, st_status;           // stereo workspaces (left handle)
     DevBuf st_kl, st_dl, st_kr, st_dr, st_n, st_ur, st_dp;  // stereo host-path staging
@@ -771,7 +772,7 @@ struct orbfe_extractor {
 
     ~orbfe_extractor() {
         for (DevBuf* b : {&cells, &xtab, &ytab, &bslot, &ptab, &pyr, &blur, &cell_cnt, &cell_keys, &keys, &act,
-                          &oct_out, &oct_cnt, &oct_ord, &level_keys, &out_kps, &out_desc, &out_n, &stage, &rects, &st_off, &st_items,
+                          &oct_out, &oct_cnt, &oct_ord, &level_keys, &lk_snap, &out_kps, &out_desc, &out_n, &stage, &rects, &st_off, &st_items,
                           &st_sad, &st_status, &st_kl, &st_dl, &st_kr, &st_dr, &st_n, &st_ur, &st_dp})
             b->release();
         drop_graph();
@@ -1325,12 +1326,29 @@ int orbfe_profile_read(orbfe_extractor* h, double* total_ms, int32_t* launches) 
 int orbfe_debug_replay(orbfe_extractor* h, unsigned stage_mask, int reps) {
     if (!h || !h->planned || h->last_run.n < 1 || reps < 0 || !h->last_run.kps) return ORBFE_ERR_ARG;
     DeviceGuard dg(h->device);
-    h->prof.run_mask = stage_mask;
+    const auto r = h->last_run;
+    // FAST adds its per-level key totals into level_keys and the oct-tree reads and clears them
+    // (0 between calls).  A FAST replay without the oct-tree starts from zero each time; an
+    // oct-tree replay without FAST restores one FAST's totals (recomputed once) before each
+    // launch; both leave the totals at zero, as a full extraction does.
+    const bool fast = (stage_mask >> ORBFE_STAGE_FAST) & 1u, oct = (stage_mask >> ORBFE_STAGE_OCTREE) & 1u;
+    const size_t lk = (size_t)r.n * kMaxLevels * sizeof(int);
     int st = ORBFE_OK;
-    for (int i = 0; i < reps && st == ORBFE_OK; ++i) {
-        const auto& r = h->last_run;
-        st = h->run(r.n, r.l0, r.kps, r.cap, r.desc, r.nout);
+    auto hip = [&](hipError_t e) { if (e != hipSuccess && st == ORBFE_OK) st = ORBFE_ERR_HIP; };
+    if (oct && !fast) {
+        if ((st = h->lk_snap.ensure(lk))) return st;
+        h->prof.run_mask = 1u << ORBFE_STAGE_FAST;
+        hip(hipMemsetAsync(h->level_keys.p, 0, lk, h->stream));
+        if (st == ORBFE_OK) st = h->run(r.n, r.l0, r.kps, r.cap, r.desc, r.nout);
+        hip(hipMemcpyAsync(h->lk_snap.p, h->level_keys.p, lk, hipMemcpyDeviceToDevice, h->stream));
     }
+    h->prof.run_mask = stage_mask;
+    for (int i = 0; i < reps && st == ORBFE_OK; ++i) {
+        if (fast && !oct) hip(hipMemsetAsync(h->level_keys.p, 0, lk, h->stream));
+        if (oct && !fast) hip(hipMemcpyAsync(h->level_keys.p, h->lk_snap.p, lk, hipMemcpyDeviceToDevice, h->stream));
+        if (st == ORBFE_OK) st = h->run(r.n, r.l0, r.kps, r.cap, r.desc, r.nout);
+    }
+    if (fast != oct) hip(hipMemsetAsync(h->level_keys.p, 0, lk, h->stream));
     h->prof.run_mask = h->stage_mask;
     return st;
 }

@@ -131,3 +131,55 @@ def test_preblur_probe_as_extracted(arith, monkeypatch):
                     assert np.array_equal(gb, ob), f"batch={batch} frame {f} level {l}: {(gb != ob).sum()} px"
     finally:
         e.close()
+
+
+def test_stage_mask_split_and_replay(monkeypatch):
+    """orbfe_set_stage_mask: a batch extracted in two calls on one handle (pyramid + FAST +
+    oct-tree, then describe — bench.py --pipeline's split) equals one full call and the oracle;
+    orbfe_debug_replay of single stages (FAST alone, the oct-tree alone, describe alone) leaves
+    the handle's state intact, so the next full extraction is still bit-exact."""
+    import torch
+    from orbslam_mapsave_amd.native import ORBextractor
+    for k in ALL_ENV:
+        monkeypatch.delenv(k, raising=False)
+    cfg = CONFIGS[0]
+    _, w, h, nf, sf, nl, ini, mn, check = cfg
+    imgs = _frames(cfg)
+    B = len(imgs)
+    dev = torch.device("cuda", 0)
+    e = ORBextractor(nf, sf, nl, ini, mn, device=0, max_width=w, max_height=h, max_batch=B)
+    try:
+        cap = e.capacity(w, h)
+        fr = torch.from_numpy(imgs).to(dev)
+        k = torch.zeros((B, cap * 28), dtype=torch.uint8, device=dev)
+        d = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
+        n = torch.zeros(B, dtype=torch.int32, device=dev)
+        e.set_stream(0)
+
+        def extract():
+            e.extract_batch_device(fr.data_ptr(), B, w, h, w, w * h, k.data_ptr(), cap, d.data_ptr(),
+                                   n.data_ptr())
+
+        def check_all(what):
+            torch.cuda.synchronize()
+            kk = k.cpu().numpy().view(np.uint8).reshape(B, cap, 28)
+            dd, nn = d.cpu().numpy(), n.cpu().numpy()
+            from orbslam_mapsave_amd.abi import KEYPOINT_DTYPE
+            for f in check:
+                okps, odesc = _oracle(cfg, f)
+                _same(kk[f, :nn[f]].copy().view(KEYPOINT_DTYPE).reshape(-1), dd[f, :nn[f]], okps, odesc,
+                      f"{what} frame {f}")
+
+        e.set_stages(("resize", "fast", "octree"))
+        extract()
+        e.set_stages(("describe",))
+        extract()
+        e.set_stages(None)
+        check_all("two-call split")
+        for st in (("fast",), ("octree",), ("describe",), ("resize",)):
+            e.replay(st, 3)
+        d.zero_()
+        extract()
+        check_all("full call after stage replays")
+    finally:
+        e.close()

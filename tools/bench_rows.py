@@ -140,6 +140,16 @@ def row_single():
             emit(f"single-frame latency from C++, {what} (640x480, 1000 kp)", "frames/s", 1, us * 1e-6, tc,
                  640 * 480 + 1000 * 60, "tests/cpp/adapter_test: mean of 2,000 calls after 100 warm-up "
                  "calls, C++ caller through include/orbfe_orbslam.hpp", cpu_units=1)
+    # SearchByBoW(KeyFrame*, Frame&) from C++ (Tracking.cc:1014's per-frame call), GPU against the
+    # one-thread CPU port in the same program
+    mb = re.search(r"BOW_LATENCY gpu_us=([0-9.]+) cpu_us=([0-9.]+) nodes=(\d+)/(\d+)", r.stdout)
+    if r.returncode == 0 and mb:
+        gu, cu = float(mb.group(1)), float(mb.group(2))
+        emit(f"(f)4 SearchByBoW from C++ (1000 x 1000 features, {mb.group(3)}/{mb.group(4)} nodes)",
+             "calls/s", 1, gu * 1e-6, cu * 1e-6, 2000 * (32 + 8),
+             "tests/cpp/adapter_test: orbfe::ORBmatcher::SearchByBoW vs oracle_search_by_bow, mean of "
+             "2,000 calls after 100 warm-up calls each; one kernel launch per call, the orientation "
+             "filter on the host", cpu_units=1)
 
 
 def row_stereo():
