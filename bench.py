@@ -228,11 +228,16 @@ def run_c5(args) -> None:
     T["frame_mp"], T["frame_mp_obs"] = slots[0], slots[1]
     slots0 = slots.clone()
     mt = ORBmatcher(0.8, False, device=local)
-    mt.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    # one stream of its own for the call and the slot reset in front of it (ordered with each
+    # other; the legacy default stream's implicit ordering is not needed)
+    cs = torch.cuda.Stream(dev)
+    mt.set_stream(cs.cuda_stream)
+    torch.cuda.synchronize(dev)
     out = {}
 
     def step():
-        slots.copy_(slots0)
+        with torch.cuda.stream(cs):
+            slots.copy_(slots0)
         out["r"] = mt.search_local_points_device(
             len(keys), d_keys.data_ptr(), d_desc.data_ptr(), None, W, H, scale, lm["tcw"], cam,
             log_scale, 0.5, M, T["xyz"].data_ptr(), T["normal"].data_ptr(),
@@ -252,7 +257,8 @@ def run_c5(args) -> None:
          for k, v in dict(inv=inv, px=px, py=py, pxr=pxr, pl=pl, vc=vc).items()}
 
     def step_a14():
-        slots.copy_(slots0)
+        with torch.cuda.stream(cs):
+            slots.copy_(slots0)
         out["a14"] = mt.search_by_projection_local_device(
             len(keys), d_keys.data_ptr(), d_desc.data_ptr(), None, W, H, sf_np, M,
             A["inv"].data_ptr(), T["bad"].data_ptr(), A["px"].data_ptr(), A["py"].data_ptr(),
@@ -468,7 +474,9 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
     torch.cuda.synchronize(dev)
 
     if mode == "pred":
-        main_stream = torch.cuda.current_stream(dev)
+        # the match's own stream (not the legacy default stream, whose implicit ordering the
+        # step does not need: every dependency is an explicit wait below)
+        main_stream = torch.cuda.Stream(dev)
 
         def bf(q, qn, r, rn, out):
             mt.set_stream(main_stream.cuda_stream)
@@ -562,7 +570,8 @@ def run_extract(args, dev, rank, world, local, W, H, NF, NREF, B, mode, steps, w
                     pm.gather_part(k, d_desc, d_n)
             for k in range(S):
                 main_stream.wait_stream(streams[k])
-            pm.finish(d_desc, d_n, d_out)
+            with torch.cuda.stream(main_stream):
+                pm.finish(d_desc, d_n, d_out)
             for k in range(S):
                 streams[k].wait_stream(main_stream)
 
