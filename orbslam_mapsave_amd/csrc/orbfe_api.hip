@@ -221,9 +221,6 @@ struct orbfe_extractor {
         return plan.pyr_ok && (plan.pyr_use[which] || force_pyr) && use_pyr && plan.geo.nlevels >= 2;
     }
     bool pyr_path(int n) const { return band_path(n); }  // one launch
-    // ORBFE_TAIL=0: batches make the top levels with the per-level kernels too instead of the
-    // one-workgroup-per-frame resize_tail_kernel (1024 threads, 144 KB of LDS: a CU to itself)
-    bool use_tail = !(std::getenv("ORBFE_TAIL") && std::strcmp(std::getenv("ORBFE_TAIL"), "0") == 0);
     // ORBFE_RS2=0: one resize launch per level where resize2_kernel would take two (A/B)
     bool use_rs2 = !(std::getenv("ORBFE_RS2") && std::strcmp(std::getenv("ORBFE_RS2"), "0") == 0);
     // ORBFE_RESIZE_TABLE=0: resize_kernel's horizontal pass by byte gathers (A/B)
@@ -423,7 +420,7 @@ struct orbfe_extractor {
         // K1 cascaded pyramid: one launch per level, 128 x 32 tiles of every frame; the small
         // top levels (tail_start ..) in one K1b launch, a workgroup per frame
         // (a batch of a few frames would leave most CUs idle in the tail: per-level launches)
-        const int ts = n >= kTailMinFrames && use_tail ? std::min(g.tail_start, L) : L;
+        const int ts = n >= kTailMinFrames ? std::min(g.tail_start, L) : L;
         // K1 as one launch (pyramid_kernel): every level of a band of every frame in LDS
         const int which = n >= pyr_small_below ? 0 : 1;
         const bool one_pyr = pyr_path(n);

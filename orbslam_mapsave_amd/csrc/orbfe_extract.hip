@@ -2311,35 +2311,6 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
     int bx, f;
     xcd_block(bx, f);
     const int lane = threadIdx.x & 63;
-    // the frame's waves: wave wv takes slots wv * G .. wv * G + G - 1 (grouped), or with
-    // a.wave_stride = W (the waves of a frame) slots wv, wv + W, wv + 2 W, ... (strided): then at
-    // any moment the frame's waves work on one run of W consecutive oct-tree slots — one level,
-    // clustered by the node list's quadrant order — so the 128-byte lines their windows share
-    // are fetched while they are still in the XCD's L2 (1080p: the frames in flight per XCD
-    // overflow it otherwise, DESIGN.md §5a)
-    const int wv = bx * (kDescBlock / 64) + (threadIdx.x >> 6);
-    const int stride = a.wave_stride;
-    const int s0 = stride ? wv : wv * kDescGroup;
-    // lane j < kDescGroup: slot s0 + j (grouped) or s0 + j W (strided) -> level, key, output
-    // index.  The level key counts are one load (lane q holds level q's) and their exclusive
-    // prefix a wave scan.  The slot's key does not depend on the counts (only its validity and
-    // output index do), so its load — and, at 1080p, the band order's — is issued first,
-    // unconditionally, at an index clamped into the slot's level segment, while the counts are
-    // in flight: the wave's start is one global round trip before the IC rows, not two.
-    // Grouped, the group's slots lie in the level of s0 or the next one (every level has >= 20
-    // slots); strided, each lane finds its level.
-    const int sslot = min(s0 + min(lane, kDescGroup - 1) * (stride ? stride : 1), a.out_total - 1);
-    int slv = 0, soff = 0, send = a.out_total;
-    for (int k = 1; k < a.nlevels; ++k) {
-        const bool ge = sslot >= a.out_off[k];
-        slv = ge ? k : slv;
-        soff = ge ? a.out_off[k] : soff;
-        send = !ge && send == a.out_total ? a.out_off[k] : send;
-    }
-    int sidx = sslot - soff;
-    if (stride && a.oct_ord)  // the oct-tree's band order (output order unchanged: my_o)
-        sidx = min(max((int)a.oct_ord[f * a.out_total + sslot], 0), send - soff - 1);
-    const int skey = (int)a.oct_out[f * a.out_total + soff + sidx];
     const int* cnt = a.oct_cnt + f * a.nlevels;
     // The wave's start is a chain of dependent loads (level key counts -> slot order -> key);
     // the counts, the blur fragments and the pattern pairs for LDS are all loaded first, and the
@@ -2354,13 +2325,6 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
         fr1 = a.frags[256 + (threadIdx.x & 127)];
     }
     if constexpr (kPatLds) patw_lds = reinterpret_cast<const int*>(c_pattern)[threadIdx.x];
-    typedef int i32x4m __attribute__((ext_vector_type(4)));
-    __shared__ uint4 frag_lds[kMfma && kFragLds ? 384 : 1];
-    // kPatLds: the pattern pairs as floats, pat_lds[q][lane] = pair lane + 64 q (x1, y1, x2, y2)
-    __shared__ float4 pat_lds[kPatLds ? 256 : 1];
-
-    // (everything that reads the counts comes after the key's load — issued first of all, above
-    // — so no wait for them lands in front of it)
     const int cq_raw = lane < a.nlevels ? cq_ld : 0;
     if (bx == 0 && threadIdx.x < 64) {
         const int n = wave_sum(max(cq_raw, 0));
@@ -2368,19 +2332,49 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
             a.n_out[f] = n;  // the true count: entries past kps_cap are not written (truncation
                              // is visible to the caller as n_out > kps_cap)
     }
+    typedef int i32x4m __attribute__((ext_vector_type(4)));
+    __shared__ uint4 frag_lds[kMfma && kFragLds ? 384 : 1];
+    // kPatLds: the pattern pairs as floats, pat_lds[q][lane] = pair lane + 64 q (x1, y1, x2, y2)
+    __shared__ float4 pat_lds[kPatLds ? 256 : 1];
+    // the frame's waves: wave wv takes slots wv * G .. wv * G + G - 1 (grouped), or with
+    // a.wave_stride = W (the waves of a frame) slots wv, wv + W, wv + 2 W, ... (strided): then at
+    // any moment the frame's waves work on one run of W consecutive oct-tree slots — one level,
+    // clustered by the node list's quadrant order — so the 128-byte lines their windows share
+    // are fetched while they are still in the XCD's L2 (1080p: the frames in flight per XCD
+    // overflow it otherwise, DESIGN.md §5a)
+    const int wv = bx * (kDescBlock / 64) + (threadIdx.x >> 6);
+    const int stride = a.wave_stride;
+    const int s0 = stride ? wv : wv * kDescGroup;
+
+    // lane j < kDescGroup: slot s0 + j (grouped) or s0 + j W (strided) -> level, key, output
+    // index.  The level key counts are one load (lane q holds level q's) and their exclusive
+    // prefix a wave scan, so a wave's start is one global round trip, not a chain of dependent
+    // loads.  Grouped, the group's slots lie in the level of s0 or the next one (every level
+    // has >= 20 slots); strided, each lane finds its level.
     const int cq = max(cq_raw, 0);
     const int pre = wave_inclusive_sum(cq) - cq;
     int my_l = 0, my_key = 0, my_o = 0;
     bool valid = false;
     if (stride) {
-        // strided: at any moment the frame's waves work on one run of W consecutive slots, so
-        // the windows of one run share their lines in L2
-        const int c = __shfl(cq, slv, 64), pr = __shfl(pre, slv, 64);  // every lane active
-        if (lane < kDescGroup && s0 + lane * stride < a.out_total && sslot - soff < c && sidx + pr < a.kps_cap) {
-            valid = true;
-            my_l = slv;
-            my_o = sidx + pr;
-            my_key = skey;
+        const int slot = min(s0 + min(lane, kDescGroup - 1) * stride, a.out_total - 1);
+        int lv = 0, off = 0;
+        for (int k = 1; k < a.nlevels; ++k) {
+            const bool ge = slot >= a.out_off[k];
+            lv = ge ? k : lv;
+            off = ge ? a.out_off[k] : off;
+        }
+        const int c = __shfl(cq, lv, 64), pr = __shfl(pre, lv, 64);  // every lane active
+        int idx = slot - off;
+        if (lane < kDescGroup && s0 + lane * stride < a.out_total && idx < c) {
+            // the oct-tree's band order: the frame's waves sweep each level top to bottom, so
+            // the windows of one run share their lines (output order unchanged: my_o)
+            if (a.oct_ord) idx = a.oct_ord[f * a.out_total + slot];
+            if (idx + pr < a.kps_cap) {
+                valid = true;
+                my_l = lv;
+                my_o = idx + pr;
+                my_key = (int)a.oct_out[f * a.out_total + off + idx];
+            }
         }
     }
     int l0 = 0;
@@ -2389,7 +2383,6 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
     const int off0 = a.out_off[l0], off1 = l1 > l0 ? a.out_off[l1] : a.out_total;
     const int c0 = __builtin_amdgcn_readlane(cq, l0), c1 = __builtin_amdgcn_readlane(cq, l1);
     const int p0 = __builtin_amdgcn_readlane(pre, l0), p1 = __builtin_amdgcn_readlane(pre, l1);
-    const int gkey = skey;  // grouped: the slot s0 + lane (clamped) loaded above
     if (!stride && lane < kDescGroup && s0 + lane < a.out_total) {
         const int slot = s0 + lane;
         const bool nx = slot >= off1;
@@ -2400,7 +2393,7 @@ __global__ __launch_bounds__(kDescBlock, kWin == kWinMfma ? (kDescGroup < 8 ? OR
                 valid = true;
                 my_l = nx ? l1 : l0;
                 my_o = o;
-                my_key = gkey;
+                my_key = (int)a.oct_out[f * a.out_total + slot];
             }
         }
     }

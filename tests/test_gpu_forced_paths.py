@@ -27,7 +27,6 @@ SWITCHES = [
     ("pyr_lds_40kb", {"ORBFE_PYR": "2", "ORBFE_PYR_LDS_KB": "40"}),
     ("pyr_small_below_2", {"ORBFE_PYR_SMALL_BELOW": "2"}),
     ("resize_one_level", {"ORBFE_PYR": "0", "ORBFE_RS2": "0"}),
-    ("no_tail", {"ORBFE_TAIL": "0"}),
     ("resize_byte_gather", {"ORBFE_PYR": "0", "ORBFE_RESIZE_TABLE": "0"}),
     ("desc_valu_blur", {"ORBFE_DESC_MFMA": "0"}),
     ("desc_grouped", {"ORBFE_DESC_STRIDE": "0"}),
