@@ -466,83 +466,149 @@ struct Bow1Args {
     int4 node[kBow1Nodes];  // (keyframe start, count, frame start, count) per common node
 };
 
+// One workgroup per common node.  The node's loop over its keyframe features t is sequential in
+// the reference (a frame feature taken by an earlier t is skipped, 212); here it is two parallel
+// steps per chunk of up to 256 keyframe features (one per thread):
+//   A. every (t, frame feature) distance, on all four waves (lane = t; the chunk's 64-lane blocks
+//      times a split of the frame features fill the waves; frame descriptors broadcast from LDS),
+//      reduced to each t's four smallest keys dist << 16 | frame rank;
+//   B. the greedy order as a fixed point (as the SearchForInitialization rounds, §4): every t
+//      decides at once against the claims of the previous round — a frame feature counts as taken
+//      for t when an earlier t (this chunk's or a finished chunk's) claimed it — and the rounds
+//      repeat until no decision changes.  After round k the decisions of the first k keyframe
+//      features are final, so the fixed point is the sequential result; it is reached in 2-4
+//      rounds on the adapter's problem.  t's best and second are its first two keys whose frame
+//      features are free — exact, since every key outside the four is larger; when fewer than two
+//      of the four are free (and more frame features exist) the wave recomputes t's two smallest
+//      free keys over the node, one such t at a time.
+// Ties: keys order equal distances by rank, so the first frame feature wins and counts as the
+// second too, as the strict < updates of 226-231 do.
+constexpr int kBow1Chunk = 256;  // keyframe features per chunk (one per thread)
+__device__ __forceinline__ void top4_insert(uint4& t, uint32_t k) {
+    t.w = min(t.w, max(t.z, k));
+    t.z = min(t.z, max(t.y, k));
+    t.y = min(t.y, max(t.x, k));
+    t.x = min(t.x, k);
+}
+
 __global__ __launch_bounds__(256) void bow_search1_kernel(Bow1Args a, float nnratio, int check_ori) {
-    const int lane = threadIdx.x & 63;
-    const int c = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-    if (c >= a.nodes) return;
-    const int4 w = a.node[c];
-    const int x0 = w.x, nx = w.y, y0 = w.z, ny = w.w;  // ny <= kBowNodeMax (host-checked)
-    int jf[4];
-    float fang[4];
-    uint4 d0[4], d1[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int r = lane + 64 * j;
-        const bool in = r < ny;
-        jf[j] = in ? a.fi[y0 + r] : -1;
-        fang[j] = in ? a.fa[y0 + r] : 0.f;
-        d0[j] = in ? a.fd[2 * (y0 + r)] : make_uint4(0, 0, 0, 0);
-        d1[j] = in ? a.fd[2 * (y0 + r) + 1] : make_uint4(0, 0, 0, 0);
+    __shared__ uint4 fdesc[2 * kBowNodeMax];   // the node's frame descriptors
+    __shared__ uint4 kdesc[2 * kBow1Chunk];    // the chunk's keyframe descriptors
+    __shared__ uint4 part[kBow1Chunk];         // partial four smallest keys, [split][t]
+    __shared__ float fang[kBowNodeMax];
+    __shared__ int prior[kBowNodeMax];         // claim of a finished chunk (node-wide t), or INT_MAX
+    __shared__ int owner[2][kBowNodeMax];      // claims of a round: smallest claiming t
+    __shared__ int res[kBowNodeMax];           // per frame feature: kf << 5 | bin, or -1
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int4 nd = a.node[blockIdx.x];
+    const int x0 = nd.x, nx = nd.y, y0 = nd.z, ny = nd.w;  // ny <= kBowNodeMax (host-checked)
+    if (tid < ny) {
+        fdesc[2 * tid] = a.fd[2 * (y0 + tid)];
+        fdesc[2 * tid + 1] = a.fd[2 * (y0 + tid) + 1];
+        fang[tid] = a.fa[y0 + tid];
+        prior[tid] = INT_MAX;
+        owner[0][tid] = INT_MAX;
+        res[tid] = -1;
     }
-    const int nj = (ny + 63) >> 6;
-    bool free_[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) free_[j] = lane + 64 * j < ny;
-    int mkf[4] = {-1, -1, -1, -1};  // the keyframe feature candidate j was matched to
-    int mbin[4] = {0, 0, 0, 0};
-    for (int xb = 0; xb < nx; xb += 64) {
-        const int xl = xb + lane;
-        int my_ikf = -1;
-        float my_ang = 0.f;
-        uint4 my0 = make_uint4(0, 0, 0, 0), my1 = my0;
-        if (xl < nx) {
-            my_ikf = a.ki[x0 + xl];
-            my_ang = a.ka[x0 + xl];
-            my0 = a.kd[2 * (x0 + xl)];
-            my1 = a.kd[2 * (x0 + xl) + 1];
+    for (int xc = 0; xc < nx; xc += kBow1Chunk) {
+        const int T = min(kBow1Chunk, nx - xc);
+        const bool mine = tid < T;  // thread tid is the chunk's t = tid (node-wide xc + tid)
+        int ikf = -1;
+        float ang = 0.f;
+        if (mine) {
+            kdesc[2 * tid] = a.kd[2 * (x0 + xc + tid)];
+            kdesc[2 * tid + 1] = a.kd[2 * (x0 + xc + tid) + 1];
+            ikf = a.ki[x0 + xc + tid];
+            ang = a.ka[x0 + xc + tid];
         }
-        const int cnt = min(64, nx - xb);
-        for (int t = 0; t < cnt; ++t) {
-            const uint4 q0 = make_uint4(__builtin_amdgcn_readlane(my0.x, t), __builtin_amdgcn_readlane(my0.y, t),
-                                        __builtin_amdgcn_readlane(my0.z, t), __builtin_amdgcn_readlane(my0.w, t));
-            const uint4 q1 = make_uint4(__builtin_amdgcn_readlane(my1.x, t), __builtin_amdgcn_readlane(my1.y, t),
-                                        __builtin_amdgcn_readlane(my1.z, t), __builtin_amdgcn_readlane(my1.w, t));
-            uint32_t key = 0xffffffffu;
-            int dist[4];
+        __syncthreads();
+        // A. wave wv: block tb of the chunk's t, frame features sp, sp + S, ...
+        const int TB = (T + 63) >> 6, S = TB == 1 ? 4 : TB == 2 ? 2 : 1;
+        if (wv < TB * S) {
+            const int tb = wv / S, sp = wv % S, t = tb * 64 + lane;
+            const uint4 q0 = kdesc[2 * t], q1 = kdesc[2 * t + 1];
+            uint4 k4 = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+            for (int r = sp; r < ny; r += S)
+                top4_insert(k4, ((uint32_t)hamming256(q0, q1, fdesc[2 * r], fdesc[2 * r + 1]) << 16) | (uint32_t)r);
+            part[sp * (TB * 64) + t] = k4;
+        }
+        __syncthreads();
+        uint4 k4 = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+        if (mine) {
+            k4 = part[tid];
+            for (int sp = 1; sp < S; ++sp) {
+                const uint4 o = part[sp * (TB * 64) + tid];
+                top4_insert(k4, o.x);
+                top4_insert(k4, o.y);
+                top4_insert(k4, o.z);
+                top4_insert(k4, o.w);
+            }
+        }
+        // B. rounds: decide against owner[cur], claim into owner[cur ^ 1]
+        const int tg = xc + tid;  // node-wide t
+        int dec = -1, cur = 0;
+        for (int round = 0; round <= T; ++round) {
+            const int* own = owner[cur];
+            uint32_t kb = 0xffffffffu, ks = 0xffffffffu;
+            bool known = !mine;  // both found among the four, or the candidates ran out
+            if (mine) {
+                const uint32_t kk[4] = {k4.x, k4.y, k4.z, k4.w};
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                dist[j] = 256;
-                if (j < nj && free_[j]) {
-                    dist[j] = hamming256(q0, q1, d0[j], d1[j]);
-                    key = min(key, ((uint32_t)dist[j] << 16) | (uint32_t)(lane + 64 * j));
+                for (int u = 0; u < 4; ++u) {
+                    if (known) break;
+                    const uint32_t k = kk[u];
+                    if (k == 0xffffffffu) { known = true; break; }  // no further frame features
+                    if (own[k & 0xffffu] < tg) continue;  // taken by an earlier t
+                    if (kb == 0xffffffffu) kb = k;
+                    else { ks = k; known = true; }
                 }
             }
-            key = __ockl_wfred_min_u32(key);
-            const int b1 = key == 0xffffffffu ? 256 : (int)(key >> 16);
-            const int brank = (int)(key & 0xffff);
-            int sec = 256;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (j < nj && free_[j] && lane + 64 * j != brank) sec = min(sec, dist[j]);
-            sec = __ockl_wfred_min_i32(sec);
-            if (b1 <= kThLow && (float)b1 < nnratio * (float)sec) {  // TH_LOW, ratio (233-237)
-                const int ikf = __builtin_amdgcn_readlane(my_ikf, t);
-                const float kang = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, my_ang), t));
+            // fewer than two of the four free: the wave recomputes those t one at a time
+            for (unsigned long long need = __ballot(!known); need; need &= need - 1) {
+                const int l = __builtin_ctzll(need);
+                const int tq = (wv << 6) + l;
+                const uint4 q0 = kdesc[2 * tq], q1 = kdesc[2 * tq + 1];
+                uint32_t kj[4], key = 0xffffffffu;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    if (lane + 64 * j == brank) {
-                        free_[j] = false;
-                        mkf[j] = ikf;
-                        mbin[j] = check_ori ? rot_bin(kang, fang[j]) : 0;
+                    const int r = lane + 64 * j;
+                    kj[j] = 0xffffffffu;
+                    if (r < ny && own[r] >= xc + tq) {
+                        kj[j] = ((uint32_t)hamming256(q0, q1, fdesc[2 * r], fdesc[2 * r + 1]) << 16) | (uint32_t)r;
+                        key = min(key, kj[j]);
                     }
                 }
+                const uint32_t b = __ockl_wfred_min_u32(key);
+                uint32_t k2 = 0xffffffffu;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (kj[j] != b) k2 = min(k2, kj[j]);
+                const uint32_t sc = __ockl_wfred_min_u32(k2);
+                if (lane == l) { kb = b; ks = sc; }
             }
+            const int b1 = kb == 0xffffffffu ? 256 : (int)(kb >> 16);
+            const int sec = ks == 0xffffffffu ? 256 : (int)(ks >> 16);
+            const int d = mine && b1 <= kThLow && (float)b1 < nnratio * (float)sec  // TH_LOW, ratio (233-237)
+                              ? (int)(kb & 0xffffu) : -1;
+            if (tid < ny) owner[cur ^ 1][tid] = prior[tid];
+            __syncthreads();
+            if (d >= 0) atomicMin(&owner[cur ^ 1][d], tg);
+            const bool changed = __syncthreads_or(d != dec);
+            dec = d;
+            cur ^= 1;
+            if (!changed) break;
         }
+        // the fixed point: record the chunk's matches; they are final for the next chunk
+        if (dec >= 0) {
+            res[dec] = (ikf << 5) | (check_ori ? rot_bin(ang, fang[dec]) : 0);
+            prior[dec] = tg;
+        }
+        __syncthreads();
+        if (tid < ny) owner[cur][tid] = prior[tid];  // the next chunk's first round
+        __syncthreads();
     }
     // every frame feature's outcome to its slot (the node's frame features are slots y0 ..)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-        if (lane + 64 * j < ny) a.out[y0 + lane + 64 * j] = mkf[j] >= 0 ? (mkf[j] << 5) | mbin[j] : -1;
+    if (tid < ny) a.out[y0 + tid] = res[tid];
 }
 
 }  // namespace orbfe
@@ -910,7 +976,7 @@ static int search_by_bow1(orbfe_matcher* m, float nnratio, int check_ori, const 
     a.out = reinterpret_cast<int*>(const_cast<uint8_t*>(d + o_out));
     const volatile int* out = reinterpret_cast<const volatile int*>(q + o_out);
     if ((st = m->flush())) return st;
-    hipLaunchKernelGGL(bow_search1_kernel, dim3((a.nodes + 3) / 4), dim3(256), 0, m->stream, a,
+    hipLaunchKernelGGL(bow_search1_kernel, dim3(a.nodes), dim3(256), 0, m->stream, a,
                        nnratio, check_ori);
     if (hipGetLastError() != hipSuccess) return ORBFE_ERR_HIP;
     if ((st = m->sync())) return st;

@@ -339,6 +339,41 @@ def test_gpu_search_by_bow_duplicates(ori, vocab_paths, frames):
     mt.close()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("ori", [True, False])
+def test_gpu_search_by_bow_large_nodes(ori, vocab_paths, frames):
+    """FeatureVectors at level 1 with the keyframe's descriptors three times over (~300 keyframe
+    features per node: the gathered kernel's keyframe features in more than one chunk, later
+    chunks' candidates taken by earlier ones) against the frame (~100 per node); the frame
+    against the tripled keyframe (a common node of more than 256 frame features) is refused with
+    ORBFE_ERR_UNSUPPORTED, as include/orbfe.h documents."""
+    from orbslam_mapsave_amd.abi import ORBFE_ERR_UNSUPPORTED, Frame
+    from orbslam_mapsave_amd.native import ORBmatcher, OrbfeError
+    ov = oracle.Vocabulary(vocab_paths["k10L4_l1_tfidf"])
+    kf, f = frames
+    keys = np.concatenate([kf.keys] * 3)
+    for r in (1, 2):
+        sl = slice(r * len(kf.keys), (r + 1) * len(kf.keys))
+        keys["angle"][sl] = np.mod(keys["angle"][sl] + 11.0 * r, 360.0).astype(np.float32)
+    k3 = Frame(keys, np.concatenate([kf.desc] * 3), S.W, S.H, kf.scale_factors)
+    mt = ORBmatcher(0.9, ori, device=0)
+    for a_, b_ in ((k3, f), (f, k3)):
+        afv = ov.transform(a_.desc, 3)[2:]
+        bfv = ov.transform(b_.desc, 3)[2:]
+        ok = np.ones(a_.n, np.uint8)
+        ok[::7] = 0
+        om, onm = oracle.search_by_bow(a_.desc, a_.keys["angle"], ok, afv, b_.desc,
+                                       b_.keys["angle"], bfv, 0.9, ori)
+        if np.diff(bfv[1]).max() > 256:
+            with pytest.raises(OrbfeError) as e:
+                mt.SearchByBoW(a_.desc, a_.keys["angle"], ok, afv, b_.desc, b_.keys["angle"], bfv)
+            assert e.value.status == ORBFE_ERR_UNSUPPORTED
+            continue
+        m, nm = mt.SearchByBoW(a_.desc, a_.keys["angle"], ok, afv, b_.desc, b_.keys["angle"], bfv)
+        assert onm > 0 and nm == onm and np.array_equal(m, om)
+    mt.close()
+
+
 def pack_slots(items, cap):
     """(desc, angle, ok, fv) per slot -> arrays in orbfe_bow_transform_batch_device's layout."""
     S_ = len(items)
