@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -454,6 +456,8 @@ __global__ __launch_bounds__(kBowSearchBlock) void bow_search_kernel(BowMatchArg
 // host applies the orientation filter (259-281, ComputeThreeMaxima over the slots) as the
 // reference does on the CPU: one launch per call.
 constexpr int kBow1Nodes = 192;
+constexpr int kSlotPending = INT_MIN;  // an output slot the kernel has not written yet
+constexpr int kSlotWaitUs = 2000;      // slot polling before the stream synchronisation
 struct Bow1Args {
     const uint4* kd;  // keyframe features in node order: descriptors (2 x uint4 each),
     const int* ki;    //   keyframe feature indices,
@@ -502,10 +506,26 @@ __global__ __launch_bounds__(256) void bow_search1_kernel(Bow1Args a, float nnra
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int4 nd = a.node[blockIdx.x];
     const int x0 = nd.x, nx = nd.y, y0 = nd.z, ny = nd.w;  // ny <= kBowNodeMax (host-checked)
+    // the frame features and the first chunk's keyframe features in one round of loads (the
+    // inputs are in device-mapped host memory: each round is a PCIe round trip)
+    uint4 f0 = make_uint4(0, 0, 0, 0), f1 = f0, c0 = f0, c1 = f0;
+    float fa = 0.f, ang = 0.f;
+    int ikf = -1;
     if (tid < ny) {
-        fdesc[2 * tid] = a.fd[2 * (y0 + tid)];
-        fdesc[2 * tid + 1] = a.fd[2 * (y0 + tid) + 1];
-        fang[tid] = a.fa[y0 + tid];
+        f0 = a.fd[2 * (y0 + tid)];
+        f1 = a.fd[2 * (y0 + tid) + 1];
+        fa = a.fa[y0 + tid];
+    }
+    if (tid < min(nx, kBow1Chunk)) {
+        c0 = a.kd[2 * (x0 + tid)];
+        c1 = a.kd[2 * (x0 + tid) + 1];
+        ikf = a.ki[x0 + tid];
+        ang = a.ka[x0 + tid];
+    }
+    if (tid < ny) {
+        fdesc[2 * tid] = f0;
+        fdesc[2 * tid + 1] = f1;
+        fang[tid] = fa;
         prior[tid] = INT_MAX;
         owner[0][tid] = INT_MAX;
         res[tid] = -1;
@@ -513,13 +533,15 @@ __global__ __launch_bounds__(256) void bow_search1_kernel(Bow1Args a, float nnra
     for (int xc = 0; xc < nx; xc += kBow1Chunk) {
         const int T = min(kBow1Chunk, nx - xc);
         const bool mine = tid < T;  // thread tid is the chunk's t = tid (node-wide xc + tid)
-        int ikf = -1;
-        float ang = 0.f;
         if (mine) {
-            kdesc[2 * tid] = a.kd[2 * (x0 + xc + tid)];
-            kdesc[2 * tid + 1] = a.kd[2 * (x0 + xc + tid) + 1];
-            ikf = a.ki[x0 + xc + tid];
-            ang = a.ka[x0 + xc + tid];
+            if (xc) {
+                c0 = a.kd[2 * (x0 + xc + tid)];
+                c1 = a.kd[2 * (x0 + xc + tid) + 1];
+                ikf = a.ki[x0 + xc + tid];
+                ang = a.ka[x0 + xc + tid];
+            }
+            kdesc[2 * tid] = c0;
+            kdesc[2 * tid + 1] = c1;
         }
         __syncthreads();
         // A. wave wv: block tb of the chunk's t, frame features sp, sp + S, ...
@@ -528,6 +550,7 @@ __global__ __launch_bounds__(256) void bow_search1_kernel(Bow1Args a, float nnra
             const int tb = wv / S, sp = wv % S, t = tb * 64 + lane;
             const uint4 q0 = kdesc[2 * t], q1 = kdesc[2 * t + 1];
             uint4 k4 = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+#pragma unroll 4
             for (int r = sp; r < ny; r += S)
                 top4_insert(k4, ((uint32_t)hamming256(q0, q1, fdesc[2 * r], fdesc[2 * r + 1]) << 16) | (uint32_t)r);
             part[sp * (TB * 64) + t] = k4;
@@ -607,8 +630,9 @@ __global__ __launch_bounds__(256) void bow_search1_kernel(Bow1Args a, float nnra
         if (tid < ny) owner[cur][tid] = prior[tid];  // the next chunk's first round
         __syncthreads();
     }
-    // every frame feature's outcome to its slot (the node's frame features are slots y0 ..)
-    if (tid < ny) a.out[y0 + tid] = res[tid];
+    // every frame feature's outcome to its slot (the node's frame features are slots y0 ..): a
+    // system-scope store, since the host polls the slots
+    if (tid < ny) __hip_atomic_store(a.out + y0 + tid, res[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace orbfe
@@ -974,12 +998,32 @@ static int search_by_bow1(orbfe_matcher* m, float nnratio, int check_ori, const 
     a.fi = reinterpret_cast<const int*>(d + o_fi);
     a.fa = reinterpret_cast<const float*>(d + o_fa);
     a.out = reinterpret_cast<int*>(const_cast<uint8_t*>(d + o_out));
-    const volatile int* out = reinterpret_cast<const volatile int*>(q + o_out);
+    volatile int* out = reinterpret_cast<volatile int*>(q + o_out);
+    for (int s = 0; s < ftot; ++s) out[s] = kSlotPending;
     if ((st = m->flush())) return st;
     hipLaunchKernelGGL(bow_search1_kernel, dim3(a.nodes), dim3(256), 0, m->stream, a,
                        nnratio, check_ori);
     if (hipGetLastError() != hipSuccess) return ORBFE_ERR_HIP;
-    if ((st = m->sync())) return st;
+    if (!m->pend.empty() || !m->dnq.empty() || m->cand_check) {
+        if ((st = m->sync())) return st;
+    } else {
+        // every slot is written once, after its node's last read of the staging buffer: the host
+        // waits on the slots themselves instead of a stream synchronisation; past kSlotWaitUs it
+        // synchronises the stream (which reports a failed kernel) and checks the slots again
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int s = 0; s < ftot; ++s) {
+            while (out[s] == kSlotPending) {
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSlotWaitUs)) {
+                    ORBFE_HIP(hipStreamSynchronize(m->stream));
+                    for (int u = s; u < ftot; ++u)
+                        if (out[u] == kSlotPending) return ORBFE_ERR_HIP;
+                    s = ftot;
+                    break;
+                }
+                __builtin_ia32_pause();
+            }
+        }
+    }
     // the orientation filter (259-281) on the host, as in the reference: the rotation histogram
     // of every match, ComputeThreeMaxima (1604-1645), matches outside the three bins dropped
     int hist[kHistLen] = {};
