@@ -550,7 +550,6 @@ __global__ __launch_bounds__(256) void bow_search1_kernel(Bow1Args a, float nnra
             const int tb = wv / S, sp = wv % S, t = tb * 64 + lane;
             const uint4 q0 = kdesc[2 * t], q1 = kdesc[2 * t + 1];
             uint4 k4 = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
-#pragma unroll 4
             for (int r = sp; r < ny; r += S)
                 top4_insert(k4, ((uint32_t)hamming256(q0, q1, fdesc[2 * r], fdesc[2 * r + 1]) << 16) | (uint32_t)r);
             part[sp * (TB * 64) + t] = k4;

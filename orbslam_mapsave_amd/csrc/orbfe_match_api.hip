@@ -5,6 +5,7 @@
 #include <map>
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <functional>
 #include <cmath>
@@ -26,23 +27,39 @@ struct UpScatter {
     uint32_t bytes[kMaxUpSeg];
 };
 // Results of a host-form call go the other way in one launch: each segment copies device
-// bytes into the (device-mapped) pinned staging buffer, so a call ends with this kernel and
-// one stream synchronisation instead of a DMA per output array.
-__global__ __launch_bounds__(256) void download_gather_kernel(UpScatter a) {
+// bytes into the (device-mapped) pinned staging buffer, so a call ends with this kernel instead
+// of a DMA per output array.  With a done word (flag, device-mapped pinned memory) the last
+// workgroup to finish writes seq to it after every workgroup's copies are released to system
+// scope: the host waits on that word instead of synchronising the stream.
+struct DnDone {
+    int* ctr;   // device counter of finished workgroups (zero between launches)
+    int* flag;  // null: no done word
+    int seq, blocks;
+};
+__global__ __launch_bounds__(256) void download_gather_kernel(UpScatter a, DnDone dd) {
     const int s = blockIdx.y;
-    if (s >= a.n) return;
-    const uint32_t nb = a.bytes[s];
-    const uint8_t* src = a.src[s];
-    uint8_t* dst = a.dst[s];
-    // dword copies when both ends are 4-byte aligned (device buffers and 256-B staging slots)
-    if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 3) == 0) {
-        const uint32_t n4 = nb >> 2;
-        const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
-        uint32_t* d4 = reinterpret_cast<uint32_t*>(dst);
-        for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) d4[i] = s4[i];
-        if (blockIdx.x == 0 && threadIdx.x < (nb & 3)) dst[4 * n4 + threadIdx.x] = src[4 * n4 + threadIdx.x];
-    } else {
-        for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nb; i += gridDim.x * 256) dst[i] = src[i];
+    if (s < a.n) {
+        const uint32_t nb = a.bytes[s];
+        const uint8_t* src = a.src[s];
+        uint8_t* dst = a.dst[s];
+        // dword copies when both ends are 4-byte aligned (device buffers and 256-B staging slots)
+        if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 3) == 0) {
+            const uint32_t n4 = nb >> 2;
+            const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
+            uint32_t* d4 = reinterpret_cast<uint32_t*>(dst);
+            for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) d4[i] = s4[i];
+            if (blockIdx.x == 0 && threadIdx.x < (nb & 3)) dst[4 * n4 + threadIdx.x] = src[4 * n4 + threadIdx.x];
+        } else {
+            for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nb; i += gridDim.x * 256) dst[i] = src[i];
+        }
+    }
+    if (!dd.flag) return;
+    __threadfence_system();  // this thread's copies, to system scope
+    __syncthreads();
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(dd.ctr, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == dd.blocks - 1) {
+        __hip_atomic_store(dd.ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(dd.flag, dd.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 __global__ __launch_bounds__(256) void upload_scatter_kernel(UpScatter a) {
@@ -136,6 +153,8 @@ struct orbfe_matcher {
         prof.release();
         if (own) hipStreamDestroy(own);
         if (stat_host) hipHostFree(stat_host);
+        if (dn_flag_host) hipHostFree(dn_flag_host);
+        dn_ctr.release();
     }
 
     // Host transfers go through a pinned staging buffer: the copy into it is a CPU memcpy and
@@ -242,7 +261,29 @@ struct orbfe_matcher {
         pend.push_back(Pending{dst, q, bytes});
         return ORBFE_OK;
     }
-    int gather() {
+    // The done word of the download gather (device-mapped pinned memory) and its counter.
+    int* dn_flag_host = nullptr;
+    int* dn_flag_dev = nullptr;
+    int dn_seq = 0;
+    DevBuf dn_ctr;
+    // *waited = true: the last launch carries the done word and the host waited on it
+    int gather(bool* waited = nullptr) {
+        if (waited) *waited = false;
+        if (waited && !dnq.empty() && !prof.on && !dn_flag_host) {
+            void* q = nullptr;
+            void* dq = nullptr;
+            if (dn_ctr.ensure(64) == ORBFE_OK && hipMemsetAsync(dn_ctr.p, 0, 64, stream) == hipSuccess &&
+                hipHostMalloc(&q, 64, hipHostMallocDefault) == hipSuccess) {
+                if (hipHostGetDevicePointer(&dq, q, 0) == hipSuccess) {
+                    dn_flag_host = static_cast<int*>(q);
+                    dn_flag_dev = static_cast<int*>(dq);
+                    *dn_flag_host = dn_seq;
+                } else {
+                    hipHostFree(q);
+                }
+            }
+        }
+        const bool flagged = waited && !dnq.empty() && !prof.on && dn_flag_host;
         for (size_t b = 0; b < dnq.size(); b += kMaxUpSeg) {
             UpScatter a;
             a.n = (int)std::min<size_t>(kMaxUpSeg, dnq.size() - b);
@@ -254,17 +295,35 @@ struct orbfe_matcher {
                 mx = std::max(mx, dnq[b + i].bytes);
             }
             const int gx = (int)std::min<size_t>(64, std::max<size_t>(1, (mx / 4 + 255) / 256));
-            hipLaunchKernelGGL(download_gather_kernel, dim3(gx, a.n), dim3(256), 0, stream, a);
+            DnDone dd{nullptr, nullptr, 0, 0};
+            if (flagged && b + kMaxUpSeg >= dnq.size()) dd = DnDone{dn_ctr.as<int>(), dn_flag_dev, ++dn_seq, gx * a.n};
+            hipLaunchKernelGGL(download_gather_kernel, dim3(gx, a.n), dim3(256), 0, stream, a, dd);
         }
         dnq.clear();
         ORBFE_HIP(hipGetLastError());
+        if (flagged) {
+            // the stream's earlier kernels finished before the gather ran; bounded wait, then the
+            // stream synchronisation (which also reports a failed kernel)
+            const volatile int* fl = dn_flag_host;
+            const auto t0 = std::chrono::steady_clock::now();
+            while (*fl != dn_seq) {
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(2000)) {
+                    ORBFE_HIP(hipStreamSynchronize(stream));
+                    if (*fl != dn_seq) return ORBFE_ERR_HIP;
+                    break;
+                }
+                __builtin_ia32_pause();
+            }
+            *waited = true;
+        }
         return ORBFE_OK;
     }
     int sync() {
         int st;
         if ((st = flush())) return st;
-        if ((st = gather())) return st;
-        ORBFE_HIP(hipStreamSynchronize(stream));
+        bool waited = false;
+        if ((st = gather(&waited))) return st;
+        if (!waited) ORBFE_HIP(hipStreamSynchronize(stream));
         if (cand_check) {  // csr_async: the candidates must have fit before results count
             int total = 0;
             for (const Pending& d : pend)
