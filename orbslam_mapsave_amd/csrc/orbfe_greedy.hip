@@ -384,16 +384,22 @@ __global__ __launch_bounds__(kGreedyBlock) void greedy_accept_kernel(GreedyArgs 
             int r = 0;
             while (r < a.conv_round && a.chg[r] != 0) ++r;
             a.stats[5] = r + 1;                            // rounds to the fixed point
+            *a.done = 0;
             if (a.hstats) {
                 a.hstats[0] = __hip_atomic_load(a.nm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 a.hstats[1] = in;
                 a.hstats[2] = a.stats[2];
                 a.hstats[3] = ovf;
-                a.hstats[4] = a.stats[4];
                 a.hstats[5] = r + 1;
             }
-            *a.done = 0;
         }
+    }
+    // hstats[4] last, released to system scope after every thread's slot writes: the host waits
+    // on it (it holds -1 until then) instead of synchronising the stream
+    if (a.hstats) {
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(&a.hstats[4], a.stats[4], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 

@@ -665,7 +665,20 @@ int sbp_local_fast(orbfe_matcher* m, const orbfe_frame_view* frame, const Frustu
     for (int k = 0; k < 6; ++k) host[k] = 0;
     if (!m->stat_host)
         ORBFE_HIP(hipMemcpyAsync(host, m->scal.p, 6 * sizeof(int), hipMemcpyDeviceToHost, m->stream));
-    ORBFE_HIP(hipStreamSynchronize(m->stream));
+    if (m->stat_host && !m->prof.on) {
+        // the accept kernel's last workgroup releases the slots and then writes stat_host[4]
+        // (-1 until then): wait on it; past 2 ms synchronise the stream (reports a failed kernel)
+        const auto t0 = std::chrono::steady_clock::now();
+        while (__atomic_load_n(&m->stat_host[4], __ATOMIC_ACQUIRE) == -1) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(2000)) {
+                ORBFE_HIP(hipStreamSynchronize(m->stream));
+                break;
+            }
+            __builtin_ia32_pause();
+        }
+    } else {
+        ORBFE_HIP(hipStreamSynchronize(m->stream));
+    }
     if (m->stat_host)
         for (int k = 0; k < 6; ++k) host[k] = __atomic_load_n(&m->stat_host[k], __ATOMIC_ACQUIRE);
     if (!host[3] && host[4] == 0) {  // no overflow, converged
