@@ -448,13 +448,13 @@ __global__ __launch_bounds__(kBowSearchBlock) void bow_search_kernel(BowMatchArg
 // two FeatureVectors as the reference does (ORBmatcher.cc:195-256: equal node ids are matched,
 // otherwise the lagging side jumps to lower_bound of the other's id) and gathers each common
 // node's features, in the reference's order, into the device-mapped pinned staging buffer —
-// keyframe features without a good map point (202-207) left out — so a wave reads its node's
-// descriptors, indices and angles in one round of loads with no index chain (the common nodes
-// themselves ride in the kernel arguments).  The node loop is bow_search_kernel's; each frame
-// feature's outcome — its keyframe feature and rotation bin, or -1 — is written to its own slot
-// of the pinned output (one slot per gathered frame feature: no counter, no atomics), and the
-// host applies the orientation filter (259-281, ComputeThreeMaxima over the slots) as the
-// reference does on the CPU: one launch per call.
+// keyframe features without a good map point (202-207) left out — so a node's workgroup reads
+// its descriptors, indices and angles in one round of loads with no index chain (the common
+// nodes themselves ride in the kernel arguments).  Each frame feature's outcome — its keyframe
+// feature and rotation bin, or -1 — is written to its own slot of the pinned output (one slot per
+// gathered frame feature: no counter, no atomics); the host waits on the slots and applies the
+// orientation filter (259-281, ComputeThreeMaxima over the slots) as the reference does on the
+// CPU: one launch per call.
 constexpr int kBow1Nodes = 192;
 constexpr int kSlotPending = INT_MIN;  // an output slot the kernel has not written yet
 constexpr int kSlotWaitUs = 2000;      // slot polling before the stream synchronisation
