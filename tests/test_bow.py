@@ -374,6 +374,46 @@ def test_gpu_search_by_bow_large_nodes(ori, vocab_paths, frames):
     mt.close()
 
 
+def _flip(rng, d, nbits):
+    """d with nbits distinct random bits flipped."""
+    out = d.copy()
+    for b in rng.choice(256, size=nbits, replace=False):
+        out[b >> 3] ^= np.uint8(1 << (b & 7))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ori", [True, False])
+@pytest.mark.parametrize("bases,copies,nkf", [(6, 6, 150), (32, 8, 600)])
+def test_gpu_search_by_bow_contended_node(bases, copies, nkf, ori):
+    """One common node where keyframe features queue for the same frame features: frame feature
+    (j, c) is base descriptor j with 4 c bits flipped, keyframe feature t is base t mod B with 2
+    bits flipped, so the t of one base take copies 0, 1, 2, ... in turn (ratio 0.99).  Later t
+    find three or all of their four nearest frame features taken (the gathered kernel's
+    wave-parallel recomputation) and the fixed point needs one round per copy of a base; at
+    (32, 8, 600) the node holds the maximum 256 frame features and 600 keyframe features (three
+    chunks).  Bit-exact against the oracle (ORBmatcher.cc:211-248)."""
+    from orbslam_mapsave_amd.native import ORBmatcher
+    rng = np.random.Generator(np.random.PCG64(bases * 1000 + nkf))
+    base = rng.integers(0, 256, size=(bases, 32), dtype=np.uint8)
+    fd = np.stack([_flip(rng, base[j], 4 * c) for j in range(bases) for c in range(copies)])
+    kd = np.stack([_flip(rng, base[t % bases], 2) for t in range(nkf)])
+    fa = rng.uniform(0, 360, size=len(fd)).astype(np.float32)
+    ka = rng.uniform(0, 360, size=nkf).astype(np.float32)
+    ok = (rng.uniform(size=nkf) < 0.9).astype(np.uint8)
+    one = lambda n: (np.array([7], np.int32), np.array([0, n], np.int32), np.arange(n, dtype=np.int32))
+    kfv, ffv = one(nkf), one(len(fd))
+    om, onm = oracle.search_by_bow(kd, ka, ok, kfv, fd, fa, ffv, 0.99, ori)
+    assert onm >= bases * 2
+    mt = ORBmatcher(0.99, ori, device=0)
+    try:
+        for _ in range(2):
+            m, nm = mt.SearchByBoW(kd, ka, ok, kfv, fd, fa, ffv)
+            assert nm == onm and np.array_equal(m, om)
+    finally:
+        mt.close()
+
+
 def pack_slots(items, cap):
     """(desc, angle, ok, fv) per slot -> arrays in orbfe_bow_transform_batch_device's layout."""
     S_ = len(items)
