@@ -475,30 +475,30 @@ struct Bow1Args {
 // steps per chunk of up to 256 keyframe features (one per thread):
 //   A. every (t, frame feature) distance, on all four waves (lane = t; the chunk's 64-lane blocks
 //      times a split of the frame features fill the waves; frame descriptors broadcast from LDS),
-//      reduced to each t's four smallest keys dist << 16 | frame rank;
+//      reduced to each t's kBowK smallest keys dist << 16 | frame rank;
 //   B. the greedy order as a fixed point (as the SearchForInitialization rounds, §4): every t
 //      decides at once against the claims of the previous round — a frame feature counts as taken
 //      for t when an earlier t (this chunk's or a finished chunk's) claimed it — and the rounds
 //      repeat until no decision changes.  After round k the decisions of the first k keyframe
 //      features are final, so the fixed point is the sequential result; it is reached in 2-4
 //      rounds on the adapter's problem.  t's best and second are its first two keys whose frame
-//      features are free — exact, since every key outside the four is larger; when fewer than two
-//      of the four are free (and more frame features exist) the wave recomputes t's two smallest
+//      features are free — exact, since every key not kept is larger; when fewer than two of the
+//      kept keys are free (and more frame features exist) the wave recomputes t's two smallest
 //      free keys over the node, one such t at a time.
 // Ties: keys order equal distances by rank, so the first frame feature wins and counts as the
 // second too, as the strict < updates of 226-231 do.
 constexpr int kBow1Chunk = 256;  // keyframe features per chunk (one per thread)
-__device__ __forceinline__ void top4_insert(uint4& t, uint32_t k) {
-    t.w = min(t.w, max(t.z, k));
-    t.z = min(t.z, max(t.y, k));
-    t.y = min(t.y, max(t.x, k));
-    t.x = min(t.x, k);
+constexpr int kBowK = 8;         // smallest keys kept per keyframe feature
+__device__ __forceinline__ void topk_insert(uint32_t (&t)[kBowK], uint32_t k) {
+#pragma unroll
+    for (int i = kBowK - 1; i > 0; --i) t[i] = min(t[i], max(t[i - 1], k));
+    t[0] = min(t[0], k);
 }
 
 __global__ __launch_bounds__(256) void bow_search1_kernel(Bow1Args a, float nnratio, int check_ori) {
     __shared__ uint4 fdesc[2 * kBowNodeMax];   // the node's frame descriptors
     __shared__ uint4 kdesc[2 * kBow1Chunk];    // the chunk's keyframe descriptors
-    __shared__ uint4 part[kBow1Chunk];         // partial four smallest keys, [split][t]
+    __shared__ uint4 part[kBowK / 4 * kBow1Chunk];  // partial smallest keys, [split][t][kBowK / 4]
     __shared__ float fang[kBowNodeMax];
     __shared__ int prior[kBowNodeMax];         // claim of a finished chunk (node-wide t), or INT_MAX
     __shared__ int owner[2][kBowNodeMax];      // claims of a round: smallest claiming t
@@ -546,24 +546,38 @@ __global__ __launch_bounds__(256) void bow_search1_kernel(Bow1Args a, float nnra
         __syncthreads();
         // A. wave wv: block tb of the chunk's t, frame features sp, sp + S, ...
         const int TB = (T + 63) >> 6, S = TB == 1 ? 4 : TB == 2 ? 2 : 1;
+        uint32_t kk[kBowK];
+#pragma unroll
+        for (int u = 0; u < kBowK; ++u) kk[u] = 0xffffffffu;
         if (wv < TB * S) {
             const int tb = wv / S, sp = wv % S, t = tb * 64 + lane;
             const uint4 q0 = kdesc[2 * t], q1 = kdesc[2 * t + 1];
-            uint4 k4 = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
             for (int r = sp; r < ny; r += S)
-                top4_insert(k4, ((uint32_t)hamming256(q0, q1, fdesc[2 * r], fdesc[2 * r + 1]) << 16) | (uint32_t)r);
-            part[sp * (TB * 64) + t] = k4;
+                topk_insert(kk, ((uint32_t)hamming256(q0, q1, fdesc[2 * r], fdesc[2 * r + 1]) << 16) | (uint32_t)r);
+            uint4* pp = part + (kBowK / 4) * (sp * (TB * 64) + t);
+#pragma unroll
+            for (int v = 0; v < kBowK / 4; ++v)
+                pp[v] = make_uint4(kk[4 * v], kk[4 * v + 1], kk[4 * v + 2], kk[4 * v + 3]);
         }
         __syncthreads();
-        uint4 k4 = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
         if (mine) {
-            k4 = part[tid];
+#pragma unroll
+            for (int v = 0; v < kBowK / 4; ++v) {
+                const uint4 o = part[(kBowK / 4) * tid + v];
+                kk[4 * v] = o.x;
+                kk[4 * v + 1] = o.y;
+                kk[4 * v + 2] = o.z;
+                kk[4 * v + 3] = o.w;
+            }
             for (int sp = 1; sp < S; ++sp) {
-                const uint4 o = part[sp * (TB * 64) + tid];
-                top4_insert(k4, o.x);
-                top4_insert(k4, o.y);
-                top4_insert(k4, o.z);
-                top4_insert(k4, o.w);
+#pragma unroll
+                for (int v = 0; v < kBowK / 4; ++v) {
+                    const uint4 o = part[(kBowK / 4) * (sp * (TB * 64) + tid) + v];
+                    topk_insert(kk, o.x);
+                    topk_insert(kk, o.y);
+                    topk_insert(kk, o.z);
+                    topk_insert(kk, o.w);
+                }
             }
         }
         // B. rounds: decide against owner[cur], claim into owner[cur ^ 1]
@@ -572,20 +586,22 @@ __global__ __launch_bounds__(256) void bow_search1_kernel(Bow1Args a, float nnra
         for (int round = 0; round <= T; ++round) {
             const int* own = owner[cur];
             uint32_t kb = 0xffffffffu, ks = 0xffffffffu;
-            bool known = !mine;  // both found among the four, or the candidates ran out
+            bool known = !mine;  // both found among the kept keys, or the candidates ran out
             if (mine) {
-                const uint32_t kk[4] = {k4.x, k4.y, k4.z, k4.w};
+                int ow[kBowK];  // every kept key's claim read at once (no chain of LDS reads)
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < kBowK; ++u) ow[u] = own[min((int)(kk[u] & 0xffffu), kBowNodeMax - 1)];
+#pragma unroll
+                for (int u = 0; u < kBowK; ++u) {
                     if (known) break;
                     const uint32_t k = kk[u];
                     if (k == 0xffffffffu) { known = true; break; }  // no further frame features
-                    if (own[k & 0xffffu] < tg) continue;  // taken by an earlier t
+                    if (ow[u] < tg) continue;  // taken by an earlier t
                     if (kb == 0xffffffffu) kb = k;
                     else { ks = k; known = true; }
                 }
             }
-            // fewer than two of the four free: the wave recomputes those t one at a time
+            // fewer than two of the kept keys free: the wave recomputes those t one at a time
             for (unsigned long long need = __ballot(!known); need; need &= need - 1) {
                 const int l = __builtin_ctzll(need);
                 const int tq = (wv << 6) + l;
