@@ -1181,10 +1181,16 @@ struct SbpKfArgs {
     int* cnt;
     const int* off;
     int2* cand;
+    int kfix;                 // kMode 2: candidate slots per point
+    int* ovf;                 // kMode 2: points with more candidates than kfix
 };
 
-template <bool FILL>
+// kMode 0: count the candidates, 1: fill the CSR lists (after the scan), 2: the fixed-slot form
+// in one pass — the first kfix candidates of point i at i * kfix, min(n, kfix) in cnt[i], and a
+// point with more raises *ovf (the host then reruns the call on the CSR path).
+template <int kMode>
 __global__ __launch_bounds__(256) void sbp_kf_cand_kernel(SbpKfArgs a) {
+    constexpr bool FILL = kMode == 1;
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per keyframe map point
     if (i >= a.n) return;
     // Every per-point input is read up front and feeds the unconditional arithmetic below, so
@@ -1216,11 +1222,11 @@ __global__ __launch_bounds__(256) void sbp_kf_cand_kernel(SbpKfArgs a) {
             } else {
                 const float radius = a.th * a.scale[lvl];
                 const uint4 q0 = a.desc[2 * i], q1 = a.desc[2 * i + 1];
-                int2* out = FILL ? a.cand + a.off[i] : nullptr;
+                int2* out = FILL ? a.cand + a.off[i] : kMode == 2 ? a.cand + (size_t)i * a.kfix : nullptr;
                 n = features_in_area_wave(
                     a.cur, u, v, radius, lvl - 1, lvl + 1, [](int) { return true; },
                     [&](int i2, int rank) {
-                        if (FILL) {
+                        if (FILL || (kMode == 2 && rank < a.kfix)) {
                             const uint4* d = a.cur.desc + 2 * i2;
                             out[rank] = make_int2(i2, hamming256(q0, q1, d[0], d[1]));
                         }
@@ -1228,7 +1234,11 @@ __global__ __launch_bounds__(256) void sbp_kf_cand_kernel(SbpKfArgs a) {
             }
         }
     }
-    if (!FILL && (threadIdx.x & 63) == 0) a.cnt[i] = n;
+    if (kMode == 0 && (threadIdx.x & 63) == 0) a.cnt[i] = n;
+    if (kMode == 2 && (threadIdx.x & 63) == 0) {
+        a.cnt[i] = min(n, a.kfix);
+        if (n > a.kfix) atomicAdd(a.ovf, 1);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -1142,7 +1142,13 @@ int orbfe_search_by_projection_keyframe(orbfe_matcher* m, int check_ori,
         (n_kf && (!kf_key_angle || !kf_mp_valid || !kf_mp_bad || !already_found || !kf_mp_xyz ||
                   !kf_mp_desc || !kf_mp_min_dist || !kf_mp_max_dist)))
         return ORBFE_ERR_ARG;
+    // the fixed-slot candidates (one kernel instead of count / scan / fill) unless a point has
+    // more than kSbpFix of them: then the call runs again on the CSR path from the saved slots
+    std::vector<int32_t> fmp_in;
+    bool fix = cur->n > 0 && n_kf > 0;
+    if (fix) fmp_in.assign(frame_mp, frame_mp + cur->n);
     return guarded(m, [&]() {
+      for (;;) {
         int st;
         SbpKfArgs a;
         // every upload is staged before the frame's flush: one H2D copy + one scatter launch;
@@ -1185,8 +1191,19 @@ int orbfe_search_by_projection_keyframe(orbfe_matcher* m, int check_ori,
         a.log_scale = log_scale_factor;
         a.th = th;
         a.status = m->scal.as<int>() + 1;
-        if ((st = m->csr_async(a, n_kf, sbp_kf_cand_kernel<false>, sbp_kf_cand_kernel<true>, 4)))
+        a.kfix = kSbpFix;
+        a.ovf = m->scal.as<int>() + 2;
+        if (fix) {
+            if ((st = m->cnt.ensure((size_t)n_kf * sizeof(int)))) return st;
+            if ((st = m->cand.ensure((size_t)n_kf * kSbpFix * sizeof(int2)))) return st;
+            a.cnt = m->cnt.as<int>();
+            a.cand = m->cand.as<int2>();
+            if ((st = m->flush())) return st;
+            hipLaunchKernelGGL(sbp_kf_cand_kernel<2>, dim3((n_kf + 3) / 4), dim3(256), 0, m->stream, a);
+            ORBFE_HIP(hipGetLastError());
+        } else if ((st = m->csr_async(a, n_kf, sbp_kf_cand_kernel<0>, sbp_kf_cand_kernel<1>, 4))) {
             return st;
+        }
         const int N = cur->n;
         GreedyArgs g{};
         g.m = n_kf;
@@ -1202,15 +1219,27 @@ int orbfe_search_by_projection_keyframe(orbfe_matcher* m, int check_ori,
         g.q_angle = m->m_f3.as<float>();  // pKF->mvKeysUn[i].angle (1549)
         g.k = a.cur.k;
         g.ids = kf_mp_ids ? m->o_i.as<int>() : nullptr;
+        if (fix) {
+            g.kfix = kSbpFix;
+            g.fcnt = m->cnt.as<int>();
+        }
         if ((st = m->greedy(g))) return st;
         if ((st = m->down(frame_mp, m->s1, (size_t)N * 4))) return st;
-        // {nmatches, status}: status != 0 is a predicted level outside the pyramid (outputs
-        // then unspecified)
-        int res[2] = {0, 0};
+        // {nmatches, status, overflow}: status != 0 is a predicted level outside the pyramid
+        // (outputs then unspecified)
+        int res[3] = {0, 0, 0};
         if ((st = m->down(res, m->scal, sizeof(res)))) return st;
         if ((st = m->sync())) return st;
+        if (fix && res[2] > 0) {  // a point past kSbpFix candidates: the CSR path from the input
+            std::memcpy(frame_mp, fmp_in.data(), (size_t)N * 4);
+            fix = false;
+            ++m->capacity_retries;
+            m->begin();
+            continue;
+        }
         *nmatches = res[0];
         return res[1];
+      }
     });
 }
 

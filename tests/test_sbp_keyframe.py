@@ -112,8 +112,11 @@ def test_oracle_vs_restatement(seed, th, od):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed,th,od,ori", [(0, 10, 100, True), (1, 3, 64, True),
-                                            (2, 10, 100, False), (3, 3, 64, True)])
+                                            (2, 10, 100, False), (3, 3, 64, True),
+                                            (4, 40, 100, True)])
 def test_gpu_sbp_keyframe(seed, th, od, ori):
+    """The host form: candidates in fixed slots (16 per map point, one kernel) and, when a point
+    has more (th = 40), the rerun on the CSR path from the saved slots — both bit-exact."""
     from orbslam_mapsave_amd.native import ORBmatcher
     c = S.sbp_keyframe_case(seed)
     m = ORBmatcher(0.9, ori, device=0)
@@ -123,4 +126,6 @@ def test_gpu_sbp_keyframe(seed, th, od, ori):
         frame_mp=c["frame_mp"], kf_ids=c["kf_ids"])
     ofmp, onm = oracle.search_by_projection_keyframe(c, th, od, ori)
     assert nm == onm and np.array_equal(fmp, ofmp)
+    if th >= 40:
+        assert m.capacity_retries() >= 1  # the fixed slots overflowed
     m.close()
