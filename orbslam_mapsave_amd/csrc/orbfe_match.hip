@@ -1112,10 +1112,14 @@ struct SbpLastArgs {
     int* cnt;
     const int* off;
     int2* cand;
+    int kfix;                 // kMode 2: candidate slots per point
+    int* ovf;                 // kMode 2: points with more candidates than kfix
 };
 
-template <bool FILL>
+// kMode as sbp_kf_cand_kernel's: 0 count, 1 fill the CSR lists, 2 fixed slots in one pass
+template <int kMode>
 __global__ __launch_bounds__(256) void sbp_last_cand_kernel(SbpLastArgs a) {
+    constexpr bool FILL = kMode == 1;
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per last-frame point
     if (i >= a.n_last) return;
     // Inputs read up front, as in sbp_kf_cand_kernel.
@@ -1138,20 +1142,24 @@ __global__ __launch_bounds__(256) void sbp_last_cand_kernel(SbpLastArgs a) {
             const int lo = a.mode == 0 ? o - 1 : a.mode == 1 ? o : 0;
             const int hi = a.mode == 0 ? o + 1 : a.mode == 1 ? -1 : o;
             const uint4 q0 = a.desc[2 * i], q1 = a.desc[2 * i + 1];
-            int2* out = FILL ? a.cand + a.off[i] : nullptr;
+            int2* out = FILL ? a.cand + a.off[i] : kMode == 2 ? a.cand + (size_t)i * a.kfix : nullptr;
             const float ur = u - a.bf * invz;
             n = features_in_area_wave(
                 a.cur, u, v, radius, lo, hi,
                 [&](int i2) { return !(a.cur.ur && a.cur.ur[i2] > 0 && fabsf(ur - a.cur.ur[i2]) > radius); },
                 [&](int i2, int rank) {
-                    if (FILL) {
+                    if (FILL || (kMode == 2 && rank < a.kfix)) {
                         const uint4* d = a.cur.desc + 2 * i2;
                         out[rank] = make_int2(i2, hamming256(q0, q1, d[0], d[1]));
                     }
                 });
         }
     }
-    if (!FILL && (threadIdx.x & 63) == 0) a.cnt[i] = n;
+    if (kMode == 0 && (threadIdx.x & 63) == 0) a.cnt[i] = n;
+    if (kMode == 2 && (threadIdx.x & 63) == 0) {
+        a.cnt[i] = min(n, a.kfix);
+        if (n > a.kfix) atomicAdd(a.ovf, 1);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -1041,6 +1041,8 @@ int orbfe_search_by_projection_local(orbfe_matcher* m, float nnratio,
     });
 }
 
+constexpr int kSbpLastFix = 64;  // SearchByProjection(last frame): fixed candidate slots per point
+
 int orbfe_search_by_projection_last(orbfe_matcher* m, int check_ori,
                                     const orbfe_frame_view* cur, const float* tcw_cur,
                                     const orbfe_camera* cam, int32_t* frame_mp,
@@ -1059,9 +1061,21 @@ int orbfe_search_by_projection_last(orbfe_matcher* m, int check_ori,
     for (int i = 0; i < n_last; ++i)
         if (last_mp_valid[i] && (last_keys[i].octave < 0 || last_keys[i].octave >= cur->nlevels))
             return ORBFE_ERR_UNSUPPORTED;
+    // fixed-slot candidates unless a point has more than kSbpLastFix (then the CSR path from the
+    // saved slots), as the keyframe overload below; 64 slots: the mono th = 15 window over three
+    // octaves holds more than 16 keypoints for some points of a 1000-keypoint frame
+    std::vector<int32_t> fmp_in, fobs_in;
+    bool fix = cur->n > 0 && n_last > 0;
+    if (fix) {
+        fmp_in.assign(frame_mp, frame_mp + cur->n);
+        fobs_in.assign(frame_mp_obs, frame_mp_obs + cur->n);
+    }
     return guarded(m, [&]() {
+      for (;;) {
         int st;
         SbpLastArgs a;
+        const int32_t zero[4] = {0, 0, 0, 0};  // nmatches, -, overflow
+        if ((st = m->up(m->scal, zero, sizeof(zero)))) return st;
         if ((st = m->frame(cur, false, a.cur))) return st;
         if ((st = m->up(m->fb_k, last_keys, (size_t)n_last * sizeof(orbfe_keypoint)))) return st;
         if ((st = m->up(m->m_u0, last_mp_valid, n_last))) return st;
@@ -1095,8 +1109,19 @@ int orbfe_search_by_projection_last(orbfe_matcher* m, int check_ori,
         const bool fwd = tlc[2] > cam->b && !mono;
         const bool bwd = -tlc[2] > cam->b && !mono;
         a.mode = fwd ? 1 : bwd ? 2 : 0;
-        if ((st = m->csr_async(a, n_last, sbp_last_cand_kernel<false>, sbp_last_cand_kernel<true>, 4)))
+        a.kfix = kSbpLastFix;
+        a.ovf = m->scal.as<int>() + 2;
+        if (fix) {
+            if ((st = m->cnt.ensure((size_t)n_last * sizeof(int)))) return st;
+            if ((st = m->cand.ensure((size_t)n_last * kSbpLastFix * sizeof(int2)))) return st;
+            a.cnt = m->cnt.as<int>();
+            a.cand = m->cand.as<int2>();
+            if ((st = m->flush())) return st;
+            hipLaunchKernelGGL(sbp_last_cand_kernel<2>, dim3((n_last + 3) / 4), dim3(256), 0, m->stream, a);
+            ORBFE_HIP(hipGetLastError());
+        } else if ((st = m->csr_async(a, n_last, sbp_last_cand_kernel<0>, sbp_last_cand_kernel<1>, 4))) {
             return st;
+        }
         const int N = cur->n;
         if ((st = m->up(m->s1, frame_mp, (size_t)N * 4))) return st;
         if ((st = m->up(m->s2, frame_mp_obs, (size_t)N * 4))) return st;
@@ -1121,11 +1146,27 @@ int orbfe_search_by_projection_last(orbfe_matcher* m, int check_ori,
         g.q_angle = m->o_f3.as<float>();
         g.k = a.cur.k;
         g.ids = last_mp_ids ? m->o_i.as<int>() : nullptr;
+        if (fix) {
+            g.kfix = kSbpLastFix;
+            g.fcnt = m->cnt.as<int>();
+        }
         if ((st = m->greedy(g))) return st;
         if ((st = m->down(frame_mp, m->s1, (size_t)N * 4))) return st;
         if ((st = m->down(frame_mp_obs, m->s2, (size_t)N * 4))) return st;
-        if ((st = m->down(nmatches, m->scal, sizeof(int)))) return st;
-        return m->sync();
+        int res[3] = {0, 0, 0};  // {nmatches, -, overflow}
+        if ((st = m->down(res, m->scal, sizeof(res)))) return st;
+        if ((st = m->sync())) return st;
+        if (fix && res[2] > 0) {  // a point past kSbpLastFix candidates: the CSR path from the input
+            std::memcpy(frame_mp, fmp_in.data(), (size_t)N * 4);
+            std::memcpy(frame_mp_obs, fobs_in.data(), (size_t)N * 4);
+            fix = false;
+            ++m->capacity_retries;
+            m->begin();
+            continue;
+        }
+        *nmatches = res[0];
+        return ORBFE_OK;
+      }
     });
 }
 
