@@ -210,7 +210,8 @@ def row_reloc():
     n = len(c["kf_valid"])
     emit("(f)3 relocalisation SearchByProjection(Frame&, KeyFrame*) (1000-point keyframe)",
          "calls/s", 1, t, tc, n * (12 + 32 + 8 + 4 + 3) + c["cur"].n * 60,
-         "host ABI (uploads included): latency-bound, ~10 launches + 2 synchronisations")
+         "host ABI (uploads included): latency-bound, 5 launches (scatter, grid, fixed-slot "
+         "candidates, one-workgroup resolver, gather) and one wait on a done word")
     m.close()
 
 
@@ -230,7 +231,8 @@ def row_track():
     n = len(c["last_valid"])
     emit("tracking SearchByProjection(CurrentFrame, LastFrame) (1000 kp each, mono th 15)",
          "calls/s", 1, t, tc, n * (12 + 32 + 28 + 8) + c["cur"].n * 60,
-         "host ABI (uploads included): one call per tracked frame, latency-bound")
+         "host ABI (uploads included): one call per tracked frame, latency-bound (fixed-slot "
+         "candidates, one wait on a done word)")
     m.close()
     f1, f2, prev = S.sfi_case(0)
     m = native.ORBmatcher(0.9, True, device=0)
@@ -353,7 +355,8 @@ def row_bow(tmpdir):
     tc = cpu_timed(lambda: oracle.search_by_bow(kf.desc, kf.keys["angle"], ok, kf_fv, f.desc,
                                                 f.keys["angle"], f_fv, 0.75, True))
     emit("(f)4 SearchByBoW(KeyFrame*, Frame&) (1000 x 1000 features, level-2 nodes)", "calls/s",
-         1, t, tc, (kf.n + f.n) * (32 + 8), "host ABI (uploads included), latency-bound")
+         1, t, tc, (kf.n + f.n) * (32 + 8), "host ABI (uploads included), latency-bound: one "
+         "workgroup per common node, the host waits on the output slots")
     # Tracking::Relocalization's candidate loop (Tracking.cc:1636-1656) as one device call:
     # the current frame against P candidate keyframes, everything resident in HBM
     from test_bow import pack_slots
