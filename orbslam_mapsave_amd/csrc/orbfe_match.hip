@@ -917,6 +917,17 @@ struct SfiRoundArgs {
     int* status;            // a query with 65536+ candidates (ranks do not fit the key)
 };
 
+// The rounds' starting state in one launch (three hipMemsetAsync calls before): decisions
+// 0xfefefefe (< -1: no decision yet, what round 0 compares against), the first two slot-list
+// counts 0, the overflow word and the per-round change flags 0.
+__global__ __launch_bounds__(256) void sfi_init_kernel(int* dec0, int nd, int* lcnt, int nl, int* chg, int nc) {
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < max(nd, max(nl, nc)); i += gridDim.x * 256) {
+        if (i < nd) dec0[i] = (int)0xfefefefe;
+        if (i < nl) lcnt[i] = 0;
+        if (i < nc) chg[i] = 0;
+    }
+}
+
 __global__ __launch_bounds__(256) void sfi_round_kernel(SfiRoundArgs a, int r) {
     // A round after a change-free one (the host launches rounds in batches, past convergence)
     // exits before touching anything: it would repeat the converged round's decisions, but it

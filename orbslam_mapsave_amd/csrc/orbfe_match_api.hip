@@ -888,8 +888,8 @@ int orbfe_search_for_initialization(orbfe_matcher* m, float nnratio, int check_o
         if ((st = m->g_chg.ensure((size_t)(n1 + 4) * sizeof(int)))) return st;  // overflow, -, rounds 0..n1
         if ((st = m->s2.ensure(std::max(n1, 1) * 2 * sizeof(int)))) return st;
         if ((st = m->flush())) return st;
-        int total = 0;
-        ORBFE_HIP(hipMemcpyAsync(&total, m->off.as<int>() + n1, sizeof(int), hipMemcpyDeviceToHost, m->stream));
+        int total = 0;  // read back with the first batch's change flags
+        if ((st = m->down_ptr(&total, m->off.as<int>() + n1, sizeof(int)))) return st;
         SfiRoundArgs r{};
         r.n1 = n1;
         r.n2 = n2;
@@ -916,9 +916,12 @@ int orbfe_search_for_initialization(orbfe_matcher* m, float nnratio, int check_o
                 r.lcnt[b] = m->g_t1.as<int>() + (size_t)b * L2;
             }
             // round 0 compares against 0xfefefefe (< -1: no decision), reads an empty list 0
-            ORBFE_HIP(hipMemsetAsync(r.dec[0], 0xfe, (size_t)std::max(n1, 1) * sizeof(int), m->stream));
-            ORBFE_HIP(hipMemsetAsync(m->g_t1.p, 0, (size_t)2 * L2 * sizeof(int), m->stream));
-            ORBFE_HIP(hipMemsetAsync(m->g_chg.p, 0, (size_t)(n1 + 4) * sizeof(int), m->stream));
+            {
+                const int nmax = std::max(std::max(std::max(n1, 1), 2 * L2), n1 + 4);
+                hipLaunchKernelGGL(sfi_init_kernel, dim3(std::min(64, (nmax + 255) / 256)), dim3(256), 0,
+                                   m->stream, r.dec[0], std::max(n1, 1), m->g_t1.as<int>(), 2 * L2,
+                                   m->g_chg.as<int>(), n1 + 4);
+            }
             int rr = 0, batch = 6, ovf = 0;
             std::vector<int> chg_h;
             while (conv < 0) {
@@ -926,10 +929,12 @@ int orbfe_search_for_initialization(orbfe_matcher* m, float nnratio, int check_o
                 for (int b = 0; b < batch && rr <= n1; ++b, ++rr)
                     hipLaunchKernelGGL(sfi_round_kernel, dim3(rb), dim3(256), 0, m->stream, r, rr);
                 ORBFE_HIP(hipGetLastError());
+                // the overflow word and the batch's change flags through the staging buffer (the
+                // gather kernel and the done word, not two pageable copies and a stream sync)
                 chg_h.assign(rr - r0 + 2, 0);
-                ORBFE_HIP(hipMemcpyAsync(chg_h.data(), m->g_chg.as<int>(), sizeof(int), hipMemcpyDeviceToHost, m->stream));
-                ORBFE_HIP(hipMemcpyAsync(chg_h.data() + 2, r.chg + r0, (rr - r0) * sizeof(int), hipMemcpyDeviceToHost, m->stream));
-                ORBFE_HIP(hipStreamSynchronize(m->stream));
+                if ((st = m->down_ptr(chg_h.data(), m->g_chg.as<int>(), sizeof(int)))) return st;
+                if ((st = m->down_ptr(chg_h.data() + 2, r.chg + r0, (size_t)(rr - r0) * sizeof(int)))) return st;
+                if ((st = m->sync())) return st;
                 if ((size_t)total > cap) {
                     if (retried) return ORBFE_ERR_HIP;
                     if ((st = m->cand.ensure((size_t)total * sizeof(int2)))) return st;
