@@ -661,6 +661,32 @@ struct orbfe_vocabulary {
     // per-call scratch / staging (host forms)
     DevBuf s_desc, s_n, s_word, s_node, s_w, o_wid, o_val, o_nw, o_nid, o_noff, o_feat, o_nn;
     hipStream_t own = nullptr, stream = nullptr;
+    // the host transform's staging: descriptors in, results out, in one device-mapped pinned
+    // block the kernels read and write directly (no H2D / D2H copies); null: DMA copies
+    uint8_t* pin = nullptr;
+    uint8_t* pin_dev = nullptr;
+    size_t pin_cap = 0;
+    uint8_t* stage(size_t bytes) {
+        if (bytes <= pin_cap) return pin;
+        if (pin) {
+            hipStreamSynchronize(stream);
+            hipHostFree(pin);
+        }
+        pin = pin_dev = nullptr;
+        pin_cap = 0;
+        void* q = nullptr;
+        void* dq = nullptr;
+        const size_t cap = std::max<size_t>(bytes, (size_t)64 << 10);
+        if (hipHostMalloc(&q, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+        if (hipHostGetDevicePointer(&dq, q, 0) != hipSuccess) {
+            hipHostFree(q);
+            return nullptr;
+        }
+        pin = static_cast<uint8_t*>(q);
+        pin_dev = static_cast<uint8_t*>(dq);
+        pin_cap = cap;
+        return pin;
+    }
 
     VocabDev dev() const {
         return VocabDev{L, nodes, nwords, scoring, weighting, child_off.as<int>(),
@@ -670,6 +696,7 @@ struct orbfe_vocabulary {
         for (DevBuf* b : {&child_off, &child_ids, &desc, &word, &weight, &s_desc, &s_n, &s_word,
                           &s_node, &s_w, &o_wid, &o_val, &o_nw, &o_nid, &o_noff, &o_feat, &o_nn})
             b->release();
+        if (pin) hipHostFree(pin);
         if (own) hipStreamDestroy(own);
     }
 };
@@ -924,6 +951,12 @@ static bool fv_ok(int nn, const int32_t* off, const int32_t* feat, int n) {
         seen[feat[i]] = 1;
     }
     return true;
+}
+
+// ORBFE_ZERO_COPY=0: the vocabulary's host transform copies through device buffers (DMA)
+static bool zero_copy_off() {
+    const char* e = std::getenv("ORBFE_ZERO_COPY");
+    return e && std::strcmp(e, "0") == 0;
 }
 
 // ORBFE_BOW1=0: the host form takes the general two-launch path (bow_search_kernel) instead of
@@ -1246,6 +1279,42 @@ int orbfe_bow_transform(orbfe_vocabulary* v, const uint8_t* desc, int n, int lev
         if ((st = v->o_feat.ensure((size_t)cap * 4))) return st;
         if ((st = v->o_nw.ensure(16))) return st;
         if ((st = v->o_nn.ensure(16))) return st;
+        {   // one pinned block: desc | n | word ids | values | node ids | node offsets | feat | nw | nn
+            auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };  // every part 16-byte aligned
+            const size_t o_n = al((size_t)cap * 32), o_wid = o_n + 16, o_val = al(o_wid + (size_t)cap * 4),
+                         o_nid = al(o_val + (size_t)cap * 8), o_noff = al(o_nid + (size_t)cap * 4),
+                         o_feat = al(o_noff + (size_t)(cap + 1) * 4), o_nw = al(o_feat + (size_t)cap * 4),
+                         o_nn = o_nw + 16, bytes = o_nn + 16;
+            uint8_t* q = zero_copy_off() ? nullptr : v->stage(bytes);
+            if (q) {
+                const uint8_t* d = v->pin_dev;
+                if (n) std::memcpy(q, desc, (size_t)n * 32);
+                std::memcpy(q + o_n, &n, sizeof(int));
+                if ((st = bow_launch(v, 1, cap, d, reinterpret_cast<const int32_t*>(d + o_n), levelsup,
+                                     reinterpret_cast<int32_t*>(const_cast<uint8_t*>(d + o_wid)),
+                                     reinterpret_cast<double*>(const_cast<uint8_t*>(d + o_val)),
+                                     reinterpret_cast<int32_t*>(const_cast<uint8_t*>(d + o_nw)),
+                                     reinterpret_cast<int32_t*>(const_cast<uint8_t*>(d + o_nid)),
+                                     reinterpret_cast<int32_t*>(const_cast<uint8_t*>(d + o_noff)),
+                                     reinterpret_cast<int32_t*>(const_cast<uint8_t*>(d + o_feat)),
+                                     reinterpret_cast<int32_t*>(const_cast<uint8_t*>(d + o_nn)))))
+                    return st;
+                ORBFE_HIP(hipStreamSynchronize(v->stream));
+                int cnt[2];
+                std::memcpy(&cnt[0], q + o_nw, sizeof(int));
+                std::memcpy(&cnt[1], q + o_nn, sizeof(int));
+                *nw = cnt[0];
+                *nn = cnt[1];
+                std::memcpy(word_ids, q + o_wid, (size_t)cnt[0] * 4);
+                std::memcpy(values, q + o_val, (size_t)cnt[0] * 8);
+                std::memcpy(node_ids, q + o_nid, (size_t)cnt[1] * 4);
+                std::memcpy(node_off, q + o_noff, (size_t)(cnt[1] + 1) * 4);
+                if (!cnt[1]) node_off[0] = 0;
+                const int nfeat = cnt[1] ? node_off[cnt[1]] : 0;
+                std::memcpy(feat, q + o_feat, (size_t)nfeat * 4);
+                return ORBFE_OK;
+            }
+        }
         if (n) ORBFE_HIP(hipMemcpyAsync(v->s_desc.p, desc, (size_t)n * 32, hipMemcpyHostToDevice, v->stream));
         ORBFE_HIP(hipMemcpyAsync(v->s_n.p, &n, sizeof(int), hipMemcpyHostToDevice, v->stream));
         if ((st = bow_launch(v, 1, cap, v->s_desc.as<uint8_t>(), v->s_n.as<int32_t>(), levelsup,

@@ -224,13 +224,19 @@ def test_oracle_search_by_bow_vs_restatement(ori, vocab_paths, frames):
 
 # ---------------------------------------------------------------------------------------------
 @pytest.mark.gpu
+@pytest.mark.parametrize("zc", ["1", "0"])
 @pytest.mark.parametrize("name", sorted(VOCABS))
-def test_gpu_bow_transform(name, vocab_paths, frames):
+def test_gpu_bow_transform(name, zc, vocab_paths, frames, monkeypatch):
+    """The host transform (Frame::ComputeBoW): through its device-mapped pinned block (the
+    kernels read the descriptors and write the vectors there) and with ORBFE_ZERO_COPY=0 through
+    DMA copies; 1000, 1, 0 and then ~2000 descriptors (the pinned block grows)."""
+    monkeypatch.setenv("ORBFE_ZERO_COPY", zc)
     from orbslam_mapsave_amd.native import Vocabulary
     gv = Vocabulary(vocab_paths[name], device=0)
     ov = oracle.Vocabulary(vocab_paths[name])
     assert (gv.k, gv.L, gv.nodes, gv.words) == (ov.k, ov.L, ov.nodes, ov.words)
-    for desc in (frames[0].desc, frames[1].desc[:1], frames[1].desc[:0]):
+    both = np.concatenate([frames[0].desc, frames[1].desc])
+    for desc in (frames[0].desc, frames[1].desc[:1], frames[1].desc[:0], both):
         for levelsup in (1, 2, gv.L):
             same(gv.transform(desc, levelsup), ov.transform(desc, levelsup))
     gv.close()

@@ -346,6 +346,11 @@ def row_bow(tmpdir):
     emit("(f)4 BoW transform, ComputeBoW (k=10 L=6 1.1M-node vocabulary, 1000 desc)",
          "frames/s", B, t, tc, nb, "device batch of 256 frames; synthetic vocabulary of ORBvoc's "
          "shape (ORBvoc.txt absent)", cpu_units=1)
+    # the per-keyframe call (Frame::ComputeBoW) through the host ABI
+    t1 = timed(lambda: gv.transform(fr[0].desc, 4), 100)
+    emit("(f)4 BoW transform, ComputeBoW of one frame (host ABI, 1000 desc, same vocabulary)",
+         "frames/s", 1, t1, tc, nb // B, "host ABI: descriptors in and vectors out through one "
+         "device-mapped pinned block, one synchronisation")
     kf, f = fr[0], S.extract_frame(0, 1000, shift=(2, -3), ini=20)
     kf_fv = ov.transform(kf.desc, 4)[2:]
     f_fv = ov.transform(f.desc, 4)[2:]

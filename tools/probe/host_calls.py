@@ -23,6 +23,31 @@ def timed(fn, k, warm=5):
     return (time.perf_counter() - t0) / k * 1e3
 
 
+def vocab_arrays(k, L, seed, anchors):
+    """tools/bench_rows.py's complete k-ary synthetic vocabulary (that module initialises torch,
+    which this probe does not load)."""
+    import numpy as np
+    rng = np.random.Generator(np.random.PCG64(seed))
+    parent, desc, word, weight = [np.zeros(1, np.int32)], [np.zeros((1, 32), np.uint8)], [np.zeros(1, np.uint8)], [np.zeros(1)]
+    prev, prev_desc, nid = np.zeros(1, np.int64), np.zeros((1, 32), np.uint8), 1
+    for level in range(1, L + 1):
+        cnt = len(prev) * k
+        if level == 1:
+            d = anchors[np.arange(cnt) % len(anchors)]
+        else:
+            bits = np.unpackbits(np.repeat(prev_desc, k, axis=0), axis=1)
+            bits ^= (rng.uniform(size=bits.shape) < 0.12).astype(np.uint8)
+            d = np.packbits(bits, axis=1)
+        leaf = level == L
+        parent.append(np.repeat(prev, k).astype(np.int32))
+        desc.append(d)
+        word.append(np.full(cnt, int(leaf), np.uint8))
+        weight.append(np.where(rng.uniform(size=cnt) < 0.03, 0.0, rng.uniform(0.5, 8.0, cnt)) if leaf else np.zeros(cnt))
+        prev, prev_desc, nid = np.arange(nid, nid + cnt), d, nid + cnt
+    return (np.concatenate(parent), np.concatenate(word), np.ascontiguousarray(np.concatenate(desc)),
+            np.concatenate(weight))
+
+
 def main():
     import scenarios as S
     from orbslam_mapsave_amd import native
@@ -40,6 +65,18 @@ def main():
     f1, f2, prev = S.sfi_case(0)
     out["sfi"] = timed(lambda: m.SearchForInitialization(f1, f2, prev, 100), 100)
     m.close()
+    # Frame::ComputeBoW through the host ABI: 1000 descriptors, a k = 10, L = 6 vocabulary
+    import ctypes as C
+    f0 = S.extract_frame(0, 1000, ini=20)
+    parent, word, desc, weight = vocab_arrays(10, 6, 0, anchors=f0.desc[::97])
+    L = native.lib()
+    st = C.c_int(0)
+    h = L.orbfe_vocabulary_create(10, 6, 0, 0, len(parent), native.ptr(parent), native.ptr(word),
+                                  native.ptr(desc), native.ptr(weight), 0, C.byref(st))
+    gv = native.Vocabulary.__new__(native.Vocabulary)
+    gv._h = C.c_void_p(h)
+    out["bow_transform"] = timed(lambda: gv.transform(f0.desc, 4), 200)
+    gv.close()
     print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in out.items()}), flush=True)
 
 
