@@ -182,6 +182,10 @@ struct orbfe_extractor {
     // orbfe_destroy reallocate it and no copying call writes it, so the caller's pointer and the
     // frame staged in it stay valid across orbfe_extract calls of any size.
     Pinned pin_in, pin_user, pin_kps, pin_desc, pin_n;
+    // orbfe_compute_stereo_matches: the pair's keypoints, descriptors and counts in one pinned
+    // block (one H2D copy into st_in), the outputs back into it (st_pin)
+    Pinned st_pin;
+    DevBuf st_in;
     // Every buffer the capture embeds is either in g1_key (outputs, pinned staging) or is a
     // plan / workspace buffer: set_plan and a growing ensure_frames drop the graphs.  One graph
     // per input source ([0] copy staging, [1] the handed-out buffer), so callers alternating the
@@ -776,7 +780,8 @@ struct orbfe_extractor {
                           &st_sad, &st_status, &st_kl, &st_dl, &st_kr, &st_dr, &st_n, &st_ur, &st_dp})
             b->release();
         drop_graph();
-        for (Pinned* q : {&pin_in, &pin_user, &pin_kps, &pin_desc, &pin_n}) q->release();
+        for (Pinned* q : {&pin_in, &pin_user, &pin_kps, &pin_desc, &pin_n, &st_pin}) q->release();
+        st_in.release();
         prof.release();
         if (own) hipStreamDestroy(own);
     }
@@ -1213,23 +1218,41 @@ int orbfe_compute_stereo_matches(orbfe_extractor* left, orbfe_extractor* right, 
         if ((st = L->st_ur.ensure((size_t)cap * sizeof(float)))) return st;
         if ((st = L->st_dp.ensure((size_t)cap * sizeof(float)))) return st;
         const int32_t counts[2] = {nl, nr};
-        ORBFE_HIP(hipMemcpyAsync(L->st_kl.p, kl, (size_t)nl * sizeof(orbfe_keypoint), hipMemcpyHostToDevice, s));
-        ORBFE_HIP(hipMemcpyAsync(L->st_dl.p, dl, (size_t)nl * 32, hipMemcpyHostToDevice, s));
+        // inputs kl | dl | kr | dr | counts staged in one pinned block and copied in by one DMA;
+        // outputs u_right | depth (one device block) and the status copied back into it
+        auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+        const size_t o_dl = al((size_t)nl * sizeof(orbfe_keypoint)), o_kr = o_dl + al((size_t)nl * 32),
+                     o_dr = o_kr + al((size_t)nr * sizeof(orbfe_keypoint)), o_n = o_dr + al((size_t)nr * 32),
+                     in_bytes = o_n + 256, o_ur = 0, o_dp = al((size_t)nl * 4), o_st = o_dp + al((size_t)nl * 4),
+                     out_bytes = o_st + 256;
+        if ((st = L->st_pin.ensure(std::max(in_bytes, out_bytes)))) return st;
+        if ((st = L->st_in.ensure(in_bytes))) return st;
+        uint8_t* q = L->st_pin.p;
+        std::memcpy(q, kl, (size_t)nl * sizeof(orbfe_keypoint));
+        std::memcpy(q + o_dl, dl, (size_t)nl * 32);
         if (nr) {
-            ORBFE_HIP(hipMemcpyAsync(L->st_kr.p, kr, (size_t)nr * sizeof(orbfe_keypoint), hipMemcpyHostToDevice, s));
-            ORBFE_HIP(hipMemcpyAsync(L->st_dr.p, dr, (size_t)nr * 32, hipMemcpyHostToDevice, s));
+            std::memcpy(q + o_kr, kr, (size_t)nr * sizeof(orbfe_keypoint));
+            std::memcpy(q + o_dr, dr, (size_t)nr * 32);
         }
-        ORBFE_HIP(hipMemcpyAsync(L->st_n.p, counts, sizeof(counts), hipMemcpyHostToDevice, s));
-        if ((st = stereo_launch(L, right, frame, 1, L->st_kl.as<orbfe_keypoint>(), L->st_dl.as<uint8_t>(),
-                                L->st_n.as<int32_t>(), L->st_kr.as<orbfe_keypoint>(),
-                                L->st_dr.as<uint8_t>(), L->st_n.as<int32_t>() + 1, cap, bf, b,
-                                L->st_ur.as<float>(), L->st_dp.as<float>())))
+        std::memcpy(q + o_n, counts, sizeof(counts));
+        ORBFE_HIP(hipMemcpyAsync(L->st_in.p, q, in_bytes, hipMemcpyHostToDevice, s));
+        uint8_t* din = L->st_in.as<uint8_t>();
+        // (st_ur holds u_right then depth: one D2H copy for both)
+        if ((st = L->st_ur.ensure(out_bytes))) return st;
+        uint8_t* dout = L->st_ur.as<uint8_t>();
+        if ((st = stereo_launch(L, right, frame, 1, reinterpret_cast<const orbfe_keypoint*>(din), din + o_dl,
+                                reinterpret_cast<const int32_t*>(din + o_n),
+                                reinterpret_cast<const orbfe_keypoint*>(din + o_kr), din + o_dr,
+                                reinterpret_cast<const int32_t*>(din + o_n) + 1, cap, bf, b,
+                                reinterpret_cast<float*>(dout + o_ur), reinterpret_cast<float*>(dout + o_dp))))
             return st;
-        int status = 0;
-        ORBFE_HIP(hipMemcpyAsync(u_right, L->st_ur.p, (size_t)nl * sizeof(float), hipMemcpyDeviceToHost, s));
-        ORBFE_HIP(hipMemcpyAsync(depth, L->st_dp.p, (size_t)nl * sizeof(float), hipMemcpyDeviceToHost, s));
-        ORBFE_HIP(hipMemcpyAsync(&status, L->st_status.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        ORBFE_HIP(hipMemcpyAsync(dout + o_st, L->st_status.p, sizeof(int), hipMemcpyDeviceToDevice, s));
+        ORBFE_HIP(hipMemcpyAsync(q, dout, out_bytes, hipMemcpyDeviceToHost, s));
         ORBFE_HIP(hipStreamSynchronize(s));
+        std::memcpy(u_right, q + o_ur, (size_t)nl * sizeof(float));
+        std::memcpy(depth, q + o_dp, (size_t)nl * sizeof(float));
+        int status = 0;
+        std::memcpy(&status, q + o_st, sizeof(int));
         return status;
     } catch (const std::bad_alloc&) {
         return ORBFE_ERR_NOMEM;

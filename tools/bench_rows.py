@@ -191,6 +191,12 @@ def row_stereo():
          "both extractors resident; bytes = keypoints + descriptors of both sides + the two SAD "
          "windows + outputs per left keypoint; the CPU leg (oracle) also rebuilds both pyramids "
          "per call, which the reference gets from its extractors", cpu_units=1)
+    # the per-frame call (Frame.cc:82): one pair through the host ABI, on batch frame 0's pyramids
+    t1 = timed(lambda: el.ComputeStereoMatches(er, okl, odl, okr, odr, 50.0, 0.1, frame=0), 100)
+    emit("(f)2 stereo ComputeStereoMatches of one pair (host ABI, 640x480, 1000 kp per side)",
+         "pairs/s", 1, t1, tc, nkp * (2 * 60 + 121 + 231 + 8),
+         "host ABI: keypoints and descriptors of both sides in by one DMA from a pinned block, "
+         "u_right | depth | status back by one; the extractors' pyramids resident", cpu_units=1)
     el.close()
     er.close()
 

@@ -77,6 +77,16 @@ def main():
     gv._h = C.c_void_p(h)
     out["bow_transform"] = timed(lambda: gv.transform(f0.desc, 4), 200)
     gv.close()
+    # Frame::ComputeStereoMatches through the host ABI on the pair the two extractors just made
+    from orbslam_mapsave_amd.synth import synthetic_stereo_pair
+    a, b = synthetic_stereo_pair(0, 640, 480)
+    el = native.ORBextractor(1000, 1.2, 8, 20, 7, device=0, max_width=640, max_height=480)
+    er = native.ORBextractor(1000, 1.2, 8, 20, 7, device=0, max_width=640, max_height=480)
+    kl, dl = el(a)
+    kr, dr = er(b)
+    out["stereo"] = timed(lambda: el.ComputeStereoMatches(er, kl, dl, kr, dr, 50.0, 0.1), 200)
+    el.close()
+    er.close()
     print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in out.items()}), flush=True)
 
 
