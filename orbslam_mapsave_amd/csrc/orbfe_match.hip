@@ -1065,10 +1065,15 @@ struct SbpLocalArgs {
     int* cnt;
     const int* off;
     int2* cand;          // (idx, dist | octave << 16)
+    int kfix;            // kMode 2: candidate slots per point
+    int* ovf;            // kMode 2: points with more candidates than kfix
 };
 
-template <bool FILL>
+// kMode 0: count, 1: fill the CSR lists, 2: fixed slots in one pass (the first kfix candidates at
+// i * kfix, min(n, kfix) in cnt[i]; a point with more raises *ovf)
+template <int kMode>
 __global__ __launch_bounds__(256) void sbp_local_cand_kernel(SbpLocalArgs a) {
+    constexpr bool FILL = kMode == 1;
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= a.mp.m) return;
     if (!a.mp.in_view[i] || a.mp.bad[i]) {
@@ -1088,19 +1093,23 @@ __global__ __launch_bounds__(256) void sbp_local_cand_kernel(SbpLocalArgs a) {
     if (FILL && a.off[i + 1] > a.cand_cap) return;
     const uint4 q0 = a.mp.desc[2 * i], q1 = a.mp.desc[2 * i + 1];
     int n = 0;
-    int2* out = FILL ? a.cand + a.off[i] : nullptr;
+    int2* out = FILL ? a.cand + a.off[i] : kMode == 2 ? a.cand + (size_t)i * a.kfix : nullptr;
     features_in_area(a.f, a.mp.px[i], a.mp.py[i], rs, pl - 1, pl, [&](int idx) {
         if (a.f.ur && a.f.ur[idx] > 0) {  // stereo consistency (91-96)
             const float er = fabsf(pxr - a.f.ur[idx]);
             if (er > r * a.scale[pl]) return;
         }
-        if (FILL) {
+        if (FILL || (kMode == 2 && n < a.kfix)) {
             const uint4* d = a.f.desc + 2 * idx;
             out[n] = make_int2(idx, hamming256(q0, q1, d[0], d[1]) | (a.f.k[idx].octave << 16));
         }
         ++n;
     });
-    if (!FILL) a.cnt[i] = n;
+    if (kMode == 0) a.cnt[i] = n;
+    if (kMode == 2) {
+        a.cnt[i] = min(n, a.kfix);
+        if (n > a.kfix) atomicAdd(a.ovf, 1);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------

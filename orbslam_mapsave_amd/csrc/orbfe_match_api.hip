@@ -996,9 +996,20 @@ int orbfe_search_by_projection_local(orbfe_matcher* m, float nnratio,
         if (mps->track_in_view[i] && !mps->is_bad[i] &&
             (mps->pred_level[i] < 0 || mps->pred_level[i] >= f->nlevels))
             return ORBFE_ERR_UNSUPPORTED;
+    // fixed-slot candidates (one kernel, no mid-call count read-back) unless a point has more
+    // than kSbpFix of them: then the CSR path from the saved slots
+    std::vector<int32_t> fmp_in, fobs_in;
+    bool fix = f->n > 0 && M > 0;
+    if (fix) {
+        fmp_in.assign(frame_mp, frame_mp + f->n);
+        fobs_in.assign(frame_mp_obs, frame_mp_obs + f->n);
+    }
     return guarded(m, [&]() {
+      for (;;) {
         int st;
         SbpLocalArgs a;
+        const int32_t zero[4] = {0, 0, 0, 0};  // nmatches, -, overflow
+        if ((st = m->up(m->scal, zero, sizeof(zero)))) return st;
         if ((st = m->frame(f, false, a.f))) return st;
         if ((st = m->up(m->m_u0, mps->track_in_view, M))) return st;
         if ((st = m->up(m->m_u1, mps->is_bad, M))) return st;
@@ -1019,9 +1030,21 @@ int orbfe_search_by_projection_local(orbfe_matcher* m, float nnratio,
         a.nlevels = f->nlevels;
         a.status = nullptr;  // levels were checked on the host
         a.cand_cap = LLONG_MAX;
-        int total = 0;
-        if ((st = m->csr(a, M, sbp_local_cand_kernel<false>, sbp_local_cand_kernel<true>, total)))
-            return st;
+        a.kfix = kSbpFix;
+        a.ovf = m->scal.as<int>() + 2;
+        if (fix) {
+            if ((st = m->cnt.ensure((size_t)M * sizeof(int)))) return st;
+            if ((st = m->cand.ensure((size_t)M * kSbpFix * sizeof(int2)))) return st;
+            a.cnt = m->cnt.as<int>();
+            a.cand = m->cand.as<int2>();
+            if ((st = m->flush())) return st;
+            hipLaunchKernelGGL(sbp_local_cand_kernel<2>, dim3((M + 255) / 256), dim3(256), 0, m->stream, a);
+            ORBFE_HIP(hipGetLastError());
+        } else {
+            int total = 0;
+            if ((st = m->csr(a, M, sbp_local_cand_kernel<0>, sbp_local_cand_kernel<1>, total)))
+                return st;
+        }
         const int N = f->n;
         if ((st = m->up(m->s1, frame_mp, (size_t)N * 4))) return st;
         if ((st = m->up(m->s2, frame_mp_obs, (size_t)N * 4))) return st;
@@ -1038,11 +1061,27 @@ int orbfe_search_by_projection_local(orbfe_matcher* m, float nnratio,
         g.fmp0 = g.fmp = m->s1.as<int>();
         g.fobs0 = g.fobs = m->s2.as<int>();
         g.ids = mp_ids ? m->o_i.as<int>() : nullptr;
+        if (fix) {
+            g.kfix = kSbpFix;
+            g.fcnt = m->cnt.as<int>();
+        }
         if ((st = m->greedy(g))) return st;
         if ((st = m->down(frame_mp, m->s1, (size_t)N * 4))) return st;
         if ((st = m->down(frame_mp_obs, m->s2, (size_t)N * 4))) return st;
-        if ((st = m->down(nmatches, m->scal, sizeof(int)))) return st;
-        return m->sync();
+        int res[3] = {0, 0, 0};  // {nmatches, -, overflow}
+        if ((st = m->down(res, m->scal, sizeof(res)))) return st;
+        if ((st = m->sync())) return st;
+        if (fix && res[2] > 0) {  // a point past kSbpFix candidates: the CSR path from the input
+            std::memcpy(frame_mp, fmp_in.data(), (size_t)N * 4);
+            std::memcpy(frame_mp_obs, fobs_in.data(), (size_t)N * 4);
+            fix = false;
+            ++m->capacity_retries;
+            m->begin();
+            continue;
+        }
+        *nmatches = res[0];
+        return ORBFE_OK;
+      }
     });
 }
 
@@ -1447,9 +1486,9 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
         a.cand = m->cand.as<int2>();
         a.cand_cap = (long long)cap;
         const int qb = std::max(1, (M + 255) / 256);
-        hipLaunchKernelGGL(sbp_local_cand_kernel<false>, dim3(qb), dim3(256), 0, m->stream, a);
+        hipLaunchKernelGGL(sbp_local_cand_kernel<0>, dim3(qb), dim3(256), 0, m->stream, a);
         hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, m->stream, m->cnt.as<int>(), M, m->off.as<int>());
-        hipLaunchKernelGGL(sbp_local_cand_kernel<true>, dim3(qb), dim3(256), 0, m->stream, a);
+        hipLaunchKernelGGL(sbp_local_cand_kernel<1>, dim3(qb), dim3(256), 0, m->stream, a);
         int total = 0;
         ORBFE_HIP(hipMemcpyAsync(&total, m->off.as<int>() + M, sizeof(int), hipMemcpyDeviceToHost, m->stream));
         GreedyArgs g{};
@@ -1544,9 +1583,9 @@ int orbfe_search_by_projection_local_device(orbfe_matcher* m, float nnratio,
             a.cand = m->cand.as<int2>();
             a.cand_cap = (long long)cap;
             const int qb = std::max(1, (M + 255) / 256);
-            hipLaunchKernelGGL(sbp_local_cand_kernel<false>, dim3(qb), dim3(256), 0, m->stream, a);
+            hipLaunchKernelGGL(sbp_local_cand_kernel<0>, dim3(qb), dim3(256), 0, m->stream, a);
             hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, m->stream, m->cnt.as<int>(), M, m->off.as<int>());
-            hipLaunchKernelGGL(sbp_local_cand_kernel<true>, dim3(qb), dim3(256), 0, m->stream, a);
+            hipLaunchKernelGGL(sbp_local_cand_kernel<1>, dim3(qb), dim3(256), 0, m->stream, a);
             int total = 0;
             ORBFE_HIP(hipMemcpyAsync(&total, m->off.as<int>() + M, sizeof(int), hipMemcpyDeviceToHost, m->stream));
             GreedyArgs g{};

@@ -62,6 +62,8 @@ def main():
     args = (c["cur"], c["tcw_cur"], c["cam"], c["last_keys"], c["last_valid"], c["last_outlier"],
             c["last_xyz"], c["last_desc"], c["last_nobs"], c["tcw_last"])
     out["sbp_last"] = timed(lambda: m.SearchByProjectionLast(*args, 15.0, True, last_ids=c["last_ids"]), 200)
+    f, mps, fmp, fobs, ids = S.sbp_local_case(0, 2000)
+    out["sbp_local"] = timed(lambda: m.SearchByProjection(f, mps, 3.0, fmp, fobs, ids), 200)
     f1, f2, prev = S.sfi_case(0)
     out["sfi"] = timed(lambda: m.SearchForInitialization(f1, f2, prev, 100), 100)
     m.close()
