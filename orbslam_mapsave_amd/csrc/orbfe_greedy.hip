@@ -82,6 +82,7 @@ __global__ __launch_bounds__(kGreedyBlock) void greedy_init_kernel(GreedyArgs a)
         a.last[t] = -1;
     }
     if (t < a.m) a.dec[t] = -2;
+    if (t < a.m + 2) a.chg[t] = 0;
     if (t < kHistoLength && a.hist) a.hist[t] = 0;
     if (t == 0) *a.nm = 0;
 }

@@ -497,10 +497,10 @@ struct orbfe_matcher {
             return ORBFE_OK;
         }
         rounds_on_device = false;
-        const int blocks = std::max(1, (std::max(std::max(M, N), 32) + kGreedyBlock - 1) / kGreedyBlock);
+        const int blocks = std::max(1, (std::max(std::max(M + 2, N), 32) + kGreedyBlock - 1) / kGreedyBlock);
         const int mblocks = std::max(1, (M + kGreedyBlock - 1) / kGreedyBlock);
         const int nblocks = std::max(1, (N + kGreedyBlock - 1) / kGreedyBlock);
-        ORBFE_HIP(hipMemsetAsync(g.chg, 0, (size_t)(M + 2) * sizeof(int), stream));
+        // (greedy_init_kernel also clears the change flags: blocks cover max(M, N, 32) >= M + 2)
         hipLaunchKernelGGL(greedy_init_kernel, dim3(blocks), dim3(kGreedyBlock), 0, stream, g);
         // rounds in batches; a round after a change-free round exits at once
         int r = 0, batch = first_batch;
@@ -509,9 +509,11 @@ struct orbfe_matcher {
             const int r0 = r;
             for (int b = 0; b < batch && r <= M; ++b, ++r)
                 hipLaunchKernelGGL(greedy_round_kernel<false>, dim3(blocks), dim3(kGreedyBlock), 0, stream, g, r);
+            // the batch's change flags through the staging gather and its done word (sync()
+            // also checks an asynchronous candidate fill's capacity first)
             chg_h.assign(r - r0, 0);
-            ORBFE_HIP(hipMemcpyAsync(chg_h.data(), g.chg + r0, (r - r0) * sizeof(int), hipMemcpyDeviceToHost, stream));
-            ORBFE_HIP(hipStreamSynchronize(stream));
+            if ((st = down_ptr(chg_h.data(), g.chg + r0, (size_t)(r - r0) * sizeof(int)))) return st;
+            if ((st = sync())) return st;
             if (total && (size_t)*total > cap) return ORBFE_ERR_CAPACITY;
             const auto z = std::find(chg_h.begin(), chg_h.end(), 0);
             if (z != chg_h.end()) {

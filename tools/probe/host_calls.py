@@ -64,6 +64,8 @@ def main():
     out["sbp_last"] = timed(lambda: m.SearchByProjectionLast(*args, 15.0, True, last_ids=c["last_ids"]), 200)
     f, mps, fmp, fobs, ids = S.sbp_local_case(0, 2000)
     out["sbp_local"] = timed(lambda: m.SearchByProjection(f, mps, 3.0, fmp, fobs, ids), 200)
+    f, mps, fmp, fobs, ids = S.sbp_local_case(0, 50000)  # past the one-workgroup resolver
+    out["sbp_local_50k"] = timed(lambda: m.SearchByProjection(f, mps, 3.0, fmp, fobs, ids), 50)
     f1, f2, prev = S.sfi_case(0)
     out["sfi"] = timed(lambda: m.SearchForInitialization(f1, f2, prev, 100), 100)
     m.close()
