@@ -240,6 +240,16 @@ def row_track():
          "host ABI (uploads included): one call per tracked frame, latency-bound (fixed-slot "
          "candidates, one wait on a done word)")
     m.close()
+    # TrackLocalMap's SearchByProjection(Frame&, vector<MapPoint*>, th) (Tracking.cc:1283,
+    # ORBmatcher.cc:38-131) through the host ABI, isInFrustum's outputs given, 2000 map points
+    f, mps, fmp, fobs, ids = S.sbp_local_case(0, 2000)
+    m = native.ORBmatcher(0.8, True, device=0)
+    t = timed(lambda: m.SearchByProjection(f, mps, 3.0, fmp, fobs, ids), 50)
+    tc = cpu_timed(lambda: oracle.search_by_projection_local(f, mps, 3.0, 0.8, fmp, fobs, ids))
+    emit("tracking SearchByProjection(Frame&, local map points) (2000 points, th 3)", "calls/s", 1,
+         t, tc, 2000 * (32 + 24) + f.n * 60,
+         "host ABI (uploads included): fixed-slot candidates, one-workgroup resolver, one wait")
+    m.close()
     f1, f2, prev = S.sfi_case(0)
     m = native.ORBmatcher(0.9, True, device=0)
     t = timed(lambda: m.SearchForInitialization(f1, f2, prev, 100), 20)
