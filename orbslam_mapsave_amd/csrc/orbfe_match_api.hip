@@ -984,6 +984,10 @@ int orbfe_search_for_initialization(orbfe_matcher* m, float nnratio, int check_o
     });
 }
 
+// host SearchByProjection (local map): up to this many map points one wave per point, beyond it
+// one thread per point
+constexpr int kSbpLocalWaveMax = 16384;
+
 int orbfe_search_by_projection_local(orbfe_matcher* m, float nnratio,
                                      const orbfe_frame_view* f, int32_t* frame_mp,
                                      int32_t* frame_mp_obs, const orbfe_mappoint_view* mps,
@@ -1040,12 +1044,19 @@ int orbfe_search_by_projection_local(orbfe_matcher* m, float nnratio,
             a.cnt = m->cnt.as<int>();
             a.cand = m->cand.as<int2>();
             if ((st = m->flush())) return st;
-            hipLaunchKernelGGL(sbp_local_cand_kernel<2>, dim3((M + 255) / 256), dim3(256), 0, m->stream, a);
+            if (M <= kSbpLocalWaveMax)
+                hipLaunchKernelGGL((sbp_local_cand_kernel<2, true>), dim3((M + 3) / 4), dim3(256), 0, m->stream, a);
+            else
+                hipLaunchKernelGGL(sbp_local_cand_kernel<2>, dim3((M + 255) / 256), dim3(256), 0, m->stream, a);
             ORBFE_HIP(hipGetLastError());
         } else {
             int total = 0;
-            if ((st = m->csr(a, M, sbp_local_cand_kernel<0>, sbp_local_cand_kernel<1>, total)))
+            if (M <= kSbpLocalWaveMax) {
+                if ((st = m->csr(a, M, sbp_local_cand_kernel<0, true>, sbp_local_cand_kernel<1, true>, total, 4)))
+                    return st;
+            } else if ((st = m->csr(a, M, sbp_local_cand_kernel<0>, sbp_local_cand_kernel<1>, total))) {
                 return st;
+            }
         }
         const int N = f->n;
         if ((st = m->up(m->s1, frame_mp, (size_t)N * 4))) return st;
