@@ -780,10 +780,10 @@ __global__ __launch_bounds__(1024) void scan_kernel(const int* counts, int n, in
 
 // ---------------------------------------------------------------------------------------------
 // Frame::GetFeaturesInArea (Frame.cc:445-498) as a batch of queries — the parity probe of the
-// grid (orbfe_features_in_area): both forms the matchers use, thread-per-query
-// (features_in_area, SearchByProjection local map) and wave-per-query (features_in_area_wave,
-// SearchForInitialization / last frame / keyframe), write each query's candidates in the
-// reference's order to items[off[q] ..).
+// grid (orbfe_features_in_area): thread-per-query (features_in_area) and wave-per-query
+// (features_in_area_wave, which the matchers use: SearchForInitialization, SearchByProjection's
+// local-map / last-frame / keyframe forms) write each query's candidates in the reference's
+// order to items[off[q] ..).
 struct FiaArgs {
     DevFrame f;
     int nq;
@@ -1070,16 +1070,16 @@ struct SbpLocalArgs {
 };
 
 // kMode 0: count, 1: fill the CSR lists, 2: fixed slots in one pass (the first kfix candidates at
-// i * kfix, min(n, kfix) in cnt[i]; a point with more raises *ovf).  kWave: one wave per map point
-// (features_in_area_wave; a local map of a few thousand points fills the chip only this way: one
-// thread per point left 8 workgroups walking their windows serially, 0.17 ms at 2,000 points),
-// otherwise one thread per point (tens of thousands of points).
-template <int kMode, bool kWave = false>
+// i * kfix, min(n, kfix) in cnt[i]; a point with more raises *ovf).  One wave per map point
+// (features_in_area_wave): one thread per point (features_in_area, round 5) left a 2,000-point
+// map 8 workgroups walking their windows serially (0.17 ms of kernel; the host call 0.252 ->
+// 0.097 ms) and was slower at 50,000 points too (the host call 0.41 -> 0.32 ms).
+template <int kMode>
 __global__ __launch_bounds__(256) void sbp_local_cand_kernel(SbpLocalArgs a) {
     constexpr bool FILL = kMode == 1;
-    const int i = kWave ? blockIdx.x * 4 + (threadIdx.x >> 6) : blockIdx.x * 256 + threadIdx.x;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= a.mp.m) return;
-    const bool lead = !kWave || (threadIdx.x & 63) == 0;  // the lane that writes the point's words
+    const bool lead = (threadIdx.x & 63) == 0;  // the lane that writes the point's words
     if (!a.mp.in_view[i] || a.mp.bad[i]) {
         if (!FILL && lead) a.cnt[i] = 0;
         return;
@@ -1098,31 +1098,17 @@ __global__ __launch_bounds__(256) void sbp_local_cand_kernel(SbpLocalArgs a) {
     const uint4 q0 = a.mp.desc[2 * i], q1 = a.mp.desc[2 * i + 1];
     int n = 0;
     int2* out = FILL ? a.cand + a.off[i] : kMode == 2 ? a.cand + (size_t)i * a.kfix : nullptr;
-    if constexpr (kWave) {
-        n = features_in_area_wave(
-            a.f, a.mp.px[i], a.mp.py[i], rs, pl - 1, pl,
-            [&](int idx) {  // stereo consistency (91-96)
-                return !(a.f.ur && a.f.ur[idx] > 0 && fabsf(pxr - a.f.ur[idx]) > r * a.scale[pl]);
-            },
-            [&](int idx, int rank) {
-                if (FILL || (kMode == 2 && rank < a.kfix)) {
-                    const uint4* d = a.f.desc + 2 * idx;
-                    out[rank] = make_int2(idx, hamming256(q0, q1, d[0], d[1]) | (a.f.k[idx].octave << 16));
-                }
-            });
-    } else {
-        features_in_area(a.f, a.mp.px[i], a.mp.py[i], rs, pl - 1, pl, [&](int idx) {
-            if (a.f.ur && a.f.ur[idx] > 0) {  // stereo consistency (91-96)
-                const float er = fabsf(pxr - a.f.ur[idx]);
-                if (er > r * a.scale[pl]) return;
-            }
-            if (FILL || (kMode == 2 && n < a.kfix)) {
+    n = features_in_area_wave(
+        a.f, a.mp.px[i], a.mp.py[i], rs, pl - 1, pl,
+        [&](int idx) {  // stereo consistency (91-96)
+            return !(a.f.ur && a.f.ur[idx] > 0 && fabsf(pxr - a.f.ur[idx]) > r * a.scale[pl]);
+        },
+        [&](int idx, int rank) {
+            if (FILL || (kMode == 2 && rank < a.kfix)) {
                 const uint4* d = a.f.desc + 2 * idx;
-                out[n] = make_int2(idx, hamming256(q0, q1, d[0], d[1]) | (a.f.k[idx].octave << 16));
+                out[rank] = make_int2(idx, hamming256(q0, q1, d[0], d[1]) | (a.f.k[idx].octave << 16));
             }
-            ++n;
         });
-    }
     if (kMode == 0 && lead) a.cnt[i] = n;
     if (kMode == 2 && lead) {
         a.cnt[i] = min(n, a.kfix);

@@ -984,10 +984,6 @@ int orbfe_search_for_initialization(orbfe_matcher* m, float nnratio, int check_o
     });
 }
 
-// host SearchByProjection (local map): up to this many map points one wave per point, beyond it
-// one thread per point
-constexpr int kSbpLocalWaveMax = 16384;
-
 int orbfe_search_by_projection_local(orbfe_matcher* m, float nnratio,
                                      const orbfe_frame_view* f, int32_t* frame_mp,
                                      int32_t* frame_mp_obs, const orbfe_mappoint_view* mps,
@@ -1044,19 +1040,12 @@ int orbfe_search_by_projection_local(orbfe_matcher* m, float nnratio,
             a.cnt = m->cnt.as<int>();
             a.cand = m->cand.as<int2>();
             if ((st = m->flush())) return st;
-            if (M <= kSbpLocalWaveMax)
-                hipLaunchKernelGGL((sbp_local_cand_kernel<2, true>), dim3((M + 3) / 4), dim3(256), 0, m->stream, a);
-            else
-                hipLaunchKernelGGL(sbp_local_cand_kernel<2>, dim3((M + 255) / 256), dim3(256), 0, m->stream, a);
+            hipLaunchKernelGGL(sbp_local_cand_kernel<2>, dim3((M + 3) / 4), dim3(256), 0, m->stream, a);
             ORBFE_HIP(hipGetLastError());
         } else {
             int total = 0;
-            if (M <= kSbpLocalWaveMax) {
-                if ((st = m->csr(a, M, sbp_local_cand_kernel<0, true>, sbp_local_cand_kernel<1, true>, total, 4)))
-                    return st;
-            } else if ((st = m->csr(a, M, sbp_local_cand_kernel<0>, sbp_local_cand_kernel<1>, total))) {
+            if ((st = m->csr(a, M, sbp_local_cand_kernel<0>, sbp_local_cand_kernel<1>, total, 4)))
                 return st;
-            }
         }
         const int N = f->n;
         if ((st = m->up(m->s1, frame_mp, (size_t)N * 4))) return st;
@@ -1498,7 +1487,7 @@ int orbfe_search_local_points_device(orbfe_matcher* m, const orbfe_frame_view* f
         a.off = m->off.as<int>();
         a.cand = m->cand.as<int2>();
         a.cand_cap = (long long)cap;
-        const int qb = std::max(1, (M + 255) / 256);
+        const int qb = std::max(1, (M + 3) / 4);  // one wave per map point
         hipLaunchKernelGGL(sbp_local_cand_kernel<0>, dim3(qb), dim3(256), 0, m->stream, a);
         hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, m->stream, m->cnt.as<int>(), M, m->off.as<int>());
         hipLaunchKernelGGL(sbp_local_cand_kernel<1>, dim3(qb), dim3(256), 0, m->stream, a);
@@ -1595,7 +1584,7 @@ int orbfe_search_by_projection_local_device(orbfe_matcher* m, float nnratio,
             a.off = m->off.as<int>();
             a.cand = m->cand.as<int2>();
             a.cand_cap = (long long)cap;
-            const int qb = std::max(1, (M + 255) / 256);
+            const int qb = std::max(1, (M + 3) / 4);  // one wave per map point
             hipLaunchKernelGGL(sbp_local_cand_kernel<0>, dim3(qb), dim3(256), 0, m->stream, a);
             hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, m->stream, m->cnt.as<int>(), M, m->off.as<int>());
             hipLaunchKernelGGL(sbp_local_cand_kernel<1>, dim3(qb), dim3(256), 0, m->stream, a);
