@@ -137,7 +137,7 @@ struct orbfe_extractor {
     DevBuf lk_snap;                   // orbfe_debug_replay: one FAST's per-level key totals
     DevBuf stage, rects;              // host colour frames / rectangle masks (level-0 inputs)
     DevBuf st_off, st_items, st_sad, st_status;           // stereo workspaces (left handle)
-    DevBuf st_kl, st_dl, st_kr, st_dr, st_n, st_ur, st_dp;  // stereo host-path staging
+    DevBuf st_ur;  // stereo host path: u_right | depth | status, copied back in one piece
     std::vector<int4> h_rects;
     // last run, for the probes
     int last_n = 0;
@@ -777,7 +777,7 @@ struct orbfe_extractor {
     ~orbfe_extractor() {
         for (DevBuf* b : {&cells, &xtab, &ytab, &bslot, &ptab, &pyr, &blur, &cell_cnt, &cell_keys, &keys, &act,
                           &oct_out, &oct_cnt, &oct_ord, &level_keys, &lk_snap, &out_kps, &out_desc, &out_n, &stage, &rects, &st_off, &st_items,
-                          &st_sad, &st_status, &st_kl, &st_dl, &st_kr, &st_dr, &st_n, &st_ur, &st_dp})
+                          &st_sad, &st_status, &st_ur})
             b->release();
         drop_graph();
         for (Pinned* q : {&pin_in, &pin_user, &pin_kps, &pin_desc, &pin_n, &st_pin}) q->release();
@@ -1210,13 +1210,6 @@ int orbfe_compute_stereo_matches(orbfe_extractor* left, orbfe_extractor* right, 
         orbfe_extractor* L = left;
         const int cap = std::max(nl, nr);
         hipStream_t s = L->stream;
-        if ((st = L->st_kl.ensure((size_t)cap * sizeof(orbfe_keypoint)))) return st;
-        if ((st = L->st_kr.ensure((size_t)cap * sizeof(orbfe_keypoint)))) return st;
-        if ((st = L->st_dl.ensure((size_t)cap * 32))) return st;
-        if ((st = L->st_dr.ensure((size_t)cap * 32))) return st;
-        if ((st = L->st_n.ensure(2 * sizeof(int32_t)))) return st;
-        if ((st = L->st_ur.ensure((size_t)cap * sizeof(float)))) return st;
-        if ((st = L->st_dp.ensure((size_t)cap * sizeof(float)))) return st;
         const int32_t counts[2] = {nl, nr};
         // inputs kl | dl | kr | dr | counts staged in one pinned block and copied in by one DMA;
         // outputs u_right | depth (one device block) and the status copied back into it
@@ -1237,7 +1230,6 @@ int orbfe_compute_stereo_matches(orbfe_extractor* left, orbfe_extractor* right, 
         std::memcpy(q + o_n, counts, sizeof(counts));
         ORBFE_HIP(hipMemcpyAsync(L->st_in.p, q, in_bytes, hipMemcpyHostToDevice, s));
         uint8_t* din = L->st_in.as<uint8_t>();
-        // (st_ur holds u_right then depth: one D2H copy for both)
         if ((st = L->st_ur.ensure(out_bytes))) return st;
         uint8_t* dout = L->st_ur.as<uint8_t>();
         if ((st = stereo_launch(L, right, frame, 1, reinterpret_cast<const orbfe_keypoint*>(din), din + o_dl,
